@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""Headline benchmark: AlexNet Blocks 1-2 fp32 inference throughput (images/s) on N MI355X.
+
+Metric/config from BASELINE.json: "images/sec (and ms/batch) AlexNet Blocks1-2 fp32 at 1/2/4/8
+MI355X". One step = the reference's V4/V5 pipeline at batch scale: rank 0 owns the global batch
+(device resident), scatters each rank's images over RCCL/xGMI, every rank runs the native
+Blocks 1-2 engine (MFMA implicit-GEMM convs + fused epilogues) on its shard, and the outputs are
+gathered back to rank 0. Scatter/compute/gather are pipelined over micro-batches (RCCL runs on its
+own stream, compute on the current stream). Weak scaling: --batch-per-gpu images per GPU.
+
+Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N``. Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import anx  # noqa: E402
+from anx.models.alexnet_blocks import AlexNetBlocks  # noqa: E402
+
+METRIC = "images/sec (and ms/batch) AlexNet Blocks1-2 fp32 at 1/2/4/8 MI355X; speedup+efficiency vs np"
+# V3 CUDA single GPU, RTX 3090, 610.661 ms for one image.
+BASELINE_IMG_PER_S = 1000.0 / 610.661
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch-per-gpu", type=int, default=128)
+    ap.add_argument("--micro", type=int, default=4, help="micro-batches per step for scatter/compute/gather overlap")
+    ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
+    ap.add_argument("--input-source", default="root", choices=["root", "local"],
+                    help="root: rank 0 scatters the batch (reference V4/V5 semantics); local: per-rank synthetic")
+    ap.add_argument("--no-gather", action="store_true", help="leave outputs on their ranks")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B = a.batch_per_gpu
+    d = anx.blocks_dims()
+    model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    M = max(1, min(a.micro, B)) if world > 1 else 1
+    mb = [B // M + (1 if i < B % M else 0) for i in range(M)]
+    offs = [sum(mb[:i]) for i in range(M)]
+
+    x_local = torch.empty(B, d.H, d.W, d.C0, device=dev)
+    y_local = torch.empty(B, d.Hp2, d.Wp2, d.C2, device=dev)
+    if rank == 0 and world > 1 and a.input_source == "root":
+        x_global = torch.rand(world, B, d.H, d.W, d.C0, device=dev, generator=g) * 0.1
+        y_global = torch.empty(world, B, d.Hp2, d.Wp2, d.C2, device=dev)
+    else:
+        x_global = y_global = None
+        if a.input_source == "local" or world == 1:
+            x_local.copy_(torch.rand(B, d.H, d.W, d.C0, device=dev, generator=g) * 0.1)
+
+    def step():
+        if world == 1:
+            model(x_local, out=y_local)
+            return
+        works = []
+        if a.input_source == "root":
+            for i in range(M):
+                sl = slice(offs[i], offs[i] + mb[i])
+                works.append(dist.scatter(x_local[sl], [x_global[r, sl] for r in range(world)] if rank == 0 else None,
+                                          src=0, async_op=True))
+        gw = []
+        for i in range(M):
+            sl = slice(offs[i], offs[i] + mb[i])
+            if works:
+                works[i].wait()
+            model(x_local[sl], out=y_local[sl])
+            if not a.no_gather:
+                gw.append(dist.gather(y_local[sl], [y_global[r, sl] for r in range(world)] if rank == 0 else None,
+                                      dst=0, async_op=True))
+        for w in gw:
+            w.wait()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = el * 1e3 / a.steps
+    imgs = B * world * a.steps / el
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(imgs, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(imgs / BASELINE_IMG_PER_S, 2),
+            "dtype": "fp32",
+            "data": "synthetic (U[0,0.1) images 227x227x3, random-init weights)",
+            "config": {
+                "model": "AlexNet Blocks1-2 (Conv1 11x11s4-ReLU-Pool3s2-Conv2 5x5p2-ReLU-Pool3s2-LRN5)",
+                "global_batch": B * world,
+                "seq_len": None,
+                "image": [d.H, d.W, d.C0],
+                "parallelism": f"dp{world}",
+                "pipeline": ("root scatter -> compute -> gather (RCCL), %d micro-batches" % M) if world > 1
+                else "single GPU",
+                "impl": a.impl,
+                "gflop_per_image": round(anx.flops_per_image() / 1e9, 4),
+                "tflops": round(imgs * anx.flops_per_image() / 1e12, 2),
+                "ms_per_batch": round(ms, 4),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,105 @@
+/* anx/c_api.h — flat C ABI of libanx (consumed by the Python package through ctypes and by
+ * the anx CLI). Every function returns 0 on success or a nonzero status; anx_last_error()
+ * returns the message of the last failure on the calling thread. Device pointers and HIP
+ * streams are passed as opaque pointers. */
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct anx_block_c {
+  int C, K, F, S, P, groups; /* conv */
+  int pool_F, pool_S;        /* max pool */
+  int has_lrn, lrn_N;        /* LRN */
+  float lrn_alpha, lrn_beta, lrn_k;
+  int lrn_mode; /* 0 = alpha/N (V1/V2), 1 = alpha (V3/V4) */
+} anx_block_c;
+
+/* Tile plan rows, half-open: in, c1, p1, q, c2, out (12 ints). */
+typedef struct anx_tile_c {
+  int in_lo, in_hi, c1_lo, c1_hi, p1_lo, p1_hi, q_lo, q_hi, c2_lo, c2_hi, out_lo, out_hi;
+} anx_tile_c;
+
+typedef struct anx_xfer_c {
+  int src, dst, lo, hi;
+} anx_xfer_c;
+
+const char* anx_last_error(void);
+int anx_abi_version(void);
+int anx_device_count(void);
+void anx_default_blocks(anx_block_c* b1, anx_block_c* b2);
+
+/* ---- planner ---- */
+/* Fills up to `cap` tiles / transfers; returns counts through the out pointers. */
+/* tiles[np]; owned_in[2*np] and owned_p1[2*np] as (lo,hi) pairs; halo lists up to `cap` each. */
+int anx_make_plan(int H, int W, int np, int mode, const anx_block_c* b1, const anx_block_c* b2, anx_tile_c* tiles,
+                  int* owned_in, int* owned_p1, anx_xfer_c* in_halos, int* n_in_halos, anx_xfer_c* p1_halos,
+                  int* n_p1_halos, int cap);
+
+/* ---- engine (Blocks 1-2) ---- */
+int anx_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,
+                      const float* bias1, const float* w2, const float* bias2, int max_batch, int impl);
+int anx_engine_destroy(void* e);
+int anx_engine_forward(void* e, const float* x, int N, float* y, void* stream);
+int anx_engine_tile_forward(void* e, const float* x, int N, const anx_tile_c* t, float* y, void* stream);
+int anx_engine_stage1(void* e, const float* x, int N, const anx_tile_c* t, void* stream);
+int anx_engine_stage2(void* e, int N, const anx_tile_c* t, float* y, void* stream);
+/* conv2 input window geometry: pointer of (image n, pool1 row r), row stride and image stride (floats). */
+int anx_engine_window(void* e, const anx_tile_c* t, int n, int r, float** ptr, size_t* row_floats,
+                      size_t* image_floats);
+
+/* ---- host engine (same contract as the device engine; V1 / V2 CPU ranks) ---- */
+int anx_cpu_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,
+                          const float* bias1, const float* w2, const float* bias2);
+int anx_cpu_engine_destroy(void* e);
+int anx_cpu_engine_tile_forward(void* e, const float* x, int N, const anx_tile_c* t, float* y);
+int anx_cpu_engine_stage1(void* e, const float* x, int N, const anx_tile_c* t);
+int anx_cpu_engine_stage2(void* e, int N, const anx_tile_c* t, float* y);
+int anx_cpu_engine_window(void* e, const anx_tile_c* t, int n, int r, float** ptr, size_t* row_floats,
+                          size_t* image_floats);
+/* strided host copy (memcpy per row) */
+int anx_memcpy2d_host(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes, size_t height);
+
+/* ---- memory ---- */
+/* hipMemcpy2DAsync (kind = default: direction inferred from the pointers). */
+int anx_memcpy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes, size_t height,
+                       void* stream);
+
+/* ---- device ops ---- */
+int anx_conv2d_direct(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C, int K,
+                      int F, int S, int P, int groups, int relu, void* stream);
+int anx_relu(float* x, size_t n, void* stream);
+int anx_maxpool_direct(const float* x, float* y, int N, int H, int W, int C, int F, int S, void* stream);
+int anx_lrn_direct(const float* x, float* y, int N, int H, int W, int C, int size, float alpha, float beta, float k,
+                   int mode, void* stream);
+/* out view: base + ((n*Hb + h + h_off)*Wb + w + w_off)*Cb + c_off + c */
+int anx_maxpool(const float* x, int N, int H, int W, int C, int F, int S, float* out, int Hb, int Wb, int Cb,
+                int h_off, int w_off, int c_off, void* stream);
+int anx_maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int F, int S, int size, float alpha,
+                    float beta, float k, int mode, void* stream);
+/* MFMA conv: plan -> sizes; pack on host; run. plan_out: 16 ints (opaque, pass back unchanged). */
+int anx_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups, int* plan_out,
+                  size_t* packed_floats, size_t* koff_ints);
+int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff);
+int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
+                    float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
+
+/* ---- CPU reference ---- */
+int anx_cpu_conv2d(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C, int K, int F,
+                   int S, int P, int groups, int relu);
+int anx_cpu_maxpool(const float* x, float* y, int N, int H, int W, int C, int F, int S);
+int anx_cpu_lrn(const float* x, float* y, int N, int H, int W, int C, int size, float alpha, float beta, float k,
+                int mode);
+/* Full Blocks 1-2 on the host (V1): x [N,H,W,C0] -> y [N,Hp2,Wp2,C2]. */
+int anx_cpu_blocks_forward(const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,
+                           const float* bias1, const float* w2, const float* bias2, const float* x, int N, float* y);
+
+/* ---- deterministic init (bit-identical to anx.utils.init) ---- */
+int anx_rng_uniform(uint64_t seed, uint64_t stream, float* out, size_t n);
+
+#ifdef __cplusplus
+}
+#endif

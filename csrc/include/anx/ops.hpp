@@ -1,0 +1,91 @@
+// anx/ops.hpp — layer operators: CPU reference kernels and HIP (gfx950) launchers.
+//
+// Layouts: activations NHWC (channel fastest, the reference's per-image
+// HWC plus a batch axis); conv weights KCFF `((k*C+c)*F+fh)*F+fw` as the reference stores them
+// (v1_serial/src/layers_serial.cpp:70). The fast MFMA path repacks KCFF once into a
+// GEMM-friendly [K][F*F*C] image (see ConvPlan) — the reference re-uploads weights every call
+// (v4_mpi_cuda/src/alexnet_mpi_cuda.cu:176-191); we keep them resident.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "anx/shapes.hpp"
+
+namespace anx {
+
+// ----------------------------------------------------------------------------------------
+// CPU reference kernels (V1 / V2 compute, golden oracle). Parity:
+// serialConvLayer/ReluLayer/MaxPoolLayer/LRNLayer (v1_serial/src/layers_serial.cpp:37-175).
+// ----------------------------------------------------------------------------------------
+namespace cpu {
+// y[N,Ho,Wo,K] = conv(x[N,H,W,C], w[K,C/g,F,F]) + b ; zero padding P, stride S, groups g.
+// `pad_top`/`pad_bottom` override P on the H axis (row tiles: only global edges are padded).
+void conv2d(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C, int K, int F,
+            int S, int P, int groups, bool relu, int pad_top = -1, int pad_bottom = -1);
+void relu(float* x, size_t n);
+void maxpool(const float* x, float* y, int N, int H, int W, int C, int F, int S);
+void lrn(const float* x, float* y, int N, int H, int W, int C, int size, float alpha, float beta, float k,
+         LrnMode mode);
+}  // namespace cpu
+
+// ----------------------------------------------------------------------------------------
+// HIP launchers. All take device pointers and a stream; none allocate or synchronise
+// (safe under hipGraph capture). Return hipSuccess or the launch error.
+// ----------------------------------------------------------------------------------------
+namespace hip {
+
+// Naive one-thread-per-output kernels: the device-side correctness oracle (the shape of the
+// reference's convKernel/poolKernel/lrnKernel, v3_cuda_only/src/layers_cuda.cu:20-152).
+hipError_t conv2d_direct(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C,
+                         int K, int F, int S, int P, int groups, bool relu, hipStream_t s);
+hipError_t relu(float* x, size_t n, hipStream_t s);
+hipError_t maxpool_direct(const float* x, float* y, int N, int H, int W, int C, int F, int S, hipStream_t s);
+hipError_t lrn_direct(const float* x, float* y, int N, int H, int W, int C, int size, float alpha, float beta,
+                      float k, LrnMode mode, hipStream_t s);
+
+// A strided NHWC destination: element (n,h,w,c) of the logical output lands at
+// base + ((n*Hb + h + h_off)*Wb + w + w_off)*Cb + c_off + c. Lets producers write straight into
+// the zero-bordered input buffer of the next conv (no pad pass) or into a channel slice.
+struct OutView {
+  float* base;
+  int Hb, Wb, Cb;
+  int h_off, w_off, c_off;
+};
+
+// Implicit-GEMM convolution on f32 MFMA (v_mfma_f32_32x32x2_f32), LDS-staged, fused
+// bias + optional ReLU epilogue. The input buffer must already hold the zero padding
+// (Hp = H + pads): the kernel performs no bounds checks on reads.
+struct ConvPlan {
+  int N, Hp, Wp, C;   // padded input dims
+  int K, F, S, groups;
+  int Ho, Wo;         // output dims
+  int Cg, Kg;         // per-group channels / filters
+  int kdim;           // F*F*Cg (real)
+  int kpad;           // kdim rounded up to BK
+  int kpad_n;         // Kg rounded up to BN
+  int variant;        // tile configuration id
+  int vec4;           // input chunks of 4 channels are contiguous & 16B aligned
+};
+ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups);
+// Packed weights: [groups][kpad_n][kpad] with k = (fh*F + fw)*Cg + c; zero padded.
+size_t packed_weight_floats(const ConvPlan& p);
+// Offset table: [kpad] int32 input offsets (relative to the pixel's window origin), -1 = padding.
+size_t koff_ints(const ConvPlan& p);
+// Host-side packing (weights come from the host in KCFF order).
+void pack_conv_weights_host(const ConvPlan& p, const float* w_kcff, std::vector<float>& packed,
+                            std::vector<int>& koff);
+hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, const int* koff,
+                       const float* bias, OutView out, bool relu, hipStream_t s);
+
+// Vectorised NHWC max-pool writing through an OutView (C % 4 == 0 required for the fast path).
+hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, OutView out, hipStream_t s);
+// Fused max-pool + cross-channel LRN (block 2 tail).
+hipError_t maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int F, int S, int size,
+                       float alpha, float beta, float k, LrnMode mode, hipStream_t s);
+
+// Zero the rows of an NHWC buffer outside [row_lo, row_hi) and the W border (halo buffers).
+hipError_t fill(float* x, size_t n, float v, hipStream_t s);
+
+}  // namespace hip
+}  // namespace anx

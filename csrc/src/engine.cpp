@@ -1,0 +1,199 @@
+// Blocks 1-2 engine (see anx/engine.hpp).
+#include "anx/engine.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "anx/rng.hpp"
+
+#define ANX_TRY(expr)                          \
+  do {                                         \
+    hipError_t _e = (expr);                    \
+    if (_e != hipSuccess) return _e;           \
+  } while (0)
+
+namespace anx {
+
+namespace {
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+template <class T>
+T* dev_alloc(size_t n) {
+  void* p = nullptr;
+  if (n == 0) n = 1;
+  check(hipMalloc(&p, n * sizeof(T)), "hipMalloc");
+  return static_cast<T*>(p);
+}
+template <class T>
+T* dev_upload(const std::vector<T>& h) {
+  T* d = dev_alloc<T>(h.size());
+  check(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy H2D");
+  return d;
+}
+}  // namespace
+
+void init_const(HostWeights& w, const BlockSpec& b1, const BlockSpec& b2, float wv, float bv) {
+  const ConvSpec &c1 = b1.conv, &c2 = b2.conv;
+  w.w1.assign(static_cast<size_t>(c1.K) * (c1.C / c1.groups) * c1.F * c1.F, wv);
+  w.b1.assign(c1.K, bv);
+  w.w2.assign(static_cast<size_t>(c2.K) * (c2.C / c2.groups) * c2.F * c2.F, wv);
+  w.b2.assign(c2.K, bv);
+}
+
+void init_random(HostWeights& w, const BlockSpec& b1, const BlockSpec& b2, unsigned seed) {
+  init_const(w, b1, b2);
+  // weights (u - 0.5) * 0.02, biases 0.1 (v1_serial/src/alexnet_serial.cpp:39-57).
+  for (size_t i = 0; i < w.w1.size(); ++i) w.w1[i] = (rng::uniform(seed, rng::kW1, i) - 0.5f) * 0.02f;
+  for (size_t i = 0; i < w.b1.size(); ++i) w.b1[i] = 0.1f;
+  for (size_t i = 0; i < w.w2.size(); ++i) w.w2[i] = (rng::uniform(seed, rng::kW2, i) - 0.5f) * 0.02f;
+  for (size_t i = 0; i < w.b2.size(); ++i) w.b2[i] = 0.1f;
+}
+
+void init_input_random(std::vector<float>& x, size_t n, unsigned seed) {
+  x.resize(n);
+  for (size_t i = 0; i < n; ++i) x[i] = rng::uniform(seed, rng::kInput, i) * 0.1f;
+}
+
+BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int W, const HostWeights& w,
+                           int max_batch, Impl impl)
+    : b1_(b1), b2_(b2), d_(blocks_dims(H, W, b1, b2)), max_batch_(max_batch), impl_(impl) {
+  if (b1.conv.P != 0) throw std::invalid_argument("conv1 padding must be 0 (row tiles read raw image rows)");
+  if (d_.Hp2 <= 0 || d_.Wp2 <= 0) throw std::invalid_argument("input too small for AlexNet blocks 1-2");
+  wq_ = d_.Wp1 + 2 * b2.conv.P;
+  const size_t per_img = std::max<size_t>(
+      {static_cast<size_t>(H) * W * d_.C0, static_cast<size_t>(d_.H1) * d_.W1 * d_.C1,
+       static_cast<size_t>(d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1, static_cast<size_t>(d_.H2) * d_.W2 * d_.C2});
+  chunk_ = static_cast<int>(std::min<size_t>(max_batch, ((1UL << 31) - 1) / per_img));
+  if (chunk_ < 1) throw std::invalid_argument("image too large for 32-bit kernel indexing");
+  w1h_ = w.w1;
+  w2h_ = w.w2;
+  w1_ = dev_upload(w.w1);
+  b1d_ = dev_upload(w.b1);
+  w2_ = dev_upload(w.w2);
+  b2d_ = dev_upload(w.b2);
+  c1_ = dev_alloc<float>(static_cast<size_t>(chunk_) * d_.H1 * d_.W1 * d_.C1);
+  q2_cap_ = static_cast<size_t>(max_batch) * (d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1;
+  q2_ = dev_alloc<float>(q2_cap_);
+  c2_ = dev_alloc<float>(static_cast<size_t>(chunk_) * d_.H2 * d_.W2 * d_.C2);
+}
+
+BlocksEngine::~BlocksEngine() {
+  for (void* p : {static_cast<void*>(w1_), static_cast<void*>(b1d_), static_cast<void*>(w2_),
+                  static_cast<void*>(b2d_), static_cast<void*>(w1p_), static_cast<void*>(w2p_),
+                  static_cast<void*>(koff1_), static_cast<void*>(koff2_), static_cast<void*>(c1_),
+                  static_cast<void*>(q2_), static_cast<void*>(c2_)})
+    if (p) (void)hipFree(p);
+}
+
+hipError_t BlocksEngine::ensure_window(const TilePlan& t, int N, hipStream_t s) {
+  if (t.q.lo == win_lo_ && t.q.hi == win_hi_ && N <= win_n_) return hipSuccess;
+  const size_t n = static_cast<size_t>(N) * t.q.size() * wq_ * d_.C1;
+  if (n > q2_cap_) return hipErrorInvalidValue;
+  ANX_TRY(hipMemsetAsync(q2_, 0, n * sizeof(float), s));
+  win_lo_ = t.q.lo;
+  win_hi_ = t.q.hi;
+  win_n_ = N;
+  return hipSuccess;
+}
+
+float* BlocksEngine::q2_row_ptr(const TilePlan& t, int n, int r) {
+  return q2_ + static_cast<size_t>(n) * q2_image_stride_floats(t) + static_cast<size_t>(r - t.q.lo) * q2_row_floats();
+}
+
+hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStream_t s) {
+  if (N > max_batch_) return hipErrorInvalidValue;
+  if (t.out.empty()) return hipSuccess;
+  ANX_TRY(ensure_window(t, N, s));
+  const ConvSpec& k1 = b1_.conv;
+  const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
+  const size_t q_img = q2_image_stride_floats(t);
+  for (int n0 = 0; n0 < N; n0 += chunk_) {
+    const int n = std::min(chunk_, N - n0);
+    const float* xc = x + n0 * in_img;
+    float* qc = q2_ + n0 * q_img;
+    if (impl_ == Impl::Mfma) {
+      const hip::ConvPlan p = hip::make_conv_plan(n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, k1.groups);
+      const int key = p.variant;
+      if (key != plan_key1_) {
+        std::vector<float> packed;
+        std::vector<int> koff;
+        hip::pack_conv_weights_host(p, w1h_.data(), packed, koff);
+        if (w1p_) ANX_TRY(hipFree(w1p_));
+        if (koff1_) ANX_TRY(hipFree(koff1_));
+        w1p_ = dev_upload(packed);
+        koff1_ = dev_upload(koff);
+        plan_key1_ = key;
+      }
+      ANX_TRY(hip::conv2d_mfma(p, xc, w1p_, koff1_, b1d_, hip::OutView{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0},
+                               true, s));
+    } else {
+      ANX_TRY(hip::conv2d_direct(xc, w1_, b1d_, c1_, n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, 0, k1.groups,
+                                 true, s));
+    }
+    ANX_TRY(hip::maxpool(c1_, n, t.c1.size(), d_.W1, d_.C1, b1_.pool.F, b1_.pool.S,
+                         hip::OutView{qc, t.q.size(), wq_, d_.C1, t.p1.lo - t.q.lo, b2_.conv.P, 0}, s));
+  }
+  return hipSuccess;
+}
+
+hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t s) {
+  if (N > max_batch_) return hipErrorInvalidValue;
+  if (t.out.empty()) return hipSuccess;
+  const ConvSpec& k2 = b2_.conv;
+  const size_t q_img = q2_image_stride_floats(t);
+  const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
+  for (int n0 = 0; n0 < N; n0 += chunk_) {
+    const int n = std::min(chunk_, N - n0);
+    const float* qc = q2_ + n0 * q_img;
+    float* yc = y + n0 * y_img;
+    if (impl_ == Impl::Mfma) {
+      const hip::ConvPlan p = hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups);
+      const int key = p.variant;
+      if (key != plan_key2_) {
+        std::vector<float> packed;
+        std::vector<int> koff;
+        hip::pack_conv_weights_host(p, w2h_.data(), packed, koff);
+        if (w2p_) ANX_TRY(hipFree(w2p_));
+        if (koff2_) ANX_TRY(hipFree(koff2_));
+        w2p_ = dev_upload(packed);
+        koff2_ = dev_upload(koff);
+        plan_key2_ = key;
+      }
+      ANX_TRY(hip::conv2d_mfma(p, qc, w2p_, koff2_, b2d_, hip::OutView{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0},
+                               true, s));
+    } else {
+      ANX_TRY(hip::conv2d_direct(qc, w2_, b2d_, c2_, n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, 0, k2.groups,
+                                 true, s));
+    }
+    const LrnSpec& l = b2_.lrn;
+    if (b2_.has_lrn) {
+      if (impl_ == Impl::Mfma) {
+        ANX_TRY(hip::maxpool_lrn(c2_, yc, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S, l.N, l.alpha, l.beta,
+                                 l.k, l.mode, s));
+      } else {
+        // oracle path: separate pool and LRN kernels, staged through the conv1 workspace
+        ANX_TRY(hip::maxpool_direct(c2_, c1_, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S, s));
+        ANX_TRY(hip::lrn_direct(c1_, yc, n, t.out.size(), d_.Wp2, d_.C2, l.N, l.alpha, l.beta, l.k, l.mode, s));
+      }
+    } else {
+      ANX_TRY(hip::maxpool(c2_, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S,
+                           hip::OutView{yc, t.out.size(), d_.Wp2, d_.C2, 0, 0, 0}, s));
+    }
+  }
+  return hipSuccess;
+}
+
+hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, float* y, hipStream_t s) {
+  ANX_TRY(stage1(x, N, t, s));
+  return stage2(N, t, y, s);
+}
+
+hipError_t BlocksEngine::forward(const float* x, int N, float* y, hipStream_t s) {
+  const DecompPlan p = make_plan(d_.H, d_.W, 1, Decomp::Overlap, b1_, b2_);
+  return tile_forward(x, N, p.tiles[0], y, s);
+}
+
+}  // namespace anx

@@ -1,0 +1,135 @@
+// Max-pool and fused max-pool + LRN for NHWC activations.
+//
+// Parity: poolKernel / lrnKernel (v3_cuda_only/src/layers_cuda.cu:78-152,
+// v4_mpi_cuda/src/layers_mpi_cuda.cu:54-89). The reference runs pool2 and LRN2 as two kernels
+// with a full HBM round trip in between and one thread per element; here pool2 + LRN is one
+// pass: pooled pixels are staged in LDS and the cross-channel window is read from LDS.
+// Both kernels move float4 (16 B/lane) per access; the pool writes through an OutView so pool1
+// lands directly inside conv2's zero-bordered input buffer (no pad kernel, no copy).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "anx/ops.hpp"
+
+namespace anx::hip {
+namespace {
+
+constexpr int kThreads = 256;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f32x4 max4(f32x4 a, f32x4 b) {
+  return f32x4{fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)};
+}
+
+__global__ void __launch_bounds__(kThreads) maxpool_vec4_kernel(const float* __restrict__ x, int N, int H, int W,
+                                                                int C, int F, int S, int Ho, int Wo, OutView o) {
+  const int C4 = C / 4;
+  const size_t total = static_cast<size_t>(N) * Ho * Wo * C4;
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const int c4 = static_cast<int>(i % C4);
+    size_t r = i / C4;
+    const int ox = static_cast<int>(r % Wo);
+    r /= Wo;
+    const int oy = static_cast<int>(r % Ho);
+    const int n = static_cast<int>(r / Ho);
+    f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int fh = 0; fh < F; ++fh) {
+      const int iy = oy * S + fh;
+      if (iy >= H) break;
+      const float* row = x + nhwc(n, iy, 0, c4 * 4, H, W, C);
+      for (int fw = 0; fw < F; ++fw) {
+        const int ix = ox * S + fw;
+        if (ix >= W) break;
+        m = max4(m, *reinterpret_cast<const f32x4*>(row + static_cast<size_t>(ix) * C));
+      }
+    }
+    float* dst = o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb + o.c_off +
+                 c4 * 4;
+    *reinterpret_cast<f32x4*>(dst) = m;
+  }
+}
+
+// One workgroup = PP output pixels x all C channels. Pass 1 pools into LDS, pass 2 applies LRN.
+__global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               int N, int H, int W, int C, int F, int S, int Ho,
+                                                               int Wo, int PP, int size, float a, float beta,
+                                                               float k) {
+  extern __shared__ __attribute__((aligned(16))) float pooled[];  // [PP][C]
+  const int C4 = C / 4;
+  const long P = static_cast<long>(N) * Ho * Wo;
+  const long p0 = static_cast<long>(blockIdx.x) * PP;
+  const int chunks = PP * C4;
+  for (int t = threadIdx.x; t < chunks; t += blockDim.x) {
+    const int pl = t / C4, c4 = t - pl * C4;
+    const long p = p0 + pl;
+    f32x4 m = {0.f, 0.f, 0.f, 0.f};
+    if (p < P) {
+      const int ox = static_cast<int>(p % Wo);
+      const long r = p / Wo;
+      const int oy = static_cast<int>(r % Ho);
+      const int n = static_cast<int>(r / Ho);
+      m = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      for (int fh = 0; fh < F; ++fh) {
+        const int iy = oy * S + fh;
+        if (iy >= H) break;
+        const float* row = x + nhwc(n, iy, 0, c4 * 4, H, W, C);
+        for (int fw = 0; fw < F; ++fw) {
+          const int ix = ox * S + fw;
+          if (ix >= W) break;
+          m = max4(m, *reinterpret_cast<const f32x4*>(row + static_cast<size_t>(ix) * C));
+        }
+      }
+    }
+    *reinterpret_cast<f32x4*>(pooled + pl * C + c4 * 4) = m;
+  }
+  __syncthreads();
+  const int half = size / 2;
+  for (int t = threadIdx.x; t < chunks; t += blockDim.x) {
+    const int pl = t / C4, c4 = t - pl * C4;
+    const long p = p0 + pl;
+    if (p >= P) continue;
+    const float* row = pooled + pl * C;
+    f32x4 out;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c4 * 4 + e;
+      const int lo = c - half < 0 ? 0 : c - half;
+      const int hi = c + half >= C ? C - 1 : c + half;
+      float s = 0.f;
+      for (int j = lo; j <= hi; ++j) s = fmaf(row[j], row[j], s);
+      out[e] = row[c] / powf(k + a * s, beta);
+    }
+    *reinterpret_cast<f32x4*>(y + p * C + c4 * 4) = out;
+  }
+}
+
+}  // namespace
+
+hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, OutView out, hipStream_t s) {
+  const int Ho = pool_out_dim(H, F, S), Wo = pool_out_dim(W, F, S);
+  const size_t total = static_cast<size_t>(N) * Ho * Wo * (C / 4);
+  if (total == 0) return hipSuccess;
+  if (C % 4 || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
+  size_t g = (total + kThreads - 1) / kThreads;
+  if (g > 65535) g = 65535;
+  maxpool_vec4_kernel<<<static_cast<unsigned>(g), kThreads, 0, s>>>(x, N, H, W, C, F, S, Ho, Wo, out);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int F, int S, int size, float alpha,
+                       float beta, float k, LrnMode mode, hipStream_t s) {
+  const int Ho = pool_out_dim(H, F, S), Wo = pool_out_dim(W, F, S);
+  const long P = static_cast<long>(N) * Ho * Wo;
+  if (P == 0) return hipSuccess;
+  if (C % 4 || C > 8192) return hipErrorInvalidValue;
+  const int PP = C >= 4096 ? 1 : 4096 / C;  // 16 KB of LDS per workgroup
+  const long blocks = (P + PP - 1) / PP;
+  const float a = mode == LrnMode::DivN ? alpha / static_cast<float>(size) : alpha;
+  maxpool_lrn_kernel<<<static_cast<unsigned>(blocks), kThreads, PP * C * sizeof(float), s>>>(
+      x, y, N, H, W, C, F, S, Ho, Wo, PP, size, a, beta, k);
+  return hipGetLastError();
+}
+
+}  // namespace anx::hip

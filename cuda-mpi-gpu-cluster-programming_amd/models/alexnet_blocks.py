@@ -1,0 +1,189 @@
+"""AlexNet Blocks 1-2 model (Conv1 11x11/4 -> ReLU -> MaxPool 3/2 -> Conv2 5x5/1 p2 -> ReLU ->
+MaxPool 3/2 -> LRN 5), NHWC float32, backed by the native engine.
+
+Parity with the reference's forward entry points:
+  * V1 ``alexnetForwardPass``            final_project/v1_serial/src/alexnet_serial.cpp:67-186
+  * V3 ``alexnetForwardPassCUDA``        final_project/v3_cuda_only/src/alexnet_cuda.cu:22-95
+  * V4 ``alexnetTileForwardCUDA``        final_project/v4_mpi_cuda/src/alexnet_mpi_cuda.cu:157-205
+    -> :meth:`AlexNetBlocks.tile_forward` (device tile of arbitrary height, exact row plan)
+  * V4's unused per-layer ``alexnetForwardPassMPI_CUDA`` (:40-154)
+    -> :meth:`stage1` / :meth:`window_get` / :meth:`window_put` / :meth:`stage2`
+       (per-layer halo exchange, the V5 path)
+
+On a GPU every call runs the libanx HIP kernels on torch's current stream (no host sync, graph
+capturable); on the CPU it runs libanx's C++ host engine (CpuBlocks). There is no eager-PyTorch
+fallback: the PyTorch oracle lives in :mod:`anx.models.reference` and is only used by tests.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from .. import _native as nat
+from ..config import IN_H, IN_W, BlockSpec, blocks, blocks_dims
+from ..parallel.plan import TilePlan, full_plan
+from ..utils.init import init_weights
+
+IMPLS = {"mfma": 0, "direct": 1}
+
+
+def _tile_c(t: TilePlan) -> nat.TileC:
+    return nat.TileC(t.inp.lo, t.inp.hi, t.c1.lo, t.c1.hi, t.p1.lo, t.p1.hi, t.q.lo, t.q.hi, t.c2.lo, t.c2.hi,
+                     t.out.lo, t.out.hi)
+
+
+class AlexNetBlocks:
+    def __init__(self, weights: dict | None = None, *, init: str = "const", seed: int = 0, lrn_mode: str = "div_n",
+                 groups2: int = 1, H: int = IN_H, W: int = IN_W, device="cuda", impl: str = "mfma",
+                 max_batch: int = 1, specs: tuple[BlockSpec, BlockSpec] | None = None):
+        self.b1, self.b2 = specs if specs is not None else blocks(lrn_mode, groups2)
+        if self.b1.has_lrn:
+            raise ValueError("the native engine implements LRN after block 2 only (the reference's topology)")
+        if self.b1.conv.P != 0:
+            raise ValueError("conv1 padding must be 0 (row tiles read raw image rows)")
+        self.H, self.W = H, W
+        self.dims = blocks_dims(H, W, self.b1, self.b2)
+        src = weights if weights is not None else init_weights(init, seed, self.b1, self.b2)
+        self.weights = {k: v.detach().to("cpu", torch.float32).contiguous() for k, v in src.items()}
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        if impl not in IMPLS:
+            raise ValueError(f"impl must be one of {sorted(IMPLS)}")
+        self.impl = impl
+        self._engine = None
+        self._cap = 0
+        self._ensure(max_batch)
+
+    @property
+    def is_cuda(self) -> bool:
+        return self.device.type == "cuda"
+
+    # ------------------------------------------------------------------ engine lifetime
+    def _ensure(self, n: int) -> None:
+        if self._engine is not None and (n <= self._cap or not self.is_cuda):
+            return
+        self.close()
+        h = C.c_void_p()
+        w = self.weights
+        args = (C.byref(nat.block_c(self.b1)), C.byref(nat.block_c(self.b2)), self.H, self.W, w["w1"].data_ptr(),
+                w["b1"].data_ptr(), w["w2"].data_ptr(), w["b2"].data_ptr())
+        if self.is_cuda:
+            with torch.cuda.device(self.device):
+                nat.call("anx_engine_create", C.byref(h), *args, max(1, n), IMPLS[self.impl])
+        else:
+            nat.call("anx_cpu_engine_create", C.byref(h), *args)
+        self._engine, self._cap = h, max(1, n)
+
+    def close(self) -> None:
+        if self._engine is not None:
+            if self.is_cuda:
+                torch.cuda.synchronize(self.device)
+                nat.lib().anx_engine_destroy(self._engine)
+            else:
+                nat.lib().anx_cpu_engine_destroy(self._engine)
+            self._engine = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ shapes
+    def out_shape(self, N: int, rows: int | None = None) -> tuple[int, int, int, int]:
+        d = self.dims
+        return (N, d.Hp2 if rows is None else rows, d.Wp2, d.C2)
+
+    def _check_in(self, x: torch.Tensor, rows: int) -> int:
+        if x.dim() != 4 or tuple(x.shape[1:]) != (rows, self.W, self.dims.C0):
+            raise ValueError(f"expected NHWC input [N,{rows},{self.W},{self.dims.C0}], got {tuple(x.shape)}")
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            raise ValueError("input must be contiguous float32")
+        if x.device != self.device:
+            raise ValueError(f"input on {x.device}, model on {self.device}")
+        return x.shape[0]
+
+    def _stream(self) -> int:
+        return nat.stream_ptr(self.device)
+
+    # ------------------------------------------------------------------ forward paths
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Full images: [N,H,W,3] -> [N,Hp2,Wp2,K2]."""
+        return self.tile_forward(x, full_plan(self.H, self.W, self.b1, self.b2), out)
+
+    __call__ = forward
+
+    def tile_forward(self, x: torch.Tensor, tile: TilePlan, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Row tile: ``x`` holds input rows ``tile.inp`` of N images; returns output rows ``tile.out``."""
+        N = self._check_in(x, tile.inp.size)
+        y = out if out is not None else torch.empty(self.out_shape(N, tile.out.size), device=self.device)
+        if tile.out.size == 0 or N == 0:
+            return y
+        self._ensure(N)
+        if self.is_cuda:
+            nat.call("anx_engine_tile_forward", self._engine, x.data_ptr(), N, C.byref(_tile_c(tile)), y.data_ptr(),
+                     self._stream())
+        else:
+            nat.call("anx_cpu_engine_tile_forward", self._engine, x.data_ptr(), N, C.byref(_tile_c(tile)),
+                     y.data_ptr())
+        return y
+
+    def stage1(self, x: torch.Tensor, tile: TilePlan) -> None:
+        """conv1+ReLU+pool1 of input rows ``tile.inp`` into the conv2 input window (rows tile.p1)."""
+        N = self._check_in(x, tile.inp.size)
+        self._ensure(N)
+        if self.is_cuda:
+            nat.call("anx_engine_stage1", self._engine, x.data_ptr(), N, C.byref(_tile_c(tile)), self._stream())
+        else:
+            nat.call("anx_cpu_engine_stage1", self._engine, x.data_ptr(), N, C.byref(_tile_c(tile)))
+
+    def stage2(self, N: int, tile: TilePlan, out: torch.Tensor | None = None) -> torch.Tensor:
+        """conv2+ReLU+pool2+LRN of the (halo-completed) window -> output rows ``tile.out``."""
+        y = out if out is not None else torch.empty(self.out_shape(N, tile.out.size), device=self.device)
+        if tile.out.size == 0 or N == 0:
+            return y
+        if self.is_cuda:
+            nat.call("anx_engine_stage2", self._engine, N, C.byref(_tile_c(tile)), y.data_ptr(), self._stream())
+        else:
+            nat.call("anx_cpu_engine_stage2", self._engine, N, C.byref(_tile_c(tile)), y.data_ptr())
+        return y
+
+    # ------------------------------------------------------------------ conv2 input window (halo slots)
+    def window_rows_shape(self, N: int, rows: int) -> tuple[int, int, int, int]:
+        return (N, rows, self.dims.Wp1 + 2 * self.b2.conv.P, self.dims.C1)
+
+    def _window_geom(self, tile: TilePlan, r: int):
+        p = C.c_void_p()
+        row, img = C.c_size_t(), C.c_size_t()
+        fn = "anx_engine_window" if self.is_cuda else "anx_cpu_engine_window"
+        nat.call(fn, self._engine, C.byref(_tile_c(tile)), 0, r, C.byref(p), C.byref(row), C.byref(img))
+        return p.value, row.value, img.value
+
+    def _copy2d(self, dst, dpitch, src, spitch, width, height):
+        if self.is_cuda:
+            nat.call("anx_memcpy2d_async", dst, dpitch, src, spitch, width, height, self._stream())
+        else:
+            nat.call("anx_memcpy2d_host", dst, dpitch, src, spitch, width, height)
+
+    def window_put(self, tile: TilePlan, lo: int, src: torch.Tensor) -> None:
+        """Write pool1 rows [lo, lo+src.shape[1]) (full padded rows, [N,rows,Wq,C1]) into the conv2
+        input window of ``tile`` — the receive side of a halo exchange."""
+        N, rows = src.shape[0], src.shape[1]
+        if rows == 0 or N == 0:
+            return
+        if not (tile.q.lo <= lo and lo + rows <= tile.q.hi):
+            raise ValueError("halo rows outside the tile's conv2 window")
+        src = src.contiguous()
+        base, row_f, img_f = self._window_geom(tile, lo)
+        self._copy2d(base, img_f * 4, src.data_ptr(), rows * row_f * 4, rows * row_f * 4, N)
+
+    def window_get(self, tile: TilePlan, lo: int, hi: int, N: int) -> torch.Tensor:
+        """Copy pool1 rows [lo, hi) of the window out as [N, hi-lo, Wq, C1] (the send side)."""
+        dst = torch.empty(self.window_rows_shape(N, hi - lo), device=self.device)
+        if hi <= lo or N == 0:
+            return dst
+        base, row_f, img_f = self._window_geom(tile, lo)
+        self._copy2d(dst.data_ptr(), (hi - lo) * row_f * 4, base, img_f * 4, (hi - lo) * row_f * 4, N)
+        return dst

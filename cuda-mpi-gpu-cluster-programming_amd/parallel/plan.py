@@ -1,0 +1,170 @@
+"""Exact receptive-field decomposition planner (Python mirror of csrc/src/plan.cpp).
+
+The reference sizes halos as F/2 rows and trims with ad-hoc formulas
+(final_project/v2_mpi_only/2.2_scatter_halo/src/main.cpp:119-230,
+final_project/v4_mpi_cuda/src/main_mpi_cuda.cpp:65-122), so its np>=2 outputs have 14/10 or 8/4
+rows instead of 13. This planner partitions the 13 OUTPUT rows
+and back-propagates the receptive field pool2 -> conv2 -> pool1 -> conv1, as the reference's unused
+``mapRangeStart/mapRangeEnd`` tried to (v4_mpi_cuda/src/alexnet_mpi_cuda.cu:27-83).
+
+All ranges are half-open [lo, hi) in the global row index of the named layer.
+``tests/test_plan.py`` checks this against the C++ planner (``anx_make_plan``) row by row.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+from ..config import BLOCK1, BLOCK2, BlockSpec, blocks_dims, conv_out_dim, pool_out_dim
+
+OVERLAP, PER_LAYER = "overlap", "per_layer"
+
+
+@dataclass(frozen=True)
+class Rows:
+    lo: int = 0
+    hi: int = 0
+
+    @property
+    def size(self) -> int:
+        return max(0, self.hi - self.lo)
+
+    @property
+    def empty(self) -> bool:
+        return self.hi <= self.lo
+
+    def clip(self, lo: int, hi: int) -> "Rows":
+        return Rows(max(self.lo, lo), min(self.hi, hi))
+
+
+EMPTY = Rows(0, 0)
+
+
+@dataclass(frozen=True)
+class TilePlan:
+    inp: Rows  # input image rows read
+    c1: Rows   # conv1 rows computed
+    p1: Rows   # pool1 rows computed locally
+    q: Rows    # conv2 input window (pool1 index space; outside [0,Hp1) = zero padding)
+    c2: Rows   # conv2 rows computed
+    out: Rows  # pool2/LRN rows produced (owned)
+
+
+EMPTY_TILE = TilePlan(EMPTY, EMPTY, EMPTY, EMPTY, EMPTY, EMPTY)
+
+
+@dataclass(frozen=True)
+class Xfer:
+    src: int
+    dst: int
+    rows: Rows
+
+
+@dataclass
+class DecompPlan:
+    np: int
+    mode: str
+    H: int
+    W: int
+    tiles: list = field(default_factory=list)
+    owned_in: list = field(default_factory=list)
+    in_halos: list = field(default_factory=list)
+    owned_p1: list = field(default_factory=list)
+    p1_halos: list = field(default_factory=list)
+
+
+def split_rows(n: int, np_: int) -> list[Rows]:
+    """First n % np ranks get one extra row (the reference's Scatterv rule,
+    v2_mpi_only/2.2_scatter_halo/src/main.cpp:102-109)."""
+    out, lo = [], 0
+    for i in range(np_):
+        cnt = n // np_ + (1 if i < n % np_ else 0)
+        out.append(Rows(lo, lo + cnt))
+        lo += cnt
+    return out
+
+
+def conv_rows_needed(out: Rows, F: int, S: int, P: int, in_rows: int) -> Rows:
+    if out.empty:
+        return EMPTY
+    return Rows(out.lo * S - P, (out.hi - 1) * S - P + F).clip(0, in_rows)
+
+
+def pool_rows_needed(out: Rows, F: int, S: int, in_rows: int) -> Rows:
+    if out.empty:
+        return EMPTY
+    return Rows(out.lo * S, (out.hi - 1) * S + F).clip(0, in_rows)
+
+
+def _halo_xfers(own: list[Rows], need: list[Rows]) -> list[Xfer]:
+    xs = []
+    for dst, nd in enumerate(need):
+        if nd.empty:
+            continue
+        for src, ow in enumerate(own):
+            if src == dst or ow.empty:
+                continue
+            r = nd.clip(ow.lo, ow.hi)
+            if not r.empty:
+                xs.append(Xfer(src, dst, r))
+    return xs
+
+
+def make_plan(H: int, W: int, np_: int, mode: str = OVERLAP, b1: BlockSpec = BLOCK1,
+              b2: BlockSpec = BLOCK2) -> DecompPlan:
+    if np_ < 1:
+        raise ValueError("np must be >= 1")
+    if mode not in (OVERLAP, PER_LAYER):
+        raise ValueError(f"mode must be {OVERLAP!r} or {PER_LAYER!r}")
+    d = blocks_dims(H, W, b1, b2)
+    p = DecompPlan(np_, mode, H, W)
+    for out in split_rows(d.Hp2, np_):
+        if out.empty:
+            p.tiles.append(EMPTY_TILE)
+            p.owned_p1.append(EMPTY)
+            continue
+        c2 = pool_rows_needed(out, b2.pool.F, b2.pool.S, d.H2)
+        q = Rows(c2.lo * b2.conv.S - b2.conv.P, (c2.hi - 1) * b2.conv.S - b2.conv.P + b2.conv.F)
+        if mode == OVERLAP:
+            p1 = q.clip(0, d.Hp1)
+        else:
+            step = b2.pool.S * b2.conv.S
+            hi = d.Hp1 if out.hi == d.Hp2 else out.hi * step
+            p1 = Rows(out.lo * step, min(hi, d.Hp1))
+        p.owned_p1.append(p1 if mode == PER_LAYER else EMPTY)
+        c1 = pool_rows_needed(p1, b1.pool.F, b1.pool.S, d.H1)
+        inp = conv_rows_needed(c1, b1.conv.F, b1.conv.S, b1.conv.P, H)
+        p.tiles.append(TilePlan(inp, c1, p1, q, c2, out))
+    live = [t for t in range(np_) if not p.tiles[t].out.empty]
+    p.owned_in = [Rows(H, H)] * np_
+    for i, t in enumerate(live):
+        lo = 0 if i == 0 else p.tiles[t].inp.lo
+        hi = H if i + 1 == len(live) else p.tiles[live[i + 1]].inp.lo
+        p.owned_in[t] = Rows(lo, max(lo, hi))
+    p.in_halos = _halo_xfers(p.owned_in, [t.inp for t in p.tiles])
+    if mode == PER_LAYER:
+        need = [EMPTY if t.out.empty else t.q.clip(0, d.Hp1) for t in p.tiles]
+        p.p1_halos = _halo_xfers(p.owned_p1, need)
+    check_plan(p, b1, b2)
+    return p
+
+
+def full_plan(H: int, W: int, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> TilePlan:
+    return make_plan(H, W, 1, OVERLAP, b1, b2).tiles[0]
+
+
+def check_plan(p: DecompPlan, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> None:
+    d = blocks_dims(p.H, p.W, b1, b2)
+    nxt = 0
+    for r, t in enumerate(p.tiles):
+        if t.out.empty:
+            continue
+        assert t.out.lo == nxt, f"rank {r}: output rows start at {t.out.lo}, expected {nxt}"
+        nxt = t.out.hi
+        assert t.inp.lo == t.c1.lo * b1.conv.S and conv_out_dim(t.inp.size, b1.conv.F, b1.conv.S, 0) == t.c1.size, \
+            f"rank {r}: conv1 window"
+        assert t.c1.lo == t.p1.lo * b1.pool.S and pool_out_dim(t.c1.size, b1.pool.F, b1.pool.S) == t.p1.size, \
+            f"rank {r}: pool1 window"
+        assert conv_out_dim(t.q.size, b2.conv.F, b2.conv.S, 0) == t.c2.size, f"rank {r}: conv2 window"
+        assert t.c2.lo == t.out.lo * b2.pool.S and pool_out_dim(t.c2.size, b2.pool.F, b2.pool.S) == t.out.size, \
+            f"rank {r}: pool2 window"
+    assert nxt == d.Hp2, "output rows do not cover the image"

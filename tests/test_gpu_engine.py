@@ -1,0 +1,174 @@
+"""GPU numerics: every native HIP kernel and engine path vs a plain PyTorch reference of the same
+op (fp64 oracle), plus golden values and row-tile/halo decompositions on the device."""
+import ctypes as C
+
+import pytest
+import torch
+
+from anx import _native as nat
+from anx.models.alexnet_blocks import AlexNetBlocks
+from anx.models.reference import blocks_forward, conv2d_nhwc, lrn_nhwc, maxpool_nhwc
+from anx.parallel.plan import OVERLAP, PER_LAYER, make_plan
+from anx.utils.init import init_input
+
+pytestmark = pytest.mark.gpu
+
+GOLD_DIV_N = [44.4152, 42.4612, 40.6967, 40.6967, 40.6967]
+GOLD_RAW = [29.2932, 25.9153, 23.3255, 23.3255, 23.3255]
+
+
+def test_native_library_loaded(cuda):
+    assert nat.lib().anx_device_count() >= 1
+
+
+@pytest.mark.parametrize("impl", ["mfma", "direct"])
+@pytest.mark.parametrize("mode,gold", [("div_n", GOLD_DIV_N), ("raw", GOLD_RAW)])
+def test_golden(cuda, impl, mode, gold):
+    m = AlexNetBlocks(device=cuda, lrn_mode=mode, impl=impl)
+    y = m(init_input(1, "const").to(cuda)).cpu()
+    assert y.flatten()[:5].tolist() == pytest.approx(gold, abs=2e-4)
+
+
+@pytest.mark.parametrize("impl", ["mfma", "direct"])
+@pytest.mark.parametrize("N", [1, 3, 64])
+def test_engine_vs_oracle(cuda, impl, N):
+    m = AlexNetBlocks(device=cuda, init="rand", seed=21, impl=impl, max_batch=N)
+    x = init_input(N, "rand", seed=21)
+    y = m(x.to(cuda)).cpu().double()
+    ref = blocks_forward(x, m.weights, m.b1, m.b2)
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-6)
+
+
+def test_engine_grouped_conv2(cuda):
+    m = AlexNetBlocks(device=cuda, init="rand", seed=4, groups2=2, max_batch=2)
+    x = init_input(2, "rand", seed=4)
+    torch.testing.assert_close(m(x.to(cuda)).cpu().double(), blocks_forward(x, m.weights, m.b1, m.b2),
+                               rtol=2e-5, atol=2e-6)
+
+
+def test_engine_large_batch_variant(cuda):
+    """batch 256 takes the 128x128 / 128x96 MFMA tiles (small batches take 64x64)."""
+    N = 256
+    m = AlexNetBlocks(device=cuda, init="rand", seed=8, max_batch=N)
+    x = init_input(N, "rand", seed=8)
+    y = m(x.to(cuda)).cpu()
+    idx = torch.tensor([0, 1, 127, 128, 200, 255])
+    ref = blocks_forward(x[idx], m.weights, m.b1, m.b2)
+    torch.testing.assert_close(y[idx].double(), ref, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("np_", [2, 4, 8])
+def test_device_tiles(cuda, np_):
+    m = AlexNetBlocks(device=cuda, init="rand", seed=9, max_batch=4)
+    x = init_input(4, "rand", seed=9).to(cuda)
+    full = m(x)
+    p = make_plan(227, 227, np_, OVERLAP)
+    parts = [m.tile_forward(x[:, t.inp.lo:t.inp.hi].contiguous(), t) for t in p.tiles if not t.out.empty]
+    torch.testing.assert_close(torch.cat(parts, dim=1), full, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("np_", [2, 4, 8])
+def test_device_per_layer_halo(cuda, np_):
+    m = AlexNetBlocks(device=cuda, init="rand", seed=10, max_batch=2)
+    x = init_input(2, "rand", seed=10).to(cuda)
+    full = m(x)
+    p = make_plan(227, 227, np_, PER_LAYER)
+    engines = [AlexNetBlocks(device=cuda, weights=m.weights, max_batch=2) for _ in range(np_)]
+    for r, t in enumerate(p.tiles):
+        if not t.out.empty:
+            engines[r].stage1(x[:, t.inp.lo:t.inp.hi].contiguous(), t)
+    for h in p.p1_halos:
+        engines[h.dst].window_put(p.tiles[h.dst], h.rows.lo,
+                                  engines[h.src].window_get(p.tiles[h.src], h.rows.lo, h.rows.hi, 2))
+    parts = [engines[r].stage2(2, t) for r, t in enumerate(p.tiles) if not t.out.empty]
+    torch.testing.assert_close(torch.cat(parts, dim=1), full, rtol=1e-6, atol=1e-6)
+
+
+# ---------------------------------------------------------------- single kernels
+def _conv_mfma(x, w, b, S, P, groups, relu, out=None):
+    """Run the native MFMA conv through the C ABI (pads on the host side of the contract)."""
+    N, H, W, Cin = x.shape
+    K = w.shape[0]
+    xp = torch.nn.functional.pad(x, (0, 0, P, P, P, P)).contiguous()
+    plan = (C.c_int * 16)()
+    npk, nko = C.c_size_t(), C.c_size_t()
+    nat.call("anx_conv_plan", N, H + 2 * P, W + 2 * P, Cin, K, w.shape[2], S, groups, plan, C.byref(npk),
+             C.byref(nko))
+    packed = torch.empty(npk.value)
+    koff = torch.empty(nko.value, dtype=torch.int32)
+    wc = w.detach().cpu().contiguous()
+    nat.call("anx_conv_pack", plan, wc.data_ptr(), packed.data_ptr(), koff.data_ptr())
+    packed, koff = packed.to(x.device), koff.to(x.device)
+    Ho, Wo = plan[8], plan[9]
+    y = torch.empty(N, Ho, Wo, K, device=x.device)
+    nat.call("anx_conv2d_mfma", plan, xp.data_ptr(), packed.data_ptr(), koff.data_ptr(), b.data_ptr(), y.data_ptr(),
+             Ho, Wo, K, 0, 0, 0, int(relu), nat.stream_ptr(x.device))
+    return y
+
+
+@pytest.mark.parametrize("shape", [
+    # N, H, W, C, K, F, S, P, groups
+    (1, 227, 227, 3, 96, 11, 4, 0, 1),
+    (2, 27, 27, 96, 256, 5, 1, 2, 1),
+    (2, 27, 27, 96, 256, 5, 1, 2, 2),
+    (1, 13, 13, 256, 384, 3, 1, 1, 1),
+    (3, 13, 13, 384, 256, 3, 1, 1, 2),
+    (1, 9, 11, 5, 40, 3, 2, 1, 1),     # ragged: C%4!=0, K not a tile multiple
+    (64, 27, 27, 96, 256, 5, 1, 2, 1),  # large-tile variant
+])
+def test_conv_mfma_vs_torch(cuda, shape):
+    N, H, W, Cin, K, F, S, P, g = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, Cin, device=cuda)
+    w = torch.randn(K, Cin // g, F, F, device=cuda) * 0.1
+    b = torch.randn(K, device=cuda)
+    y = _conv_mfma(x, w, b, S, P, g, relu=True)
+    ref = conv2d_nhwc(x.double(), w.double(), b.double(), S, P, g, relu=True)
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+def test_conv_direct_vs_torch(cuda):
+    torch.manual_seed(1)
+    x = torch.randn(2, 20, 21, 6, device=cuda)
+    w = torch.randn(8, 3, 5, 5, device=cuda)
+    b = torch.randn(8, device=cuda)
+    y = torch.empty(2, 10, 11, 8, device=cuda)
+    nat.call("anx_conv2d_direct", x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), 2, 20, 21, 6, 8, 5, 2, 2, 2,
+             0, nat.stream_ptr(cuda))
+    torch.testing.assert_close(y.double(), conv2d_nhwc(x.double(), w.double(), b.double(), 2, 2, 2), rtol=1e-5,
+                               atol=1e-4)
+
+
+def test_relu(cuda):
+    x = torch.randn(1001, device=cuda)
+    ref = torch.relu(x)
+    nat.call("anx_relu", x.data_ptr(), x.numel(), nat.stream_ptr(cuda))
+    torch.testing.assert_close(x, ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("vec", [True, False])
+def test_maxpool(cuda, vec):
+    x = torch.randn(3, 27, 26, 96, device=cuda)
+    ref = maxpool_nhwc(x, 3, 2)
+    y = torch.empty_like(ref)
+    if vec:
+        nat.call("anx_maxpool", x.data_ptr(), 3, 27, 26, 96, 3, 2, y.data_ptr(), 13, 12, 96, 0, 0, 0,
+                 nat.stream_ptr(cuda))
+    else:
+        nat.call("anx_maxpool_direct", x.data_ptr(), y.data_ptr(), 3, 27, 26, 96, 3, 2, nat.stream_ptr(cuda))
+    torch.testing.assert_close(y, ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_lrn_and_fused_pool_lrn(cuda, mode):
+    x = torch.rand(2, 27, 27, 256, device=cuda) * 4
+    pooled = maxpool_nhwc(x, 3, 2)
+    ref = lrn_nhwc(pooled.double(), 5, 1e-4, 0.75, 2.0, "div_n" if mode == 0 else "raw")
+    y = torch.empty_like(pooled)
+    nat.call("anx_lrn_direct", pooled.data_ptr(), y.data_ptr(), 2, 13, 13, 256, 5, 1e-4, 0.75, 2.0, mode,
+             nat.stream_ptr(cuda))
+    torch.testing.assert_close(y.double(), ref, rtol=1e-6, atol=1e-6)
+    y2 = torch.empty_like(pooled)
+    nat.call("anx_maxpool_lrn", x.data_ptr(), y2.data_ptr(), 2, 27, 27, 256, 3, 2, 5, 1e-4, 0.75, 2.0, mode,
+             nat.stream_ptr(cuda))
+    torch.testing.assert_close(y2.double(), ref, rtol=1e-6, atol=1e-6)
