@@ -71,7 +71,7 @@ _SIGS = {
     "anx_cpu_engine_window": (_I, [_P, C.POINTER(TileC), _I, _I, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_SZ)]),
     "anx_memcpy2d_host": (_I, [_P, _SZ, _P, _SZ, _SZ, _SZ]),
     "anx_memcpy2d_async": (_I, [_P, _SZ, _P, _SZ, _SZ, _SZ, _P]),
-    "anx_conv2d_direct": (_I, [_P, _P, _P, _P] + [_I] * 10 + [_I, _P]),
+    "anx_conv2d_direct": (_I, [_P, _P, _P, _P] + [_I] * 10 + [_P]),
     "anx_relu": (_I, [_P, _SZ, _P]),
     "anx_maxpool_direct": (_I, [_P, _P] + [_I] * 6 + [_P]),
     "anx_lrn_direct": (_I, [_P, _P, _I, _I, _I, _I, _I, _F, _F, _F, _I, _P]),
