@@ -26,6 +26,7 @@ import torch.distributed as dist  # noqa: E402
 
 import anx  # noqa: E402
 from anx.models.alexnet_blocks import AlexNetBlocks  # noqa: E402
+from anx.parallel.pipeline import PipelineConfig, ScatterComputeGather  # noqa: E402
 
 METRIC = "images/sec (and ms/batch) AlexNet Blocks1-2 fp32 at 1/2/4/8 MI355X; speedup+efficiency vs np"
 # V3 CUDA single GPU, RTX 3090, 610.661 ms for one image.
@@ -43,6 +44,7 @@ def parse():
     ap.add_argument("--input-source", default="root", choices=["root", "local"],
                     help="root: rank 0 scatters the batch (reference V4/V5 semantics); local: per-rank synthetic")
     ap.add_argument("--no-gather", action="store_true", help="leave outputs on their ranks")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu = gloo rehearsal (tests only)")
     return ap.parse_args()
 
 
@@ -53,68 +55,46 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if a.device == "cuda":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+    else:  # CPU rehearsal of the same pipeline over gloo (tests; no GPU)
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
 
     B = a.batch_per_gpu
     d = anx.blocks_dims()
     model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B)
+    cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather)
+    pipe = ScatterComputeGather(model, cfg, (d.H, d.W, d.C0), (d.Hp2, d.Wp2, d.C2), dev)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    M = max(1, min(a.micro, B)) if world > 1 else 1
-    mb = [B // M + (1 if i < B % M else 0) for i in range(M)]
-    offs = [sum(mb[:i]) for i in range(M)]
-
-    x_local = torch.empty(B, d.H, d.W, d.C0, device=dev)
-    y_local = torch.empty(B, d.Hp2, d.Wp2, d.C2, device=dev)
-    if rank == 0 and world > 1 and a.input_source == "root":
-        x_global = torch.rand(world, B, d.H, d.W, d.C0, device=dev, generator=g) * 0.1
-        y_global = torch.empty(world, B, d.Hp2, d.Wp2, d.C2, device=dev)
+    if pipe.x_global is not None:
+        pipe.x_global.copy_(torch.rand(pipe.x_global.shape, device=dev, generator=g) * 0.1)
     else:
-        x_global = y_global = None
-        if a.input_source == "local" or world == 1:
-            x_local.copy_(torch.rand(B, d.H, d.W, d.C0, device=dev, generator=g) * 0.1)
-
-    def step():
-        if world == 1:
-            model(x_local, out=y_local)
-            return
-        works = []
-        if a.input_source == "root":
-            for i in range(M):
-                sl = slice(offs[i], offs[i] + mb[i])
-                works.append(dist.scatter(x_local[sl], [x_global[r, sl] for r in range(world)] if rank == 0 else None,
-                                          src=0, async_op=True))
-        gw = []
-        for i in range(M):
-            sl = slice(offs[i], offs[i] + mb[i])
-            if works:
-                works[i].wait()
-            model(x_local[sl], out=y_local[sl])
-            if not a.no_gather:
-                gw.append(dist.gather(y_local[sl], [y_global[r, sl] for r in range(world)] if rank == 0 else None,
-                                      dst=0, async_op=True))
-        for w in gw:
-            w.wait()
+        pipe.x.copy_(torch.rand(pipe.x.shape, device=dev, generator=g) * 0.1)
+    step = pipe.step
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
 
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el], device=dev, dtype=torch.float64 if dev.type == "cuda" else torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ms = el * 1e3 / a.steps
@@ -139,8 +119,9 @@ def main():
                 "seq_len": None,
                 "image": [d.H, d.W, d.C0],
                 "parallelism": f"dp{world}",
-                "pipeline": ("root scatter -> compute -> gather (RCCL), %d micro-batches" % M) if world > 1
-                else "single GPU",
+                "pipeline": ("root scatter -> compute -> gather (RCCL), %d micro-batches" % len(pipe.splits))
+                if world > 1 else "single GPU",
+                "input_source": a.input_source,
                 "impl": a.impl,
                 "gflop_per_image": round(anx.flops_per_image() / 1e9, 4),
                 "tflops": round(imgs * anx.flops_per_image() / 1e12, 2),

@@ -1,0 +1,114 @@
+"""Command line: ``python -m anx <command>`` (or ``python anx.py``-style via the repo alias).
+
+  run      run one staged version (v1 v2.1 v2.2 v3 v4 v5) in this process / torchrun rank
+  launch   start N ranks of ``run`` on this node (the reference's ``mpirun -np N ./template``)
+  plan     print the exact row decomposition for np ranks
+  bench    shortcut for the headline benchmark (bench.py)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+
+
+def _run_args(ap):
+    ap.add_argument("--version", "-v", default="v3", choices=["v1", "v2.1", "v2.2", "v3", "v4", "v5"])
+    ap.add_argument("--batch", "-b", type=int, default=1)
+    ap.add_argument("--init", default="const", choices=["const", "rand"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--lrn-alpha-mode", default=None, choices=["div_n", "raw"])
+    ap.add_argument("--groups", type=int, default=1, choices=[1, 2], help="Conv2 groups (2 = AlexNet paper)")
+    ap.add_argument("--decomp", default=None, choices=["overlap", "per_layer"])
+    ap.add_argument("--strategy", default="rows", choices=["rows", "batch"])
+    ap.add_argument("--iters", type=int, default=0, help="warm iterations after the cold run")
+    ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
+    ap.add_argument("--check", action="store_true", help="compare with the PyTorch fp64 oracle")
+    ap.add_argument("--cpu-rehearsal", action="store_true", help="run a GPU version's program on CPU ranks")
+    ap.add_argument("--quiet", action="store_true")
+
+
+def cmd_run(a):
+    from .versions import RunConfig, run
+    cfg = RunConfig(version=a.version, batch=a.batch, init=a.init, seed=a.seed, lrn_mode=a.lrn_alpha_mode,
+                    groups2=a.groups, decomp=a.decomp, strategy=a.strategy, iters=a.iters, impl=a.impl,
+                    check=a.check, quiet=a.quiet, cpu_rehearsal=a.cpu_rehearsal)
+    run(cfg)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(np_: int, argv: list[str], timeout: float | None = None) -> int:
+    """Start np ranks of ``python -m anx run <argv>`` with torch.distributed env (rendezvous on
+    127.0.0.1). Returns the first nonzero exit code (fail-stop, like MPI_Abort)."""
+    port = _free_port()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    procs = []
+    for r in range(np_):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(np_), LOCAL_WORLD_SIZE=str(np_),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", "import anx.__main__ as m; m.main()", "run", *argv],
+                                      env=env, cwd=root))
+    rc = 0
+    for p in procs:
+        try:
+            c = p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            c = 124
+        rc = rc or c
+    if rc:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def cmd_launch(a, rest):
+    raise SystemExit(launch(a.np, rest, a.timeout))
+
+
+def cmd_plan(a):
+    from .parallel.plan import make_plan
+    p = make_plan(227, 227, a.np, a.decomp)
+    for r, t in enumerate(p.tiles):
+        print(f"rank {r}: out {t.out.lo}..{t.out.hi - 1}  pool1 {t.p1.lo}..{t.p1.hi - 1}  conv1 {t.c1.lo}..{t.c1.hi - 1}"
+              f"  input {t.inp.lo}..{t.inp.hi - 1}  owned input {p.owned_in[r].lo}..{p.owned_in[r].hi - 1}")
+    for x in p.in_halos:
+        print(f"input halo rows {x.rows.lo}..{x.rows.hi - 1}: rank {x.src} -> {x.dst}")
+    for x in p.p1_halos:
+        print(f"pool1 halo rows {x.rows.lo}..{x.rows.hi - 1}: rank {x.src} -> {x.dst}")
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    ap = argparse.ArgumentParser(prog="anx")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    _run_args(sub.add_parser("run"))
+    lp = sub.add_parser("launch")
+    lp.add_argument("--np", "-n", type=int, required=True)
+    lp.add_argument("--timeout", type=float, default=None)
+    pp = sub.add_parser("plan")
+    pp.add_argument("--np", "-n", type=int, default=4)
+    pp.add_argument("--decomp", default="overlap", choices=["overlap", "per_layer"])
+    sub.add_parser("bench")
+    if argv and argv[0] == "launch":
+        a, rest = ap.parse_known_args(argv)
+        if rest and rest[0] == "--":
+            rest = rest[1:]
+        return cmd_launch(a, rest)
+    if argv and argv[0] == "bench":
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        raise SystemExit(subprocess.call([sys.executable, os.path.join(root, "bench.py"), *argv[1:]]))
+    a = ap.parse_args(argv)
+    {"run": cmd_run, "plan": cmd_plan}[a.cmd](a)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,82 @@
+"""Multi-process tests of the distributed paths on CPU ranks over gloo (world_size 2 and 4).
+
+The reference "tested" distribution only by eyeballing mpirun --oversubscribe output;
+these assert that every decomposition returns exactly the single-process result.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _pipeline_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import anx  # noqa: F401
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.parallel.pipeline import PipelineConfig, ScatterComputeGather
+    from anx.utils.init import init_input
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    d = anx.blocks_dims()
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    pipe = ScatterComputeGather(m, PipelineConfig(2, micro=2), (d.H, d.W, d.C0), (d.Hp2, d.Wp2, d.C2), "cpu")
+    if rank == 0:
+        pipe.x_global.copy_(init_input(2 * world, "rand", seed=2).view(world, 2, d.H, d.W, d.C0))
+    pipe.step()
+    if rank == 0:
+        q.put(pipe.y_global.clone())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_scatter_compute_gather_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    y = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, ROOT)
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.utils.init import init_input
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    ref = m(init_input(2 * world, "rand", seed=2))
+    torch.testing.assert_close(y.view_as(ref), ref, rtol=0, atol=0)
+
+
+def test_bench_contract_gloo():
+    """bench.py under torch.distributed.run (gloo/CPU rehearsal) prints ONE valid JSON line on rank 0."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "2", "--micro", "2", "--device", "cpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in rec
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 4 and rec["value"] > 0
