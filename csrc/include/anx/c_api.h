@@ -84,6 +84,8 @@ int anx_maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int F,
 int anx_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups, int* plan_out,
                   size_t* packed_floats, size_t* koff_ints);
 int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff);
+/* tuning: force tile variant `id` for kind 0 (vec4 gather) / 1 (scalar gather); -1 = heuristic */
+int anx_conv_force_variant(int kind, int id);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

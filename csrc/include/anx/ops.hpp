@@ -75,6 +75,9 @@ size_t koff_ints(const ConvPlan& p);
 // Host-side packing (weights come from the host in KCFF order).
 void pack_conv_weights_host(const ConvPlan& p, const float* w_kcff, std::vector<float>& packed,
                             std::vector<int>& koff);
+// Force a tile variant for subsequent plans (kind 0: Cg%4==0 convs, 1: scalar-gather convs;
+// id -1 restores the heuristic). Tuning/A-B only; returns -1 for an invalid pair.
+int conv_force_variant(int kind, int id);
 hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, const int* koff,
                        const float* bias, OutView out, bool relu, hipStream_t s);
 

@@ -323,6 +323,11 @@ int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff
   });
 }
 
+int anx_conv_force_variant(int kind, int id) {
+  if (anx::hip::conv_force_variant(kind, id) != 0) return fail("invalid conv variant");
+  return 0;
+}
+
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream) {
   const auto p = plan_from_ints(plan);

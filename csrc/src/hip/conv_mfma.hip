@@ -61,7 +61,7 @@ __device__ __forceinline__ int pixel_origin(const ConvArgs& a, int m) {
   return ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool VEC4>
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool VEC4, int NBUF>
 __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -76,9 +76,14 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
   constexpr int A_ROW_STEP = kThreads / A_UNITS_PER_ROW;
   constexpr int B_ROW_STEP = kThreads / (kBK / 4);
 
-  __shared__ __attribute__((aligned(16))) float lds[(BM + BN) * kLDA];
+  // One dynamic LDS array (guide §5 item 4a: a second __shared__ object can de-pipeline the
+  // loop): [A tile | B tile | koff table]. The k->offset table is staged once per workgroup so
+  // the per-tile gather never waits on a global load before issuing its A loads.
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int kStage = (BM + BN) * kLDA;  // floats per LDS stage (A tile + B tile)
   float* As = lds;
   float* Bs = lds + BM * kLDA;
+  int* koff_s = reinterpret_cast<int*>(lds + NBUF * kStage);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -94,53 +99,63 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
 
   const float* __restrict__ x = a.x + g * a.Cg;
   const float* __restrict__ wg = a.w + static_cast<size_t>(g) * a.kpad_n * a.kpad;
-  const int* __restrict__ koff = a.koff;
+  for (int i = tid; i < a.kpad; i += kThreads) koff_s[i] = a.koff[i];
 
-  // Per-thread A rows (fixed over the K loop): window origin offsets, -1 for rows past M.
+  // Per-thread A rows (fixed over the K loop): window origin offsets; rows past M point at
+  // pixel 0 (always a valid address) and are zeroed by the a_ok mask after the load.
   const int a_unit = tid % A_UNITS_PER_ROW;
   int a_org[A_LOADS];
+  unsigned a_ok = 0;
 #pragma unroll
   for (int j = 0; j < A_LOADS; ++j) {
     const int m = m0 + tid / A_UNITS_PER_ROW + j * A_ROW_STEP;
-    a_org[j] = m < a.M ? pixel_origin(a, m) : -1;
+    a_org[j] = m < a.M ? pixel_origin(a, m) : 0;
+    a_ok |= (m < a.M ? 1u : 0u) << j;
   }
+  __syncthreads();  // koff_s visible
   const int b_unit = tid % (kBK / 4);
   const float* b_src = wg + static_cast<size_t>(n0 + tid / (kBK / 4)) * a.kpad + b_unit * 4;
 
   using AReg = typename std::conditional<VEC4, f32x4, float>::type;
   AReg ra[A_LOADS];
   f32x4 rb[B_LOADS];
+  bool kok = true;  // k chunk of the staged tile is real (not zero padding)
 
+  // Unconditional loads from always-valid addresses; the zero-masking happens at LDS-store
+  // time (store_tile), AFTER the MFMAs of the current tile, so no instruction consumes a loaded
+  // value early and the loads stay in flight across the whole compute phase.
   auto load_tile = [&](int kt) {
     const int kbase = kt * kBK;
-    const int ko = koff[kbase + (VEC4 ? a_unit * 4 : a_unit)];
+    const int ko_raw = koff_s[kbase + (VEC4 ? a_unit * 4 : a_unit)];
+    kok = ko_raw >= 0;
+    const int ko = kok ? ko_raw : 0;
 #pragma unroll
     for (int j = 0; j < A_LOADS; ++j) {
-      if constexpr (VEC4) {
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (ko >= 0 && a_org[j] >= 0) v = *reinterpret_cast<const f32x4*>(x + a_org[j] + ko);
-        ra[j] = v;
-      } else {
-        ra[j] = (ko >= 0 && a_org[j] >= 0) ? x[a_org[j] + ko] : 0.f;
-      }
+      if constexpr (VEC4)
+        ra[j] = *reinterpret_cast<const f32x4*>(x + a_org[j] + ko);
+      else
+        ra[j] = x[a_org[j] + ko];
     }
 #pragma unroll
     for (int j = 0; j < B_LOADS; ++j)
       rb[j] = *reinterpret_cast<const f32x4*>(b_src + static_cast<size_t>(j) * B_ROW_STEP * a.kpad + kbase);
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](int buf) {
+    float* As_ = As + buf * kStage;
+    float* Bs_ = Bs + buf * kStage;
 #pragma unroll
     for (int j = 0; j < A_LOADS; ++j) {
       const int row = tid / A_UNITS_PER_ROW + j * A_ROW_STEP;
+      const bool ok = kok && ((a_ok >> j) & 1u);
       if constexpr (VEC4)
-        *reinterpret_cast<f32x4*>(As + row * kLDA + a_unit * 4) = ra[j];
+        *reinterpret_cast<f32x4*>(As_ + row * kLDA + a_unit * 4) = ok ? ra[j] : f32x4{0.f, 0.f, 0.f, 0.f};
       else
-        As[row * kLDA + a_unit] = ra[j];
+        As_[row * kLDA + a_unit] = ok ? ra[j] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < B_LOADS; ++j) {
       const int row = tid / (kBK / 4) + j * B_ROW_STEP;
-      *reinterpret_cast<f32x4*>(Bs + row * kLDA + b_unit * 4) = rb[j];
+      *reinterpret_cast<f32x4*>(Bs_ + row * kLDA + b_unit * 4) = rb[j];
     }
   };
 
@@ -151,21 +166,17 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
   const int r = lane & 31, h = lane >> 5;
-  const float* a_rd = As + (wm * WM + r) * kLDA + h * (kBK / 2);
-  const float* b_rd = Bs + (wn * WN + r) * kLDA + h * (kBK / 2);
+  const int a_rd = (wm * WM + r) * kLDA + h * (kBK / 2);
+  const int b_rd = BM * kLDA + (wn * WN + r) * kLDA + h * (kBK / 2);
 
-  load_tile(0);
-  store_tile();
-  __syncthreads();
-  for (int kt = 0; kt < a.ktiles; ++kt) {
-    if (kt + 1 < a.ktiles) load_tile(kt + 1);
+  auto compute = [&](const float* base) {
 #pragma unroll
     for (int s4 = 0; s4 < kBK / 8; ++s4) {
       f32x4 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f32x4*>(a_rd + i * 32 * kLDA + s4 * 4);
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f32x4*>(base + a_rd + i * 32 * kLDA + s4 * 4);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f32x4*>(b_rd + j * 32 * kLDA + s4 * 4);
+      for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f32x4*>(base + b_rd + j * 32 * kLDA + s4 * 4);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -174,9 +185,30 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
-    if (kt + 1 < a.ktiles) {
-      store_tile();
+  };
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  if constexpr (NBUF == 1) {
+    // single LDS buffer: compute, barrier, restage, barrier
+    for (int kt = 0; kt < a.ktiles; ++kt) {
+      if (kt + 1 < a.ktiles) load_tile(kt + 1);
+      compute(lds);
+      __syncthreads();
+      if (kt + 1 < a.ktiles) {
+        store_tile(0);
+        __syncthreads();
+      }
+    }
+  } else {
+    // two LDS buffers: the restage of tile k+1 goes to the buffer read in iteration k-1, which
+    // every wave finished before the previous barrier -> one barrier per K tile.
+    for (int kt = 0; kt < a.ktiles; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < a.ktiles) load_tile(kt + 1);
+      compute(lds + cur * kStage);
+      if (kt + 1 < a.ktiles) store_tile(cur ^ 1);
       __syncthreads();
     }
   }
@@ -209,17 +241,32 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
 struct Variant {
   int BM, BN;
   bool vec4;
+  int nbuf;
 };
-// id -> tile configuration (keep in sync with the dispatch switch below).
+// id -> tile configuration (keep in sync with the dispatch switch in conv2d_mfma).
 constexpr Variant kVariants[] = {
-    {128, 128, true},   // 0: large Cg%4==0 convs (conv2, conv3-5): 2x2 waves of 64x64
-    {128, 96, false},   // 1: conv1-like (C=3, K=96): 4x1 waves of 32x96, scalar gather
-    {64, 64, true},     // 2: small problems (batch 1): 2x2 waves of 32x32
-    {64, 64, false},    // 3: small problems, scalar gather
-    {128, 128, false},  // 4: large, scalar gather (Cg%4 != 0)
+    {128, 128, true, 1},   // 0: large Cg%4==0 convs (conv2, conv3-5): 2x2 waves of 64x64
+    {128, 96, false, 1},   // 1: conv1-like (C=3, K=96): 4x1 waves of 32x96, scalar gather
+    {64, 64, true, 1},     // 2: small problems (batch 1): 2x2 waves of 32x32
+    {64, 64, false, 1},    // 3: small problems, scalar gather
+    {128, 128, false, 1},  // 4: large, scalar gather (Cg%4 != 0)
+    {128, 128, true, 2},   // 5: = 0 with double-buffered LDS (one barrier per K tile)
+    {128, 96, false, 2},   // 6: = 1 with double-buffered LDS
+    {256, 128, true, 1},   // 7: 2x2 waves of 128x64 (8 accumulators per wave)
+    {256, 96, false, 1},   // 8: conv1-like, 4x1 waves of 64x96 (6 accumulators per wave)
 };
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+// Tuning override for in-process A/B (anx_conv_force_variant): [0] vec4 convs, [1] scalar convs.
+int g_force[2] = {-1, -1};
 
 }  // namespace
+
+int conv_force_variant(int kind, int id) {
+  if (kind < 0 || kind > 1 || id < -1 || id >= kNumVariants) return -1;
+  if (id >= 0 && kVariants[id].vec4 != (kind == 0)) return -1;
+  g_force[kind] = id;
+  return 0;
+}
 
 ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups) {
   ConvPlan p{};
@@ -246,7 +293,7 @@ ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int g
     p.variant = p.vec4 ? 2 : 3;
   else
     p.variant = p.vec4 ? 0 : 4;
-  if (p.variant == 1 && p.vec4) p.variant = 1;  // scalar gather is fine for K=96 either way
+  if (g_force[p.vec4 ? 0 : 1] >= 0) p.variant = g_force[p.vec4 ? 0 : 1];
   const int BN = kVariants[p.variant].BN;
   p.kpad_n = (p.Kg + BN - 1) / BN * BN;
   return p;
@@ -311,12 +358,19 @@ hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, 
   a.n_mtiles = static_cast<int>((M + v.BM - 1) / v.BM);
   a.n_ntiles = p.kpad_n / v.BN;
   dim3 grid(a.n_mtiles * a.n_ntiles, 1, p.groups);
+  const size_t lds = static_cast<size_t>(v.nbuf) * (v.BM + v.BN) * kLDA * sizeof(float) +
+                     static_cast<size_t>(p.kpad) * sizeof(int);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   switch (p.variant) {
-    case 0: conv_mfma_kernel<128, 128, 2, 2, true><<<grid, kThreads, 0, s>>>(a); break;
-    case 1: conv_mfma_kernel<128, 96, 4, 1, false><<<grid, kThreads, 0, s>>>(a); break;
-    case 2: conv_mfma_kernel<64, 64, 2, 2, true><<<grid, kThreads, 0, s>>>(a); break;
-    case 3: conv_mfma_kernel<64, 64, 2, 2, false><<<grid, kThreads, 0, s>>>(a); break;
-    case 4: conv_mfma_kernel<128, 128, 2, 2, false><<<grid, kThreads, 0, s>>>(a); break;
+    case 0: conv_mfma_kernel<128, 128, 2, 2, true, 1><<<grid, kThreads, lds, s>>>(a); break;
+    case 1: conv_mfma_kernel<128, 96, 4, 1, false, 1><<<grid, kThreads, lds, s>>>(a); break;
+    case 2: conv_mfma_kernel<64, 64, 2, 2, true, 1><<<grid, kThreads, lds, s>>>(a); break;
+    case 3: conv_mfma_kernel<64, 64, 2, 2, false, 1><<<grid, kThreads, lds, s>>>(a); break;
+    case 4: conv_mfma_kernel<128, 128, 2, 2, false, 1><<<grid, kThreads, lds, s>>>(a); break;
+    case 5: conv_mfma_kernel<128, 128, 2, 2, true, 2><<<grid, kThreads, lds, s>>>(a); break;
+    case 6: conv_mfma_kernel<128, 96, 4, 1, false, 2><<<grid, kThreads, lds, s>>>(a); break;
+    case 7: conv_mfma_kernel<256, 128, 2, 2, true, 1><<<grid, kThreads, lds, s>>>(a); break;
+    case 8: conv_mfma_kernel<256, 96, 4, 1, false, 1><<<grid, kThreads, lds, s>>>(a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
