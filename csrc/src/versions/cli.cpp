@@ -1,0 +1,747 @@
+// anx — the native CLI: the reference's five staged programs in one binary.
+//
+//   anx --version v1|v2.1|v2.2|v3|v4|v5 [--batch N] [--init const|rand] [--seed S]
+//       [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer] [--iters K]
+//       [--impl mfma|direct] [--check] [--no-json]
+//
+// Multi-rank versions run under `anxrun -np N anx ...` (or torchrun-style RANK/WORLD_SIZE env).
+// Each run prints the reference's stdout contract and one `ANX_JSON {...}` line with
+// cold (first call incl. setup, like the reference's timers) and warm (steady-state mean) timings,
+// per-phase breakdown, checksum (CRC-32 of the fp32 output, identical to the Python package's) and,
+// with --check, the max error vs a single-process host recomputation.
+//
+// Reference programs: v1_serial/src/main.cpp:10-78, v2_mpi_only/2.1_broadcast_all/src/main.cpp:10-109,
+// v2_mpi_only/2.2_scatter_halo/src/main.cpp:23-290, v3_cuda_only/src/main_cuda.cpp:12-44,
+// v4_mpi_cuda/src/main_mpi_cuda.cpp:20-163; V5 is empty in the reference (README.md:158-166).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "anx/comm.hpp"
+#include "anx/cpu_engine.hpp"
+#include "anx/engine.hpp"
+#include "anx/plan.hpp"
+#include "anx/rng.hpp"
+
+using namespace anx;
+
+namespace {
+
+struct Options {
+  std::string version = "v3";
+  int batch = 1;
+  std::string init = "const";
+  unsigned seed = 0;
+  std::string lrn;     // "" = version default
+  int groups = 1;
+  std::string decomp;  // "" = version default
+  int iters = 0;
+  std::string impl = "mfma";
+  bool check = false;
+  bool json = true;
+};
+
+[[noreturn]] void usage(const char* msg) {
+  std::fprintf(stderr,
+               "%s\nusage: anx --version v1|v2.1|v2.2|v3|v4|v5 [--batch N] [--init const|rand] [--seed S]\n"
+               "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
+               "           [--iters K] [--impl mfma|direct] [--check] [--no-json]\n",
+               msg);
+  std::exit(2);
+}
+
+Options parse(int argc, char** argv) {
+  Options o;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) usage(("missing value for " + a).c_str());
+      return argv[++i];
+    };
+    if (a == "--version" || a == "-v") o.version = val();
+    else if (a == "--batch" || a == "-b") o.batch = std::atoi(val().c_str());
+    else if (a == "--init") o.init = val();
+    else if (a == "--seed") o.seed = static_cast<unsigned>(std::atoi(val().c_str()));
+    else if (a == "--lrn-alpha-mode") o.lrn = val();
+    else if (a == "--groups") o.groups = std::atoi(val().c_str());
+    else if (a == "--decomp") o.decomp = val();
+    else if (a == "--iters") o.iters = std::atoi(val().c_str());
+    else if (a == "--impl") o.impl = val();
+    else if (a == "--check") o.check = true;
+    else if (a == "--no-json") o.json = false;
+    else if (a == "-h" || a == "--help") usage("");
+    else usage(("unknown argument " + a).c_str());
+  }
+  static const char* vs[] = {"v1", "v2.1", "v2.2", "v3", "v4", "v5"};
+  if (std::find(std::begin(vs), std::end(vs), o.version) == std::end(vs)) usage("bad --version");
+  if (o.lrn.empty()) o.lrn = (o.version == "v1" || o.version == "v2.1" || o.version == "v2.2") ? "div_n" : "raw";
+  if (o.decomp.empty()) o.decomp = o.version == "v5" ? "per_layer" : "overlap";
+  if (o.batch < 1) usage("--batch must be >= 1");
+  return o;
+}
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+uint32_t crc32(const void* data, size_t n) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      table[i] = c;
+    }
+    init = true;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  const auto* p = static_cast<const unsigned char*>(data);
+  for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Ordered phase accumulator.
+struct Phases {
+  std::vector<std::pair<std::string, double>> v;
+  void add(const std::string& k, double ms) {
+    for (auto& p : v)
+      if (p.first == k) {
+        p.second += ms;
+        return;
+      }
+    v.push_back({k, ms});
+  }
+  double total() const {
+    double t = 0;
+    for (auto& p : v) t += p.second;
+    return t;
+  }
+  std::string json(double scale = 1.0) const {
+    std::string s = "{";
+    char buf[96];
+    for (size_t i = 0; i < v.size(); ++i) {
+      std::snprintf(buf, sizeof buf, "%s\"%s\": %.4f", i ? ", " : "", v[i].first.c_str(), v[i].second * scale);
+      s += buf;
+    }
+    return s + "}";
+  }
+};
+
+// Copy `nrows` rows (each `row_floats`) of N images between row-windowed buffers: image n of src holds
+// rows [0, src_rows) with the copied block starting at src_off; dst likewise. Host or device.
+void copy_rows(float* dst, int dst_rows, int dst_off, const float* src, int src_rows, int src_off, int nrows,
+               size_t row_floats, int N, bool device, hipStream_t s) {
+  if (nrows <= 0 || N <= 0) return;
+  const size_t w = static_cast<size_t>(nrows) * row_floats * sizeof(float);
+  const size_t dp = static_cast<size_t>(dst_rows) * row_floats * sizeof(float);
+  const size_t sp = static_cast<size_t>(src_rows) * row_floats * sizeof(float);
+  float* d = dst + static_cast<size_t>(dst_off) * row_floats;
+  const float* q = src + static_cast<size_t>(src_off) * row_floats;
+  if (device) {
+    hip_check(hipMemcpy2DAsync(d, dp, q, sp, w, N, hipMemcpyDeviceToDevice, s), "hipMemcpy2DAsync");
+  } else {
+    for (int n = 0; n < N; ++n)
+      std::memcpy(reinterpret_cast<char*>(d) + n * dp, reinterpret_cast<const char*>(q) + n * sp, w);
+  }
+}
+
+struct Setup {
+  Options o;
+  RankInfo ri;
+  BlockSpec b1, b2;
+  BlocksDims d;
+  HostWeights w;
+  std::vector<float> x;  // full input (rank 0; every rank for v2.1)
+  size_t in_row, out_row;
+};
+
+Setup make_setup(const Options& o, const RankInfo& ri) {
+  Setup s;
+  s.o = o;
+  s.ri = ri;
+  s.b1 = kBlock1;
+  s.b2 = kBlock2;
+  s.b2.conv.groups = o.groups;
+  s.b2.lrn.mode = o.lrn == "raw" ? LrnMode::Raw : LrnMode::DivN;
+  s.d = blocks_dims(kInH, kInW, s.b1, s.b2);
+  s.in_row = static_cast<size_t>(s.d.W) * s.d.C0;
+  s.out_row = static_cast<size_t>(s.d.Wp2) * s.d.C2;
+  if (o.init == "rand")
+    init_random(s.w, s.b1, s.b2, o.seed);
+  else
+    init_const(s.w, s.b1, s.b2);
+  return s;
+}
+
+void fill_input(Setup& s) {
+  const size_t n = static_cast<size_t>(s.o.batch) * s.d.H * s.in_row;
+  if (s.o.init == "rand")
+    init_input_random(s.x, n, s.o.seed);
+  else
+    s.x.assign(n, 1.0f);
+}
+
+void bcast_weights(HostComm& c, HostWeights& w) {
+  c.bcast(w.w1.data(), w.w1.size() * 4, 0);
+  c.bcast(w.b1.data(), w.b1.size() * 4, 0);
+  c.bcast(w.w2.data(), w.w2.size() * 4, 0);
+  c.bcast(w.b2.data(), w.b2.size() * 4, 0);
+}
+
+void report(const Setup& s, int np, const std::vector<float>& y, double cold_ms, double warm_ms,
+            const Phases& cold, const Phases& warm, int warm_iters, double err) {
+  const Options& o = s.o;
+  char vals[512] = {0};
+  for (int i = 0; i < 10 && i < static_cast<int>(y.size()); ++i) {
+    char b[32];
+    std::snprintf(b, sizeof b, "%s%g", i ? " " : "", std::round(y[i] * 1e4) / 1e4);
+    std::strcat(vals, b);
+  }
+  const double t = warm_iters ? warm_ms : cold_ms;
+  const std::string shape = std::to_string(s.d.Hp2) + "x" + std::to_string(s.d.Wp2) + "x" + std::to_string(s.d.C2);
+  if (o.version == "v1") {
+    const int dims[6][3] = {{s.d.H, s.d.W, s.d.C0},    {s.d.H1, s.d.W1, s.d.C1},   {s.d.Hp1, s.d.Wp1, s.d.C1},
+                            {s.d.H2, s.d.W2, s.d.C2}, {s.d.Hp2, s.d.Wp2, s.d.C2}, {s.d.Hp2, s.d.Wp2, s.d.C2}};
+    const char* names[6] = {"Input", "Conv1", "Pool1", "Conv2", "Pool2", "LRN2"};
+    for (int i = 0; i < 6; ++i)
+      std::printf("  [%s] Dimensions: H=%d, W=%d, C=%d\n", names[i], dims[i][0], dims[i][1], dims[i][2]);
+    std::printf("AlexNet Serial Forward Pass completed in %.3f ms\n", t);
+    std::printf("Final Output (first 10 values): %s\n", vals);
+  } else if (o.version == "v2.1" || o.version == "v2.2") {
+    std::printf("shape: %s\n", shape.c_str());
+    std::string five(vals);
+    int sp = 0;
+    for (size_t i = 0; i < five.size(); ++i)
+      if (five[i] == ' ' && ++sp == 5) five.resize(i);
+    std::printf("Sample values: %s\n", five.c_str());
+    std::printf("Execution Time: %.3f ms\n", t);
+  } else if (o.version == "v3") {
+    std::printf("AlexNet HIP Forward Pass completed in %.3f ms\n", t);
+    std::printf("Final Output (first 10 values): %s\n", vals);
+  } else {
+    std::printf("Final Output Shape: %s\n", shape.c_str());
+    std::printf("Final Output (first 10 values): %s\n", vals);
+    std::printf("AlexNet %s+HIP Forward Pass completed in %.3f ms\n", o.version == "v5" ? "RCCL" : "MPI", t);
+  }
+  if (o.json) {
+    std::printf(
+        "ANX_JSON {\"version\": \"%s\", \"np\": %d, \"batch\": %d, \"shape\": [%d, %d, %d], \"checksum\": %u, "
+        "\"cold_ms\": %.4f, \"warm_ms\": %s, \"images_per_s\": %s, \"phases_cold\": %s, \"phases_warm\": %s, "
+        "\"max_abs_err\": %s, \"lrn_mode\": \"%s\", \"decomp\": \"%s\", \"impl\": \"%s\", \"native\": true}\n",
+        o.version.c_str(), np, o.batch, s.d.Hp2, s.d.Wp2, s.d.C2, crc32(y.data(), y.size() * 4), cold_ms,
+        warm_iters ? std::to_string(warm_ms).c_str() : "null",
+        warm_iters ? std::to_string(o.batch / (warm_ms / 1e3)).c_str() : "null", cold.json().c_str(),
+        warm.json(warm_iters ? 1.0 / warm_iters : 1.0).c_str(), err >= 0 ? std::to_string(err).c_str() : "null",
+        o.lrn.c_str(), o.decomp.c_str(), o.impl.c_str());
+  }
+  std::fflush(stdout);
+}
+
+double check_err(const Setup& s, const std::vector<float>& y) {
+  std::vector<float> x = s.x;
+  if (x.empty()) {
+    Setup t = s;
+    fill_input(t);
+    x = t.x;
+  }
+  CpuBlocks ref(s.b1, s.b2, s.d.H, s.d.W, s.w);
+  std::vector<float> r(y.size());
+  ref.forward(x.data(), s.o.batch, r.data());
+  double e = 0;
+  for (size_t i = 0; i < y.size(); ++i) e = std::max(e, static_cast<double>(std::fabs(y[i] - r[i])));
+  return e;
+}
+
+// ------------------------------------------------------------------------------ V1 / V3 (single process)
+int run_single(Setup& s) {
+  const int N = s.o.batch;
+  Phases cold, warm;
+  const double t0 = now_ms();
+  fill_input(s);
+  std::vector<float> y(static_cast<size_t>(N) * s.d.Hp2 * s.out_row);
+  double cold_ms = 0, warm_ms = 0;
+  if (s.o.version == "v1") {
+    CpuBlocks eng(s.b1, s.b2, s.d.H, s.d.W, s.w);
+    cold.add("setup", now_ms() - t0);
+    double a = now_ms();
+    eng.forward(s.x.data(), N, y.data());
+    cold.add("compute", now_ms() - a);
+    cold_ms = now_ms() - t0;
+    for (int i = 0; i < s.o.iters; ++i) {
+      a = now_ms();
+      eng.forward(s.x.data(), N, y.data());
+      warm.add("compute", now_ms() - a);
+    }
+  } else {
+    int ndev = 0;
+    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (ndev < 1) throw std::runtime_error("v3 needs a GPU");
+    hip_check(hipSetDevice(s.ri.local_rank % ndev), "hipSetDevice");
+    hipStream_t st;
+    hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+    BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma);
+    float *dx, *dy;
+    hip_check(hipMalloc(&dx, s.x.size() * 4), "hipMalloc");
+    hip_check(hipMalloc(&dy, y.size() * 4), "hipMalloc");
+    cold.add("setup", now_ms() - t0);
+    auto step = [&](Phases& ph) {
+      double a = now_ms();
+      hip_check(hipMemcpyAsync(dx, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice, st), "H2D");
+      hip_check(hipStreamSynchronize(st), "sync");
+      ph.add("h2d", now_ms() - a);
+      a = now_ms();
+      hip_check(eng.forward(dx, N, dy, st), "forward");
+      hip_check(hipStreamSynchronize(st), "sync");
+      ph.add("compute", now_ms() - a);
+      a = now_ms();
+      hip_check(hipMemcpyAsync(y.data(), dy, y.size() * 4, hipMemcpyDeviceToHost, st), "D2H");
+      hip_check(hipStreamSynchronize(st), "sync");
+      ph.add("d2h", now_ms() - a);
+    };
+    step(cold);
+    cold_ms = now_ms() - t0;
+    for (int i = 0; i < s.o.iters; ++i) step(warm);
+    hip_check(hipFree(dx), "free");
+    hip_check(hipFree(dy), "free");
+    hip_check(hipStreamDestroy(st), "free");
+  }
+  warm_ms = s.o.iters ? warm.total() / s.o.iters : 0;
+  report(s, 1, y, cold_ms, warm_ms, cold, warm, s.o.iters, s.o.check ? check_err(s, y) : -1);
+  return 0;
+}
+
+// ------------------------------------------------------------------------------ V2.1 (replicated)
+int run_v21(Setup& s, HostComm& c) {
+  const int N = s.o.batch;
+  Phases cold, warm;
+  c.barrier();
+  const double t0 = now_ms();
+  double a = now_ms();
+  if (c.rank() == 0) fill_input(s);
+  else s.x.resize(static_cast<size_t>(N) * s.d.H * s.in_row);
+  bcast_weights(c, s.w);
+  c.bcast(s.x.data(), s.x.size() * 4, 0);  // M3: the whole image to every rank (main.cpp:71)
+  cold.add("bcast", now_ms() - a);
+  CpuBlocks eng(s.b1, s.b2, s.d.H, s.d.W, s.w);
+  std::vector<float> y(static_cast<size_t>(N) * s.d.Hp2 * s.out_row);
+  auto step = [&](Phases& ph) {
+    double t = now_ms();
+    eng.forward(s.x.data(), N, y.data());  // every rank computes everything (P1)
+    ph.add("compute", now_ms() - t);
+    t = now_ms();
+    c.barrier();
+    ph.add("barrier", now_ms() - t);
+  };
+  step(cold);
+  double cold_ms = now_ms() - t0;
+  for (int i = 0; i < s.o.iters; ++i) step(warm);
+  double tm[2] = {cold_ms, s.o.iters ? warm.total() / s.o.iters : 0};
+  c.allreduce_max(tm, 2);
+  if (c.rank() == 0) report(s, c.size(), y, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y) : -1);
+  c.barrier();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------ V2.2 / V4 (host-staged rows)
+int run_rows_host(Setup& s, HostComm& c, bool gpu) {
+  const int N = s.o.batch, rank = c.rank(), np = c.size();
+  const Decomp mode = s.o.decomp == "per_layer" ? Decomp::PerLayer : Decomp::Overlap;
+  const DecompPlan plan = make_plan(s.d.H, s.d.W, np, mode, s.b1, s.b2);
+  const TilePlan& t = plan.tiles[rank];
+  const RowRange own = plan.owned_in[rank];
+  Phases cold, warm;
+  c.barrier();
+  const double t0 = now_ms();
+  double a = now_ms();
+  if (rank == 0) fill_input(s);
+  bcast_weights(c, s.w);  // M4/M5
+  cold.add("bcast", now_ms() - a);
+  a = now_ms();
+  std::unique_ptr<CpuBlocks> ceng;
+  std::unique_ptr<BlocksEngine> geng;
+  hipStream_t st = nullptr;
+  float *d_in = nullptr, *d_y = nullptr, *h_in = nullptr, *h_y = nullptr;
+  std::vector<float> tile_in(static_cast<size_t>(N) * t.in.size() * s.in_row);
+  std::vector<float> y_loc(static_cast<size_t>(N) * t.out.size() * s.out_row);
+  std::vector<float> own_buf(static_cast<size_t>(N) * own.size() * s.in_row);
+  if (gpu) {
+    int ndev = 0;
+    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (ndev < 1) throw std::runtime_error("v4 needs a GPU");
+    hip_check(hipSetDevice(s.ri.local_rank % ndev), "hipSetDevice");  // fixes reference D4
+    hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+    geng = std::make_unique<BlocksEngine>(s.b1, s.b2, s.d.H, s.d.W, s.w, N,
+                                          s.o.impl == "direct" ? Impl::Direct : Impl::Mfma);
+    hip_check(hipMalloc(&d_in, std::max<size_t>(1, tile_in.size()) * 4), "hipMalloc");
+    hip_check(hipMalloc(&d_y, std::max<size_t>(1, y_loc.size()) * 4), "hipMalloc");
+    hip_check(hipHostMalloc(&h_in, std::max<size_t>(1, tile_in.size()) * 4, hipHostMallocDefault), "pinned");
+    hip_check(hipHostMalloc(&h_y, std::max<size_t>(1, y_loc.size()) * 4, hipHostMallocDefault), "pinned");
+  } else {
+    ceng = std::make_unique<CpuBlocks>(s.b1, s.b2, s.d.H, s.d.W, s.w);
+  }
+  cold.add("setup", now_ms() - a);
+  std::vector<float> y_full(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
+  std::vector<std::vector<float>> stage(np);
+  std::vector<std::vector<float>> hbufs;
+
+  auto step = [&](Phases& ph) {
+    // scatter owned input rows (Scatterv, M9)
+    double q = now_ms();
+    if (rank == 0) {
+      for (int r = 0; r < np; ++r) {
+        const RowRange o = plan.owned_in[r];
+        if (o.empty()) continue;
+        float* dst = r == 0 ? own_buf.data() : (stage[r].resize(static_cast<size_t>(N) * o.size() * s.in_row),
+                                               stage[r].data());
+        copy_rows(dst, o.size(), 0, s.x.data(), s.d.H, o.lo, o.size(), s.in_row, N, false, nullptr);
+        if (r) c.isend(dst, stage[r].size() * 4, r);
+      }
+    } else if (!own.empty()) {
+      c.irecv(own_buf.data(), own_buf.size() * 4, 0);
+    }
+    c.wait_all();
+    ph.add("scatter", now_ms() - q);
+    // input halo exchange (M10/M12) — planner transfers, both directions in one group
+    q = now_ms();
+    hbufs.clear();
+    std::vector<std::pair<RowRange, float*>> recvs;
+    for (const HaloXfer& h : plan.in_halos) {
+      if (h.src == rank) {
+        hbufs.emplace_back(static_cast<size_t>(N) * h.rows.size() * s.in_row);
+        copy_rows(hbufs.back().data(), h.rows.size(), 0, own_buf.data(), own.size(), h.rows.lo - own.lo,
+                  h.rows.size(), s.in_row, N, false, nullptr);
+      } else if (h.dst == rank) {
+        hbufs.emplace_back(static_cast<size_t>(N) * h.rows.size() * s.in_row);
+      }
+    }
+    size_t bi = 0;
+    for (const HaloXfer& h : plan.in_halos) {
+      if (h.src == rank) c.isend(hbufs[bi++].data(), static_cast<size_t>(N) * h.rows.size() * s.in_row * 4, h.dst);
+      else if (h.dst == rank) {
+        c.irecv(hbufs[bi].data(), static_cast<size_t>(N) * h.rows.size() * s.in_row * 4, h.src);
+        recvs.push_back({h.rows, hbufs[bi++].data()});
+      }
+    }
+    c.wait_all();
+    if (!t.out.empty()) {
+      const int lo = std::max(own.lo, t.in.lo), hi = std::min(own.hi, t.in.hi);
+      copy_rows(tile_in.data(), t.in.size(), lo - t.in.lo, own_buf.data(), own.size(), lo - own.lo, hi - lo,
+                s.in_row, N, false, nullptr);
+      for (auto& rv : recvs)
+        copy_rows(tile_in.data(), t.in.size(), rv.first.lo - t.in.lo, rv.second, rv.first.size(), 0,
+                  rv.first.size(), s.in_row, N, false, nullptr);
+    }
+    ph.add("halo", now_ms() - q);
+    // compute (V4: host -> device -> host around the tile, pinned buffers)
+    if (!t.out.empty()) {
+      if (gpu) {
+        q = now_ms();
+        std::memcpy(h_in, tile_in.data(), tile_in.size() * 4);
+        hip_check(hipMemcpyAsync(d_in, h_in, tile_in.size() * 4, hipMemcpyHostToDevice, st), "H2D");
+        hip_check(hipStreamSynchronize(st), "sync");
+        ph.add("h2d", now_ms() - q);
+        q = now_ms();
+        if (mode == Decomp::Overlap) {
+          hip_check(geng->tile_forward(d_in, N, t, d_y, st), "tile_forward");
+        } else {
+          throw std::runtime_error("v4 supports --decomp overlap (per-layer halos are the v5 path)");
+        }
+        hip_check(hipStreamSynchronize(st), "sync");
+        ph.add("compute", now_ms() - q);
+        q = now_ms();
+        hip_check(hipMemcpyAsync(h_y, d_y, y_loc.size() * 4, hipMemcpyDeviceToHost, st), "D2H");
+        hip_check(hipStreamSynchronize(st), "sync");
+        std::memcpy(y_loc.data(), h_y, y_loc.size() * 4);
+        ph.add("d2h", now_ms() - q);
+      } else {
+        q = now_ms();
+        if (mode == Decomp::Overlap) {
+          ceng->tile_forward(tile_in.data(), N, t, y_loc.data());
+        } else {
+          throw std::runtime_error("v2.2 supports --decomp overlap");
+        }
+        ph.add("compute", now_ms() - q);
+      }
+    }
+    // gather output rows (Gatherv, M16)
+    q = now_ms();
+    if (rank == 0) {
+      for (int r = 1; r < np; ++r) {
+        const RowRange o = plan.tiles[r].out;
+        if (o.empty()) continue;
+        stage[r].resize(static_cast<size_t>(N) * o.size() * s.out_row);
+        c.irecv(stage[r].data(), stage[r].size() * 4, r);
+      }
+      c.wait_all();
+      for (int r = 0; r < np; ++r) {
+        const RowRange o = plan.tiles[r].out;
+        if (o.empty()) continue;
+        copy_rows(y_full.data(), s.d.Hp2, o.lo, r == 0 ? y_loc.data() : stage[r].data(), o.size(), 0, o.size(),
+                  s.out_row, N, false, nullptr);
+      }
+    } else if (!t.out.empty()) {
+      c.send(y_loc.data(), y_loc.size() * 4, 0);
+    }
+    ph.add("gather", now_ms() - q);
+  };
+  step(cold);
+  double cold_ms = now_ms() - t0;
+  for (int i = 0; i < s.o.iters; ++i) step(warm);
+  double tm[2] = {cold_ms, s.o.iters ? warm.total() / s.o.iters : 0};
+  c.allreduce_max(tm, 2);
+  if (rank == 0) report(s, np, y_full, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y_full) : -1);
+  if (gpu) {
+    (void)hipFree(d_in);
+    (void)hipFree(d_y);
+    (void)hipHostFree(h_in);
+    (void)hipHostFree(h_y);
+    (void)hipStreamDestroy(st);
+  }
+  c.barrier();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------ V5 (device-resident RCCL)
+int run_v5(Setup& s, HostComm& c) {
+  const int N = s.o.batch, rank = c.rank(), np = c.size();
+  const Decomp mode = s.o.decomp == "overlap" ? Decomp::Overlap : Decomp::PerLayer;
+  const DecompPlan plan = make_plan(s.d.H, s.d.W, np, mode, s.b1, s.b2);
+  const TilePlan& t = plan.tiles[rank];
+  const RowRange own = plan.owned_in[rank];
+  int ndev = 0;
+  hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+  if (ndev < 1) throw std::runtime_error("v5 needs a GPU");
+  if (np > ndev) throw std::runtime_error("v5 needs one GPU per rank (RCCL rejects shared devices)");
+  const int dev = s.ri.local_rank % ndev;
+  Phases cold, warm;
+  c.barrier();
+  const double t0 = now_ms();
+  double a = now_ms();
+  if (rank == 0) fill_input(s);
+  bcast_weights(c, s.w);
+  DeviceComm dc(c, dev);
+  hipStream_t st;
+  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma);
+  auto dalloc = [](size_t n) {
+    float* p = nullptr;
+    hip_check(hipMalloc(&p, std::max<size_t>(1, n) * 4), "hipMalloc");
+    return p;
+  };
+  float* d_x = rank == 0 ? dalloc(s.x.size()) : nullptr;
+  float* d_own = dalloc(static_cast<size_t>(N) * own.size() * s.in_row);
+  float* d_tile = dalloc(static_cast<size_t>(N) * t.in.size() * s.in_row);
+  float* d_y = dalloc(static_cast<size_t>(N) * t.out.size() * s.out_row);
+  float* d_yfull = rank == 0 ? dalloc(static_cast<size_t>(N) * s.d.Hp2 * s.out_row) : nullptr;
+  std::vector<float*> d_stage(np, nullptr);
+  if (rank == 0)
+    for (int r = 1; r < np; ++r) {
+      const size_t in_n = static_cast<size_t>(N) * plan.owned_in[r].size() * s.in_row;
+      const size_t out_n = static_cast<size_t>(N) * plan.tiles[r].out.size() * s.out_row;
+      d_stage[r] = dalloc(std::max(in_n, out_n));
+    }
+  // halo buffers (input rows and pool1 window rows), sized for the largest transfer
+  size_t hmax = 1;
+  for (auto& h : plan.in_halos) hmax = std::max(hmax, static_cast<size_t>(N) * h.rows.size() * s.in_row);
+  for (auto& h : plan.p1_halos) hmax = std::max(hmax, static_cast<size_t>(N) * h.rows.size() * eng.q2_row_floats());
+  std::vector<float*> d_halo;
+  for (size_t i = 0; i < plan.in_halos.size() + plan.p1_halos.size(); ++i) d_halo.push_back(dalloc(hmax));
+  if (rank == 0)
+    hip_check(hipMemcpy(d_x, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice), "H2D input");
+  std::vector<float> y_host(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
+  hip_check(hipDeviceSynchronize(), "sync");
+  cold.add("setup", now_ms() - a);
+  hipStream_t cs = dc.stream();
+
+  auto sync_all = [&]() {
+    hip_check(hipStreamSynchronize(cs), "sync");
+    hip_check(hipStreamSynchronize(st), "sync");
+  };
+  auto step = [&](Phases& ph) {
+    // scatter owned rows: root packs per destination on device, grouped ncclSend/Recv
+    double q = now_ms();
+    dc.after(st);
+    if (rank == 0) {
+      for (int r = 0; r < np; ++r) {
+        const RowRange o = plan.owned_in[r];
+        if (o.empty()) continue;
+        copy_rows(r == 0 ? d_own : d_stage[r], o.size(), 0, d_x, s.d.H, o.lo, o.size(), s.in_row, N, true, cs);
+      }
+    }
+    dc.group_start();
+    if (rank == 0) {
+      for (int r = 1; r < np; ++r)
+        if (!plan.owned_in[r].empty())
+          dc.send(d_stage[r], static_cast<size_t>(N) * plan.owned_in[r].size() * s.in_row * 4, r);
+    } else if (!own.empty()) {
+      dc.recv(d_own, static_cast<size_t>(N) * own.size() * s.in_row * 4, 0);
+    }
+    dc.group_end();
+    sync_all();
+    ph.add("scatter", now_ms() - q);
+    // input halos, device to device
+    q = now_ms();
+    size_t hi = 0;
+    std::vector<std::pair<RowRange, float*>> recvs;
+    for (const HaloXfer& h : plan.in_halos) {
+      if (h.src == rank)
+        copy_rows(d_halo[hi], h.rows.size(), 0, d_own, own.size(), h.rows.lo - own.lo, h.rows.size(), s.in_row, N,
+                  true, cs);
+      if (h.src == rank || h.dst == rank) ++hi;
+    }
+    hi = 0;
+    dc.group_start();
+    for (const HaloXfer& h : plan.in_halos) {
+      const size_t bytes = static_cast<size_t>(N) * h.rows.size() * s.in_row * 4;
+      if (h.src == rank) dc.send(d_halo[hi++], bytes, h.dst);
+      else if (h.dst == rank) {
+        dc.recv(d_halo[hi], bytes, h.src);
+        recvs.push_back({h.rows, d_halo[hi++]});
+      }
+    }
+    dc.group_end();
+    if (!t.out.empty()) {
+      const int lo = std::max(own.lo, t.in.lo), up = std::min(own.hi, t.in.hi);
+      copy_rows(d_tile, t.in.size(), lo - t.in.lo, d_own, own.size(), lo - own.lo, up - lo, s.in_row, N, true, cs);
+      for (auto& rv : recvs)
+        copy_rows(d_tile, t.in.size(), rv.first.lo - t.in.lo, rv.second, rv.first.size(), 0, rv.first.size(),
+                  s.in_row, N, true, cs);
+    }
+    dc.before(st);
+    sync_all();
+    ph.add("halo_in", now_ms() - q);
+    // conv1 + pool1 on the compute stream
+    q = now_ms();
+    if (!t.out.empty()) hip_check(eng.stage1(d_tile, N, t, st), "stage1");
+    hip_check(hipStreamSynchronize(st), "sync");
+    ph.add("compute", now_ms() - q);
+    // pool1 halos straight between the conv2 input windows of neighbouring GPUs
+    q = now_ms();
+    if (mode == Decomp::PerLayer) {
+      dc.after(st);
+      const size_t rowf = eng.q2_row_floats();
+      const int qrows = t.q.size();
+      std::vector<std::pair<RowRange, float*>> prv;
+      size_t pi = plan.in_halos.size();
+      size_t pk = pi;
+      for (const HaloXfer& h : plan.p1_halos)
+        if (h.src == rank) {
+          copy_rows(d_halo[pk], h.rows.size(), 0, eng.q2_row_ptr(t, 0, t.q.lo), qrows, h.rows.lo - t.q.lo,
+                    h.rows.size(), rowf, N, true, cs);
+          ++pk;
+        } else if (h.dst == rank) {
+          ++pk;
+        }
+      dc.group_start();
+      for (const HaloXfer& h : plan.p1_halos) {
+        const size_t bytes = static_cast<size_t>(N) * h.rows.size() * rowf * 4;
+        if (h.src == rank) dc.send(d_halo[pi++], bytes, h.dst);
+        else if (h.dst == rank) {
+          dc.recv(d_halo[pi], bytes, h.src);
+          prv.push_back({h.rows, d_halo[pi++]});
+        }
+      }
+      dc.group_end();
+      for (auto& rv : prv)
+        copy_rows(eng.q2_row_ptr(t, 0, t.q.lo), qrows, rv.first.lo - t.q.lo, rv.second, rv.first.size(), 0,
+                  rv.first.size(), rowf, N, true, cs);
+      dc.before(st);
+      sync_all();
+    }
+    ph.add("halo_p1", now_ms() - q);
+    q = now_ms();
+    if (!t.out.empty()) hip_check(eng.stage2(N, t, d_y, st), "stage2");
+    hip_check(hipStreamSynchronize(st), "sync");
+    ph.add("compute", now_ms() - q);
+    // gather to rank 0 over RCCL, then one D2H of the full output
+    q = now_ms();
+    dc.after(st);
+    dc.group_start();
+    if (rank == 0) {
+      for (int r = 1; r < np; ++r)
+        if (!plan.tiles[r].out.empty())
+          dc.recv(d_stage[r], static_cast<size_t>(N) * plan.tiles[r].out.size() * s.out_row * 4, r);
+    } else if (!t.out.empty()) {
+      dc.send(d_y, static_cast<size_t>(N) * t.out.size() * s.out_row * 4, 0);
+    }
+    dc.group_end();
+    if (rank == 0) {
+      for (int r = 0; r < np; ++r) {
+        const RowRange o = plan.tiles[r].out;
+        if (o.empty()) continue;
+        copy_rows(d_yfull, s.d.Hp2, o.lo, r == 0 ? d_y : d_stage[r], o.size(), 0, o.size(), s.out_row, N, true, cs);
+      }
+      hip_check(hipMemcpyAsync(y_host.data(), d_yfull, y_host.size() * 4, hipMemcpyDeviceToHost, cs), "D2H");
+    }
+    sync_all();
+    ph.add("gather", now_ms() - q);
+  };
+  step(cold);
+  double cold_ms = now_ms() - t0;
+  for (int i = 0; i < s.o.iters; ++i) step(warm);
+  double tm[2] = {cold_ms, s.o.iters ? warm.total() / s.o.iters : 0};
+  c.allreduce_max(tm, 2);
+  if (rank == 0) report(s, np, y_host, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y_host) : -1);
+  for (float* p : {d_x, d_own, d_tile, d_y, d_yfull})
+    if (p) (void)hipFree(p);
+  for (float* p : d_stage)
+    if (p) (void)hipFree(p);
+  for (float* p : d_halo) (void)hipFree(p);
+  (void)hipStreamDestroy(st);
+  c.barrier();
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const Options o = parse(argc, argv);
+  const RankInfo ri = rank_info_from_env();
+  try {
+    Setup s = make_setup(o, ri);
+    if (o.version == "v1" || o.version == "v3") {
+      if (ri.world > 1) throw std::runtime_error(o.version + " is a single-process version");
+      return run_single(s);
+    }
+    const char* tmo = std::getenv("ANX_COMM_TIMEOUT");
+    HostComm c(ri, tmo ? std::atof(tmo) : 300.0);
+    // Fault injection for the fail-stop tests: ANX_FAULT=exit:R | hang:R makes rank R
+    // exit(3) or stall after bootstrap; the peers must abort (comm watchdog / closed sockets).
+    if (const char* f = std::getenv("ANX_FAULT")) {
+      const std::string fs(f);
+      const size_t colon = fs.find(':');
+      if (colon != std::string::npos && std::atoi(fs.c_str() + colon + 1) == ri.rank) {
+        if (fs.compare(0, colon, "exit") == 0) c.abort("injected fault (exit)", 3);
+        if (fs.compare(0, colon, "hang") == 0)
+          for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+      }
+    }
+    try {
+      if (o.version == "v2.1") return run_v21(s, c);
+      if (o.version == "v2.2") return run_rows_host(s, c, false);
+      if (o.version == "v4") return run_rows_host(s, c, true);
+      return run_v5(s, c);
+    } catch (const std::exception& e) {
+      c.abort(e.what());  // coordinated fail-stop (the reference's CUDA_CHECK -> MPI_Abort, N29)
+    }
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "[anx rank %d] error: %s\n", ri.rank, e.what());
+    return 1;
+  }
+}

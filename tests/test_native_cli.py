@@ -1,0 +1,100 @@
+"""The native CLI (`anx`, C++) and launcher (`anxrun`): the reference's per-version executables.
+CPU versions run here; GPU versions are marked. Outputs must match the Python package bit for bit
+(same C++ kernels, same counter-based RNG) — CRC-32 checksums are compared."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "cuda-mpi-gpu-cluster-programming_amd", "bin")
+ANX, ANXRUN = os.path.join(BIN, "anx"), os.path.join(BIN, "anxrun")
+
+pytestmark = pytest.mark.skipif(not os.path.exists(ANX), reason="native CLI not built")
+
+
+def native(args, np_=None, timeout=300, env=None, expect=0):
+    cmd = ([ANXRUN, "-np", str(np_), "--timeout", str(timeout), ANX] if np_ else [ANX]) + args
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout + 30,
+                         env=dict(os.environ, OMP_NUM_THREADS="1", **(env or {})))
+    ok = out.returncode != 0 if expect == "nonzero" else out.returncode == expect
+    assert ok, f"rc={out.returncode}\n" + out.stdout[-2000:] + out.stderr[-3000:]
+    recs = [json.loads(l[len("ANX_JSON "):]) for l in out.stdout.splitlines() if l.startswith("ANX_JSON ")]
+    return (recs[0] if recs else None), out
+
+
+@pytest.fixture(scope="module")
+def py_serial():
+    sys.path.insert(0, ROOT)
+    from anx.versions import RunConfig, run
+    return run(RunConfig(version="v1", init="rand", seed=3, batch=2, quiet=True)).checksum
+
+
+def test_v1_golden_and_contract():
+    rec, out = native(["--version", "v1"])
+    assert "AlexNet Serial Forward Pass completed in" in out.stdout
+    assert "44.4152 42.4612 40.6967" in out.stdout
+    assert rec["shape"] == [13, 13, 256] and rec["native"] is True
+
+
+def test_v1_matches_python(py_serial):
+    rec, _ = native(["--version", "v1", "--init", "rand", "--seed", "3", "--batch", "2", "--check"])
+    assert rec["checksum"] == py_serial
+    assert rec["max_abs_err"] == 0.0
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_v21(py_serial, np_):
+    rec, out = native(["--version", "v2.1", "--init", "rand", "--seed", "3", "--batch", "2"], np_)
+    assert rec["np"] == np_ and rec["checksum"] == py_serial
+    assert "Execution Time:" in out.stdout
+
+
+@pytest.mark.parametrize("np_", [2, 4, 7])
+def test_v22(py_serial, np_):
+    rec, out = native(["--version", "v2.2", "--init", "rand", "--seed", "3", "--batch", "2", "--iters", "1"], np_)
+    assert rec["checksum"] == py_serial and "shape: 13x13x256" in out.stdout
+    assert set(rec["phases_warm"]) >= {"scatter", "halo", "compute", "gather"}
+
+
+def test_fail_stop_exit():
+    """A rank that dies takes the job down (MPI_Abort semantics), nonzero exit, no hang."""
+    _, out = native(["--version", "v2.2"], 3, timeout=60, env={"ANX_FAULT": "exit:1"}, expect="nonzero")
+    assert "injected fault" in out.stderr
+
+
+def test_fail_stop_hang_watchdog():
+    """A stalled rank trips the comm watchdog of its peers (ANX_COMM_TIMEOUT) -> abort."""
+    _, out = native(["--version", "v2.2"], 2, timeout=60, env={"ANX_FAULT": "hang:1", "ANX_COMM_TIMEOUT": "3"},
+                    expect="nonzero")
+    assert "timeout" in out.stderr
+
+
+@pytest.mark.gpu
+def test_native_v3_gpu(cuda):
+    rec, out = native(["--version", "v3", "--iters", "3"])
+    assert "29.2932 25.9153 23.3255" in out.stdout
+    assert rec["warm_ms"] is not None
+
+
+@pytest.mark.gpu
+def test_native_v3_batch_check(cuda):
+    rec, _ = native(["--version", "v3", "--batch", "32", "--init", "rand", "--check", "--iters", "2"])
+    assert rec["max_abs_err"] < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("np_", [2, 3])
+def test_native_v4_shared_gpu(cuda, np_):
+    ref, _ = native(["--version", "v3", "--init", "rand", "--seed", "5", "--batch", "3"])
+    rec, out = native(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", "--iters", "2"], np_)
+    assert "Final Output Shape: 13x13x256" in out.stdout
+    assert rec["checksum"] == ref["checksum"]
+
+
+@pytest.mark.gpu
+def test_native_v5_single_rank(cuda):
+    rec, _ = native(["--version", "v5", "--init", "rand", "--batch", "4", "--check", "--iters", "2"], 1)
+    assert rec["max_abs_err"] < 1e-3
