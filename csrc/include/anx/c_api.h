@@ -86,6 +86,11 @@ int anx_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups,
 int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff);
 /* tuning: force tile variant `id` for kind 0 (vec4 gather) / 1 (scalar gather); -1 = heuristic */
 int anx_conv_force_variant(int kind, int id);
+/* Conv2 (5x5 s1) algorithm on the MFMA path: 0 auto (Winograd F(3,5) when eligible), 1 direct, 2 Winograd */
+int anx_set_conv2_algo(int algo);
+int anx_get_conv2_algo(void);
+/* fused Winograd kernel tuning: bit0 K-slice 48, bit1 XCD-aware order (default 3) */
+int anx_wino_fused_cfg(int cfg);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

@@ -23,6 +23,13 @@ enum class Impl : int {
   Direct = 1,  // naive one-thread-per-output kernels (device oracle)
 };
 
+// Algorithm for 5x5 stride-1 convolutions (Conv2) on the Mfma path: Auto picks Winograd
+// F(3x3,5x5) whenever eligible. Process-wide; read when a stage is launched.
+// WinogradUnfused = input transform + separate batched GEMM (M in HBM) + output transform (A/B).
+enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2, WinogradUnfused = 3 };
+void set_conv2_algo(ConvAlgo a);
+ConvAlgo conv2_algo();
+
 struct HostWeights {
   std::vector<float> w1, b1, w2, b2;  // KCFF weights, biases
 };
@@ -82,6 +89,11 @@ class BlocksEngine {
   // zero-state cache for the conv2 window
   int win_lo_ = 1 << 30, win_hi_ = -(1 << 30), win_n_ = -1;
   int plan_key1_ = -1, plan_key2_ = -1;
+  // Winograd conv2: transformed weights packed for the batched GEMM + V / M workspaces
+  float *u2p_ = nullptr, *wv_ = nullptr, *wm_ = nullptr;
+  int* ukoff_ = nullptr;
+  int wino_key_ = -1;
+  size_t wv_cap_ = 0, wm_cap_ = 0;
   std::vector<float> w1h_, w2h_;  // KCFF host copies for re-packing on geometry change
 };
 

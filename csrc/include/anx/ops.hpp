@@ -81,6 +81,26 @@ int conv_force_variant(int kind, int id);
 hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, const int* koff,
                        const float* bias, OutView out, bool relu, hipStream_t s);
 
+// Winograd F(3x3,5x5) for stride-1 5x5 convolutions over a pre-padded input window (winograd.hip).
+struct WinoPlan {
+  int N, Hq, Wq, C, K, groups;
+  int Ho, Wo, ty, tx, P;  // output dims, 3x3 tiles per column/row, total tiles
+  ConvPlan gemm;          // the 49*groups batched GEMMs as one grouped 1x1 conv
+};
+bool wino_eligible(int F, int S, int C, int K, int groups);
+WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups);
+size_t wino_v_floats(const WinoPlan& w);
+size_t wino_m_floats(const WinoPlan& w);
+// U = G g G^T in fp64, laid out as KCFF weights of the grouped 1x1 GEMM ([49*K][C/g]).
+void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
+hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s);
+hipError_t wino_output(const WinoPlan& w, const float* Mt, const float* bias, float* y, bool relu, hipStream_t s);
+// Tuning (A/B): bit0 = K-slice 48 instead of 32, bit1 = XCD-aware block order. Default 1 (measured: BK 48 +5%, XCD order +-0).
+int wino_set_fused_cfg(int cfg);
+// Batched GEMM + output transform in one kernel (M stays in registers); U packed as for w.gemm.
+hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
+                      hipStream_t s);
+
 // Vectorised NHWC max-pool writing through an OutView (C % 4 == 0 required for the fast path).
 hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, OutView out, hipStream_t s);
 // Fused max-pool + cross-channel LRN (block 2 tail).

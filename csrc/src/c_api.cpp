@@ -323,6 +323,18 @@ int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff
   });
 }
 
+int anx_set_conv2_algo(int algo) {
+  if (algo < 0 || algo > 3)
+    return fail("conv2 algo must be 0 (auto), 1 (direct), 2 (winograd) or 3 (winograd, unfused GEMM)");
+  anx::set_conv2_algo(static_cast<anx::ConvAlgo>(algo));
+  return 0;
+}
+int anx_get_conv2_algo(void) { return static_cast<int>(anx::conv2_algo()); }
+int anx_wino_fused_cfg(int cfg) {
+  if (anx::hip::wino_set_fused_cfg(cfg) != 0) return fail("fused cfg must be 0..3");
+  return 0;
+}
+
 int anx_conv_force_variant(int kind, int id) {
   if (anx::hip::conv_force_variant(kind, id) != 0) return fail("invalid conv variant");
   return 0;

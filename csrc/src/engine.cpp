@@ -35,6 +35,12 @@ T* dev_upload(const std::vector<T>& h) {
 }
 }  // namespace
 
+namespace {
+ConvAlgo g_conv2_algo = ConvAlgo::Auto;
+}
+void set_conv2_algo(ConvAlgo a) { g_conv2_algo = a; }
+ConvAlgo conv2_algo() { return g_conv2_algo; }
+
 void init_const(HostWeights& w, const BlockSpec& b1, const BlockSpec& b2, float wv, float bv) {
   const ConvSpec &c1 = b1.conv, &c2 = b2.conv;
   w.w1.assign(static_cast<size_t>(c1.K) * (c1.C / c1.groups) * c1.F * c1.F, wv);
@@ -65,7 +71,9 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
   wq_ = d_.Wp1 + 2 * b2.conv.P;
   const size_t per_img = std::max<size_t>(
       {static_cast<size_t>(H) * W * d_.C0, static_cast<size_t>(d_.H1) * d_.W1 * d_.C1,
-       static_cast<size_t>(d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1, static_cast<size_t>(d_.H2) * d_.W2 * d_.C2});
+       static_cast<size_t>(d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1, static_cast<size_t>(d_.H2) * d_.W2 * d_.C2,
+       // Winograd M buffer: 49 transform points x K per 3x3 output tile
+       static_cast<size_t>((d_.H2 + 2) / 3) * ((d_.W2 + 2) / 3) * 49 * d_.C2});
   chunk_ = static_cast<int>(std::min<size_t>(max_batch, ((1UL << 31) - 1) / per_img));
   if (chunk_ < 1) throw std::invalid_argument("image too large for 32-bit kernel indexing");
   w1h_ = w.w1;
@@ -78,13 +86,24 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
   q2_cap_ = static_cast<size_t>(max_batch) * (d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1;
   q2_ = dev_alloc<float>(q2_cap_);
   c2_ = dev_alloc<float>(static_cast<size_t>(chunk_) * d_.H2 * d_.W2 * d_.C2);
+  if (impl == Impl::Mfma && hip::wino_eligible(b2.conv.F, b2.conv.S, d_.C1, d_.C2, b2.conv.groups)) {
+    // Winograd workspaces for a full-height window of chunk_ images (row tiles need less).
+    const hip::WinoPlan w = hip::make_wino_plan(chunk_, d_.Hp1 + 2 * b2.conv.P, wq_, d_.C1, d_.C2, b2.conv.groups);
+    if (hip::wino_m_floats(w) < (1UL << 31)) {
+      wv_cap_ = hip::wino_v_floats(w);
+      wm_cap_ = hip::wino_m_floats(w);
+      wv_ = dev_alloc<float>(wv_cap_);
+      wm_ = dev_alloc<float>(wm_cap_);
+    }
+  }
 }
 
 BlocksEngine::~BlocksEngine() {
   for (void* p : {static_cast<void*>(w1_), static_cast<void*>(b1d_), static_cast<void*>(w2_),
                   static_cast<void*>(b2d_), static_cast<void*>(w1p_), static_cast<void*>(w2p_),
                   static_cast<void*>(koff1_), static_cast<void*>(koff2_), static_cast<void*>(c1_),
-                  static_cast<void*>(q2_), static_cast<void*>(c2_)})
+                  static_cast<void*>(q2_), static_cast<void*>(c2_), static_cast<void*>(u2p_),
+                  static_cast<void*>(ukoff_), static_cast<void*>(wv_), static_cast<void*>(wm_)})
     if (p) (void)hipFree(p);
 }
 
@@ -149,7 +168,30 @@ hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t 
     const int n = std::min(chunk_, N - n0);
     const float* qc = q2_ + n0 * q_img;
     float* yc = y + n0 * y_img;
-    if (impl_ == Impl::Mfma) {
+    const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && g_conv2_algo != ConvAlgo::Direct;
+    if (wino) {
+      const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
+      if (hip::wino_v_floats(w) > wv_cap_ || hip::wino_m_floats(w) > wm_cap_) return hipErrorInvalidValue;
+      if (w.gemm.variant != wino_key_) {
+        std::vector<float> u, packed;
+        std::vector<int> koff;
+        hip::wino_transform_weights_host(w, w2h_.data(), u);
+        hip::pack_conv_weights_host(w.gemm, u.data(), packed, koff);
+        if (u2p_) ANX_TRY(hipFree(u2p_));
+        if (ukoff_) ANX_TRY(hipFree(ukoff_));
+        u2p_ = dev_upload(packed);
+        ukoff_ = dev_upload(koff);
+        wino_key_ = w.gemm.variant;
+      }
+      ANX_TRY(hip::wino_input(w, qc, wv_, s));
+      if (g_conv2_algo == ConvAlgo::WinogradUnfused) {
+        ANX_TRY(hip::conv2d_mfma(w.gemm, wv_, u2p_, ukoff_, nullptr,
+                                 hip::OutView{wm_, 1, 1, w.gemm.K, 0, 0, 0}, false, s));
+        ANX_TRY(hip::wino_output(w, wm_, b2d_, c2_, true, s));
+      } else {
+        ANX_TRY(hip::wino_fused(w, wv_, u2p_, b2d_, c2_, true, s));
+      }
+    } else if (impl_ == Impl::Mfma) {
       const hip::ConvPlan p = hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups);
       const int key = p.variant;
       if (key != plan_key2_) {

@@ -286,7 +286,7 @@ ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int g
   p.kpad = (p.kdim + kBK - 1) / kBK * kBK;
   p.vec4 = (p.Cg % 4 == 0 && C % 4 == 0) ? 1 : 0;
   const long M = static_cast<long>(N) * p.Ho * p.Wo;
-  const bool small = M * p.Kg < 256L * 128 * 128;  // fewer tiles than CUs at 128x128
+  const bool small = M * p.K < 256L * 128 * 128;  // fewer 128x128 tiles (all groups) than CUs
   if (p.Kg == 96 && !small)
     p.variant = 1;
   else if (small)

@@ -1,0 +1,406 @@
+// Winograd F(3x3, 5x5) convolution for stride-1 5x5 layers (AlexNet Conv2), fp32 end to end.
+//
+//   Y = A^T [ U (.) V ] A,  U = G g G^T (49 x C x K, once per weight set, host fp64 -> fp32),
+//                           V = B^T d B (per 7x7 input tile and channel), 3x3 outputs per tile.
+// 49 multiplies per 9 outputs instead of 225: Conv2's 896 MFLOP/image become 195 MFLOP/image of
+// MFMA work. The reference has no fast-convolution algorithm (direct loops everywhere:
+// v3_cuda_only/src/layers_cuda.cu:20-46). fp32 error of this point set is ~5e-7 of sum|terms|
+// (tools/winograd_numerics.py), the same order as the fp32 accumulation error of the direct sum.
+//
+// Three launches, all on the caller's stream:
+//   1. input transform  : window [N][Hq][Wq][C] -> V [P][49][C]        (VALU, float4 over channels)
+//   2. 49 batched GEMMs : V x U -> M [P][49][K]  = a grouped 1x1 conv on the MFMA implicit-GEMM
+//                         kernel (conv_mfma.hip), groups = 49 * conv_groups
+//   3. output transform : M -> Y = A^T M A + bias, ReLU, NHWC conv output (VALU, float4 over filters)
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "anx/ops.hpp"
+#include "anx/winograd_f35.hpp"
+
+namespace anx::hip {
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+constexpr int kT = 256;
+constexpr int kN = wino::kN, kM = wino::kM;
+
+// One thread per (tile, channel): consecutive threads read consecutive channels (coalesced NHWC),
+// the 7x7 patch streams through t = B^T d one input row at a time (t: 49 registers).
+__global__ void __launch_bounds__(kT) wino_in_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
+                                                     int Hq, int Wq, int C, int ty, int tx) {
+  const long total = static_cast<long>(N) * ty * tx * C;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(i % C);
+    const long p = i / C;
+    const int tj = static_cast<int>(p % tx);
+    const long q = p / tx;
+    const int ti = static_cast<int>(q % ty);
+    const int n = static_cast<int>(q / ty);
+    float t[kN][kN];
+#pragma unroll
+    for (int a = 0; a < kN; ++a)
+#pragma unroll
+      for (int v = 0; v < kN; ++v) t[a][v] = 0.f;
+#pragma unroll
+    for (int u = 0; u < kN; ++u) {
+      const int yy = ti * kM + u;
+      float row[kN];
+#pragma unroll
+      for (int v = 0; v < kN; ++v) {
+        const int xx = tj * kM + v;
+        row[v] = (yy < Hq && xx < Wq) ? x[((static_cast<size_t>(n) * Hq + yy) * Wq + xx) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int a = 0; a < kN; ++a)
+        if (wino::kBT[a][u] != 0.f)
+#pragma unroll
+          for (int v = 0; v < kN; ++v) t[a][v] = fmaf(wino::kBT[a][u], row[v], t[a][v]);
+    }
+    // V = t B, stored [p][a*7+b][c]
+    float* out = V + static_cast<size_t>(p) * (kN * kN) * C + c;
+#pragma unroll
+    for (int a = 0; a < kN; ++a)
+#pragma unroll
+      for (int b = 0; b < kN; ++b) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < kN; ++v)
+          if (wino::kBT[b][v] != 0.f) s2 = fmaf(wino::kBT[b][v], t[a][v], s2);
+        out[static_cast<size_t>(a * kN + b) * C] = s2;
+      }
+  }
+}
+
+__global__ void __launch_bounds__(kT) wino_out_kernel(const float* __restrict__ Mt, const float* __restrict__ bias,
+                                                      float* __restrict__ y, int N, int Ho, int Wo, int K, int ty,
+                                                      int tx, int relu) {
+  const int K4 = K / 4;
+  const long total = static_cast<long>(N) * ty * tx * K4;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int k4 = static_cast<int>(i % K4);
+    const long p = i / K4;
+    const int tj = static_cast<int>(p % tx);
+    const long q = p / tx;
+    const int ti = static_cast<int>(q % ty);
+    const int n = static_cast<int>(q / ty);
+    const float* src = Mt + static_cast<size_t>(p) * (kN * kN) * K + k4 * 4;
+    // t = A^T M (3 x 7), then Y = t A (3 x 3)
+    f32x4 t[kM][kN];
+#pragma unroll
+    for (int i3 = 0; i3 < kM; ++i3)
+#pragma unroll
+      for (int b = 0; b < kN; ++b) t[i3][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < kN; ++a)
+#pragma unroll
+      for (int b = 0; b < kN; ++b) {
+        const f32x4 m = *reinterpret_cast<const f32x4*>(src + static_cast<size_t>(a * kN + b) * K);
+#pragma unroll
+        for (int i3 = 0; i3 < kM; ++i3)
+          if (wino::kAT[i3][a] != 0.f) t[i3][b] += wino::kAT[i3][a] * m;
+      }
+    const f32x4 bv = bias ? *reinterpret_cast<const f32x4*>(bias + k4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i3 = 0; i3 < kM; ++i3) {
+      const int oy = ti * kM + i3;
+      if (oy >= Ho) break;
+#pragma unroll
+      for (int j3 = 0; j3 < kM; ++j3) {
+        const int ox = tj * kM + j3;
+        if (ox >= Wo) break;
+        f32x4 s = bv;
+#pragma unroll
+        for (int b = 0; b < kN; ++b)
+          if (wino::kAT[j3][b] != 0.f) s += wino::kAT[j3][b] * t[i3][b];
+        if (relu) s = f32x4{fmaxf(s.x, 0.f), fmaxf(s.y, 0.f), fmaxf(s.z, 0.f), fmaxf(s.w, 0.f)};
+        *reinterpret_cast<f32x4*>(y + ((static_cast<size_t>(n) * Ho + oy) * Wo + ox) * K + k4 * 4) = s;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused batched GEMM + output transform. A workgroup owns 64 tiles x 64 filters (2x2 waves of a
+// 32x32 v_mfma_f32_32x32x2_f32 tile) and walks the 49 transform points ab: for each ab it forms
+// M_ab = V_ab[64 x Cg] . U_ab[Cg x 64] in one 16-register accumulator (K = Cg in LDS-staged BK=32
+// slices, same staging/k-permutation as conv_mfma.hip), then folds it straight into the 3x3
+// outputs: Y[i][j] += A^T[i][a] A^T[j][b] M_ab. M never touches memory (it was 520 MB per 128
+// images as a separate GEMM output), and bias + ReLU + the NHWC store happen once at the end.
+// Per lane: 16 (tile, filter) pairs x 9 outputs = 144 Y registers + 16 accumulators.
+constexpr int kFBK = 32, kFLDA = kFBK + 4, kFB = 64;
+
+struct FusedArgs {
+  const float* V;      // [P][49][C]
+  const float* U;      // packed [49*groups][kpad_n][kpad]
+  const float* bias;   // [K]
+  float* y;            // [N][Ho][Wo][K]
+  int P, C, Cg, Kg, K, groups, kpad, kpad_n;
+  int N, Ho, Wo, ty, tx, relu, n_ptiles, n_ntiles;
+};
+
+// A^T indexed by the runtime transform point: a copy of wino::kAT in constant memory (scalar loads).
+struct ATTable {
+  float v[kM][kN];
+};
+constexpr ATTable make_at() {
+  ATTable t{};
+  for (int i = 0; i < kM; ++i)
+    for (int j = 0; j < kN; ++j) t.v[i][j] = wino::kAT[i][j];
+  return t;
+}
+__constant__ ATTable c_at = make_at();
+#define c_AT c_at.v
+
+template <int BK, bool XCD>
+__global__ void __launch_bounds__(256) wino_fused_kernel(FusedArgs a) {
+  using f32x16 = __attribute__((ext_vector_type(16))) float;
+  constexpr int LDA = BK + 4;          // +16 B per row: conflict-free ds_read_b128 (row stride odd in 16 B)
+  constexpr int U4 = BK / 4;           // float4 units per staged row
+  constexpr int NJ = kFB * U4 / 256;   // float4 loads per thread per operand
+  static_assert(NJ * 256 == kFB * U4, "BK must be a multiple of 16");
+  __shared__ __attribute__((aligned(16))) float lds[2 * kFB * LDA];
+  float* As = lds;
+  float* Bs = lds + kFB * LDA;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = blockIdx.z;
+  int pt, nt;
+  if constexpr (XCD) {
+    // the n_ntiles blocks that re-read one V slab run on one XCD (blocks b, b+8, ... share an L2)
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    nt = j % a.n_ntiles;
+    pt = (j / a.n_ntiles) * 8 + xcd;
+    if (pt >= a.n_ptiles) return;
+  } else {
+    pt = blockIdx.x / a.n_ntiles;
+    nt = blockIdx.x - pt * a.n_ntiles;
+  }
+  const int p0 = pt * kFB, n0 = nt * kFB;
+  int srow[NJ], scol[NJ], prow[NJ];
+  unsigned pok = 0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int u = tid + 256 * j;
+    srow[j] = u / U4;
+    scol[j] = (u - srow[j] * U4) * 4;
+    const int p = p0 + srow[j];
+    pok |= (p < a.P ? 1u : 0u) << j;
+    prow[j] = p < a.P ? p : 0;
+  }
+  const float* Vg = a.V + g * a.Cg;
+  const int ksteps = a.kpad / BK;
+  const int total = kN * kN * ksteps;
+  f32x4 ra[NJ], rb[NJ];
+  auto load = [&](int it) {
+    const int ab = it / ksteps, kk = (it - ab * ksteps) * BK;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int kc = kk + scol[j];
+      const bool kin = kc < a.Cg;  // K padding (Cg not a multiple of BK)
+      ra[j] = *reinterpret_cast<const f32x4*>(Vg + (static_cast<size_t>(prow[j]) * (kN * kN) + ab) * a.C +
+                                             (kin ? kc : 0));
+      if (!kin || !((pok >> j) & 1u)) ra[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      rb[j] = *reinterpret_cast<const f32x4*>(
+          a.U + (static_cast<size_t>(ab * a.groups + g) * a.kpad_n + n0 + srow[j]) * a.kpad + kc);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      *reinterpret_cast<f32x4*>(As + srow[j] * LDA + scol[j]) = ra[j];
+      *reinterpret_cast<f32x4*>(Bs + srow[j] * LDA + scol[j]) = rb[j];
+    }
+  };
+  const int r = lane & 31, h = lane >> 5;
+  const float* a_rd = As + (wm * 32 + r) * LDA + h * (BK / 2);
+  const float* b_rd = Bs + (wn * 32 + r) * LDA + h * (BK / 2);
+  f32x16 acc = {};
+  float Y[9][16];
+#pragma unroll
+  for (int q = 0; q < 9; ++q)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) Y[q][e] = 0.f;
+
+  load(0);
+  store();
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    if (it + 1 < total) load(it + 1);
+#pragma unroll
+    for (int s4 = 0; s4 < BK / 8; ++s4) {
+      const f32x4 af = *reinterpret_cast<const f32x4*>(a_rd + s4 * 4);
+      const f32x4 bf = *reinterpret_cast<const f32x4*>(b_rd + s4 * 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+    }
+    const int ab = it / ksteps;
+    if (it - ab * ksteps == ksteps - 1) {
+      // fold M_ab into the 3x3 outputs (coefficients are wave-uniform: scalar registers)
+      const int aa = ab / kN, bb = ab - aa * kN;
+      float co[9];
+#pragma unroll
+      for (int i3 = 0; i3 < kM; ++i3)
+#pragma unroll
+        for (int j3 = 0; j3 < kM; ++j3) co[i3 * kM + j3] = c_AT[i3][aa] * c_AT[j3][bb];
+#pragma unroll
+      for (int q = 0; q < 9; ++q)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) Y[q][e] = fmaf(co[q], acc[e], Y[q][e]);
+      acc = f32x16{};
+    }
+    __syncthreads();
+    if (it + 1 < total) {
+      store();
+      __syncthreads();
+    }
+  }
+  // epilogue: lane holds filter f (col) and tiles (rows) (e&3) + 8*(e>>2) + 4h
+  const int f = n0 + wn * 32 + r;
+  if (f >= a.Kg) return;
+  const int fk = g * a.Kg + f;
+  const float bv = a.bias ? a.bias[fk] : 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int p = p0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (p >= a.P) continue;
+    const int tj = p % a.tx;
+    const int q = p / a.tx;
+    const int ti = q % a.ty;
+    const int n = q / a.ty;
+#pragma unroll
+    for (int i3 = 0; i3 < kM; ++i3) {
+      const int oy = ti * kM + i3;
+      if (oy >= a.Ho) break;
+#pragma unroll
+      for (int j3 = 0; j3 < kM; ++j3) {
+        const int ox = tj * kM + j3;
+        if (ox >= a.Wo) break;
+        float v = Y[i3 * kM + j3][e] + bv;
+        if (a.relu) v = fmaxf(v, 0.f);
+        a.y[((static_cast<size_t>(n) * a.Ho + oy) * a.Wo + ox) * a.K + fk] = v;
+      }
+    }
+  }
+}
+
+// fused-kernel configuration: bit0 = BK 48 (when Cg allows), bit1 = XCD-aware block order
+int g_fused_cfg = 1;
+
+unsigned grid_for(long n) {
+  long g = (n + kT - 1) / kT;
+  return static_cast<unsigned>(g > 65535 ? 65535 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+int wino_set_fused_cfg(int cfg) {
+  if (cfg < 0 || cfg > 3) return -1;
+  g_fused_cfg = cfg;
+  return 0;
+}
+
+WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups) {
+  WinoPlan w{};
+  w.N = N;
+  w.Hq = Hq;
+  w.Wq = Wq;
+  w.C = C;
+  w.K = K;
+  w.groups = groups;
+  w.Ho = Hq - (wino::kR - 1);
+  w.Wo = Wq - (wino::kR - 1);
+  w.ty = (w.Ho + kM - 1) / kM;
+  w.tx = (w.Wo + kM - 1) / kM;
+  w.P = N * w.ty * w.tx;
+  // 49*groups independent GEMMs [P x C/g] x [C/g x K/g] as one grouped 1x1 "conv" over P pixels
+  w.gemm = make_conv_plan(w.P, 1, 1, kN * kN * C, kN * kN * K, 1, 1, kN * kN * groups);
+  return w;
+}
+
+bool wino_eligible(int F, int S, int C, int K, int groups) {
+  return F == wino::kR && S == 1 && C % 4 == 0 && K % 4 == 0 && (C / groups) % 4 == 0 && (K / groups) % 4 == 0;
+}
+
+size_t wino_v_floats(const WinoPlan& w) { return static_cast<size_t>(w.P) * kN * kN * w.C; }
+size_t wino_m_floats(const WinoPlan& w) { return static_cast<size_t>(w.P) * kN * kN * w.K; }
+
+void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff) {
+  // U[(ab*groups + g)*Kg + k][c] = (G g_{k,c} G^T)[a][b], computed in fp64 then rounded once.
+  const int Cg = w.C / w.groups, Kg = w.K / w.groups, R = wino::kR;
+  u_kcff.assign(static_cast<size_t>(kN * kN) * w.K * Cg, 0.f);
+  for (int g = 0; g < w.groups; ++g)
+    for (int k = 0; k < Kg; ++k)
+      for (int c = 0; c < Cg; ++c) {
+        const float* f = w_kcff + ((static_cast<size_t>(g * Kg + k) * Cg + c) * R) * R;
+        double tmp[kN][wino::kR];
+        for (int a = 0; a < kN; ++a)
+          for (int v = 0; v < R; ++v) {
+            double s = 0;
+            for (int u = 0; u < R; ++u) s += wino::kG[a][u] * f[u * R + v];
+            tmp[a][v] = s;
+          }
+        for (int a = 0; a < kN; ++a)
+          for (int b = 0; b < kN; ++b) {
+            double s = 0;
+            for (int v = 0; v < R; ++v) s += tmp[a][v] * wino::kG[b][v];
+            const int ab = a * kN + b;
+            u_kcff[(static_cast<size_t>(ab * w.groups + g) * Kg + k) * Cg + c] = static_cast<float>(s);
+          }
+      }
+}
+
+hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s) {
+  const long n = static_cast<long>(w.P) * w.C;
+  wino_in_kernel<<<grid_for(n), kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
+  return hipGetLastError();
+}
+
+hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
+                      hipStream_t s) {
+  FusedArgs a{};
+  a.V = V;
+  a.U = U;
+  a.bias = bias;
+  a.y = y;
+  a.P = w.P;
+  a.C = w.C;
+  a.Cg = w.C / w.groups;
+  a.Kg = w.K / w.groups;
+  a.K = w.K;
+  a.groups = w.groups;
+  a.kpad = w.gemm.kpad;
+  a.kpad_n = w.gemm.kpad_n;
+  a.N = w.N;
+  a.Ho = w.Ho;
+  a.Wo = w.Wo;
+  a.ty = w.ty;
+  a.tx = w.tx;
+  a.relu = relu ? 1 : 0;
+  a.n_ptiles = (w.P + kFB - 1) / kFB;
+  a.n_ntiles = (a.Kg + kFB - 1) / kFB;
+  if (a.n_ntiles * kFB > a.kpad_n || a.Cg % 4) return hipErrorInvalidValue;
+  const int bk = (a.kpad % 48 == 0 && g_fused_cfg & 1) ? 48 : 32;
+  const bool xcd = (g_fused_cfg & 2) != 0;
+  dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
+  if (bk == 48 && xcd)
+    wino_fused_kernel<48, true><<<grid, 256, 0, s>>>(a);
+  else if (bk == 48)
+    wino_fused_kernel<48, false><<<grid, 256, 0, s>>>(a);
+  else if (xcd)
+    wino_fused_kernel<32, true><<<grid, 256, 0, s>>>(a);
+  else
+    wino_fused_kernel<32, false><<<grid, 256, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t wino_output(const WinoPlan& w, const float* Mt, const float* bias, float* y, bool relu, hipStream_t s) {
+  const long n = static_cast<long>(w.P) * (w.K / 4);
+  wino_out_kernel<<<grid_for(n), kT, 0, s>>>(Mt, bias, y, w.N, w.Ho, w.Wo, w.K, w.ty, w.tx, relu ? 1 : 0);
+  return hipGetLastError();
+}
+
+}  // namespace anx::hip

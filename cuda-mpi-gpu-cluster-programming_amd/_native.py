@@ -80,6 +80,9 @@ _SIGS = {
     "anx_conv_plan": (_I, [_I] * 8 + [C.POINTER(_I), C.POINTER(_SZ), C.POINTER(_SZ)]),
     "anx_conv_pack": (_I, [C.POINTER(_I), _P, _P, _P]),
     "anx_conv_force_variant": (_I, [_I, _I]),
+    "anx_set_conv2_algo": (_I, [_I]),
+    "anx_get_conv2_algo": (_I, []),
+    "anx_wino_fused_cfg": (_I, [_I]),
     "anx_conv2d_mfma": (_I, [C.POINTER(_I), _P, _P, _P, _P, _P] + [_I] * 6 + [_I, _P]),
     "anx_cpu_conv2d": (_I, [_P, _P, _P, _P] + [_I] * 10),
     "anx_cpu_maxpool": (_I, [_P, _P] + [_I] * 6),

@@ -3,7 +3,7 @@
 interleaved rounds in ONE process, report median and min).
 
 usage: tools/ab_variants.py --arms "0:1,5:6,7:8" --batch 128
-each arm = <vec4 variant>:<scalar variant> (-1 = heuristic)."""
+each arm = <vec4 variant>:<scalar variant>[:<conv2 algo 0 auto|1 direct|2 winograd>] (-1 = heuristic)."""
 import argparse
 import json
 import os
@@ -19,20 +19,22 @@ from anx.models.alexnet_blocks import AlexNetBlocks  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--arms", default="-1:-1,5:6,7:8")
+    ap.add_argument("--arms", default="-1:-1:1,-1:-1:2")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--check", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    arms = [tuple(int(v) for v in s.split(":")) for s in a.arms.split(",")]
+    arms = [tuple(int(v) for v in (s + ":0:3").split(":")[:4]) for s in a.arms.split(",")]
     models = []
     x = torch.rand(a.batch, 227, 227, 3, device=dev) * 0.1
     ref = None
-    for v4, sc in arms:
+    for v4, sc, al, fc in arms:
         nat.call("anx_conv_force_variant", 0, v4)
         nat.call("anx_conv_force_variant", 1, sc)
+        nat.call("anx_set_conv2_algo", al)
+        nat.call("anx_wino_fused_cfg", fc)
         m = AlexNetBlocks(init="rand", device=dev, max_batch=a.batch)
         y = m(x)  # packs weights for the forced variants
         torch.cuda.synchronize()
@@ -46,6 +48,8 @@ def main():
             # the variant is chosen at plan time (every call): force it for this arm's launches
             nat.call("anx_conv_force_variant", 0, arms[i][0])
             nat.call("anx_conv_force_variant", 1, arms[i][1])
+            nat.call("anx_set_conv2_algo", arms[i][2])
+            nat.call("anx_wino_fused_cfg", arms[i][3])
             m(x, out=y)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -57,9 +61,11 @@ def main():
     nat.call("anx_conv_force_variant", 0, -1)
     nat.call("anx_conv_force_variant", 1, -1)
     f = anx.flops_per_image()
-    for (v4, sc), t, (_, _, err) in zip(arms, times, models):
+    nat.call("anx_set_conv2_algo", 0)
+    nat.call("anx_wino_fused_cfg", 3)
+    for (v4, sc, al, fc), t, (_, _, err) in zip(arms, times, models):
         med = sorted(t)[len(t) // 2]
-        print(json.dumps({"arm": f"{v4}:{sc}", "batch": a.batch, "ms_median": round(med, 4), "ms_min": round(min(t), 4),
+        print(json.dumps({"arm": f"{v4}:{sc}:{al}:{fc}", "batch": a.batch, "ms_median": round(med, 4), "ms_min": round(min(t), 4),
                           "img_per_s": round(a.batch / med * 1e3, 1), "tflops": round(a.batch * f / med / 1e9, 2),
                           "max_abs_diff_vs_arm0": err}))
 
