@@ -39,7 +39,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch-per-gpu", type=int, default=128)
-    ap.add_argument("--micro", type=int, default=4, help="micro-batches per step for scatter/compute/gather overlap")
+    # 2 micro-batches of 64: the second half's scatter overlaps the first half's compute, and 64-image
+    # launches keep the conv kernels at ~96% of their batch-128 throughput (tools/sweep_batch.py).
+    ap.add_argument("--micro", type=int, default=2, help="micro-batches per step for scatter/compute/gather overlap")
     ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
     ap.add_argument("--input-source", default="root", choices=["root", "local"],
                     help="root: rank 0 scatters the batch (reference V4/V5 semantics); local: per-rank synthetic")

@@ -127,32 +127,39 @@ HostComm::HostComm(const RankInfo& ri, double timeout_s)
   if (world_ == 1) return;
   int my_port = 0;
   const int lfd = listen_on(rank_ == 0 ? ri.master_port : 0, world_ + 4, &my_port);
-  std::vector<int32_t> ports(world_, 0);
-  ports[rank_] = my_port;
+  // table[2*r] = IPv4 of rank r as rank 0 sees it (so ranks may live on different nodes),
+  // table[2*r+1] = its listen port
+  std::vector<uint32_t> table(2 * static_cast<size_t>(world_), 0);
   const sockaddr_in master = resolve(ri.master_addr, ri.master_port);
+  table[0] = master.sin_addr.s_addr;
+  table[1] = static_cast<uint32_t>(my_port);
   if (rank_ == 0) {
-    // star bootstrap: every rank reports (rank, listen port)
+    // star bootstrap: every rank reports (rank, listen port); its address comes from accept()
     for (int i = 1; i < world_; ++i) {
-      int fd = accept(lfd, nullptr, nullptr);
+      sockaddr_in peer{};
+      socklen_t plen = sizeof peer;
+      int fd = accept(lfd, reinterpret_cast<sockaddr*>(&peer), &plen);
       if (fd < 0) die("accept");
       set_nodelay(fd);
       int32_t hdr[2];
       read_all(fd, hdr, sizeof hdr);
       if (hdr[0] <= 0 || hdr[0] >= world_ || fd_[hdr[0]] != -1) die("bad hello");
       fd_[hdr[0]] = fd;
-      ports[hdr[0]] = hdr[1];
+      table[2 * hdr[0]] = peer.sin_addr.s_addr;
+      table[2 * hdr[0] + 1] = static_cast<uint32_t>(hdr[1]);
     }
-    for (int i = 1; i < world_; ++i) write_all(fd_[i], ports.data(), ports.size() * sizeof(int32_t));
+    for (int i = 1; i < world_; ++i) write_all(fd_[i], table.data(), table.size() * sizeof(uint32_t));
   } else {
     int fd = connect_retry(master, timeout_s_);
     int32_t hdr[2] = {rank_, my_port};
     write_all(fd, hdr, sizeof hdr);
-    read_all(fd, ports.data(), ports.size() * sizeof(int32_t));
+    read_all(fd, table.data(), table.size() * sizeof(uint32_t));
     fd_[0] = fd;
     // mesh: connect to every lower non-zero rank, then accept every higher rank
     for (int j = 1; j < rank_; ++j) {
       sockaddr_in a = master;
-      a.sin_port = htons(static_cast<uint16_t>(ports[j]));
+      a.sin_addr.s_addr = table[2 * j];
+      a.sin_port = htons(static_cast<uint16_t>(table[2 * j + 1]));
       int c = connect_retry(a, timeout_s_);
       int32_t me = rank_;
       write_all(c, &me, sizeof me);

@@ -42,7 +42,11 @@ static void usage() {
 }
 
 int main(int argc, char** argv) {
-  int np = 1, port = 0;
+  // Multi-node (the reference's hostfile runs, scripts/2_final_multi_machine.sh:396-410): start
+  // `anxrun -np <per node> --nnodes K --node-rank R --master-addr <node 0> --port P` on every node;
+  // global rank = R * np + local rank.
+  int np = 1, port = 0, nnodes = 1, node_rank = 0;
+  std::string master = "127.0.0.1";
   double timeout = 0;
   int i = 1;
   for (; i < argc; ++i) {
@@ -53,6 +57,12 @@ int main(int argc, char** argv) {
       timeout = std::atof(argv[++i]);
     } else if (a == "--port" && i + 1 < argc) {
       port = std::atoi(argv[++i]);
+    } else if (a == "--nnodes" && i + 1 < argc) {
+      nnodes = std::atoi(argv[++i]);
+    } else if (a == "--node-rank" && i + 1 < argc) {
+      node_rank = std::atoi(argv[++i]);
+    } else if (a == "--master-addr" && i + 1 < argc) {
+      master = argv[++i];
     } else if (a == "--") {
       ++i;
       break;
@@ -60,8 +70,14 @@ int main(int argc, char** argv) {
       break;
     }
   }
-  if (i >= argc || np < 1) usage();
-  if (!port) port = free_port();
+  if (i >= argc || np < 1 || nnodes < 1 || node_rank < 0 || node_rank >= nnodes) usage();
+  if (!port) {
+    if (nnodes > 1) {
+      std::fprintf(stderr, "anxrun: --port is required with --nnodes > 1\n");
+      return 2;
+    }
+    port = free_port();
+  }
   std::vector<pid_t> kids;
   for (int r = 0; r < np; ++r) {
     pid_t pid = fork();
@@ -70,10 +86,10 @@ int main(int argc, char** argv) {
       return 1;
     }
     if (pid == 0) {
-      setenv("ANX_RANK", std::to_string(r).c_str(), 1);
+      setenv("ANX_RANK", std::to_string(node_rank * np + r).c_str(), 1);
       setenv("ANX_LOCAL_RANK", std::to_string(r).c_str(), 1);
-      setenv("ANX_WORLD_SIZE", std::to_string(np).c_str(), 1);
-      setenv("ANX_MASTER_ADDR", "127.0.0.1", 1);
+      setenv("ANX_WORLD_SIZE", std::to_string(np * nnodes).c_str(), 1);
+      setenv("ANX_MASTER_ADDR", master.c_str(), 1);
       setenv("ANX_MASTER_PORT", std::to_string(port).c_str(), 1);
       execvp(argv[i], argv + i);
       std::perror("execvp");

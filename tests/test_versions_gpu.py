@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 def test_v3_golden_raw(cuda):
     rec, out = run_cli(["--version", "v3", "--iters", "3"])
     assert "AlexNet HIP Forward Pass completed in" in out
-    assert rec["first10"][:3] == pytest.approx([29.2932, 25.9153, 23.3255], abs=2e-4)
+    assert rec["first10"][:3] == pytest.approx([29.2932, 25.9153, 23.3255], abs=1e-3)
     assert rec["warm_ms"] is not None
 
 
