@@ -1,0 +1,79 @@
+#!/bin/bash
+# The staged-version test/bench matrix (the reference's scripts/0_run_final_project.sh and
+# 1_final_unique_machine.sh): build once, run
+#   V1 np1; V2.1 and V2.2 x np {1,2,4}; V3 np1; V4 x np {1,2,4}; V5 x np {1..#GPUs}
+# through the native CLI, parse every run, check shape AND that every multi-rank checksum equals the
+# single-process one, and write a session directory with per-run logs, a 20-column CSV and a summary.
+#
+# usage: scripts/run_matrix.sh [--batch N] [--iters K] [--init const|rand] [--no-build] [--cpu-only]
+set -uo pipefail
+source "$(dirname "$0")/common.sh"
+
+BATCH=1; ITERS=3; INIT=rand; BUILD=1; CPU_ONLY=0
+while [ $# -gt 0 ]; do
+  case "$1" in
+    --batch) BATCH="$2"; shift 2 ;;
+    --iters) ITERS="$2"; shift 2 ;;
+    --init) INIT="$2"; shift 2 ;;
+    --no-build) BUILD=0; shift ;;
+    --cpu-only) CPU_ONLY=1; shift ;;
+    *) echo "unknown option $1"; exit 2 ;;
+  esac
+done
+
+HOST=$(hostname 2>/dev/null || echo host)
+TS=$(date +%Y%m%d_%H%M%S)
+SESSION="matrix_${TS}_${HOST}"
+OUT="$ANX_ROOT/logs/$SESSION"
+mkdir -p "$OUT"
+CSV="$OUT/summary_report_${SESSION}.csv"
+csv_init "$CSV"
+GIT=$(git -C "$ANX_ROOT" rev-parse --short HEAD 2>/dev/null || echo unknown)
+ARCH=$(detect_gpu_arch)
+NGPU=0
+[ "$CPU_ONLY" -eq 0 ] && NGPU=$(gpu_count)
+echo "session $SESSION  arch=$ARCH gpus=$NGPU batch=$BATCH iters=$ITERS init=$INIT"
+
+BUILD_OK=1; BUILD_MSG=ok; MAKE_LOG="$OUT/build.log"
+if [ "$BUILD" -eq 1 ]; then
+  if ! python3 "$ANX_ROOT/__graft_entry__.py" build > "$MAKE_LOG" 2>&1; then BUILD_OK=0; BUILD_MSG=build_failed; fi
+fi
+
+declare -A REF_SUM=()
+run_case() {  # version np
+  local v="$1" np="$2" log="$OUT/run_${1}_np${2}.log"
+  local lrn=""; case "$v" in v3|v4|v5) lrn="--lrn-alpha-mode div_n" ;; esac
+  local args="--version $v --batch $BATCH --init $INIT --iters $ITERS $lrn"
+  local cls
+  if [ "$np" -eq 1 ] && { [ "$v" = v1 ] || [ "$v" = v3 ]; }; then
+    cls=$(run_and_classify "$log" 600 "$ANX_BIN/anx" $args)
+  else
+    cls=$(run_and_classify "$log" 900 "$ANX_BIN/anxrun" -np "$np" --timeout 800 "$ANX_BIN/anx" $args)
+  fi
+  read -r t shape first sum < <(parse_anx_json "$log")
+  local status="OK" msg="ok" sym="✔"
+  if [ "$cls" != 0 ]; then status="FAIL($cls)"; msg="run_failed_class_$cls"; sym="✘";
+  elif [ "$shape" != "13x13x256" ]; then status="BADSHAPE"; msg="shape_$shape"; sym="✘";
+  else
+    local key="$BATCH"
+    if [ -z "${REF_SUM[$key]:-}" ]; then REF_SUM[$key]="$sum";
+    elif [ "${REF_SUM[$key]}" != "$sum" ]; then status="MISMATCH"; msg="checksum_differs"; sym="✘"; fi
+  fi
+  csv_row "$CSV" "$SESSION" "$HOST" "$GIT" "$(date +%s)" "$v" "$np" "$MAKE_LOG" "$BUILD_OK" "$BUILD_MSG" "$log" \
+    "$([ "$cls" = 0 ] && echo 1 || echo 0)" "" "$msg" "$([ "$t" != NA ] && echo 1 || echo 0)" "" "$sym" "$status" \
+    "$t" "$shape" "$first"
+  summary_add "$v" "$np" "$BATCH" "$t" "$shape" "$status" "$sum"
+}
+
+run_case v1 1
+for np in 1 2 4; do run_case v2.1 "$np"; done
+for np in 1 2 4; do run_case v2.2 "$np"; done
+if [ "$NGPU" -ge 1 ]; then
+  run_case v3 1
+  for np in 1 2 4; do run_case v4 "$np"; done
+  for np in 1 2 4 8; do [ "$np" -le "$NGPU" ] && run_case v5 "$np"; done
+fi
+summary_print | tee "$OUT/summary.txt"
+echo "csv: $CSV"
+grep -q '✘' "$CSV" && exit 1
+exit 0
