@@ -48,6 +48,7 @@ struct Options {
   std::string decomp;  // "" = version default
   int iters = 0;
   std::string impl = "mfma";
+  std::string conv2_algo = "auto";  // auto | direct | winograd
   bool check = false;
   bool json = true;
 };
@@ -56,7 +57,8 @@ struct Options {
   std::fprintf(stderr,
                "%s\nusage: anx --version v1|v2.1|v2.2|v3|v4|v5 [--batch N] [--init const|rand] [--seed S]\n"
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
-               "           [--iters K] [--impl mfma|direct] [--check] [--no-json]\n",
+               "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd] [--check]\n"
+               "           [--no-json]\n",
                msg);
   std::exit(2);
 }
@@ -78,6 +80,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--decomp") o.decomp = val();
     else if (a == "--iters") o.iters = std::atoi(val().c_str());
     else if (a == "--impl") o.impl = val();
+    else if (a == "--conv2-algo") o.conv2_algo = val();
     else if (a == "--check") o.check = true;
     else if (a == "--no-json") o.json = false;
     else if (a == "-h" || a == "--help") usage("");
@@ -712,6 +715,11 @@ int run_v5(Setup& s, HostComm& c) {
 
 int main(int argc, char** argv) {
   const Options o = parse(argc, argv);
+  // Winograd conv2 sums in a different order per row tile (tile origins move with the decomposition):
+  // results match to ~1e-7 relative, not bitwise; `direct` makes every decomposition bit-identical.
+  set_conv2_algo(o.conv2_algo == "direct"     ? ConvAlgo::Direct
+                 : o.conv2_algo == "winograd" ? ConvAlgo::Winograd
+                                              : ConvAlgo::Auto);
   const RankInfo ri = rank_info_from_env();
   try {
     Setup s = make_setup(o, ri);

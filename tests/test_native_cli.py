@@ -90,10 +90,15 @@ def test_native_v3_batch_check(cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize("np_", [2, 3])
 def test_native_v4_shared_gpu(cuda, np_):
-    ref, _ = native(["--version", "v3", "--init", "rand", "--seed", "5", "--batch", "3"])
-    rec, out = native(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", "--iters", "2"], np_)
+    # direct conv2: every decomposition is bit-identical to the single-GPU run
+    d = ["--conv2-algo", "direct"]
+    ref, _ = native(["--version", "v3", "--init", "rand", "--seed", "5", "--batch", "3", *d])
+    rec, out = native(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", "--iters", "2", *d], np_)
     assert "Final Output Shape: 13x13x256" in out.stdout
     assert rec["checksum"] == ref["checksum"]
+    # Winograd conv2 (default): tile origins move with the row split -> equal to ~1e-7, not bitwise
+    rec, _ = native(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", "--check"], np_)
+    assert rec["max_abs_err"] < 1e-3
 
 
 @pytest.mark.gpu
