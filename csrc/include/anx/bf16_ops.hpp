@@ -1,0 +1,79 @@
+// anx/bf16_ops.hpp — bf16 MFMA kernels of the full-AlexNet extension (conv_bf16.hip) and the
+// full-network engine (full_engine.cpp). Activations are bf16 NHWC, accumulation fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "anx/shapes.hpp"
+
+namespace anx {
+namespace hip {
+
+struct OutViewB {
+  __bf16* base;
+  int Hb, Wb, Cb;
+  int h_off, w_off, c_off;
+};
+
+struct ConvPlanB {
+  int N, Hp, Wp, C, K, F, S, groups;
+  int Ho, Wo, Cg, Kg, kdim, kpad, kpad_n, variant, vec8;
+};
+
+uint16_t f32_to_bf16_bits(float f);
+ConvPlanB make_conv_plan_bf16(int N, int Hp, int Wp, int C, int K, int F, int S, int groups);
+size_t packed_weight_elems_bf16(const ConvPlanB& p);
+void pack_conv_weights_bf16(const ConvPlanB& p, const float* w_kcff, std::vector<uint16_t>& packed,
+                            std::vector<int>& koff);
+// out_f32 != nullptr: write fp32 (contiguous [M][K]) instead of the bf16 view (final logits).
+hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, const int* koff, const float* bias,
+                       OutViewB out, float* out_f32, bool relu, hipStream_t s);
+hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S, OutViewB out, hipStream_t s);
+hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
+                            float beta, float k, LrnMode mode, OutViewB out, hipStream_t s);
+hipError_t f32_to_bf16(const float* x, void* y, size_t n, hipStream_t s);
+
+}  // namespace hip
+
+// Full AlexNet (extension): the reference's Blocks 1-2 followed by the AlexNet tail
+// Conv3 3x3/1 p1 (256->384) -> ReLU -> Conv4 (384->384) -> ReLU -> Conv5 (384->256) -> ReLU ->
+// MaxPool 3/2 -> FC6 9216->4096 -> ReLU -> FC7 4096->4096 -> ReLU -> FC8 4096->classes.
+struct FullWeights {
+  // KCFF conv weights / [out][in] FC weights (FC6 input order = NHWC flatten of 6x6x256) + biases
+  std::vector<float> w[8], b[8];
+};
+void full_weight_shapes(int classes, int groups2, size_t wn[8], size_t bn[8]);
+
+class FullEngine {
+ public:
+  FullEngine(const FullWeights& w, int classes, int max_batch, int groups2 = 1, LrnMode lrn = LrnMode::DivN);
+  ~FullEngine();
+  FullEngine(const FullEngine&) = delete;
+  FullEngine& operator=(const FullEngine&) = delete;
+  // x: [N,227,227,3] fp32 device; logits: [N,classes] fp32 device.
+  hipError_t forward(const float* x, int N, float* logits, hipStream_t s);
+  int classes() const { return classes_; }
+  int max_batch() const { return max_batch_; }
+
+ private:
+  struct Layer {
+    int C, K, F, S, groups;
+    void* wp = nullptr;
+    int* koff = nullptr;
+    float* bias = nullptr;
+    int key = -1;
+    std::vector<float> host;  // KCFF fp32 (re-pack when the tile variant changes)
+  };
+  hipError_t conv(Layer& L, int N, int Hp, int Wp, const void* x, hip::OutViewB out, float* out_f32, bool relu,
+                  hipStream_t s);
+  Layer L_[8];
+  int classes_, max_batch_, chunk_;
+  LrnMode lrn_;
+  void *xb_ = nullptr, *c1_ = nullptr, *q2_ = nullptr, *c2_ = nullptr, *q3_ = nullptr, *q4_ = nullptr,
+       *q5_ = nullptr, *c5_ = nullptr, *f6_ = nullptr, *f7_ = nullptr, *f8_ = nullptr;
+};
+
+}  // namespace anx

@@ -51,6 +51,14 @@ int anx_engine_stage2(void* e, int N, const anx_tile_c* t, float* y, void* strea
 int anx_engine_window(void* e, const anx_tile_c* t, int n, int r, float** ptr, size_t* row_floats,
                       size_t* image_floats);
 
+/* ---- full AlexNet bf16 engine (extension) ----
+ * weights: 8 KCFF/[out][in] fp32 host arrays (conv1..5, fc6..8), biases: 8 fp32 host arrays. */
+int anx_full_weight_sizes(int classes, int groups2, size_t* wn, size_t* bn);
+int anx_full_create(void** out, const float* const* weights, const float* const* biases, int classes,
+                    int max_batch, int groups2, int lrn_mode);
+int anx_full_destroy(void* e);
+int anx_full_forward(void* e, const float* x, int N, float* logits, void* stream);
+
 /* ---- host engine (same contract as the device engine; V1 / V2 CPU ranks) ---- */
 int anx_cpu_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,
                           const float* bias1, const float* w2, const float* bias2);

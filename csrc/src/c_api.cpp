@@ -6,6 +6,7 @@
 #include <exception>
 #include <string>
 
+#include "anx/bf16_ops.hpp"
 #include "anx/cpu_engine.hpp"
 #include "anx/engine.hpp"
 #include "anx/ops.hpp"
@@ -201,6 +202,37 @@ int anx_engine_window(void* e, const anx_tile_c* t, int n, int r, float** ptr, s
   *row_floats = eng->q2_row_floats();
   *image_floats = eng->q2_image_stride_floats(tp);
   return 0;
+}
+
+int anx_full_weight_sizes(int classes, int groups2, size_t* wn, size_t* bn) {
+  anx::full_weight_shapes(classes, groups2, wn, bn);
+  return 0;
+}
+
+int anx_full_create(void** out, const float* const* weights, const float* const* biases, int classes,
+                    int max_batch, int groups2, int lrn_mode) {
+  return guarded("anx_full_create", [&] {
+    size_t wn[8], bn[8];
+    anx::full_weight_shapes(classes, groups2, wn, bn);
+    anx::FullWeights w;
+    for (int i = 0; i < 8; ++i) {
+      w.w[i].assign(weights[i], weights[i] + wn[i]);
+      w.b[i].assign(biases[i], biases[i] + bn[i]);
+    }
+    *out = new anx::FullEngine(w, classes, max_batch, groups2, static_cast<anx::LrnMode>(lrn_mode));
+    return 0;
+  });
+}
+
+int anx_full_destroy(void* e) {
+  delete static_cast<anx::FullEngine*>(e);
+  return 0;
+}
+
+int anx_full_forward(void* e, const float* x, int N, float* logits, void* stream) {
+  return guarded("anx_full_forward", [&] {
+    return hip_status(static_cast<anx::FullEngine*>(e)->forward(x, N, logits, S(stream)), "full forward");
+  });
 }
 
 int anx_cpu_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,

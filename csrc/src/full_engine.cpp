@@ -1,0 +1,127 @@
+// Full AlexNet engine (bf16 extension, see anx/bf16_ops.hpp). Weights are packed to bf16 once and
+// stay resident; every activation between layers lives in a persistent bf16 workspace, with the
+// padded layers' inputs kept as zero-bordered windows that the producing kernel writes into.
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+#include "anx/bf16_ops.hpp"
+
+#define ANX_TRY(expr)                \
+  do {                               \
+    hipError_t _e = (expr);          \
+    if (_e != hipSuccess) return _e; \
+  } while (0)
+
+namespace anx {
+
+namespace {
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+void* dalloc(size_t bytes) {
+  void* p = nullptr;
+  check(hipMalloc(&p, std::max<size_t>(bytes, 16)), "hipMalloc");
+  return p;
+}
+// C, K, F, S per layer (groups filled in per instance for conv2)
+constexpr int kGeom[8][4] = {{3, 96, 11, 4},      {96, 256, 5, 1},    {256, 384, 3, 1},   {384, 384, 3, 1},
+                             {384, 256, 3, 1},    {9216, 4096, 1, 1}, {4096, 4096, 1, 1}, {4096, 0, 1, 1}};
+}  // namespace
+
+void full_weight_shapes(int classes, int groups2, size_t wn[8], size_t bn[8]) {
+  for (int i = 0; i < 8; ++i) {
+    const int C = kGeom[i][0], K = i == 7 ? classes : kGeom[i][1], F = kGeom[i][2];
+    const int g = i == 1 ? groups2 : 1;
+    wn[i] = static_cast<size_t>(K) * (C / g) * F * F;
+    bn[i] = static_cast<size_t>(K);
+  }
+}
+
+FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int groups2, LrnMode lrn)
+    : classes_(classes), max_batch_(max_batch), lrn_(lrn) {
+  size_t wn[8], bn[8];
+  full_weight_shapes(classes, groups2, wn, bn);
+  for (int i = 0; i < 8; ++i) {
+    if (w.w[i].size() != wn[i] || w.b[i].size() != bn[i])
+      throw std::invalid_argument("full AlexNet: weight " + std::to_string(i) + " has the wrong size");
+    Layer& L = L_[i];
+    L.C = kGeom[i][0];
+    L.K = i == 7 ? classes : kGeom[i][1];
+    L.F = kGeom[i][2];
+    L.S = kGeom[i][3];
+    L.groups = i == 1 ? groups2 : 1;
+    L.host = w.w[i];
+    L.bias = static_cast<float*>(dalloc(bn[i] * 4));
+    check(hipMemcpy(L.bias, w.b[i].data(), bn[i] * 4, hipMemcpyHostToDevice), "H2D bias");
+  }
+  chunk_ = std::max(1, std::min(max_batch, static_cast<int>(((1UL << 31) - 1) / (55UL * 55 * 96))));
+  const size_t n = static_cast<size_t>(chunk_);
+  xb_ = dalloc(n * 227 * 227 * 3 * 2);
+  c1_ = dalloc(n * 55 * 55 * 96 * 2);
+  q2_ = dalloc(n * 31 * 31 * 96 * 2);
+  c2_ = dalloc(n * 27 * 27 * 256 * 2);
+  q3_ = dalloc(n * 15 * 15 * 256 * 2);
+  q4_ = dalloc(n * 15 * 15 * 384 * 2);
+  q5_ = dalloc(n * 15 * 15 * 384 * 2);
+  c5_ = dalloc(n * 13 * 13 * 256 * 2);
+  f6_ = dalloc(n * 9216 * 2);
+  f7_ = dalloc(n * 4096 * 2);
+  f8_ = dalloc(n * 4096 * 2);
+  // zero borders of the padded windows once; kernels only ever write the interiors
+  check(hipMemset(q2_, 0, n * 31 * 31 * 96 * 2), "memset");
+  check(hipMemset(q3_, 0, n * 15 * 15 * 256 * 2), "memset");
+  check(hipMemset(q4_, 0, n * 15 * 15 * 384 * 2), "memset");
+  check(hipMemset(q5_, 0, n * 15 * 15 * 384 * 2), "memset");
+}
+
+FullEngine::~FullEngine() {
+  for (Layer& L : L_)
+    for (void* p : {L.wp, static_cast<void*>(L.koff), static_cast<void*>(L.bias)})
+      if (p) (void)hipFree(p);
+  for (void* p : {xb_, c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_})
+    if (p) (void)hipFree(p);
+}
+
+hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip::OutViewB out, float* out_f32,
+                            bool relu, hipStream_t s) {
+  const hip::ConvPlanB p = hip::make_conv_plan_bf16(N, Hp, Wp, L.C, L.K, L.F, L.S, L.groups);
+  if (p.variant != L.key) {  // pack for this tile variant (first use / batch-size class change)
+    std::vector<uint16_t> pk;
+    std::vector<int> ko;
+    hip::pack_conv_weights_bf16(p, L.host.data(), pk, ko);
+    if (L.wp) ANX_TRY(hipFree(L.wp));
+    if (L.koff) ANX_TRY(hipFree(L.koff));
+    ANX_TRY(hipMalloc(&L.wp, pk.size() * 2));
+    ANX_TRY(hipMalloc(&L.koff, ko.size() * 4));
+    ANX_TRY(hipMemcpy(L.wp, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+    ANX_TRY(hipMemcpy(L.koff, ko.data(), ko.size() * 4, hipMemcpyHostToDevice));
+    L.key = p.variant;
+  }
+  return hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s);
+}
+
+hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t s) {
+  using hip::OutViewB;
+  auto B = [](void* p) { return static_cast<__bf16*>(p); };
+  for (int n0 = 0; n0 < N; n0 += chunk_) {
+    const int n = std::min(chunk_, N - n0);
+    ANX_TRY(hip::f32_to_bf16(x + static_cast<size_t>(n0) * 227 * 227 * 3, xb_, static_cast<size_t>(n) * 227 * 227 * 3, s));
+    ANX_TRY(conv(L_[0], n, 227, 227, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
+    ANX_TRY(hip::maxpool_bf16(c1_, n, 55, 55, 96, 3, 2, OutViewB{B(q2_), 31, 31, 96, 2, 2, 0}, s));
+    ANX_TRY(conv(L_[1], n, 31, 31, q2_, OutViewB{B(c2_), 27, 27, 256, 0, 0, 0}, nullptr, true, s));
+    ANX_TRY(hip::maxpool_lrn_bf16(c2_, n, 27, 27, 256, 3, 2, 5, 1e-4f, 0.75f, 2.0f, lrn_,
+                                  OutViewB{B(q3_), 15, 15, 256, 1, 1, 0}, s));
+    ANX_TRY(conv(L_[2], n, 15, 15, q3_, OutViewB{B(q4_), 15, 15, 384, 1, 1, 0}, nullptr, true, s));
+    ANX_TRY(conv(L_[3], n, 15, 15, q4_, OutViewB{B(q5_), 15, 15, 384, 1, 1, 0}, nullptr, true, s));
+    ANX_TRY(conv(L_[4], n, 15, 15, q5_, OutViewB{B(c5_), 13, 13, 256, 0, 0, 0}, nullptr, true, s));
+    ANX_TRY(hip::maxpool_bf16(c5_, n, 13, 13, 256, 3, 2, OutViewB{B(f6_), 6, 6, 256, 0, 0, 0}, s));
+    ANX_TRY(conv(L_[5], n, 1, 1, f6_, OutViewB{B(f7_), 1, 1, 4096, 0, 0, 0}, nullptr, true, s));
+    ANX_TRY(conv(L_[6], n, 1, 1, f7_, OutViewB{B(f8_), 1, 1, 4096, 0, 0, 0}, nullptr, true, s));
+    ANX_TRY(conv(L_[7], n, 1, 1, f8_, OutViewB{nullptr, 1, 1, classes_, 0, 0, 0},
+                 logits + static_cast<size_t>(n0) * classes_, false, s));
+  }
+  return hipSuccess;
+}
+
+}  // namespace anx

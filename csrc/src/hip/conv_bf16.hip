@@ -1,0 +1,386 @@
+// bf16 path for the full-AlexNet extension (BASELINE.json config "Full AlexNet Conv1-5 + FC6-8
+// bf16"): implicit-GEMM convolution / fully-connected layers on v_mfma_f32_32x32x16_bf16 with fp32
+// accumulation, fused bias + ReLU, bf16 NHWC activations; bf16 max-pool and max-pool+LRN that write
+// straight into the next layer's zero-bordered window.
+//
+// Same structure as the fp32 kernel (conv_mfma.hip): 4 waves x (TM*32) x (TN*32) accumulators,
+// LDS-staged K slices (BK = 64 bf16 here) with a lane-contiguous k permutation — for the bf16 MFMA
+// lane (r, h) at k-step s holds A[r][16s + 8h + j], j = 0..7, i.e. one ds_read_b128 per operand
+// per MFMA. Row stride BK+8 elements = 144 B (odd multiple of 16 B): conflict-free b128 reads.
+// An FC layer is the 1x1 case: N images are N "pixels" of a 1x1 input with C = in_features.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <type_traits>
+#include <vector>
+
+#include "anx/bf16_ops.hpp"
+
+namespace anx::hip {
+namespace {
+
+using bf16 = __bf16;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+
+constexpr int kThreads = 256;
+constexpr int kBK = 64;
+constexpr int kLDA = kBK + 8;
+
+struct ArgsB {
+  const bf16* x;
+  const bf16* w;
+  const int* koff;
+  const float* bias;
+  void* out;
+  int M, HoWo, Wo, Hp, Wp, C, S, Cg, Kg, kpad, kpad_n, ktiles;
+  int Hb, Wb, Cb, h_off, w_off, c_off, relu, n_ntiles;
+};
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool VEC8, typename OutT>
+__global__ void __launch_bounds__(kThreads) conv_bf16_kernel(ArgsB a) {
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 32, TN = WN / 32;
+  constexpr int A_UNITS = VEC8 ? kBK / 8 : kBK;  // per staged row
+  constexpr int A_LOADS = BM * A_UNITS / kThreads;
+  constexpr int B_LOADS = BN * (kBK / 8) / kThreads;
+  constexpr int A_STEP = kThreads / A_UNITS, B_STEP = kThreads / (kBK / 8);
+  static_assert(A_LOADS * kThreads == BM * A_UNITS && B_LOADS * kThreads == BN * (kBK / 8), "tile split");
+  extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
+  bf16* As = lds_b;
+  bf16* Bs = lds_b + BM * kLDA;
+  int* koff_s = reinterpret_cast<int*>(lds_b + (BM + BN) * kLDA);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N, g = blockIdx.z;
+  const int mt = blockIdx.x / a.n_ntiles, nt = blockIdx.x - mt * a.n_ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const bf16* x = a.x + g * a.Cg;
+  const bf16* wg = a.w + static_cast<size_t>(g) * a.kpad_n * a.kpad;
+  for (int i = tid; i < a.kpad; i += kThreads) koff_s[i] = a.koff[i];
+  const int au = tid % A_UNITS;
+  int org[A_LOADS];
+  unsigned ok = 0;
+#pragma unroll
+  for (int j = 0; j < A_LOADS; ++j) {
+    const int m = m0 + tid / A_UNITS + j * A_STEP;
+    int o = 0;
+    if (m < a.M) {
+      const int n = m / a.HoWo, r = m - n * a.HoWo, oy = r / a.Wo, ox = r - oy * a.Wo;
+      o = ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
+    }
+    org[j] = o;
+    ok |= (m < a.M ? 1u : 0u) << j;
+  }
+  const int bu = tid % (kBK / 8);
+  const bf16* bsrc = wg + static_cast<size_t>(n0 + tid / (kBK / 8)) * a.kpad + bu * 8;
+  __syncthreads();
+
+  using AReg = typename std::conditional<VEC8, u32x4, bf16>::type;
+  AReg ra[A_LOADS];
+  u32x4 rb[B_LOADS];
+  bool kok = true;
+  auto load = [&](int kt) {
+    const int kb = kt * kBK;
+    const int ko_raw = koff_s[kb + (VEC8 ? au * 8 : au)];
+    kok = ko_raw >= 0;
+    const int ko = kok ? ko_raw : 0;
+#pragma unroll
+    for (int j = 0; j < A_LOADS; ++j) {
+      if constexpr (VEC8)
+        ra[j] = *reinterpret_cast<const u32x4*>(x + org[j] + ko);
+      else
+        ra[j] = x[org[j] + ko];
+    }
+#pragma unroll
+    for (int j = 0; j < B_LOADS; ++j)
+      rb[j] = *reinterpret_cast<const u32x4*>(bsrc + static_cast<size_t>(j) * B_STEP * a.kpad + kb);
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < A_LOADS; ++j) {
+      const int row = tid / A_UNITS + j * A_STEP;
+      const bool v = kok && ((ok >> j) & 1u);
+      if constexpr (VEC8)
+        *reinterpret_cast<u32x4*>(As + row * kLDA + au * 8) = v ? ra[j] : u32x4{0u, 0u, 0u, 0u};
+      else
+        As[row * kLDA + au] = v ? ra[j] : static_cast<bf16>(0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < B_LOADS; ++j)
+      *reinterpret_cast<u32x4*>(Bs + (tid / (kBK / 8) + j * B_STEP) * kLDA + bu * 8) = rb[j];
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+  const int r = lane & 31, h = lane >> 5;
+  const bf16* ard = As + (wm * WM + r) * kLDA + h * 8;
+  const bf16* brd = Bs + (wn * WN + r) * kLDA + h * 8;
+  load(0);
+  store();
+  __syncthreads();
+  for (int kt = 0; kt < a.ktiles; ++kt) {
+    if (kt + 1 < a.ktiles) load(kt + 1);
+#pragma unroll
+    for (int s = 0; s < kBK / 16; ++s) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ard + i * 32 * kLDA + s * 16);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(brd + j * 32 * kLDA + s * 16);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    if (kt + 1 < a.ktiles) {
+      store();
+      __syncthreads();
+    }
+  }
+  OutT* out = static_cast<OutT*>(a.out);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int f = n0 + wn * WN + j * 32 + r;
+    const bool fok = f < a.Kg;
+    const float bv = (fok && a.bias) ? a.bias[g * a.Kg + f] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (!fok || m >= a.M) continue;
+        const int n = m / a.HoWo, rr = m - n * a.HoWo, oy = rr / a.Wo, ox = rr - oy * a.Wo;
+        float v = acc[i][j][e] + bv;
+        if (a.relu) v = fmaxf(v, 0.f);
+        out[(static_cast<size_t>(n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off + g * a.Kg + f] =
+            static_cast<OutT>(v);
+      }
+  }
+}
+
+// ---- bf16 max-pool (8 channels per thread) and max-pool + LRN (fp32 math) ----
+__global__ void __launch_bounds__(256) pool_bf16_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
+                                                        int F, int S, int Ho, int Wo, OutViewB o) {
+  const int C8 = C / 8;
+  const long total = static_cast<long>(N) * Ho * Wo * C8;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c8 = static_cast<int>(i % C8);
+    long q = i / C8;
+    const int ox = static_cast<int>(q % Wo);
+    q /= Wo;
+    const int oy = static_cast<int>(q % Ho), n = static_cast<int>(q / Ho);
+    float m[8];
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    for (int fh = 0; fh < F; ++fh)
+      for (int fw = 0; fw < F; ++fw) {
+        const int iy = oy * S + fh, ix = ox * S + fw;
+        if (iy >= H || ix >= W) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((static_cast<size_t>(n) * H + iy) * W + ix) * C + c8 * 8);
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], static_cast<float>(v[e]));
+      }
+    bf16x8 r;
+    for (int e = 0; e < 8; ++e) r[e] = static_cast<bf16>(m[e]);
+    *reinterpret_cast<bf16x8*>(o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
+                               o.c_off + c8 * 8) = r;
+  }
+}
+
+__global__ void __launch_bounds__(256) pool_lrn_bf16_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
+                                                            int F, int S, int Ho, int Wo, int PP, int size, float a,
+                                                            float beta, float k, OutViewB o) {
+  extern __shared__ float pooled[];  // [PP][C]
+  const long P = static_cast<long>(N) * Ho * Wo, p0 = static_cast<long>(blockIdx.x) * PP;
+  for (int t = threadIdx.x; t < PP * C; t += blockDim.x) {
+    const int pl = t / C, c = t - pl * C;
+    const long p = p0 + pl;
+    float m = 0.f;
+    if (p < P) {
+      const int ox = static_cast<int>(p % Wo);
+      const long q = p / Wo;
+      const int oy = static_cast<int>(q % Ho), n = static_cast<int>(q / Ho);
+      m = -INFINITY;
+      for (int fh = 0; fh < F; ++fh)
+        for (int fw = 0; fw < F; ++fw) {
+          const int iy = oy * S + fh, ix = ox * S + fw;
+          if (iy < H && ix < W) m = fmaxf(m, static_cast<float>(x[((static_cast<size_t>(n) * H + iy) * W + ix) * C + c]));
+        }
+    }
+    pooled[pl * C + c] = m;
+  }
+  __syncthreads();
+  const int half = size / 2;
+  for (int t = threadIdx.x; t < PP * C; t += blockDim.x) {
+    const int pl = t / C, c = t - pl * C;
+    const long p = p0 + pl;
+    if (p >= P) continue;
+    float s = 0.f;
+    for (int j = c - half < 0 ? 0 : c - half; j <= (c + half >= C ? C - 1 : c + half); ++j)
+      s = fmaf(pooled[pl * C + j], pooled[pl * C + j], s);
+    const int ox = static_cast<int>(p % Wo);
+    const long q = p / Wo;
+    const int oy = static_cast<int>(q % Ho), n = static_cast<int>(q / Ho);
+    o.base[(static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb + o.c_off + c] =
+        static_cast<bf16>(pooled[pl * C + c] / powf(k + a * s, beta));
+  }
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, size_t n) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x)
+    y[i] = static_cast<bf16>(x[i]);
+}
+
+struct VariantB {
+  int BM, BN;
+  bool vec8;
+};
+constexpr VariantB kVB[] = {{128, 128, true}, {128, 96, false}, {64, 64, true}, {64, 64, false}, {128, 128, false}};
+
+unsigned grid1d(long n) {
+  long g = (n + 255) / 256;
+  return static_cast<unsigned>(g > 65535 ? 65535 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+ConvPlanB make_conv_plan_bf16(int N, int Hp, int Wp, int C, int K, int F, int S, int groups) {
+  ConvPlanB p{};
+  p.N = N;
+  p.Hp = Hp;
+  p.Wp = Wp;
+  p.C = C;
+  p.K = K;
+  p.F = F;
+  p.S = S;
+  p.groups = groups;
+  p.Ho = conv_out_dim(Hp, F, S, 0);
+  p.Wo = conv_out_dim(Wp, F, S, 0);
+  p.Cg = C / groups;
+  p.Kg = K / groups;
+  p.kdim = F * F * p.Cg;
+  p.kpad = (p.kdim + kBK - 1) / kBK * kBK;
+  p.vec8 = (p.Cg % 8 == 0 && C % 8 == 0) ? 1 : 0;
+  const long M = static_cast<long>(N) * p.Ho * p.Wo;
+  const bool small = M * K < 256L * 128 * 128;
+  if (p.Kg == 96 && !small && !p.vec8) p.variant = 1;
+  else if (small) p.variant = p.vec8 ? 2 : 3;
+  else p.variant = p.vec8 ? 0 : 4;
+  p.kpad_n = (p.Kg + kVB[p.variant].BN - 1) / kVB[p.variant].BN * kVB[p.variant].BN;
+  return p;
+}
+
+size_t packed_weight_elems_bf16(const ConvPlanB& p) { return static_cast<size_t>(p.groups) * p.kpad_n * p.kpad; }
+
+void pack_conv_weights_bf16(const ConvPlanB& p, const float* w_kcff, std::vector<uint16_t>& packed,
+                            std::vector<int>& koff) {
+  packed.assign(packed_weight_elems_bf16(p), 0);
+  koff.assign(p.kpad, -1);
+  for (int g = 0; g < p.groups; ++g)
+    for (int n = 0; n < p.Kg; ++n)
+      for (int fh = 0; fh < p.F; ++fh)
+        for (int fw = 0; fw < p.F; ++fw)
+          for (int c = 0; c < p.Cg; ++c) {
+            const float v = w_kcff[((static_cast<size_t>(g * p.Kg + n) * p.Cg + c) * p.F + fh) * p.F + fw];
+            packed[(static_cast<size_t>(g) * p.kpad_n + n) * p.kpad + (fh * p.F + fw) * p.Cg + c] = f32_to_bf16_bits(v);
+          }
+  for (int fh = 0; fh < p.F; ++fh)
+    for (int fw = 0; fw < p.F; ++fw)
+      for (int c = 0; c < p.Cg; ++c) koff[(fh * p.F + fw) * p.Cg + c] = (fh * p.Wp + fw) * p.C + c;
+}
+
+uint16_t f32_to_bf16_bits(float f) {  // round to nearest even, NaN kept NaN
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return static_cast<uint16_t>((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, const int* koff, const float* bias,
+                       OutViewB out, float* out_f32, bool relu, hipStream_t s) {
+  const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
+  if (M == 0) return hipSuccess;
+  if (static_cast<long>(p.N) * p.Hp * p.Wp * p.C >= (1L << 31)) return hipErrorInvalidValue;
+  const VariantB v = kVB[p.variant];
+  ArgsB a{};
+  a.x = static_cast<const bf16*>(x);
+  a.w = static_cast<const bf16*>(wpacked);
+  a.koff = koff;
+  a.bias = bias;
+  a.out = out_f32 ? static_cast<void*>(out_f32) : static_cast<void*>(out.base);
+  a.M = static_cast<int>(M);
+  a.HoWo = p.Ho * p.Wo;
+  a.Wo = p.Wo;
+  a.Hp = p.Hp;
+  a.Wp = p.Wp;
+  a.C = p.C;
+  a.S = p.S;
+  a.Cg = p.Cg;
+  a.Kg = p.Kg;
+  a.kpad = p.kpad;
+  a.kpad_n = p.kpad_n;
+  a.ktiles = p.kpad / kBK;
+  a.Hb = out.Hb;
+  a.Wb = out.Wb;
+  a.Cb = out.Cb;
+  a.h_off = out.h_off;
+  a.w_off = out.w_off;
+  a.c_off = out.c_off;
+  a.relu = relu ? 1 : 0;
+  a.n_ntiles = p.kpad_n / v.BN;
+  const dim3 grid(static_cast<unsigned>((M + v.BM - 1) / v.BM) * a.n_ntiles, 1, p.groups);
+  const size_t lds = static_cast<size_t>(v.BM + v.BN) * kLDA * 2 + static_cast<size_t>(p.kpad) * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+#define ANX_LAUNCH(BM, BN, WMW, WNW, V8)                                                              \
+  do {                                                                                                \
+    if (out_f32)                                                                                      \
+      conv_bf16_kernel<BM, BN, WMW, WNW, V8, float><<<grid, kThreads, lds, s>>>(a);                   \
+    else                                                                                              \
+      conv_bf16_kernel<BM, BN, WMW, WNW, V8, bf16><<<grid, kThreads, lds, s>>>(a);                    \
+  } while (0)
+  switch (p.variant) {
+    case 0: ANX_LAUNCH(128, 128, 2, 2, true); break;
+    case 1: ANX_LAUNCH(128, 96, 4, 1, false); break;
+    case 2: ANX_LAUNCH(64, 64, 2, 2, true); break;
+    case 3: ANX_LAUNCH(64, 64, 2, 2, false); break;
+    case 4: ANX_LAUNCH(128, 128, 2, 2, false); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef ANX_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S, OutViewB out, hipStream_t s) {
+  const int Ho = pool_out_dim(H, F, S), Wo = pool_out_dim(W, F, S);
+  if (C % 8 || out.Cb % 8 || out.c_off % 8) return hipErrorInvalidValue;
+  const long n = static_cast<long>(N) * Ho * Wo * (C / 8);
+  if (n == 0) return hipSuccess;
+  pool_bf16_kernel<<<grid1d(n), 256, 0, s>>>(static_cast<const bf16*>(x), N, H, W, C, F, S, Ho, Wo, out);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
+                            float beta, float k, LrnMode mode, OutViewB out, hipStream_t s) {
+  const int Ho = pool_out_dim(H, F, S), Wo = pool_out_dim(W, F, S);
+  const long P = static_cast<long>(N) * Ho * Wo;
+  if (P == 0) return hipSuccess;
+  const int PP = C >= 4096 ? 1 : 4096 / C;
+  const float a = mode == LrnMode::DivN ? alpha / size : alpha;
+  pool_lrn_bf16_kernel<<<static_cast<unsigned>((P + PP - 1) / PP), 256, PP * C * 4, s>>>(
+      static_cast<const bf16*>(x), N, H, W, C, F, S, Ho, Wo, PP, size, a, beta, k, out);
+  return hipGetLastError();
+}
+
+hipError_t f32_to_bf16(const float* x, void* y, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  f32_to_bf16_kernel<<<grid1d(static_cast<long>(n)), 256, 0, s>>>(x, static_cast<bf16*>(y), n);
+  return hipGetLastError();
+}
+
+}  // namespace anx::hip

@@ -70,6 +70,10 @@ _SIGS = {
     "anx_cpu_engine_stage2": (_I, [_P, _I, C.POINTER(TileC), _P]),
     "anx_cpu_engine_window": (_I, [_P, C.POINTER(TileC), _I, _I, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_SZ)]),
     "anx_memcpy2d_host": (_I, [_P, _SZ, _P, _SZ, _SZ, _SZ]),
+    "anx_full_weight_sizes": (_I, [_I, _I, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "anx_full_create": (_I, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), _I, _I, _I, _I]),
+    "anx_full_destroy": (_I, [_P]),
+    "anx_full_forward": (_I, [_P, _P, _I, _P, _P]),
     "anx_memcpy2d_async": (_I, [_P, _SZ, _P, _SZ, _SZ, _SZ, _P]),
     "anx_conv2d_direct": (_I, [_P, _P, _P, _P] + [_I] * 10 + [_P]),
     "anx_relu": (_I, [_P, _SZ, _P]),

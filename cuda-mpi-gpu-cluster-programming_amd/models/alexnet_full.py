@@ -1,0 +1,113 @@
+"""Full AlexNet (extension model family, BASELINE.json config "Full AlexNet Conv1-5 + FC6-8 bf16,
+batch=2048"): the reference's Blocks 1-2 (Conv1-ReLU-Pool1-Conv2-ReLU-Pool2-LRN2) followed by the
+AlexNet tail Conv3/4/5 (3x3, pad 1) + Pool5 + FC6/FC7/FC8, inference in bf16 with fp32 accumulation
+on v_mfma_f32_32x32x16_bf16 (csrc/src/hip/conv_bf16.hip, csrc/src/full_engine.cpp).
+
+The reference itself stops after Block 2; this family exists because the benchmark
+configs name it. FC layers run on the same implicit-GEMM kernel as 1x1 convolutions.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .. import _native as nat
+from ..utils.init import STREAM_EXTRA, uniform
+
+LAYERS = ("conv1", "conv2", "conv3", "conv4", "conv5", "fc6", "fc7", "fc8")
+FLOPS_PER_IMAGE = 2.0 * (55 * 55 * 96 * 363 + 27 * 27 * 256 * 2400 + 13 * 13 * 384 * 2304 + 13 * 13 * 384 * 3456 +
+                         13 * 13 * 256 * 3456 + 9216 * 4096 + 4096 * 4096 + 4096 * 1000)
+
+
+def weight_shapes(classes: int = 1000, groups2: int = 1):
+    wn, bn = (C.c_size_t * 8)(), (C.c_size_t * 8)()
+    nat.call("anx_full_weight_sizes", classes, groups2, wn, bn)
+    conv = [(96, 3, 11, 11), (256, 96 // groups2, 5, 5), (384, 256, 3, 3), (384, 384, 3, 3), (256, 384, 3, 3)]
+    fc = [(4096, 9216), (4096, 4096), (classes, 4096)]
+    shapes = conv + fc
+    assert [int(np.prod(s)) for s in shapes] == list(wn)
+    return shapes, [int(b) for b in bn]
+
+
+def init_full_weights(seed: int = 0, classes: int = 1000, groups2: int = 1) -> dict:
+    """He-uniform weights from the counter-based RNG (deterministic on every rank), zero biases."""
+    shapes, bsz = weight_shapes(classes, groups2)
+    out = {}
+    for i, (name, s) in enumerate(zip(LAYERS, shapes)):
+        fan_in = int(np.prod(s[1:]))
+        bound = float(np.sqrt(6.0 / fan_in))
+        u = uniform(seed, STREAM_EXTRA + i, int(np.prod(s)))
+        out["w_" + name] = torch.from_numpy(((u * 2 - 1) * bound).astype(np.float32).reshape(s))
+        out["b_" + name] = torch.zeros(bsz[i])
+    return out
+
+
+class AlexNetFull:
+    def __init__(self, weights: dict | None = None, *, seed: int = 0, classes: int = 1000, device="cuda",
+                 max_batch: int = 1, groups2: int = 1, lrn_mode: str = "div_n"):
+        self.classes, self.groups2, self.lrn_mode = classes, groups2, lrn_mode
+        self.weights = {k: v.detach().to("cpu", torch.float32).contiguous()
+                        for k, v in (weights or init_full_weights(seed, classes, groups2)).items()}
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("the bf16 full-AlexNet engine is GPU-only (use reference_forward on the CPU)")
+        self._h = None
+        self._cap = 0
+        self._ensure(max_batch)
+
+    def _ensure(self, n):
+        if self._h is not None and n <= self._cap:
+            return
+        self.close()
+        ws = (C.c_void_p * 8)(*[self.weights["w_" + k].data_ptr() for k in LAYERS])
+        bs = (C.c_void_p * 8)(*[self.weights["b_" + k].data_ptr() for k in LAYERS])
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            nat.call("anx_full_create", C.byref(h), ws, bs, self.classes, max(1, n), self.groups2,
+                     0 if self.lrn_mode == "div_n" else 1)
+        self._h, self._cap = h, max(1, n)
+
+    def close(self):
+        if self._h is not None:
+            torch.cuda.synchronize(self.device)
+            nat.lib().anx_full_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """x: [N,227,227,3] fp32 NHWC on the device -> logits [N, classes] fp32."""
+        if tuple(x.shape[1:]) != (227, 227, 3) or x.dtype != torch.float32 or not x.is_contiguous():
+            raise ValueError("expected contiguous fp32 NHWC [N,227,227,3]")
+        N = x.shape[0]
+        self._ensure(N)
+        y = out if out is not None else torch.empty(N, self.classes, device=self.device)
+        nat.call("anx_full_forward", self._h, x.data_ptr(), N, y.data_ptr(), nat.stream_ptr(self.device))
+        return y
+
+    __call__ = forward
+
+
+def reference_forward(x: torch.Tensor, w: dict, groups2: int = 1, lrn_mode: str = "div_n",
+                      dtype=torch.float32) -> torch.Tensor:
+    """Plain PyTorch oracle (NHWC in, logits out) of the same topology."""
+    h = x.permute(0, 3, 1, 2).to(dtype)
+    g = lambda k: w[k].to(h.device, dtype)  # noqa: E731
+    h = F.max_pool2d(F.relu(F.conv2d(h, g("w_conv1"), g("b_conv1"), stride=4)), 3, 2)
+    h = F.max_pool2d(F.relu(F.conv2d(h, g("w_conv2"), g("b_conv2"), padding=2, groups=groups2)), 3, 2)
+    a = 1e-4 if lrn_mode == "div_n" else 1e-4 * 5
+    h = F.local_response_norm(h, 5, alpha=a, beta=0.75, k=2.0)
+    h = F.relu(F.conv2d(h, g("w_conv3"), g("b_conv3"), padding=1))
+    h = F.relu(F.conv2d(h, g("w_conv4"), g("b_conv4"), padding=1))
+    h = F.max_pool2d(F.relu(F.conv2d(h, g("w_conv5"), g("b_conv5"), padding=1)), 3, 2)
+    h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)  # NHWC flatten (the engine's FC6 input order)
+    h = F.relu(F.linear(h, g("w_fc6"), g("b_fc6")))
+    h = F.relu(F.linear(h, g("w_fc7"), g("b_fc7")))
+    return F.linear(h, g("w_fc8"), g("b_fc8"))
