@@ -51,6 +51,7 @@ struct Options {
   std::string conv2_algo = "auto";  // auto | direct | winograd
   bool check = false;
   bool json = true;
+  std::string weights;  // directory with raw fp32 w1/b1/w2/b2 .bin (overrides --init for weights)
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -58,7 +59,7 @@ struct Options {
                "%s\nusage: anx --version v1|v2.1|v2.2|v3|v4|v5 [--batch N] [--init const|rand] [--seed S]\n"
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
                "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd] [--check]\n"
-               "           [--no-json]\n",
+               "           [--weights DIR] [--no-json]\n",
                msg);
   std::exit(2);
 }
@@ -83,6 +84,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--conv2-algo") o.conv2_algo = val();
     else if (a == "--check") o.check = true;
     else if (a == "--no-json") o.json = false;
+    else if (a == "--weights") o.weights = val();
     else if (a == "-h" || a == "--help") usage("");
     else usage(("unknown argument " + a).c_str());
   }
@@ -189,6 +191,22 @@ Setup make_setup(const Options& o, const RankInfo& ri) {
     init_random(s.w, s.b1, s.b2, o.seed);
   else
     init_const(s.w, s.b1, s.b2);
+  if (!o.weights.empty()) {
+    // raw fp32 checkpoint written by anx.utils.io.save_weights_raw (w1.bin b1.bin w2.bin b2.bin)
+    auto rd = [&](const char* name, std::vector<float>& v) {
+      const std::string path = o.weights + "/" + name + ".bin";
+      FILE* f = std::fopen(path.c_str(), "rb");
+      if (!f) throw std::runtime_error("cannot open " + path);
+      const size_t got = std::fread(v.data(), sizeof(float), v.size(), f);
+      const bool extra = std::fgetc(f) != EOF;
+      std::fclose(f);
+      if (got != v.size() || extra) throw std::runtime_error(path + ": wrong size for this configuration");
+    };
+    rd("w1", s.w.w1);
+    rd("b1", s.w.b1);
+    rd("w2", s.w.w2);
+    rd("b2", s.w.b2);
+  }
   return s;
 }
 
