@@ -47,6 +47,8 @@ def parse():
                     help="root: rank 0 scatters the batch (reference V4/V5 semantics); local: per-rank synthetic")
     ap.add_argument("--no-gather", action="store_true", help="leave outputs on their ranks")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu = gloo rehearsal (tests only)")
+    ap.add_argument("--model", default="blocks", choices=["blocks", "full"],
+                    help="blocks = the headline AlexNet Blocks1-2 fp32; full = full AlexNet bf16 extension")
     return ap.parse_args()
 
 
@@ -69,9 +71,15 @@ def main():
 
     B = a.batch_per_gpu
     d = anx.blocks_dims()
-    model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B)
+    if a.model == "full":  # extension config: full AlexNet bf16 (BASELINE.json config 5)
+        from anx.models.alexnet_full import FLOPS_PER_IMAGE, AlexNetFull
+        model = AlexNetFull(seed=1234, device=dev, max_batch=B)
+        out_shape, flops = (1000,), FLOPS_PER_IMAGE
+    else:
+        model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B)
+        out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
     cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather)
-    pipe = ScatterComputeGather(model, cfg, (d.H, d.W, d.C0), (d.Hp2, d.Wp2, d.C2), dev)
+    pipe = ScatterComputeGather(model, cfg, (d.H, d.W, d.C0), out_shape, dev)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     if pipe.x_global is not None:
@@ -101,7 +109,18 @@ def main():
         el = float(t.item())
     ms = el * 1e3 / a.steps
     imgs = B * world * a.steps / el
-    if rank == 0:
+    if rank == 0 and a.model == "full":
+        rec = {
+            "metric": "images/sec full AlexNet (Conv1-5 + FC6-8) bf16 inference on MI355X (extension)",
+            "value": round(imgs, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic (random images 227x227x3, He-uniform random weights)",
+            "config": {"model": "AlexNet full (reference Blocks1-2 + Conv3-5 + FC6-8, 1000 classes)",
+                       "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
+                       "gflop_per_image": round(flops / 1e9, 4), "tflops": round(imgs * flops / 1e12, 2)},
+        }
+        print(json.dumps(rec), flush=True)
+    elif rank == 0:
         rec = {
             "metric": METRIC,
             "value": round(imgs, 2),
