@@ -5,8 +5,9 @@ Metric/config from BASELINE.json: "images/sec (and ms/batch) AlexNet Blocks1-2 f
 MI355X". One step = the reference's V4/V5 pipeline at batch scale: rank 0 owns the global batch
 (device resident), scatters each rank's images over RCCL/xGMI, every rank runs the native
 Blocks 1-2 engine (MFMA implicit-GEMM convs + fused epilogues) on its shard, and the outputs are
-gathered back to rank 0. Scatter/compute/gather are pipelined over micro-batches (RCCL runs on its
-own stream, compute on the current stream). Weak scaling: --batch-per-gpu images per GPU.
+gathered back to rank 0. RCCL runs on its own stream, compute on the current stream, and the
+scatter of step k+1 runs while step k computes (double-buffered inputs, --no-prefetch to serialise);
+--micro splits each step into micro-batches. Weak scaling: --batch-per-gpu images per GPU.
 
 Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
 bench.py --gpus N``. Rank 0 prints ONE JSON line.
@@ -39,9 +40,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch-per-gpu", type=int, default=128)
-    # 2 micro-batches of 64: the second half's scatter overlaps the first half's compute, and 64-image
-    # launches keep the conv kernels at ~96% of their batch-128 throughput (tools/sweep_batch.py).
-    ap.add_argument("--micro", type=int, default=2, help="micro-batches per step for scatter/compute/gather overlap")
+    # With cross-step prefetch the whole per-rank batch is one launch (128-image launches run the conv
+    # kernels ~4% faster than 2 x 64, tools/sweep_batch.py); without it, --micro 2 overlaps the second
+    # half's scatter with the first half's compute.
+    ap.add_argument("--micro", type=int, default=1, help="micro-batches per step for scatter/compute/gather overlap")
+    ap.add_argument("--no-prefetch", action="store_true", help="scatter each step's input inside that step only")
     ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
     ap.add_argument("--input-source", default="root", choices=["root", "local"],
                     help="root: rank 0 scatters the batch (reference V4/V5 semantics); local: per-rank synthetic")
@@ -78,7 +81,8 @@ def main():
     else:
         model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B)
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
-    cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather)
+    cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather,
+                         prefetch=not a.no_prefetch)
     pipe = ScatterComputeGather(model, cfg, (d.H, d.W, d.C0), out_shape, dev)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -140,7 +144,8 @@ def main():
                 "seq_len": None,
                 "image": [d.H, d.W, d.C0],
                 "parallelism": f"dp{world}",
-                "pipeline": ("root scatter -> compute -> gather (RCCL), %d micro-batches" % len(pipe.splits))
+                "pipeline": ("root scatter -> compute -> gather (RCCL), %d micro-batches%s"
+                             % (len(pipe.splits), ", next-step scatter overlapped" if pipe.prefetch else ""))
                 if world > 1 else "single GPU",
                 "input_source": a.input_source,
                 "impl": a.impl,

@@ -10,7 +10,11 @@ batch scale and MI355X-first:
 * collectives are RCCL scatter/gather (grouped point-to-point from/to the root, one direct xGMI
   link per peer) issued asynchronously on RCCL's stream, split into micro-batches so the scatter
   of micro-batch i+1 and the gather of i-1 overlap the compute of i on the compute stream;
-* buffers are allocated once and reused every step (the reference re-mallocs per call, D5).
+* buffers are allocated once and reused every step (the reference re-mallocs per call, D5);
+* ``prefetch=True`` pipelines ACROSS steps: the input of step k+1 is scattered into the second of
+  two input buffers while step k computes, so the root's xGMI egress (world-1 links, each carrying
+  one peer's shard) overlaps the compute instead of preceding it. Every step still scatters,
+  computes and gathers its full batch; only the order changes.
 """
 from __future__ import annotations
 
@@ -36,6 +40,7 @@ class PipelineConfig:
     micro: int = 4
     scatter: bool = True   # rank 0 owns the global batch and scatters it
     gather: bool = True    # outputs are gathered to rank 0
+    prefetch: bool = False  # scatter step k+1 while step k computes (double-buffered x and y)
 
 
 class ScatterComputeGather:
@@ -50,14 +55,61 @@ class ScatterComputeGather:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         B = cfg.batch_per_rank
         self.splits = micro_splits(B, cfg.micro if self.world > 1 else 1)
-        self.x = torch.empty((B, *in_shape), device=self.device)
-        self.y = torch.empty((B, *out_shape), device=self.device)
+        self.prefetch = cfg.prefetch and self.world > 1
+        nbuf = 2 if self.prefetch else 1
+        self._xb = [torch.empty((B, *in_shape), device=self.device) for _ in range(nbuf)]
+        self._yb = [torch.empty((B, *out_shape), device=self.device) for _ in range(nbuf)]
+        self.x, self.y = self._xb[0], self._yb[0]
+        self._k = 0
+        self._scatter_pending = None          # works that fill the input of the next step
+        self._gather_pending = [None] * nbuf  # works still reading y buffer i
         # single rank: no scatter/gather buffers at all (the V3 shape: compute on resident data)
         root = self.rank == 0 and self.world > 1
         self.x_global = torch.empty((self.world, B, *in_shape), device=self.device) if root and cfg.scatter else None
         self.y_global = torch.empty((self.world, B, *out_shape), device=self.device) if root and cfg.gather else None
 
+    def _scatter(self, x):
+        root = self.rank == 0
+        works = []
+        for lo, hi in self.splits:
+            src = [self.x_global[r, lo:hi] for r in range(self.world)] if root else None
+            works.append(dist.scatter(x[lo:hi], src, src=0, group=self.group, async_op=True))
+        return works
+
+    def _step_prefetch(self) -> None:
+        cur = self._k % 2
+        x, y = self._xb[cur], self._yb[cur]
+        if self.cfg.scatter and self._scatter_pending is None:  # pipeline fill (first step only)
+            self._scatter_pending = self._scatter(x)
+        mine = self._scatter_pending or []
+        # prefetch the next step's input into the other buffer. RCCL orders it after everything
+        # already enqueued on this stream (the previous step's compute, the last reader of that buffer).
+        self._scatter_pending = self._scatter(self._xb[cur ^ 1]) if self.cfg.scatter else None
+        for w in mine:
+            w.wait()
+        if self._gather_pending[cur] is not None:  # y[cur] is still being gathered from 2 steps ago
+            for w in self._gather_pending[cur]:
+                w.wait()
+        gw = []
+        for lo, hi in self.splits:
+            self.model(x[lo:hi], out=y[lo:hi])
+            if self.cfg.gather:
+                dst = [self.y_global[r, lo:hi] for r in range(self.world)] if self.rank == 0 else None
+                gw.append(dist.gather(y[lo:hi], dst, dst=0, group=self.group, async_op=True))
+        self._gather_pending[cur] = gw
+        self.x, self.y = x, y
+        self._k += 1
+
+    def drain(self) -> None:
+        """Wait for every outstanding prefetch/gather (the last step's outputs are then in y_global)."""
+        for ws in [self._scatter_pending or []] + [g or [] for g in self._gather_pending]:
+            for w in ws:
+                w.wait()
+        self._gather_pending = [None] * len(self._gather_pending)
+
     def step(self) -> None:
+        if self.prefetch:
+            return self._step_prefetch()
         if self.world == 1:
             if self.x_global is not None:
                 self.x.copy_(self.x_global[0])
@@ -66,11 +118,7 @@ class ScatterComputeGather:
                 self.y_global[0].copy_(self.y)
             return
         root = self.rank == 0
-        sw = []
-        if self.cfg.scatter:
-            for lo, hi in self.splits:
-                src = [self.x_global[r, lo:hi] for r in range(self.world)] if root else None
-                sw.append(dist.scatter(self.x[lo:hi], src, src=0, group=self.group, async_op=True))
+        sw = self._scatter(self.x) if self.cfg.scatter else []
         gw = []
         for i, (lo, hi) in enumerate(self.splits):
             if sw:

@@ -23,7 +23,7 @@ def free_port():
         return s.getsockname()[1]
 
 
-def _pipeline_worker(rank, world, port, q):
+def _pipeline_worker(rank, world, port, q, prefetch=False):
     sys.path.insert(0, ROOT)
     import anx  # noqa: F401
     from anx.models.alexnet_blocks import AlexNetBlocks
@@ -34,22 +34,26 @@ def _pipeline_worker(rank, world, port, q):
     torch.set_num_threads(1)
     d = anx.blocks_dims()
     m = AlexNetBlocks(init="rand", seed=2, device="cpu")
-    pipe = ScatterComputeGather(m, PipelineConfig(2, micro=2), (d.H, d.W, d.C0), (d.Hp2, d.Wp2, d.C2), "cpu")
+    pipe = ScatterComputeGather(m, PipelineConfig(2, micro=2, prefetch=prefetch), (d.H, d.W, d.C0),
+                                (d.Hp2, d.Wp2, d.C2), "cpu")
     if rank == 0:
         pipe.x_global.copy_(init_input(2 * world, "rand", seed=2).view(world, 2, d.H, d.W, d.C0))
-    pipe.step()
+    for _ in range(3 if prefetch else 1):
+        pipe.step()
+    pipe.drain()
     if rank == 0:
         q.put(pipe.y_global.clone())
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_scatter_compute_gather_gloo():
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_scatter_compute_gather_gloo(prefetch):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, q, prefetch)) for r in range(world)]
     for p in procs:
         p.start()
     y = q.get(timeout=300)
