@@ -14,6 +14,7 @@
 //   3. output transform : M -> Y = A^T M A + bias, ReLU, NHWC conv output (VALU, float4 over filters)
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <vector>
 
 #include "anx/ops.hpp"
@@ -287,8 +288,176 @@ __global__ void __launch_bounds__(256) wino_fused_kernel(FusedArgs a) {
   }
 }
 
-// fused-kernel configuration: bit0 = BK 48 (when Cg allows), bit1 = XCD-aware block order
-int g_fused_cfg = 1;
+// ---------------------------------------------------------------------------------------------
+// Same computation, staged by LDS-DMA. The register-staged kernel above needs ~246 VGPR+AGPR
+// (144 Y + 16 acc + 24 staging + addressing), so it runs at 2 waves/SIMD and every K slice's
+// global loads must land within one slice of MFMAs. Here the operand tiles go global -> LDS with
+// global_load_lds_dwordx4 (no staging registers) into a 3-deep ring: slice it+2 is in flight
+// while slice it computes, retired by a counted `s_waitcnt vmcnt` and ONE raw s_barrier per slice
+// (a __syncthreads() would drain the in-flight DMA: cdna_hip_programming.md §5 "Pipelining
+// across barriers"). The freed registers hold a second accumulator, so the 144-FMA output fold
+// of point ab runs on the VALU while the MFMAs of point ab+1 are in flight.
+//
+// LDS image: rows of BK floats, unpadded (the DMA writes lane-linear 1 KiB pieces); the 16-byte
+// unit u of row r is stored at unit u ^ ((r >> 2) & 3), which makes the ds_read_b128 lane groups
+// of the 32x32 fragment reads hit 16 distinct bank quads. The swizzle is applied on the global
+// source address of each lane.
+using lds_f32 = __attribute__((address_space(3))) float;
+// 16 B per lane, global -> LDS (lane i lands at lds + 16*i; lds must be wave-uniform)
+__device__ __forceinline__ void glds16(const float* g, lds_f32* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BK>
+__global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
+  using f32x16 = __attribute__((ext_vector_type(16))) float;
+  constexpr int U4 = BK / 4;              // 16-B units per row
+  constexpr int NI = kFB * U4 / 256;      // DMA instructions per thread per operand
+  static_assert(NI * 256 == kFB * U4 && U4 % 4 == 0, "BK must be a multiple of 16");
+  constexpr int TILE = kFB * BK;          // floats per operand tile
+  constexpr int STAGE = 2 * TILE;         // A tile | B tile
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = blockIdx.z;
+  const int pt = blockIdx.x / a.n_ntiles, nt = blockIdx.x - pt * a.n_ntiles;
+  const int p0 = pt * kFB, n0 = nt * kFB;
+
+  // per-lane source offsets of this thread's NI A units and NI B units (swizzled unit order)
+  int aoff[NI], boff[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int U = (j * 4 + wave) * 64 + lane;
+    const int row = U / U4;
+    const int u = (U - row * U4) ^ ((row >> 2) & 3);
+    const int p = p0 + row;
+    aoff[j] = (p < a.P ? p : 0) * (kN * kN) * a.C + 4 * u;
+    boff[j] = (n0 + row) * a.kpad + 4 * u;
+  }
+  const float* Vg = a.V + g * a.Cg;
+  const int ksteps = a.kpad / BK;
+  const int total = kN * kN * ksteps;
+  lds_f32* lds3 = (lds_f32*)(lds);  // generic -> LDS address space (C-style cast required)
+
+  auto issue = [&](int it) {
+    const int ab = it / ksteps, kk = (it - ab * ksteps) * BK;
+    const float* va = Vg + ab * a.C + kk;
+    const float* ub = a.U + static_cast<size_t>(ab * a.groups + g) * a.kpad_n * a.kpad + kk;
+    lds_f32* st = lds3 + (it % 3) * STAGE;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      glds16(va + aoff[j], st + (j * 4 + wave) * 256);
+      glds16(ub + boff[j], st + TILE + (j * 4 + wave) * 256);
+    }
+  };
+
+  const int r = lane & 31, h = lane >> 5;
+  const int swz = (r >> 2) & 3;  // rows wm*32 + r and wn*32 + r share it
+  int rd[BK / 8];                // unit (h*BK/8 + s4) of my row, swizzled, in floats
+#pragma unroll
+  for (int s4 = 0; s4 < BK / 8; ++s4) rd[s4] = 4 * ((h * (BK / 8) + s4) ^ swz);
+  const int a_row = (wm * 32 + r) * BK, b_row = TILE + (wn * 32 + r) * BK;
+
+  float Y[9][16];
+#pragma unroll
+  for (int q = 0; q < 9; ++q)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) Y[q][e] = 0.f;
+  f32x16 acc0 = {}, acc1 = {};
+
+  auto mfma_slice = [&](int it, f32x16& acc) {
+    const float* base = lds + (it % 3) * STAGE;
+#pragma unroll
+    for (int s4 = 0; s4 < BK / 8; ++s4) {
+      const f32x4 af = *reinterpret_cast<const f32x4*>(base + a_row + rd[s4]);
+      const f32x4 bf = *reinterpret_cast<const f32x4*>(base + b_row + rd[s4]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+    }
+  };
+  auto fold = [&](int ab, f32x16& acc) {
+    const int aa = ab / kN, bb = ab - aa * kN;
+    float co[9];
+#pragma unroll
+    for (int i3 = 0; i3 < kM; ++i3)
+#pragma unroll
+      for (int j3 = 0; j3 < kM; ++j3) co[i3 * kM + j3] = c_AT[i3][aa] * c_AT[j3][bb];
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) Y[q][e] = fmaf(co[q], acc[e], Y[q][e]);
+    acc = f32x16{};
+  };
+  // one K slice: retire slice it (counted wait + barrier), refill the ring slot freed by it-1
+  auto step = [&](int it, f32x16& acc) {
+    if (it + 1 < total)
+      wait_vmcnt<2 * NI>();
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // keep the DMA refill and the ds_reads below the barrier
+    if (it + 2 < total) issue(it + 2);
+    mfma_slice(it, acc);
+  };
+
+  issue(0);
+  if (total > 1) issue(1);
+  // ab pairs: even ab accumulate in acc0, odd in acc1; the fold of the previous point is issued
+  // after the first slice of the next one, so the VALU work overlaps in-flight MFMAs.
+  int it = 0;
+  for (int ab = 0; ab < kN * kN; ab += 2) {
+    for (int ks = 0; ks < ksteps; ++ks, ++it) {
+      step(it, acc0);
+      if (ks == 0 && ab > 0) fold(ab - 1, acc1);
+    }
+    if (ab + 1 < kN * kN) {
+      for (int ks = 0; ks < ksteps; ++ks, ++it) {
+        step(it, acc1);
+        if (ks == 0) fold(ab, acc0);
+      }
+    }
+  }
+  // kN*kN is odd: the last point (48, even) is still in acc0
+  fold(kN * kN - 1, acc0);
+
+  const int f = n0 + wn * 32 + r;
+  if (f >= a.Kg) return;
+  const int fk = g * a.Kg + f;
+  const float bv = a.bias ? a.bias[fk] : 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int p = p0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (p >= a.P) continue;
+    const int tj = p % a.tx;
+    const int q = p / a.tx;
+    const int ti = q % a.ty;
+    const int n = q / a.ty;
+#pragma unroll
+    for (int i3 = 0; i3 < kM; ++i3) {
+      const int oy = ti * kM + i3;
+      if (oy >= a.Ho) break;
+#pragma unroll
+      for (int j3 = 0; j3 < kM; ++j3) {
+        const int ox = tj * kM + j3;
+        if (ox >= a.Wo) break;
+        float v = Y[i3 * kM + j3][e] + bv;
+        if (a.relu) v = fmaxf(v, 0.f);
+        a.y[((static_cast<size_t>(n) * a.Ho + oy) * a.Wo + ox) * a.K + fk] = v;
+      }
+    }
+  }
+}
+
+// fused-kernel configuration: bit0 = BK 48 (when Cg allows), bit1 = XCD-aware block order,
+// bit2 = LDS-DMA ring (when Cg % BK == 0). ANX_WINO_FUSED_CFG overrides the default (profiling).
+int default_fused_cfg() {
+  const char* e = std::getenv("ANX_WINO_FUSED_CFG");
+  const int v = e ? std::atoi(e) : -1;
+  return v >= 0 && v <= 7 ? v : 5;
+}
+int g_fused_cfg = default_fused_cfg();
 
 unsigned grid_for(long n) {
   long g = (n + kT - 1) / kT;
@@ -298,7 +467,7 @@ unsigned grid_for(long n) {
 }  // namespace
 
 int wino_set_fused_cfg(int cfg) {
-  if (cfg < 0 || cfg > 3) return -1;
+  if (cfg < 0 || cfg > 7) return -1;
   g_fused_cfg = cfg;
   return 0;
 }
@@ -383,6 +552,15 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
   a.n_ptiles = (w.P + kFB - 1) / kFB;
   a.n_ntiles = (a.Kg + kFB - 1) / kFB;
   if (a.n_ntiles * kFB > a.kpad_n || a.Cg % 4) return hipErrorInvalidValue;
+  if ((g_fused_cfg & 4) && a.Cg % 48 == 0 && a.kpad == a.Cg) {
+    constexpr int kLds = 3 * 2 * kFB * 48 * sizeof(float);  // 72 KiB ring
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wino_fused_glds_kernel<48>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    if (attr != hipSuccess) return attr;
+    dim3 grid(a.n_ptiles * a.n_ntiles, 1, w.groups);
+    wino_fused_glds_kernel<48><<<grid, 256, kLds, s>>>(a);
+    return hipGetLastError();
+  }
   const int bk = (a.kpad % 48 == 0 && g_fused_cfg & 1) ? 48 : 32;
   const bool xcd = (g_fused_cfg & 2) != 0;
   dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);

@@ -62,7 +62,7 @@ def main():
     nat.call("anx_conv_force_variant", 1, -1)
     f = anx.flops_per_image()
     nat.call("anx_set_conv2_algo", 0)
-    nat.call("anx_wino_fused_cfg", 3)
+    nat.call("anx_wino_fused_cfg", 5)
     for (v4, sc, al, fc), t, (_, _, err) in zip(arms, times, models):
         med = sorted(t)[len(t) // 2]
         print(json.dumps({"arm": f"{v4}:{sc}:{al}:{fc}", "batch": a.batch, "ms_median": round(med, 4), "ms_min": round(min(t), 4),
