@@ -65,10 +65,14 @@ struct ConvPlan {
   int kpad;           // kdim rounded up to BK
   int kpad_n;         // Kg rounded up to BN
   int variant;        // tile configuration id
-  int vec4;           // input chunks of 4 channels are contiguous & 16B aligned
+  int vec4;           // A is gathered in 4-float units (16-B loads)
+  int taps4;          // Cg%4 != 0 (conv1, C=3): each filter row's F*C contiguous floats are cut
+                      // into 4-float units, the last one shifted back to end at F*C (its
+                      // overlap gets zero weight) -> kdim = F*4*ceil(F*C/4), 16-B gathers
 };
 ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups);
-// Packed weights: [groups][kpad_n][kpad] with k = (fh*F + fw)*Cg + c; zero padded.
+// Packed weights: [groups][kpad_n][kpad] with k = (fh*F + fw)*Cg + c (taps4: k = (fh*U + u)*4 + e
+// over the 4-float units u of filter row fh); zero padded.
 size_t packed_weight_floats(const ConvPlan& p);
 // Offset table: [kpad] int32 input offsets (relative to the pixel's window origin), -1 = padding.
 size_t koff_ints(const ConvPlan& p);

@@ -80,7 +80,7 @@ hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 // ConvPlan <-> 16 ints
 void plan_to_ints(const anx::hip::ConvPlan& p, int* o) {
   const int v[16] = {p.N, p.Hp, p.Wp, p.C, p.K, p.F, p.S, p.groups, p.Ho, p.Wo, p.Cg, p.Kg, p.kdim, p.kpad, p.kpad_n,
-                     p.variant | (p.vec4 << 8)};
+                     p.variant | (p.vec4 << 8) | (p.taps4 << 9)};
   std::memcpy(o, v, sizeof v);
 }
 anx::hip::ConvPlan plan_from_ints(const int* o) {
@@ -102,6 +102,7 @@ anx::hip::ConvPlan plan_from_ints(const int* o) {
   p.kpad_n = o[14];
   p.variant = o[15] & 0xff;
   p.vec4 = (o[15] >> 8) & 1;
+  p.taps4 = (o[15] >> 9) & 1;
   return p;
 }
 }  // namespace

@@ -36,6 +36,9 @@ constexpr int kLDA = kBK + 4;
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+// A gathers may start at any float (taps4 units of a C=3 image row): 4-byte alignment, still one
+// global_load_dwordx4 (ROCm runs gfx9 in unaligned-access mode).
+using f32x4u = __attribute__((ext_vector_type(4), aligned(4))) float;
 
 struct ConvArgs {
   const float* x;
@@ -132,7 +135,7 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < A_LOADS; ++j) {
       if constexpr (VEC4)
-        ra[j] = *reinterpret_cast<const f32x4*>(x + a_org[j] + ko);
+        ra[j] = *reinterpret_cast<const f32x4u*>(x + a_org[j] + ko);
       else
         ra[j] = x[a_org[j] + ko];
     }
@@ -254,6 +257,8 @@ constexpr Variant kVariants[] = {
     {128, 96, false, 2},   // 6: = 1 with double-buffered LDS
     {256, 128, true, 1},   // 7: 2x2 waves of 128x64 (8 accumulators per wave)
     {256, 96, false, 1},   // 8: conv1-like, 4x1 waves of 64x96 (6 accumulators per wave)
+    {128, 96, true, 1},    // 9: conv1 with taps4 units: 4x1 waves of 32x96, 16-B gathers
+    {256, 96, true, 1},    // 10: = 9 with 64x96 per wave
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 // Tuning override for in-process A/B (anx_conv_force_variant): [0] vec4 convs, [1] scalar convs.
@@ -283,12 +288,19 @@ ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int g
   p.Cg = C / groups;
   p.Kg = K / groups;
   p.kdim = F * F * p.Cg;
-  p.kpad = (p.kdim + kBK - 1) / kBK * kBK;
   p.vec4 = (p.Cg % 4 == 0 && C % 4 == 0) ? 1 : 0;
+  // taps4 needs each filter row's (fw, c) floats contiguous (groups == 1); a forced scalar variant
+  // (A/B tuning) keeps the scalar gather.
+  p.taps4 = (!p.vec4 && groups == 1 && F * C >= 4 && g_force[1] < 0) ? 1 : 0;
+  if (p.taps4) {
+    p.kdim = F * 4 * ((F * C + 3) / 4);
+    p.vec4 = 1;
+  }
+  p.kpad = (p.kdim + kBK - 1) / kBK * kBK;
   const long M = static_cast<long>(N) * p.Ho * p.Wo;
   const bool small = M * p.K < 256L * 128 * 128;  // fewer 128x128 tiles (all groups) than CUs
   if (p.Kg == 96 && !small)
-    p.variant = 1;
+    p.variant = p.vec4 ? 9 : 1;
   else if (small)
     p.variant = p.vec4 ? 2 : 3;
   else
@@ -306,6 +318,24 @@ void pack_conv_weights_host(const ConvPlan& p, const float* w_kcff, std::vector<
                             std::vector<int>& koff) {
   packed.assign(packed_weight_floats(p), 0.f);
   koff.assign(koff_ints(p), -1);
+  if (p.taps4) {
+    // filter row fh = L = F*C contiguous floats; unit u covers [start, start+4), the last unit
+    // shifted back to [L-4, L): floats already covered by unit U-2 keep a zero weight there.
+    const int L = p.F * p.C, U = (L + 3) / 4;
+    for (int fh = 0; fh < p.F; ++fh)
+      for (int u = 0; u < U; ++u)
+        for (int e = 0; e < 4; ++e) {
+          const int k = (fh * U + u) * 4 + e;
+          const int start = u < U - 1 ? 4 * u : L - 4;
+          const int f = start + e;
+          koff[k] = fh * p.Wp * p.C + f;
+          if (u == U - 1 && f < 4 * (U - 1)) continue;
+          const int fw = f / p.C, c = f % p.C;
+          for (int n = 0; n < p.Kg; ++n)
+            packed[static_cast<size_t>(n) * p.kpad + k] = w_kcff[((static_cast<size_t>(n) * p.C + c) * p.F + fh) * p.F + fw];
+        }
+    return;
+  }
   for (int g = 0; g < p.groups; ++g)
     for (int n = 0; n < p.Kg; ++n)
       for (int fh = 0; fh < p.F; ++fh)
@@ -371,6 +401,8 @@ hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, 
     case 6: conv_mfma_kernel<128, 96, 4, 1, false, 2><<<grid, kThreads, lds, s>>>(a); break;
     case 7: conv_mfma_kernel<256, 128, 2, 2, true, 1><<<grid, kThreads, lds, s>>>(a); break;
     case 8: conv_mfma_kernel<256, 96, 4, 1, false, 1><<<grid, kThreads, lds, s>>>(a); break;
+    case 9: conv_mfma_kernel<128, 96, 4, 1, true, 1><<<grid, kThreads, lds, s>>>(a); break;
+    case 10: conv_mfma_kernel<256, 96, 4, 1, true, 1><<<grid, kThreads, lds, s>>>(a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
