@@ -13,3 +13,8 @@ _spec = _ilu.spec_from_file_location("anx", _os.path.join(_dir, "__init__.py"), 
 _mod = _ilu.module_from_spec(_spec)
 _sys.modules["anx"] = _mod
 _spec.loader.exec_module(_mod)
+
+if __name__ == "__main__":  # ``python -m anx <command>`` from the repo root
+    from anx.__main__ import main as _main
+
+    _main()

@@ -21,6 +21,8 @@ struct OutViewB {
 struct ConvPlanB {
   int N, Hp, Wp, C, K, F, S, groups;
   int Ho, Wo, Cg, Kg, kdim, kpad, kpad_n, variant, vec8;
+  int taps8;  // C%8 != 0 (conv1): each filter row's F*C contiguous bf16 cut into 8-element units,
+              // the last shifted back to end at F*C (overlap zero-weighted) -> 16-B gathers
 };
 
 uint16_t f32_to_bf16_bits(float f);
@@ -28,9 +30,18 @@ ConvPlanB make_conv_plan_bf16(int N, int Hp, int Wp, int C, int K, int F, int S,
 size_t packed_weight_elems_bf16(const ConvPlanB& p);
 void pack_conv_weights_bf16(const ConvPlanB& p, const float* w_kcff, std::vector<uint16_t>& packed,
                             std::vector<int>& koff);
+// Split-K for the fully-connected layers (1x1 "convs" with M = batch): ksplit K slices write fp32
+// partial slabs [ksplit][M][K] to ws, splitk_reduce_bf16 sums them + bias (+ReLU) into the output.
+struct SplitK {
+  int ksplit = 1;
+  float* ws = nullptr;
+};
+int fc_split_k(const ConvPlanB& p);  // chosen slice count (1 = no split)
+hipError_t splitk_reduce_bf16(const float* ws, int ksplit, int M, int K, const float* bias, bool relu, OutViewB out,
+                              float* out_f32, hipStream_t s);
 // out_f32 != nullptr: write fp32 (contiguous [M][K]) instead of the bf16 view (final logits).
 hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, const int* koff, const float* bias,
-                       OutViewB out, float* out_f32, bool relu, hipStream_t s);
+                       OutViewB out, float* out_f32, bool relu, hipStream_t s, SplitK split = {});
 hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S, OutViewB out, hipStream_t s);
 hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
                             float beta, float k, LrnMode mode, OutViewB out, hipStream_t s);
@@ -74,6 +85,7 @@ class FullEngine {
   LrnMode lrn_;
   void *xb_ = nullptr, *c1_ = nullptr, *q2_ = nullptr, *c2_ = nullptr, *q3_ = nullptr, *q4_ = nullptr,
        *q5_ = nullptr, *c5_ = nullptr, *f6_ = nullptr, *f7_ = nullptr, *f8_ = nullptr;
+  float* ws_ = nullptr;  // split-K partial slabs of the FC layers (sized for every batch <= chunk_)
 };
 
 }  // namespace anx

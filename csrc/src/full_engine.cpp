@@ -73,13 +73,21 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
   check(hipMemset(q3_, 0, n * 15 * 15 * 256 * 2), "memset");
   check(hipMemset(q4_, 0, n * 15 * 15 * 384 * 2), "memset");
   check(hipMemset(q5_, 0, n * 15 * 15 * 384 * 2), "memset");
+  size_t ws = 0;  // largest split-K slab set over the FC layers and every batch the engine can see
+  for (int i = 5; i < 8; ++i)
+    for (int b = 1; b <= chunk_; ++b) {
+      const hip::ConvPlanB p = hip::make_conv_plan_bf16(b, 1, 1, L_[i].C, L_[i].K, 1, 1, 1);
+      const int ks = hip::fc_split_k(p);
+      if (ks > 1) ws = std::max(ws, static_cast<size_t>(ks) * b * L_[i].K);
+    }
+  if (ws) ws_ = static_cast<float*>(dalloc(ws * 4));
 }
 
 FullEngine::~FullEngine() {
   for (Layer& L : L_)
     for (void* p : {L.wp, static_cast<void*>(L.koff), static_cast<void*>(L.bias)})
       if (p) (void)hipFree(p);
-  for (void* p : {xb_, c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_})
+  for (void* p : {xb_, c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_, static_cast<void*>(ws_)})
     if (p) (void)hipFree(p);
 }
 
@@ -97,6 +105,11 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
     ANX_TRY(hipMemcpy(L.wp, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
     ANX_TRY(hipMemcpy(L.koff, ko.data(), ko.size() * 4, hipMemcpyHostToDevice));
     L.key = p.variant;
+  }
+  const int ks = hip::fc_split_k(p);
+  if (ks > 1) {  // FC layer at a small batch: K split over ~one workgroup per CU, then a reduce
+    ANX_TRY(hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s, hip::SplitK{ks, ws_}));
+    return hip::splitk_reduce_bf16(ws_, ks, N, L.K, L.bias, relu, out, out_f32, s);
   }
   return hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s);
 }

@@ -10,6 +10,7 @@
 // An FC layer is the 1x1 case: N images are N "pixels" of a 1x1 input with C = in_features.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <type_traits>
 #include <vector>
@@ -23,6 +24,8 @@ using bf16 = __bf16;
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+// taps8 gathers start at any bf16 (2-byte alignment); still one global_load_dwordx4 on gfx950.
+using u32x4u = __attribute__((ext_vector_type(4), aligned(2))) unsigned;
 
 constexpr int kThreads = 256;
 constexpr int kBK = 64;
@@ -36,10 +39,12 @@ struct ArgsB {
   void* out;
   int M, HoWo, Wo, Hp, Wp, C, S, Cg, Kg, kpad, kpad_n, ktiles;
   int Hb, Wb, Cb, h_off, w_off, c_off, relu, n_ntiles;
+  int kt_per;           // K tiles per blockIdx.y slice (split-K; = ktiles when not split)
+  size_t split_stride;  // output elements between split-K partial slabs
 };
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool VEC8, typename OutT>
-__global__ void __launch_bounds__(kThreads) conv_bf16_kernel(ArgsB a) {
+__global__ void __launch_bounds__(kThreads, VEC8 ? 3 : 2) conv_bf16_kernel(ArgsB a) {
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 32, TN = WN / 32;
   constexpr int A_UNITS = VEC8 ? kBK / 8 : kBK;  // per staged row
   constexpr int A_LOADS = BM * A_UNITS / kThreads;
@@ -50,6 +55,7 @@ __global__ void __launch_bounds__(kThreads) conv_bf16_kernel(ArgsB a) {
   bf16* As = lds_b;
   bf16* Bs = lds_b + BM * kLDA;
   int* koff_s = reinterpret_cast<int*>(lds_b + (BM + BN) * kLDA);
+  int* ooff_s = koff_s + a.kpad;  // output offset per tile row (-1 past M), from the prologue
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N, g = blockIdx.z;
@@ -63,12 +69,15 @@ __global__ void __launch_bounds__(kThreads) conv_bf16_kernel(ArgsB a) {
   unsigned ok = 0;
 #pragma unroll
   for (int j = 0; j < A_LOADS; ++j) {
-    const int m = m0 + tid / A_UNITS + j * A_STEP;
-    int o = 0;
+    const int row = tid / A_UNITS + j * A_STEP;
+    const int m = m0 + row;
+    int o = 0, oo = -1;
     if (m < a.M) {
       const int n = m / a.HoWo, r = m - n * a.HoWo, oy = r / a.Wo, ox = r - oy * a.Wo;
       o = ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
+      oo = ((n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off;
     }
+    if (au == 0) ooff_s[row] = oo;
     org[j] = o;
     ok |= (m < a.M ? 1u : 0u) << j;
   }
@@ -88,7 +97,7 @@ __global__ void __launch_bounds__(kThreads) conv_bf16_kernel(ArgsB a) {
 #pragma unroll
     for (int j = 0; j < A_LOADS; ++j) {
       if constexpr (VEC8)
-        ra[j] = *reinterpret_cast<const u32x4*>(x + org[j] + ko);
+        ra[j] = *reinterpret_cast<const u32x4u*>(x + org[j] + ko);
       else
         ra[j] = x[org[j] + ko];
     }
@@ -118,11 +127,14 @@ __global__ void __launch_bounds__(kThreads) conv_bf16_kernel(ArgsB a) {
   const int r = lane & 31, h = lane >> 5;
   const bf16* ard = As + (wm * WM + r) * kLDA + h * 8;
   const bf16* brd = Bs + (wn * WN + r) * kLDA + h * 8;
-  load(0);
-  store();
+  const int kt0 = blockIdx.y * a.kt_per, kt1 = min(a.ktiles, kt0 + a.kt_per);
+  if (kt0 < kt1) {
+    load(kt0);
+    store();
+  }
   __syncthreads();
-  for (int kt = 0; kt < a.ktiles; ++kt) {
-    if (kt + 1 < a.ktiles) load(kt + 1);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    if (kt + 1 < kt1) load(kt + 1);
 #pragma unroll
     for (int s = 0; s < kBK / 16; ++s) {
       bf16x8 af[TM], bfr[TN];
@@ -137,29 +149,32 @@ __global__ void __launch_bounds__(kThreads) conv_bf16_kernel(ArgsB a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
-    if (kt + 1 < a.ktiles) {
+    if (kt + 1 < kt1) {
       store();
       __syncthreads();
     }
   }
-  OutT* out = static_cast<OutT*>(a.out);
+  OutT* out = static_cast<OutT*>(a.out) + blockIdx.y * a.split_stride + g * a.Kg;
+  using i32x4 = __attribute__((ext_vector_type(4))) int;
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int f = n0 + wn * WN + j * 32 + r;
-    const bool fok = f < a.Kg;
-    const float bv = (fok && a.bias) ? a.bias[g * a.Kg + f] : 0.f;
+  for (int i = 0; i < TM; ++i) {
+    i32x4 oo[4];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int q = 0; q < 4; ++q) oo[q] = *reinterpret_cast<const i32x4*>(ooff_s + wm * WM + i * 32 + 8 * q + 4 * h);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int f = n0 + wn * WN + j * 32 + r;
+      if (f >= a.Kg) continue;
+      const float bv = a.bias ? a.bias[g * a.Kg + f] : 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (!fok || m >= a.M) continue;
-        const int n = m / a.HoWo, rr = m - n * a.HoWo, oy = rr / a.Wo, ox = rr - oy * a.Wo;
+        const int o = oo[e >> 2][e & 3];
+        if (o < 0) continue;
         float v = acc[i][j][e] + bv;
         if (a.relu) v = fmaxf(v, 0.f);
-        out[(static_cast<size_t>(n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off + g * a.Kg + f] =
-            static_cast<OutT>(v);
+        out[o + f] = static_cast<OutT>(v);
       }
+    }
   }
 }
 
@@ -191,42 +206,76 @@ __global__ void __launch_bounds__(256) pool_bf16_kernel(const bf16* __restrict__
   }
 }
 
+// One workgroup = PP output pixels x C channels; 8 channels per thread (16-B bf16 loads/stores).
+// Pass 1 pools into LDS as fp32, pass 2 applies LRN from LDS: own 8 channels by two ds_read_b128,
+// the +-2 neighbours by two ds_read_b64 (size-5 window), fp32 math, one bf16x8 store.
 __global__ void __launch_bounds__(256) pool_lrn_bf16_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
                                                             int F, int S, int Ho, int Wo, int PP, int size, float a,
                                                             float beta, float k, OutViewB o) {
-  extern __shared__ float pooled[];  // [PP][C]
+  using f32x4 = __attribute__((ext_vector_type(4))) float;
+  using f32x2 = __attribute__((ext_vector_type(2))) float;
+  extern __shared__ __attribute__((aligned(16))) float pooled[];  // [PP][C]
+  const int C8 = C / 8;
   const long P = static_cast<long>(N) * Ho * Wo, p0 = static_cast<long>(blockIdx.x) * PP;
-  for (int t = threadIdx.x; t < PP * C; t += blockDim.x) {
-    const int pl = t / C, c = t - pl * C;
+  for (int t = threadIdx.x; t < PP * C8; t += blockDim.x) {
+    const int pl = t / C8, c0 = (t - pl * C8) * 8;
     const long p = p0 + pl;
-    float m = 0.f;
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = p < P ? -INFINITY : 0.f;
     if (p < P) {
       const int ox = static_cast<int>(p % Wo);
       const long q = p / Wo;
       const int oy = static_cast<int>(q % Ho), n = static_cast<int>(q / Ho);
-      m = -INFINITY;
-      for (int fh = 0; fh < F; ++fh)
+      for (int fh = 0; fh < F; ++fh) {
+        const int iy = oy * S + fh;
+        if (iy >= H) break;
         for (int fw = 0; fw < F; ++fw) {
-          const int iy = oy * S + fh, ix = ox * S + fw;
-          if (iy < H && ix < W) m = fmaxf(m, static_cast<float>(x[((static_cast<size_t>(n) * H + iy) * W + ix) * C + c]));
+          const int ix = ox * S + fw;
+          if (ix >= W) break;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((static_cast<size_t>(n) * H + iy) * W + ix) * C + c0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], static_cast<float>(v[e]));
         }
+      }
     }
-    pooled[pl * C + c] = m;
+    *reinterpret_cast<f32x4*>(pooled + pl * C + c0) = f32x4{m[0], m[1], m[2], m[3]};
+    *reinterpret_cast<f32x4*>(pooled + pl * C + c0 + 4) = f32x4{m[4], m[5], m[6], m[7]};
   }
   __syncthreads();
   const int half = size / 2;
-  for (int t = threadIdx.x; t < PP * C; t += blockDim.x) {
-    const int pl = t / C, c = t - pl * C;
+  for (int t = threadIdx.x; t < PP * C8; t += blockDim.x) {
+    const int pl = t / C8, c0 = (t - pl * C8) * 8;
     const long p = p0 + pl;
     if (p >= P) continue;
-    float s = 0.f;
-    for (int j = c - half < 0 ? 0 : c - half; j <= (c + half >= C ? C - 1 : c + half); ++j)
-      s = fmaf(pooled[pl * C + j], pooled[pl * C + j], s);
+    const float* row = pooled + pl * C;
+    bf16x8 r;
+    if (half == 2) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(row + c0), hi = *reinterpret_cast<const f32x4*>(row + c0 + 4);
+      const f32x2 lf = c0 >= 2 ? *reinterpret_cast<const f32x2*>(row + c0 - 2) : f32x2{0.f, 0.f};
+      const f32x2 rt = c0 + 8 < C ? *reinterpret_cast<const f32x2*>(row + c0 + 8) : f32x2{0.f, 0.f};
+      const float w[12] = {lf.x, lf.y, lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, rt.x, rt.y};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int u = e; u < e + 5; ++u) s2 = fmaf(w[u], w[u], s2);
+        r[e] = static_cast<bf16>(w[e + 2] / powf(k + a * s2, beta));
+      }
+    } else {
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        float s2 = 0.f;
+        for (int j = c - half < 0 ? 0 : c - half; j <= (c + half >= C ? C - 1 : c + half); ++j)
+          s2 = fmaf(row[j], row[j], s2);
+        r[e] = static_cast<bf16>(row[c] / powf(k + a * s2, beta));
+      }
+    }
     const int ox = static_cast<int>(p % Wo);
     const long q = p / Wo;
     const int oy = static_cast<int>(q % Ho), n = static_cast<int>(q / Ho);
-    o.base[(static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb + o.c_off + c] =
-        static_cast<bf16>(pooled[pl * C + c] / powf(k + a * s, beta));
+    *reinterpret_cast<bf16x8*>(o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
+                               o.c_off + c0) = r;
   }
 }
 
@@ -240,7 +289,8 @@ struct VariantB {
   int BM, BN;
   bool vec8;
 };
-constexpr VariantB kVB[] = {{128, 128, true}, {128, 96, false}, {64, 64, true}, {64, 64, false}, {128, 128, false}};
+constexpr VariantB kVB[] = {{128, 128, true}, {128, 96, false}, {64, 64, true},
+                            {64, 64, false},  {128, 128, false}, {128, 96, true}};
 
 unsigned grid1d(long n) {
   long g = (n + 255) / 256;
@@ -264,11 +314,18 @@ ConvPlanB make_conv_plan_bf16(int N, int Hp, int Wp, int C, int K, int F, int S,
   p.Cg = C / groups;
   p.Kg = K / groups;
   p.kdim = F * F * p.Cg;
-  p.kpad = (p.kdim + kBK - 1) / kBK * kBK;
   p.vec8 = (p.Cg % 8 == 0 && C % 8 == 0) ? 1 : 0;
+  p.taps8 = (!p.vec8 && groups == 1 && F * C >= 8) ? 1 : 0;
+  if (p.taps8) {
+    p.kdim = F * 8 * ((F * C + 7) / 8);
+    p.vec8 = 1;
+  }
+  p.kpad = (p.kdim + kBK - 1) / kBK * kBK;
   const long M = static_cast<long>(N) * p.Ho * p.Wo;
   const bool small = M * K < 256L * 128 * 128;
-  if (p.Kg == 96 && !small && !p.vec8) p.variant = 1;
+  const bool fc = Hp == 1 && Wp == 1 && F == 1;  // fully-connected layer: 128x128 tiles + split-K
+  if (fc && p.vec8) p.variant = 0;
+  else if (p.Kg == 96 && !small) p.variant = p.vec8 ? 5 : 1;
   else if (small) p.variant = p.vec8 ? 2 : 3;
   else p.variant = p.vec8 ? 0 : 4;
   p.kpad_n = (p.Kg + kVB[p.variant].BN - 1) / kVB[p.variant].BN * kVB[p.variant].BN;
@@ -281,6 +338,21 @@ void pack_conv_weights_bf16(const ConvPlanB& p, const float* w_kcff, std::vector
                             std::vector<int>& koff) {
   packed.assign(packed_weight_elems_bf16(p), 0);
   koff.assign(p.kpad, -1);
+  if (p.taps8) {  // same unit scheme as the fp32 taps4 packing (conv_mfma.hip), 8 elements per unit
+    const int L = p.F * p.C, U = (L + 7) / 8;
+    for (int fh = 0; fh < p.F; ++fh)
+      for (int u = 0; u < U; ++u)
+        for (int e = 0; e < 8; ++e) {
+          const int k = (fh * U + u) * 8 + e;
+          const int f = (u < U - 1 ? 8 * u : L - 8) + e;
+          koff[k] = fh * p.Wp * p.C + f;
+          if (u == U - 1 && f < 8 * (U - 1)) continue;
+          for (int n = 0; n < p.Kg; ++n)
+            packed[static_cast<size_t>(n) * p.kpad + k] =
+                f32_to_bf16_bits(w_kcff[((static_cast<size_t>(n) * p.C + f % p.C) * p.F + fh) * p.F + f / p.C]);
+        }
+    return;
+  }
   for (int g = 0; g < p.groups; ++g)
     for (int n = 0; n < p.Kg; ++n)
       for (int fh = 0; fh < p.F; ++fh)
@@ -303,7 +375,7 @@ uint16_t f32_to_bf16_bits(float f) {  // round to nearest even, NaN kept NaN
 }
 
 hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, const int* koff, const float* bias,
-                       OutViewB out, float* out_f32, bool relu, hipStream_t s) {
+                       OutViewB out, float* out_f32, bool relu, hipStream_t s, SplitK split) {
   const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
   if (M == 0) return hipSuccess;
   if (static_cast<long>(p.N) * p.Hp * p.Wp * p.C >= (1L << 31)) return hipErrorInvalidValue;
@@ -334,8 +406,21 @@ hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, c
   a.c_off = out.c_off;
   a.relu = relu ? 1 : 0;
   a.n_ntiles = p.kpad_n / v.BN;
-  const dim3 grid(static_cast<unsigned>((M + v.BM - 1) / v.BM) * a.n_ntiles, 1, p.groups);
-  const size_t lds = static_cast<size_t>(v.BM + v.BN) * kLDA * 2 + static_cast<size_t>(p.kpad) * 4;
+  const int ksplit = std::max(1, split.ksplit);
+  a.kt_per = (a.ktiles + ksplit - 1) / ksplit;
+  if (ksplit > 1) {  // fp32 partial slabs [ksplit][M][Kg] in split.ws, no bias/ReLU (splitk_reduce_bf16)
+    if (p.groups != 1 || p.Ho != 1 || p.Wo != 1 || !split.ws) return hipErrorInvalidValue;
+    out_f32 = split.ws;
+    a.out = split.ws;
+    a.bias = nullptr;
+    a.relu = 0;
+    a.Hb = a.Wb = 1;
+    a.Cb = p.Kg;
+    a.h_off = a.w_off = a.c_off = 0;
+    a.split_stride = static_cast<size_t>(M) * p.Kg;
+  }
+  const dim3 grid(static_cast<unsigned>((M + v.BM - 1) / v.BM) * a.n_ntiles, ksplit, p.groups);
+  const size_t lds = static_cast<size_t>(v.BM + v.BN) * kLDA * 2 + static_cast<size_t>(p.kpad + v.BM) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
 #define ANX_LAUNCH(BM, BN, WMW, WNW, V8)                                                              \
   do {                                                                                                \
@@ -350,9 +435,55 @@ hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, c
     case 2: ANX_LAUNCH(64, 64, 2, 2, true); break;
     case 3: ANX_LAUNCH(64, 64, 2, 2, false); break;
     case 4: ANX_LAUNCH(128, 128, 2, 2, false); break;
+    case 5: ANX_LAUNCH(128, 96, 4, 1, true); break;
     default: return hipErrorInvalidValue;
   }
 #undef ANX_LAUNCH
+  return hipGetLastError();
+}
+
+namespace {
+// y[m][n] = act(sum_s ws[s][m][n] + bias[n]); 4 features per thread, bf16 (OutViewB) or fp32 out
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int ksplit, int M, int K,
+                                                            const float* __restrict__ bias, int relu, OutViewB o,
+                                                            float* __restrict__ out_f32) {
+  using f32x4 = __attribute__((ext_vector_type(4))) float;
+  const int K4 = K / 4;
+  const long total = static_cast<long>(M) * K4;
+  const size_t slab = static_cast<size_t>(M) * K;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int m = static_cast<int>(i / K4), n = static_cast<int>(i - static_cast<long>(m) * K4) * 4;
+    f32x4 v = bias ? *reinterpret_cast<const f32x4*>(bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < ksplit; ++s) v += *reinterpret_cast<const f32x4*>(ws + s * slab + static_cast<size_t>(m) * K + n);
+    if (relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+    if (out_f32) {
+      *reinterpret_cast<f32x4*>(out_f32 + static_cast<size_t>(m) * K + n) = v;
+    } else {
+      using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+      *reinterpret_cast<bf16x4*>(o.base + static_cast<size_t>(m) * o.Cb + o.c_off + n) =
+          bf16x4{static_cast<bf16>(v.x), static_cast<bf16>(v.y), static_cast<bf16>(v.z), static_cast<bf16>(v.w)};
+    }
+  }
+}
+}  // namespace
+
+int fc_split_k(const ConvPlanB& p) {
+  if (p.Ho != 1 || p.Wo != 1 || p.groups != 1 || p.Kg % 4) return 1;
+  const VariantB v = kVB[p.variant];
+  const long tiles = (static_cast<long>(p.N) + v.BM - 1) / v.BM * (p.kpad_n / v.BN);
+  const int ktiles = p.kpad / kBK;
+  // ~256 workgroups (one per CU) but at least 4 K tiles per slice (guide: projection GEMM at M=256)
+  const long want = (256 + tiles - 1) / tiles;
+  return static_cast<int>(std::max<long>(1, std::min<long>(want, ktiles / 4)));
+}
+
+hipError_t splitk_reduce_bf16(const float* ws, int ksplit, int M, int K, const float* bias, bool relu, OutViewB out,
+                              float* out_f32, hipStream_t s) {
+  if (K % 4 || (!out_f32 && (out.Cb % 4 || out.c_off % 4))) return hipErrorInvalidValue;
+  const long n = static_cast<long>(M) * (K / 4);
+  if (n == 0) return hipSuccess;
+  splitk_reduce_kernel<<<grid1d(n), 256, 0, s>>>(ws, ksplit, M, K, bias, relu ? 1 : 0, out, out_f32);
   return hipGetLastError();
 }
 
@@ -370,6 +501,7 @@ hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, in
   const int Ho = pool_out_dim(H, F, S), Wo = pool_out_dim(W, F, S);
   const long P = static_cast<long>(N) * Ho * Wo;
   if (P == 0) return hipSuccess;
+  if (C % 8 || out.Cb % 8 || out.c_off % 8 || C > 8192) return hipErrorInvalidValue;
   const int PP = C >= 4096 ? 1 : 4096 / C;
   const float a = mode == LrnMode::DivN ? alpha / size : alpha;
   pool_lrn_bf16_kernel<<<static_cast<unsigned>((P + PP - 1) / PP), 256, PP * C * 4, s>>>(

@@ -56,16 +56,8 @@ struct ConvArgs {
   int n_mtiles, n_ntiles;
 };
 
-__device__ __forceinline__ int pixel_origin(const ConvArgs& a, int m) {
-  const int n = m / a.HoWo;
-  const int r = m - n * a.HoWo;
-  const int oy = r / a.Wo;
-  const int ox = r - oy * a.Wo;
-  return ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
-}
-
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool VEC4, int NBUF>
-__global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
+__global__ void __launch_bounds__(kThreads, (BM * BN <= 128 * 96) ? 4 : 1) conv_mfma_kernel(ConvArgs a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves per workgroup");
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
@@ -87,6 +79,8 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
   float* As = lds;
   float* Bs = lds + BM * kLDA;
   int* koff_s = reinterpret_cast<int*>(lds + NBUF * kStage);
+  // output pixel offset of each of the BM rows (-1 past M), filled by the prologue's divisions
+  int* ooff_s = koff_s + a.kpad;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -111,8 +105,19 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
   unsigned a_ok = 0;
 #pragma unroll
   for (int j = 0; j < A_LOADS; ++j) {
-    const int m = m0 + tid / A_UNITS_PER_ROW + j * A_ROW_STEP;
-    a_org[j] = m < a.M ? pixel_origin(a, m) : 0;
+    const int row = tid / A_UNITS_PER_ROW + j * A_ROW_STEP;
+    const int m = m0 + row;
+    int oo = -1;
+    a_org[j] = 0;
+    if (m < a.M) {
+      const int n = m / a.HoWo;
+      const int rr = m - n * a.HoWo;
+      const int oy = rr / a.Wo;
+      const int ox = rr - oy * a.Wo;
+      a_org[j] = ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
+      oo = ((n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off;
+    }
+    if (tid % A_UNITS_PER_ROW == 0) ooff_s[row] = oo;
     a_ok |= (m < a.M ? 1u : 0u) << j;
   }
   __syncthreads();  // koff_s visible
@@ -216,26 +221,27 @@ __global__ void __launch_bounds__(kThreads) conv_mfma_kernel(ConvArgs a) {
     }
   }
 
-  // Epilogue: D row (pixel) = (reg&3) + 8*(reg>>2) + 4*h ; D col (filter) = lane&31.
+  // Epilogue: D row (pixel) = (reg&3) + 8*(reg>>2) + 4*h ; D col (filter) = lane&31. The row ->
+  // output offset map comes from LDS (4 consecutive rows per ds_read_b128), no divisions here.
+  using i32x4 = __attribute__((ext_vector_type(4))) int;
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int f = n0 + wn * WN + j * 32 + r;
-    const bool fok = f < a.Kg;
-    const float bv = (fok && a.bias) ? a.bias[g * a.Kg + f] : 0.f;
+  for (int i = 0; i < TM; ++i) {
+    i32x4 oo[4];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int q = 0; q < 4; ++q) oo[q] = *reinterpret_cast<const i32x4*>(ooff_s + wm * WM + i * 32 + 8 * q + 4 * h);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int f = n0 + wn * WN + j * 32 + r;
+      if (f >= a.Kg) continue;
+      const float bv = a.bias ? a.bias[g * a.Kg + f] : 0.f;
+      float* dst = a.out + g * a.Kg + f;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const int m = m0 + wm * WM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (!fok || m >= a.M) continue;
-        const int n = m / a.HoWo;
-        const int rr = m - n * a.HoWo;
-        const int oy = rr / a.Wo;
-        const int ox = rr - oy * a.Wo;
+        const int o = oo[reg >> 2][reg & 3];
+        if (o < 0) continue;
         float v = acc[i][j][reg] + bv;
         if (a.relu) v = fmaxf(v, 0.f);
-        a.out[(static_cast<size_t>(n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off + g * a.Kg + f] =
-            v;
+        dst[o] = v;
       }
     }
   }
@@ -389,7 +395,7 @@ hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, 
   a.n_ntiles = p.kpad_n / v.BN;
   dim3 grid(a.n_mtiles * a.n_ntiles, 1, p.groups);
   const size_t lds = static_cast<size_t>(v.nbuf) * (v.BM + v.BN) * kLDA * sizeof(float) +
-                     static_cast<size_t>(p.kpad) * sizeof(int);
+                     static_cast<size_t>(p.kpad + v.BM) * sizeof(int);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   switch (p.variant) {
     case 0: conv_mfma_kernel<128, 128, 2, 2, true, 1><<<grid, kThreads, lds, s>>>(a); break;

@@ -91,15 +91,35 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __re
     const long p = p0 + pl;
     if (p >= P) continue;
     const float* row = pooled + pl * C;
+    const int c0 = c4 * 4;
     f32x4 out;
+    if (half == 2) {
+      // AlexNet's size-5 window: one ds_read_b128 for the own 4 channels and two ds_read_b64 for
+      // the 2 neighbours on each side (lane-contiguous, conflict-free; 20 strided ds_read_b32
+      // per thread were 4-way bank conflicted). Channels outside [0, C) contribute fmaf(0,0,s)
+      // = s, so the sums are bitwise those of the clamped loop below.
+      using f32x2 = __attribute__((ext_vector_type(2))) float;
+      const f32x4 own = *reinterpret_cast<const f32x4*>(row + c0);
+      const f32x2 lft = c0 >= 2 ? *reinterpret_cast<const f32x2*>(row + c0 - 2) : f32x2{0.f, 0.f};
+      const f32x2 rgt = c0 + 4 < C ? *reinterpret_cast<const f32x2*>(row + c0 + 4) : f32x2{0.f, 0.f};
+      const float w[8] = {lft.x, lft.y, own.x, own.y, own.z, own.w, rgt.x, rgt.y};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = c4 * 4 + e;
-      const int lo = c - half < 0 ? 0 : c - half;
-      const int hi = c + half >= C ? C - 1 : c + half;
-      float s = 0.f;
-      for (int j = lo; j <= hi; ++j) s = fmaf(row[j], row[j], s);
-      out[e] = row[c] / powf(k + a * s, beta);
+      for (int e = 0; e < 4; ++e) {
+        float s = 0.f;
+#pragma unroll
+        for (int t = e; t < e + 5; ++t) s = fmaf(w[t], w[t], s);
+        out[e] = w[e + 2] / powf(k + a * s, beta);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = c0 + e;
+        const int lo = c - half < 0 ? 0 : c - half;
+        const int hi = c + half >= C ? C - 1 : c + half;
+        float s = 0.f;
+        for (int j = lo; j <= hi; ++j) s = fmaf(row[j], row[j], s);
+        out[e] = row[c] / powf(k + a * s, beta);
+      }
     }
     *reinterpret_cast<f32x4*>(y + p * C + c4 * 4) = out;
   }
