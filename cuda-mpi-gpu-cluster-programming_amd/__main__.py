@@ -23,7 +23,8 @@ def _run_args(ap):
     ap.add_argument("--lrn-alpha-mode", default=None, choices=["div_n", "raw"])
     ap.add_argument("--groups", type=int, default=1, choices=[1, 2], help="Conv2 groups (2 = AlexNet paper)")
     ap.add_argument("--decomp", default=None, choices=["overlap", "per_layer"])
-    ap.add_argument("--strategy", default="rows", choices=["rows", "batch"])
+    ap.add_argument("--strategy", default="rows", choices=["rows", "batch", "filter"],
+                    help="multi-rank split: rows (spatial + halos), batch (images), filter (Conv2 filters, P7)")
     ap.add_argument("--iters", type=int, default=0, help="warm iterations after the cold run")
     ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
     ap.add_argument("--conv2-algo", default="auto", choices=["auto", "direct", "winograd"])

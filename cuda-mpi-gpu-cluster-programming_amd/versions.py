@@ -32,6 +32,7 @@ from .config import blocks_dims, flops_per_image
 from .parallel import comm
 from .parallel.plan import OVERLAP, PER_LAYER
 from .parallel.strategies import batch_forward, replicate_forward, rows_forward
+from .parallel.tensor import filter_parallel_forward
 from .utils.init import init_input, init_weights
 from .utils.timer import PhaseTimer
 
@@ -47,7 +48,7 @@ class RunConfig:
     lrn_mode: str | None = None   # default: div_n for v1/v2.x, raw for v3..v5 (reference parity, D1)
     groups2: int = 1
     decomp: str | None = None     # overlap | per_layer (default: overlap, per_layer for v5)
-    strategy: str = "rows"        # rows | batch (multi-rank versions)
+    strategy: str = "rows"        # rows | batch | filter (multi-rank versions)
     iters: int = 0                # warm iterations after the cold run
     impl: str = "mfma"
     check: bool = False
@@ -136,10 +137,12 @@ def run(cfg: RunConfig) -> RunResult | None:
         set_conv2_algo(cfg.conv2_algo)
         model = AlexNetBlocks(w, specs=(b1, b2), device=device, impl=cfg.impl, max_batch=cfg.batch)
         x = init_input(cfg.batch, cfg.init, cfg.seed) if rank == 0 else None
-        if cfg.version == "v2.1":
-            # broadcast-all: every rank receives the whole input (M3, main.cpp:71)
+        if cfg.version == "v2.1" or (cfg.strategy == "filter" and cfg.version in ("v2.2", "v4", "v5")):
+            # broadcast-all: every rank receives the whole input (M3, main.cpp:71); the filter
+            # (tensor-parallel) strategy also replicates Block 1 and needs the whole input
             xb = x if rank == 0 else torch.empty(cfg.batch, d.H, d.W, d.C0)
             if ws > 1:
+                xb = xb.to(device) if backend == "nccl" else xb  # RCCL broadcasts device memory
                 dist.broadcast(xb, 0)
             x = xb
         if x is not None:
@@ -158,6 +161,10 @@ def run(cfg: RunConfig) -> RunResult | None:
             return y if rank == 0 else None
         if cfg.strategy == "batch":
             return batch_forward(model, x, cfg.batch, comm_device=comm_dev, timer=tm)
+        if cfg.strategy == "filter":
+            with tm.phase("compute"):
+                return filter_parallel_forward(x.to(device), model.weights, b1, b2, gather="root",
+                                               comm_device=comm_dev)
         return rows_forward(model, x, cfg.batch, decomp=cfg.decomp, comm_device=comm_dev, timer=tm)
 
     if ws > 1:

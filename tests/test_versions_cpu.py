@@ -57,3 +57,12 @@ def test_gpu_versions_cpu_rehearsal(serial, version, extra):
                         "--seed", "3", "--batch", "2", *extra], 3)
     assert "Final Output Shape: 13x13x256" in out
     assert rec["checksum"] == serial["checksum"]
+
+
+@pytest.mark.parametrize("np_", [2, 4])
+def test_v22_filter_parallel(serial, np_):
+    """P7: Conv2 filters split over CPU ranks with an LRN channel halo == the serial V1 output."""
+    rec, _ = run_cli(["--version", "v2.2", "--strategy", "filter", "--init", "rand", "--seed", "3", "--batch", "2"],
+                     np_)
+    assert rec["shape"] == [13, 13, 256]
+    assert rec["checksum"] == serial["checksum"]

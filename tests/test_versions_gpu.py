@@ -32,3 +32,10 @@ def test_v4_two_ranks_one_gpu(cuda, extra):
 def test_v5_single_rank(cuda):
     rec, _ = run_cli(["--version", "v5", "--init", "rand", "--check", "--batch", "4"])
     assert rec["max_abs_err"] < 1e-3
+
+
+def test_v4_filter_parallel_two_ranks_one_gpu(cuda):
+    """P7 filter split on GPU ranks (host-staged channel halo + gather) vs the fp64 oracle."""
+    rec, out = run_cli(["--version", "v4", "--strategy", "filter", "--init", "rand", "--check", "--batch", "3"], 2)
+    assert "Final Output Shape: 13x13x256" in out
+    assert rec["max_abs_err"] < 1e-3
