@@ -88,12 +88,13 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
   c2_ = dev_alloc<float>(static_cast<size_t>(chunk_) * d_.H2 * d_.W2 * d_.C2);
   if (impl == Impl::Mfma && hip::wino_eligible(b2.conv.F, b2.conv.S, d_.C1, d_.C2, b2.conv.groups)) {
     // Winograd workspaces for a full-height window of chunk_ images (row tiles need less).
-    const hip::WinoPlan w = hip::make_wino_plan(chunk_, d_.Hp1 + 2 * b2.conv.P, wq_, d_.C1, d_.C2, b2.conv.groups);
-    if (hip::wino_m_floats(w) < (1UL << 31)) {
-      wv_cap_ = hip::wino_v_floats(w);
-      wm_cap_ = hip::wino_m_floats(w);
+    // The M buffer (49 x K per tile: 520 MB at 128 images) only exists for the unfused A/B path and
+    // is allocated on its first use; the default fused kernel never materialises M.
+    const hip::WinoPlan wp = hip::make_wino_plan(chunk_, d_.Hp1 + 2 * b2.conv.P, wq_, d_.C1, d_.C2, b2.conv.groups);
+    if (hip::wino_m_floats(wp) < (1UL << 31)) {
+      wv_cap_ = hip::wino_v_floats(wp);
+      wm_cap_ = hip::wino_m_floats(wp);
       wv_ = dev_alloc<float>(wv_cap_);
-      wm_ = dev_alloc<float>(wm_cap_);
     }
   }
 }
@@ -185,6 +186,7 @@ hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t 
       }
       ANX_TRY(hip::wino_input(w, qc, wv_, s));
       if (g_conv2_algo == ConvAlgo::WinogradUnfused) {
+        if (!wm_) ANX_TRY(hipMalloc(reinterpret_cast<void**>(&wm_), wm_cap_ * sizeof(float)));
         ANX_TRY(hip::conv2d_mfma(w.gemm, wv_, u2p_, ukoff_, nullptr,
                                  hip::OutView{wm_, 1, 1, w.gemm.K, 0, 0, 0}, false, s));
         ANX_TRY(hip::wino_output(w, wm_, b2d_, c2_, true, s));

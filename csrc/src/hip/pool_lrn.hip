@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __re
       for (int e = 0; e < 4; ++e) {
         float s = 0.f;
 #pragma unroll
-        for (int t = e; t < e + 5; ++t) s = fmaf(w[t], w[t], s);
+        for (int u = e; u < e + 5; ++u) s = fmaf(w[u], w[u], s);
         out[e] = w[e + 2] / powf(k + a * s, beta);
       }
     } else {

@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(kT) wino_out_kernel(const float* __restrict__ 
 // outputs: Y[i][j] += A^T[i][a] A^T[j][b] M_ab. M never touches memory (it was 520 MB per 128
 // images as a separate GEMM output), and bias + ReLU + the NHWC store happen once at the end.
 // Per lane: 16 (tile, filter) pairs x 9 outputs = 144 Y registers + 16 accumulators.
-constexpr int kFBK = 32, kFLDA = kFBK + 4, kFB = 64;
+constexpr int kFB = 64;  // tiles x filters per fused workgroup
 
 struct FusedArgs {
   const float* V;      // [P][49][C]
