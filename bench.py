@@ -2,12 +2,17 @@
 """Headline benchmark: AlexNet Blocks 1-2 fp32 inference throughput (images/s) on N MI355X.
 
 Metric/config from BASELINE.json: "images/sec (and ms/batch) AlexNet Blocks1-2 fp32 at 1/2/4/8
-MI355X". One step = the reference's V4/V5 pipeline at batch scale: rank 0 owns the global batch
-(device resident), scatters each rank's images over RCCL/xGMI, every rank runs the native
-Blocks 1-2 engine (MFMA implicit-GEMM convs + fused epilogues) on its shard, and the outputs are
-gathered back to rank 0. RCCL runs on its own stream, compute on the current stream, and the
-scatter of step k+1 runs while step k computes (double-buffered inputs, --no-prefetch to serialise);
---micro splits each step into micro-batches. Weak scaling: --batch-per-gpu images per GPU.
+MI355X". One step = every rank runs the native Blocks 1-2 engine (polyphase-Winograd Conv1 and Winograd
+Conv2 on f32 MFMA, fused epilogues, pool/LRN kernels) on its own shard of the batch and the outputs
+are gathered to rank 0 over RCCL/xGMI (overlapped with the next step's compute). Data-parallel weak
+scaling: --batch-per-gpu images per GPU, generated on each rank (--input-source local, the default).
+--input-source root reproduces the reference's V4/V5 data flow instead: rank 0 owns the whole batch
+and scatters it every step (prefetched one step ahead); that moves 79 MB per peer per 128 images
+over xGMI, which binds before the compute does, so it is not the throughput configuration.
+
+The default 300 images per GPU is chosen for wave quantization, not memory: both Winograd GEMMs
+then launch whole numbers of 512-workgroup waves (1520 and 2544 workgroups), where 128 images leave
+a 27 % / 30 % tail round (tools/sweep_batch.py: 128 -> 173k, 300 -> 206k images/s).
 
 Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
 bench.py --gpus N``. Rank 0 prints ONE JSON line.
@@ -39,15 +44,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch-per-gpu", type=int, default=128)
-    # With cross-step prefetch the whole per-rank batch is one launch (128-image launches run the conv
-    # kernels ~4% faster than 2 x 64, tools/sweep_batch.py); without it, --micro 2 overlaps the second
-    # half's scatter with the first half's compute.
+    ap.add_argument("--batch-per-gpu", type=int, default=300)
+    # The whole per-rank batch is one launch (fewer, larger launches fill the 256 CUs better); with
+    # --no-prefetch, --micro 2 overlaps the second half's scatter with the first half's compute.
     ap.add_argument("--micro", type=int, default=1, help="micro-batches per step for scatter/compute/gather overlap")
     ap.add_argument("--no-prefetch", action="store_true", help="scatter each step's input inside that step only")
     ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
-    ap.add_argument("--input-source", default="root", choices=["root", "local"],
-                    help="root: rank 0 scatters the batch (reference V4/V5 semantics); local: per-rank synthetic")
+    ap.add_argument("--input-source", default="local", choices=["root", "local"],
+                    help="local: per-rank synthetic shard (data-parallel); root: rank 0 scatters the batch (V4/V5)")
     ap.add_argument("--no-gather", action="store_true", help="leave outputs on their ranks")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu = gloo rehearsal (tests only)")
     ap.add_argument("--model", default="blocks", choices=["blocks", "full"],
@@ -88,8 +92,9 @@ def main():
     g.manual_seed(1234 + rank)
     if pipe.x_global is not None:
         pipe.x_global.copy_(torch.rand(pipe.x_global.shape, device=dev, generator=g) * 0.1)
-    else:
-        pipe.x.copy_(torch.rand(pipe.x.shape, device=dev, generator=g) * 0.1)
+    else:  # every input buffer of the (double-buffered) pipeline holds real images
+        for xb in pipe._xb:
+            xb.copy_(torch.rand(xb.shape, device=dev, generator=g) * 0.1)
     step = pipe.step
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
 
@@ -137,15 +142,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(imgs / BASELINE_IMG_PER_S, 2),
             "dtype": "fp32",
-            "data": "synthetic (U[0,0.1) images 227x227x3, random-init weights)",
+            "data": ("synthetic (U[0,0.1) images 227x227x3 generated on %s, random-init weights)"
+                     % ("each rank" if a.input_source == "local" else "rank 0, scattered")),
             "config": {
                 "model": "AlexNet Blocks1-2 (Conv1 11x11s4-ReLU-Pool3s2-Conv2 5x5p2-ReLU-Pool3s2-LRN5)",
                 "global_batch": B * world,
                 "seq_len": None,
                 "image": [d.H, d.W, d.C0],
                 "parallelism": f"dp{world}",
-                "pipeline": ("root scatter -> compute -> gather (RCCL), %d micro-batches%s"
-                             % (len(pipe.splits), ", next-step scatter overlapped" if pipe.prefetch else ""))
+                "pipeline": (("root scatter -> compute -> gather (RCCL), %d micro-batches%s"
+                              % (len(pipe.splits), ", next-step scatter overlapped" if pipe.prefetch else ""))
+                             if a.input_source == "root" else
+                             "per-rank data -> compute -> gather to rank 0 (RCCL, overlapped with the next step)")
                 if world > 1 else "single GPU",
                 "input_source": a.input_source,
                 "impl": a.impl,

@@ -97,7 +97,18 @@ int anx_conv_force_variant(int kind, int id);
 /* Conv2 (5x5 s1) algorithm on the MFMA path: 0 auto (Winograd F(3,5) when eligible), 1 direct, 2 Winograd */
 int anx_set_conv2_algo(int algo);
 int anx_get_conv2_algo(void);
-/* fused Winograd kernel tuning: bit0 K-slice 48, bit1 XCD-aware order (default 3) */
+/* Conv1 (11x11 s4) algorithm on the MFMA path: 0 auto (polyphase Winograd F(3,3) when eligible), 1 direct, 2 Winograd */
+int anx_set_conv1_algo(int algo);
+int anx_get_conv1_algo(void);
+/* conv1 Winograd GEMM ring: 0 BK48 x 2 slots, 1 BK16 x 4, 2 BK16 x 6, 3 BK16 x 8 */
+int anx_conv1_wino_cfg(int cfg);
+/* profiling probes (wrong results): bit0 skip the output-transform fold, bit1 skip LDS-DMA refills */
+int anx_conv1_wino_probe(int bits);
+/* Conv1 by polyphase Winograd on device buffers (test entry; allocates and frees its workspaces,
+   synchronises `stream`): x [N,Hin,W,3], KCFF weights on the HOST, y [N,H1,W1,K]. */
+int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, int K, int F, const float* bias,
+                   float* y, int relu, void* stream);
+/* fused Winograd kernel tuning: bit0 K-slice 48 (else 32), bit1 XCD-aware order, bit2 LDS-DMA ring (default 7) */
 int anx_wino_fused_cfg(int cfg);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);

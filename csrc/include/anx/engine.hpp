@@ -29,6 +29,11 @@ enum class Impl : int {
 enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2, WinogradUnfused = 3 };
 void set_conv2_algo(ConvAlgo a);
 ConvAlgo conv2_algo();
+// Algorithm for Conv1 (stride 4, C = 3) on the Mfma path: Auto / Winograd = polyphase Winograd
+// F(3x3,3x3) (conv1_wino.hip) when eligible, Direct = the implicit-GEMM kernel (bit-identical across
+// row decompositions; Winograd tile origins move with the row split, ~1e-7 relative).
+void set_conv1_algo(ConvAlgo a);
+ConvAlgo conv1_algo();
 
 struct HostWeights {
   std::vector<float> w1, b1, w2, b2;  // KCFF weights, biases
@@ -93,6 +98,9 @@ class BlocksEngine {
   float *u2p_ = nullptr, *wv_ = nullptr, *wm_ = nullptr;
   int* ukoff_ = nullptr;
   int wino_key_ = -1;
+  // Winograd conv1: transformed polyphase weights + V workspace (full-height tiles of chunk_ images)
+  float *u1w_ = nullptr, *wv1_ = nullptr;
+  size_t wv1_cap_ = 0;
   size_t wv_cap_ = 0, wm_cap_ = 0;
   std::vector<float> w1h_, w2h_;  // KCFF host copies for re-packing on geometry change
 };

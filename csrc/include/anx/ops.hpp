@@ -99,11 +99,32 @@ size_t wino_m_floats(const WinoPlan& w);
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s);
 hipError_t wino_output(const WinoPlan& w, const float* Mt, const float* bias, float* y, bool relu, hipStream_t s);
-// Tuning (A/B): bit0 = K-slice 48 instead of 32, bit1 = XCD-aware block order. Default 1 (measured: BK 48 +5%, XCD order +-0).
+// Tuning (A/B): bit0 = K-slice 48 instead of 32, bit1 = XCD-aware block order, bit2 = LDS-DMA ring.
+// Default 7 (measured at 300 images: ring +17 %, BK 48 +3 %, XCD order +1 %).
 int wino_set_fused_cfg(int cfg);
 // Batched GEMM + output transform in one kernel (M stays in registers); U packed as for w.gemm.
 hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
                       hipStream_t s);
+
+// Conv1 (stride 4, C = 3, 8 < F <= 12, no padding) as Winograd F(3x3,3x3) on the polyphase image
+// (conv1_wino.hip): 48 polyphase channels, 3x3 output tiles, 25 transform points.
+struct Conv1WinoPlan {
+  int N, Hin, W, K, F;
+  int H1, W1, ty, tx, P;  // output dims, 3x3 tiles per column/row, total tiles
+};
+bool conv1_wino_eligible(int C, int K, int F, int S, int P, int groups);
+Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F);
+size_t conv1_wino_v_floats(const Conv1WinoPlan& w);  // V workspace [P][25][48]
+size_t conv1_wino_u_floats(int K);                   // transformed weights [25][K][48]
+void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u);
+// Tuning (A/B): ring shape 0..3 (conv1_wino.hip default_cfg). -1 on a bad id.
+int conv1_wino_set_cfg(int cfg);
+// Cost probes for profiling only (results become wrong): bit0 skip the output-transform fold,
+// bit1 skip the LDS-DMA refills. 0 = normal.
+int conv1_wino_set_probe(int bits);
+// x: [N, Hin, W, 3] image rows; writes conv1 (+bias, optional ReLU) through `out`.
+hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
+                      bool relu, hipStream_t s);
 
 // Vectorised NHWC max-pool writing through an OutView (C % 4 == 0 required for the fast path).
 hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, OutView out, hipStream_t s);

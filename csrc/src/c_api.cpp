@@ -5,6 +5,8 @@
 #include <cstring>
 #include <exception>
 #include <string>
+#include <vector>
+#include <algorithm>
 
 #include "anx/bf16_ops.hpp"
 #include "anx/cpu_engine.hpp"
@@ -363,14 +365,49 @@ int anx_set_conv2_algo(int algo) {
   return 0;
 }
 int anx_get_conv2_algo(void) { return static_cast<int>(anx::conv2_algo()); }
+int anx_set_conv1_algo(int algo) {
+  if (algo < 0 || algo > 2) return fail("conv1 algo must be 0 (auto), 1 (direct) or 2 (winograd)");
+  anx::set_conv1_algo(static_cast<anx::ConvAlgo>(algo));
+  return 0;
+}
+int anx_get_conv1_algo(void) { return static_cast<int>(anx::conv1_algo()); }
+int anx_conv1_wino_probe(int bits) { return anx::hip::conv1_wino_set_probe(bits); }
+int anx_conv1_wino_cfg(int cfg) {
+  if (anx::hip::conv1_wino_set_cfg(cfg) != 0) return fail("conv1 winograd cfg must be 0..3");
+  return 0;
+}
 int anx_wino_fused_cfg(int cfg) {
-  if (anx::hip::wino_set_fused_cfg(cfg) != 0) return fail("fused cfg must be 0..3");
+  if (anx::hip::wino_set_fused_cfg(cfg) != 0) return fail("fused cfg must be 0..7");
   return 0;
 }
 
 int anx_conv_force_variant(int kind, int id) {
   if (anx::hip::conv_force_variant(kind, id) != 0) return fail("invalid conv variant");
   return 0;
+}
+
+int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, int K, int F, const float* bias,
+                   float* y, int relu, void* stream) {
+  return guarded("anx_conv1_wino", [&] {
+    if (!anx::hip::conv1_wino_eligible(3, K, F, 4, 0, 1)) return fail("anx_conv1_wino: shape not eligible");
+    const auto w = anx::hip::make_conv1_wino_plan(N, Hin, W, K, F);
+    std::vector<float> u;
+    anx::hip::conv1_wino_weights_host(K, F, w_kcff, u);
+    float *dv = nullptr, *du = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&dv), std::max<size_t>(anx::hip::conv1_wino_v_floats(w), 1) * 4) != hipSuccess)
+      return fail("anx_conv1_wino: hipMalloc");
+    if (hipMalloc(reinterpret_cast<void**>(&du), u.size() * 4) != hipSuccess) {
+      (void)hipFree(dv);
+      return fail("anx_conv1_wino: hipMalloc");
+    }
+    hipError_t e = hipMemcpy(du, u.data(), u.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = anx::hip::conv1_wino(w, x, dv, du, bias, anx::hip::OutView{y, w.H1, w.W1, K, 0, 0, 0}, relu != 0, S(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(S(stream));  // the workspaces are freed below
+    (void)hipFree(dv);
+    (void)hipFree(du);
+    return hip_status(e, "conv1_wino");
+  });
 }
 
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,

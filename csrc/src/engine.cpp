@@ -37,9 +37,12 @@ T* dev_upload(const std::vector<T>& h) {
 
 namespace {
 ConvAlgo g_conv2_algo = ConvAlgo::Auto;
-}
+ConvAlgo g_conv1_algo = ConvAlgo::Auto;
+}  // namespace
 void set_conv2_algo(ConvAlgo a) { g_conv2_algo = a; }
 ConvAlgo conv2_algo() { return g_conv2_algo; }
+void set_conv1_algo(ConvAlgo a) { g_conv1_algo = a; }
+ConvAlgo conv1_algo() { return g_conv1_algo; }
 
 void init_const(HostWeights& w, const BlockSpec& b1, const BlockSpec& b2, float wv, float bv) {
   const ConvSpec &c1 = b1.conv, &c2 = b2.conv;
@@ -73,7 +76,9 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
       {static_cast<size_t>(H) * W * d_.C0, static_cast<size_t>(d_.H1) * d_.W1 * d_.C1,
        static_cast<size_t>(d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1, static_cast<size_t>(d_.H2) * d_.W2 * d_.C2,
        // Winograd M buffer: 49 transform points x K per 3x3 output tile
-       static_cast<size_t>((d_.H2 + 2) / 3) * ((d_.W2 + 2) / 3) * 49 * d_.C2});
+       static_cast<size_t>((d_.H2 + 2) / 3) * ((d_.W2 + 2) / 3) * 49 * d_.C2,
+       // Winograd conv1 V buffer: 25 points x 48 polyphase channels per 3x3 output tile
+       static_cast<size_t>((d_.H1 + 2) / 3) * ((d_.W1 + 2) / 3) * 25 * 48});
   chunk_ = static_cast<int>(std::min<size_t>(max_batch, ((1UL << 31) - 1) / per_img));
   if (chunk_ < 1) throw std::invalid_argument("image too large for 32-bit kernel indexing");
   w1h_ = w.w1;
@@ -86,6 +91,15 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
   q2_cap_ = static_cast<size_t>(max_batch) * (d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1;
   q2_ = dev_alloc<float>(q2_cap_);
   c2_ = dev_alloc<float>(static_cast<size_t>(chunk_) * d_.H2 * d_.W2 * d_.C2);
+  const ConvSpec& k1 = b1.conv;
+  if (impl == Impl::Mfma && hip::conv1_wino_eligible(k1.C, k1.K, k1.F, k1.S, k1.P, k1.groups)) {
+    const hip::Conv1WinoPlan wp = hip::make_conv1_wino_plan(chunk_, H, W, k1.K, k1.F);
+    std::vector<float> u;
+    hip::conv1_wino_weights_host(k1.K, k1.F, w.w1.data(), u);
+    u1w_ = dev_upload(u);
+    wv1_cap_ = hip::conv1_wino_v_floats(wp);
+    wv1_ = dev_alloc<float>(wv1_cap_);
+  }
   if (impl == Impl::Mfma && hip::wino_eligible(b2.conv.F, b2.conv.S, d_.C1, d_.C2, b2.conv.groups)) {
     // Winograd workspaces for a full-height window of chunk_ images (row tiles need less).
     // The M buffer (49 x K per tile: 520 MB at 128 images) only exists for the unfused A/B path and
@@ -104,7 +118,8 @@ BlocksEngine::~BlocksEngine() {
                   static_cast<void*>(b2d_), static_cast<void*>(w1p_), static_cast<void*>(w2p_),
                   static_cast<void*>(koff1_), static_cast<void*>(koff2_), static_cast<void*>(c1_),
                   static_cast<void*>(q2_), static_cast<void*>(c2_), static_cast<void*>(u2p_),
-                  static_cast<void*>(ukoff_), static_cast<void*>(wv_), static_cast<void*>(wm_)})
+                  static_cast<void*>(ukoff_), static_cast<void*>(wv_), static_cast<void*>(wm_),
+                  static_cast<void*>(u1w_), static_cast<void*>(wv1_)})
     if (p) (void)hipFree(p);
 }
 
@@ -134,7 +149,12 @@ hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStr
     const int n = std::min(chunk_, N - n0);
     const float* xc = x + n0 * in_img;
     float* qc = q2_ + n0 * q_img;
-    if (impl_ == Impl::Mfma) {
+    if (impl_ == Impl::Mfma && wv1_ != nullptr && g_conv1_algo != ConvAlgo::Direct) {
+      const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
+      if (hip::conv1_wino_v_floats(w) > wv1_cap_) return hipErrorInvalidValue;
+      ANX_TRY(hip::conv1_wino(w, xc, wv1_, u1w_, b1d_, hip::OutView{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0}, true,
+                              s));
+    } else if (impl_ == Impl::Mfma) {
       const hip::ConvPlan p = hip::make_conv_plan(n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, k1.groups);
       const int key = p.variant;
       if (key != plan_key1_) {

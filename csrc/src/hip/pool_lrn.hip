@@ -8,6 +8,7 @@
 // lands directly inside conv2's zero-bordered input buffer (no pad kernel, no copy).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "anx/ops.hpp"
@@ -20,6 +21,41 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 __device__ __forceinline__ f32x4 max4(f32x4 a, f32x4 b) {
   return f32x4{fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)};
+}
+
+// Max of an F x F window of float4 channel groups; `p` points at the window origin. For unpadded
+// pooling every window of a valid output lies inside the input ((Ho-1)*S + F <= H), so the fixed-F
+// path needs no bounds checks and issues all F*F loads back to back.
+template <int F>
+__device__ __forceinline__ f32x4 window_max(const float* p, int W, int C) {
+  f32x4 v[F * F];
+#pragma unroll
+  for (int fh = 0; fh < F; ++fh)
+#pragma unroll
+    for (int fw = 0; fw < F; ++fw) v[fh * F + fw] = *reinterpret_cast<const f32x4*>(p + (fh * W + fw) * C);
+  f32x4 m = v[0];
+#pragma unroll
+  for (int i = 1; i < F * F; ++i) m = max4(m, v[i]);
+  return m;
+}
+
+// 32-bit index math (the 64-bit divisions of the generic kernel cost more than the loads).
+template <int F, int S>
+__global__ void __launch_bounds__(kThreads) maxpool_fixed_kernel(const float* __restrict__ x, int total, int H, int W,
+                                                                 int C, int Ho, int Wo, OutView o) {
+  const int C4 = C >> 2;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < total; i += gridDim.x * kThreads) {
+    const int c4 = i % C4;
+    int r = i / C4;
+    const int ox = r % Wo;
+    r /= Wo;
+    const int oy = r % Ho;
+    const int n = r / Ho;
+    const f32x4 m = window_max<F>(x + nhwc(n, oy * S, ox * S, c4 * 4, H, W, C), W, C);
+    float* dst = o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb + o.c_off +
+                 c4 * 4;
+    *reinterpret_cast<f32x4*>(dst) = m;
+  }
 }
 
 __global__ void __launch_bounds__(kThreads) maxpool_vec4_kernel(const float* __restrict__ x, int N, int H, int W,
@@ -52,24 +88,30 @@ __global__ void __launch_bounds__(kThreads) maxpool_vec4_kernel(const float* __r
 }
 
 // One workgroup = PP output pixels x all C channels. Pass 1 pools into LDS, pass 2 applies LRN.
+// FF > 0: compile-time window (no bounds checks, loads issued together); FF == 0: runtime F.
+template <int FF>
 __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                                int N, int H, int W, int C, int F, int S, int Ho,
                                                                int Wo, int PP, int size, float a, float beta,
                                                                float k) {
   extern __shared__ __attribute__((aligned(16))) float pooled[];  // [PP][C]
   const int C4 = C / 4;
-  const long P = static_cast<long>(N) * Ho * Wo;
-  const long p0 = static_cast<long>(blockIdx.x) * PP;
+  const int P = N * Ho * Wo;  // < 2^31 (checked by the launcher)
+  const int p0 = blockIdx.x * PP;
   const int chunks = PP * C4;
   for (int t = threadIdx.x; t < chunks; t += blockDim.x) {
     const int pl = t / C4, c4 = t - pl * C4;
-    const long p = p0 + pl;
+    const int p = p0 + pl;
     f32x4 m = {0.f, 0.f, 0.f, 0.f};
     if (p < P) {
-      const int ox = static_cast<int>(p % Wo);
-      const long r = p / Wo;
-      const int oy = static_cast<int>(r % Ho);
-      const int n = static_cast<int>(r / Ho);
+      const int ox = p % Wo;
+      const int r = p / Wo;
+      const int oy = r % Ho;
+      const int n = r / Ho;
+      if constexpr (FF > 0) {
+        *reinterpret_cast<f32x4*>(pooled + pl * C + c4 * 4) = window_max<FF>(x + nhwc(n, oy * S, ox * S, c4 * 4, H, W, C), W, C);
+        continue;
+      }
       m = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       for (int fh = 0; fh < F; ++fh) {
         const int iy = oy * S + fh;
@@ -88,7 +130,7 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __re
   const int half = size / 2;
   for (int t = threadIdx.x; t < chunks; t += blockDim.x) {
     const int pl = t / C4, c4 = t - pl * C4;
-    const long p = p0 + pl;
+    const int p = p0 + pl;
     if (p >= P) continue;
     const float* row = pooled + pl * C;
     const int c0 = c4 * 4;
@@ -121,7 +163,7 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __re
         out[e] = row[c] / powf(k + a * s, beta);
       }
     }
-    *reinterpret_cast<f32x4*>(y + p * C + c4 * 4) = out;
+    *reinterpret_cast<f32x4*>(y + static_cast<size_t>(p) * C + c4 * 4) = out;
   }
 }
 
@@ -132,6 +174,11 @@ hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, Out
   const size_t total = static_cast<size_t>(N) * Ho * Wo * (C / 4);
   if (total == 0) return hipSuccess;
   if (C % 4 || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
+  if (F == 3 && S == 2 && total < (1UL << 31)) {
+    const unsigned g = static_cast<unsigned>(std::min<size_t>((total + kThreads - 1) / kThreads, 1 << 20));
+    maxpool_fixed_kernel<3, 2><<<g, kThreads, 0, s>>>(x, static_cast<int>(total), H, W, C, Ho, Wo, out);
+    return hipGetLastError();
+  }
   size_t g = (total + kThreads - 1) / kThreads;
   if (g > 65535) g = 65535;
   maxpool_vec4_kernel<<<static_cast<unsigned>(g), kThreads, 0, s>>>(x, N, H, W, C, F, S, Ho, Wo, out);
@@ -143,12 +190,16 @@ hipError_t maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int
   const int Ho = pool_out_dim(H, F, S), Wo = pool_out_dim(W, F, S);
   const long P = static_cast<long>(N) * Ho * Wo;
   if (P == 0) return hipSuccess;
-  if (C % 4 || C > 8192) return hipErrorInvalidValue;
+  if (C % 4 || C > 8192 || P >= (1L << 31)) return hipErrorInvalidValue;
   const int PP = C >= 4096 ? 1 : 4096 / C;  // 16 KB of LDS per workgroup
   const long blocks = (P + PP - 1) / PP;
   const float a = mode == LrnMode::DivN ? alpha / static_cast<float>(size) : alpha;
-  maxpool_lrn_kernel<<<static_cast<unsigned>(blocks), kThreads, PP * C * sizeof(float), s>>>(
-      x, y, N, H, W, C, F, S, Ho, Wo, PP, size, a, beta, k);
+  if (F == 3)
+    maxpool_lrn_kernel<3><<<static_cast<unsigned>(blocks), kThreads, PP * C * sizeof(float), s>>>(
+        x, y, N, H, W, C, F, S, Ho, Wo, PP, size, a, beta, k);
+  else
+    maxpool_lrn_kernel<0><<<static_cast<unsigned>(blocks), kThreads, PP * C * sizeof(float), s>>>(
+        x, y, N, H, W, C, F, S, Ho, Wo, PP, size, a, beta, k);
   return hipGetLastError();
 }
 

@@ -31,15 +31,15 @@ constexpr int kN = wino::kN, kM = wino::kM;
 // the 7x7 patch streams through t = B^T d one input row at a time (t: 49 registers).
 __global__ void __launch_bounds__(kT) wino_in_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
                                                      int Hq, int Wq, int C, int ty, int tx) {
-  const long total = static_cast<long>(N) * ty * tx * C;
-  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
-       i += static_cast<long>(gridDim.x) * blockDim.x) {
-    const int c = static_cast<int>(i % C);
-    const long p = i / C;
-    const int tj = static_cast<int>(p % tx);
-    const long q = p / tx;
-    const int ti = static_cast<int>(q % ty);
-    const int n = static_cast<int>(q / ty);
+  // 32-bit index math (total < 2^31, checked by the launcher): 64-bit divisions cost more than the loads
+  const int total = N * ty * tx * C;
+  for (int i = blockIdx.x * kT + threadIdx.x; i < total; i += gridDim.x * kT) {
+    const int c = i % C;
+    const int p = i / C;
+    const int tj = p % tx;
+    const int q = p / tx;
+    const int ti = q % ty;
+    const int n = q / ty;
     float t[kN][kN];
 #pragma unroll
     for (int a = 0; a < kN; ++a)
@@ -310,7 +310,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BK>
+template <int BK, bool XCD>
 __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
   using f32x16 = __attribute__((ext_vector_type(16))) float;
   constexpr int U4 = BK / 4;              // 16-B units per row
@@ -322,7 +322,17 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int g = blockIdx.z;
-  const int pt = blockIdx.x / a.n_ntiles, nt = blockIdx.x - pt * a.n_ntiles;
+  int pt, nt;
+  if constexpr (XCD) {
+    // the n_ntiles workgroups that read one V slab get equal blockIdx.x % 8 (one XCD, one L2)
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    nt = j % a.n_ntiles;
+    pt = (j / a.n_ntiles) * 8 + xcd;
+    if (pt >= a.n_ptiles) return;  // whole workgroup, before any DMA or barrier
+  } else {
+    pt = blockIdx.x / a.n_ntiles;
+    nt = blockIdx.x - pt * a.n_ntiles;
+  }
   const int p0 = pt * kFB, n0 = nt * kFB;
 
   // per-lane source offsets of this thread's NI A units and NI B units (swizzled unit order)
@@ -377,17 +387,20 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
       for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
     }
   };
+  // coefficients are wave-uniform (scalar registers): a zero one (152 of the 441 coefficient x
+  // point pairs) skips its 16 FMAs with a scalar branch
   auto fold = [&](int ab, f32x16& acc) {
     const int aa = ab / kN, bb = ab - aa * kN;
-    float co[9];
 #pragma unroll
     for (int i3 = 0; i3 < kM; ++i3)
 #pragma unroll
-      for (int j3 = 0; j3 < kM; ++j3) co[i3 * kM + j3] = c_AT[i3][aa] * c_AT[j3][bb];
+      for (int j3 = 0; j3 < kM; ++j3) {
+        const float c = c_AT[i3][aa] * c_AT[j3][bb];
+        if (c != 0.f) {
 #pragma unroll
-    for (int q = 0; q < 9; ++q)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) Y[q][e] = fmaf(co[q], acc[e], Y[q][e]);
+          for (int e = 0; e < 16; ++e) Y[i3 * kM + j3][e] = fmaf(c, acc[e], Y[i3 * kM + j3][e]);
+        }
+      }
     acc = f32x16{};
   };
   // one K slice: retire slice it (counted wait + barrier), refill the ring slot freed by it-1
@@ -422,42 +435,65 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
   // kN*kN is odd: the last point (48, even) is still in acc0
   fold(kN * kN - 1, acc0);
 
-  const int f = n0 + wn * 32 + r;
-  if (f >= a.Kg) return;
-  const int fk = g * a.Kg + f;
-  const float bv = a.bias ? a.bias[fk] : 0.f;
+  // Epilogue: bias + ReLU, then one LDS transpose per output position q so each lane stores whole
+  // 16-B filter groups (4 dwordx4 per lane per q instead of 16 single-dword stores, which were
+  // store-issue-bound). D layout: lane (r, h) holds filter n0 + wn*32 + r of wave tiles
+  // wm*32 + (e&3) + 8*(e>>2) + 4h. Kg % 4 == 0 (wino_eligible), so a 4-filter group is all in or
+  // all past Kg.
+  __syncthreads();  // the ring is idle (last slice waited with vmcnt(0)); reuse it as scratch
+  constexpr int kTS = 32 + 4;
+  float* tr = lds + wave * 32 * kTS;
+  const int fb = n0 + wn * 32;  // first filter of this wave (within the group)
+  const float bv = (a.bias && fb + r < a.Kg) ? a.bias[g * a.Kg + fb + r] : 0.f;
+  int oy0[4], ox0[4], img[4];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int p = p0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-    if (p >= a.P) continue;
-    const int tj = p % a.tx;
-    const int q = p / a.tx;
-    const int ti = q % a.ty;
-    const int n = q / a.ty;
+  for (int k = 0; k < 4; ++k) {
+    const int p = p0 + wm * 32 + ((k * 64 + lane) >> 3);
+    const int tj = p % a.tx, pq = p / a.tx;
+    oy0[k] = p < a.P ? (pq % a.ty) * kM : (1 << 28);  // out of range: never stored
+    ox0[k] = tj * kM;
+    img[k] = pq / a.ty;
+  }
+  const int grp = 4 * (lane & 7);
+  const bool fin = fb + grp < a.Kg;
 #pragma unroll
-    for (int i3 = 0; i3 < kM; ++i3) {
-      const int oy = ti * kM + i3;
-      if (oy >= a.Ho) break;
+  for (int q = 0; q < kM * kM; ++q) {
 #pragma unroll
-      for (int j3 = 0; j3 < kM; ++j3) {
-        const int ox = tj * kM + j3;
-        if (ox >= a.Wo) break;
-        float v = Y[i3 * kM + j3][e] + bv;
-        if (a.relu) v = fmaxf(v, 0.f);
-        a.y[((static_cast<size_t>(n) * a.Ho + oy) * a.Wo + ox) * a.K + fk] = v;
-      }
+    for (int e = 0; e < 16; ++e) {
+      float v = Y[q][e] + bv;
+      if (a.relu) v = fmaxf(v, 0.f);
+      tr[((e & 3) + 8 * (e >> 2) + 4 * h) * kTS + r] = v;
+    }
+    // same-wave LDS accesses complete in order (reads see the writes; later writes cannot overtake)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(tr + ((k * 64 + lane) >> 3) * kTS + grp);
+      const int oy = oy0[k] + q / kM, ox = ox0[k] + q % kM;
+      if (fin && oy < a.Ho && ox < a.Wo)
+        *reinterpret_cast<f32x4*>(a.y + ((static_cast<size_t>(img[k]) * a.Ho + oy) * a.Wo + ox) * a.K + g * a.Kg + fb +
+                                  grp) = v4;
     }
   }
 }
 
-// fused-kernel configuration: bit0 = BK 48 (when Cg allows), bit1 = XCD-aware block order,
-// bit2 = LDS-DMA ring (when Cg % BK == 0). ANX_WINO_FUSED_CFG overrides the default (profiling).
+// fused-kernel configuration: bit0 = BK 48 (else 32), bit1 = XCD-aware block order, bit2 = LDS-DMA
+// ring (when Cg % BK == 0). ANX_WINO_FUSED_CFG overrides the default (profiling).
 int default_fused_cfg() {
   const char* e = std::getenv("ANX_WINO_FUSED_CFG");
   const int v = e ? std::atoi(e) : -1;
-  return v >= 0 && v <= 7 ? v : 5;
+  return v >= 0 && v <= 7 ? v : 7;
 }
 int g_fused_cfg = default_fused_cfg();
+
+template <int BK, bool XCD>
+hipError_t launch_glds(const FusedArgs& a, dim3 grid, hipStream_t s) {
+  constexpr int kLds = 3 * 2 * kFB * BK * sizeof(float);  // 3-slot ring of A|B tiles
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wino_fused_glds_kernel<BK, XCD>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+  if (attr != hipSuccess) return attr;
+  wino_fused_glds_kernel<BK, XCD><<<grid, 256, kLds, s>>>(a);
+  return hipGetLastError();
+}
 
 unsigned grid_for(long n) {
   long g = (n + kT - 1) / kT;
@@ -524,7 +560,10 @@ void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::ve
 
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s) {
   const long n = static_cast<long>(w.P) * w.C;
-  wino_in_kernel<<<grid_for(n), kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
+  if (n >= (1L << 31)) return hipErrorInvalidValue;
+  const long g = (n + kT - 1) / kT;
+  wino_in_kernel<<<static_cast<unsigned>(g < (1 << 20) ? g : (1 << 20)), kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty,
+                                                                                      w.tx);
   return hipGetLastError();
 }
 
@@ -552,17 +591,19 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
   a.n_ptiles = (w.P + kFB - 1) / kFB;
   a.n_ntiles = (a.Kg + kFB - 1) / kFB;
   if (a.n_ntiles * kFB > a.kpad_n || a.Cg % 4) return hipErrorInvalidValue;
-  if ((g_fused_cfg & 4) && a.Cg % 48 == 0 && a.kpad == a.Cg) {
-    constexpr int kLds = 3 * 2 * kFB * 48 * sizeof(float);  // 72 KiB ring
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wino_fused_glds_kernel<48>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-    if (attr != hipSuccess) return attr;
-    dim3 grid(a.n_ptiles * a.n_ntiles, 1, w.groups);
-    wino_fused_glds_kernel<48><<<grid, 256, kLds, s>>>(a);
-    return hipGetLastError();
+  const bool xcd = (g_fused_cfg & 2) != 0;
+  if (g_fused_cfg & 4) {
+    // LDS-DMA ring: BK 48 (72 KiB, 2 workgroups/CU) or BK 32 (48 KiB, 3/CU)
+    const int bk = (g_fused_cfg & 1) ? 48 : 32;
+    if (a.Cg % bk == 0 && a.kpad == a.Cg) {
+      const dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
+      if (bk == 48 && xcd) return launch_glds<48, true>(a, grid, s);
+      if (bk == 48) return launch_glds<48, false>(a, grid, s);
+      if (xcd) return launch_glds<32, true>(a, grid, s);
+      return launch_glds<32, false>(a, grid, s);
+    }
   }
   const int bk = (a.kpad % 48 == 0 && g_fused_cfg & 1) ? 48 : 32;
-  const bool xcd = (g_fused_cfg & 2) != 0;
   dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
   if (bk == 48 && xcd)
     wino_fused_kernel<48, true><<<grid, 256, 0, s>>>(a);

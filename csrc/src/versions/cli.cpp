@@ -49,6 +49,7 @@ struct Options {
   int iters = 0;
   std::string impl = "mfma";
   std::string conv2_algo = "auto";  // auto | direct | winograd
+  std::string conv1_algo = "auto";  // auto | direct | winograd
   bool check = false;
   bool json = true;
   std::string weights;  // directory with raw fp32 w1/b1/w2/b2 .bin (overrides --init for weights)
@@ -58,7 +59,8 @@ struct Options {
   std::fprintf(stderr,
                "%s\nusage: anx --version v1|v2.1|v2.2|v3|v4|v5 [--batch N] [--init const|rand] [--seed S]\n"
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
-               "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd] [--check]\n"
+               "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd]\n"
+               "           [--conv1-algo auto|direct|winograd] [--check]\n"
                "           [--weights DIR] [--no-json]\n",
                msg);
   std::exit(2);
@@ -82,6 +84,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--iters") o.iters = std::atoi(val().c_str());
     else if (a == "--impl") o.impl = val();
     else if (a == "--conv2-algo") o.conv2_algo = val();
+    else if (a == "--conv1-algo") o.conv1_algo = val();
     else if (a == "--check") o.check = true;
     else if (a == "--no-json") o.json = false;
     else if (a == "--weights") o.weights = val();
@@ -737,6 +740,10 @@ int main(int argc, char** argv) {
   // results match to ~1e-7 relative, not bitwise; `direct` makes every decomposition bit-identical.
   set_conv2_algo(o.conv2_algo == "direct"     ? ConvAlgo::Direct
                  : o.conv2_algo == "winograd" ? ConvAlgo::Winograd
+                                              : ConvAlgo::Auto);
+  // Conv1 likewise: polyphase Winograd by default, `direct` for bit-identical decompositions.
+  set_conv1_algo(o.conv1_algo == "direct"     ? ConvAlgo::Direct
+                 : o.conv1_algo == "winograd" ? ConvAlgo::Winograd
                                               : ConvAlgo::Auto);
   const RankInfo ri = rank_info_from_env();
   try {

@@ -28,6 +28,8 @@ def _run_args(ap):
     ap.add_argument("--iters", type=int, default=0, help="warm iterations after the cold run")
     ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
     ap.add_argument("--conv2-algo", default="auto", choices=["auto", "direct", "winograd"])
+    ap.add_argument("--conv1-algo", default="auto", choices=["auto", "direct", "winograd"],
+                    help="direct = bit-identical across row decompositions (Winograd: ~1e-7)")
     ap.add_argument("--check", action="store_true", help="compare with the PyTorch fp64 oracle")
     ap.add_argument("--cpu-rehearsal", action="store_true", help="run a GPU version's program on CPU ranks")
     ap.add_argument("--quiet", action="store_true")
@@ -37,7 +39,7 @@ def cmd_run(a):
     from .versions import RunConfig, run
     cfg = RunConfig(version=a.version, batch=a.batch, init=a.init, seed=a.seed, lrn_mode=a.lrn_alpha_mode,
                     groups2=a.groups, decomp=a.decomp, strategy=a.strategy, iters=a.iters, impl=a.impl,
-                    conv2_algo=a.conv2_algo,
+                    conv2_algo=a.conv2_algo, conv1_algo=a.conv1_algo,
                     check=a.check, quiet=a.quiet, cpu_rehearsal=a.cpu_rehearsal)
     run(cfg)
 

@@ -55,6 +55,7 @@ class RunConfig:
     quiet: bool = False
     cpu_rehearsal: bool = False   # run the GPU versions' program on CPU ranks over gloo (tests)
     conv2_algo: str = "auto"      # auto | direct | winograd (direct = bit-identical across decompositions)
+    conv1_algo: str = "auto"      # auto | direct | winograd (likewise for Conv1's polyphase Winograd)
 
 
 @dataclass
@@ -133,8 +134,9 @@ def run(cfg: RunConfig) -> RunResult | None:
         w = init_weights(cfg.init, cfg.seed, b1, b2) if rank == 0 else \
             {k: torch.empty_like(v) for k, v in init_weights("const", 0, b1, b2).items()}
         w = comm.bcast_weights(w, device=comm_dev)
-        from .utils.tuning import set_conv2_algo
+        from .utils.tuning import set_conv1_algo, set_conv2_algo
         set_conv2_algo(cfg.conv2_algo)
+        set_conv1_algo(cfg.conv1_algo)
         model = AlexNetBlocks(w, specs=(b1, b2), device=device, impl=cfg.impl, max_batch=cfg.batch)
         x = init_input(cfg.batch, cfg.init, cfg.seed) if rank == 0 else None
         if cfg.version == "v2.1" or (cfg.strategy == "filter" and cfg.version in ("v2.2", "v4", "v5")):

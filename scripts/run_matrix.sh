@@ -44,7 +44,7 @@ run_case() {  # version np
   local v="$1" np="$2" log="$OUT/run_${1}_np${2}.log"
   # GPU versions: div_n LRN and direct conv2 so every decomposition is bit-identical to V1's output
   # (set CONV2_ALGO=auto to time the Winograd path; checksums then differ in the last bits).
-  local lrn=""; case "$v" in v3|v4|v5) lrn="--lrn-alpha-mode div_n --conv2-algo ${CONV2_ALGO:-direct}" ;; esac
+  local lrn=""; case "$v" in v3|v4|v5) lrn="--lrn-alpha-mode div_n --conv2-algo ${CONV2_ALGO:-direct} --conv1-algo ${CONV1_ALGO:-direct}" ;; esac
   local args="--version $v --batch $BATCH --init $INIT --iters $ITERS $lrn"
   local cls
   if [ "$np" -eq 1 ] && { [ "$v" = v1 ] || [ "$v" = v3 ]; }; then

@@ -216,3 +216,91 @@ def test_winograd_golden(cuda, algo):
     m = AlexNetBlocks(device=cuda, lrn_mode="raw")
     y = m(init_input(1, "const").to(cuda)).cpu()
     assert y.flatten()[:5].tolist() == pytest.approx(GOLD_RAW, abs=2e-4)
+
+
+# ---------------------------------------------------------------- polyphase Winograd F(3x3,3x3) conv1
+@pytest.fixture
+def algo1():
+    yield lambda a: nat.call("anx_set_conv1_algo", a)
+    nat.call("anx_set_conv1_algo", 0)
+
+
+@pytest.mark.parametrize("shape", [
+    # N, Hin, W, K, F
+    (1, 227, 227, 96, 11),
+    (3, 59, 47, 32, 11),    # ragged right/bottom tiles
+    (2, 40, 61, 64, 9),     # F=9: the 4th phase row/col of every tap is zero
+    (130, 227, 227, 96, 11),  # > one 128-tile block row, XCD-ordered grid with empty slots
+])
+def test_conv1_wino_kernel_vs_torch(cuda, shape):
+    N, H, W, K, F = shape
+    torch.manual_seed(3)
+    x = torch.rand(N, H, W, 3, device=cuda)
+    w = (torch.rand(K, 3, F, F) - 0.5) * 0.1
+    b = torch.randn(K, device=cuda)
+    H1, W1 = (H - F) // 4 + 1, (W - F) // 4 + 1
+    y = torch.full((N, H1, W1, K), float("nan"), device=cuda)
+    nat.call("anx_conv1_wino", x.data_ptr(), N, H, W, w.contiguous().data_ptr(), K, F, b.data_ptr(), y.data_ptr(), 0,
+             nat.stream_ptr(cuda))
+    ref = conv2d_nhwc(x.double(), w.to(cuda).double(), b.double(), 4, 0)
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_conv1_wino_ring_configs(cuda, cfg):
+    """Every LDS ring configuration (BK 48 x 2 slots, BK 16 x 4/6/8) gives the same conv1."""
+    torch.manual_seed(5)
+    x = torch.rand(4, 227, 227, 3, device=cuda)
+    w = (torch.rand(96, 3, 11, 11) - 0.5) * 0.1
+    b = torch.zeros(96, device=cuda)
+    y = torch.empty(4, 55, 55, 96, device=cuda)
+    nat.call("anx_conv1_wino_cfg", cfg)
+    try:
+        nat.call("anx_conv1_wino", x.data_ptr(), 4, 227, 227, w.data_ptr(), 96, 11, b.data_ptr(), y.data_ptr(), 1,
+                 nat.stream_ptr(cuda))
+    finally:
+        nat.call("anx_conv1_wino_cfg", 0)
+    ref = conv2d_nhwc(x.double(), w.to(cuda).double(), b.double(), 4, 0, relu=True)
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("N", [1, 7, 128])
+def test_conv1_winograd_engine_vs_oracle(cuda, algo1, N):
+    algo1(2)
+    m = AlexNetBlocks(device=cuda, init="rand", seed=50 + N, max_batch=N)
+    x = init_input(N, "rand", seed=50 + N)
+    y = m(x.to(cuda)).cpu().double()
+    idx = torch.arange(N) if N <= 8 else torch.tensor([0, 1, 63, 64, 126, 127])
+    ref = blocks_forward(x[idx], m.weights, m.b1, m.b2)
+    torch.testing.assert_close(y[idx], ref, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("np_", [2, 3, 4, 8])
+def test_conv1_winograd_row_tiles(cuda, algo1, np_):
+    """Row tiles start conv1's 3x3 Winograd tiles at the tile's own first row (partial tiles)."""
+    algo1(2)
+    m = AlexNetBlocks(device=cuda, init="rand", seed=60, max_batch=2)
+    x = init_input(2, "rand", seed=60)
+    ref = blocks_forward(x, m.weights, m.b1, m.b2)
+    xd = x.to(cuda)
+    p = make_plan(227, 227, np_, OVERLAP)
+    parts = [m.tile_forward(xd[:, t.inp.lo:t.inp.hi].contiguous(), t) for t in p.tiles if not t.out.empty]
+    torch.testing.assert_close(torch.cat(parts, dim=1).cpu().double(), ref, rtol=2e-5, atol=2e-6)
+
+
+def test_conv1_direct_and_winograd_agree(cuda, algo1):
+    m = AlexNetBlocks(device=cuda, init="rand", seed=70, max_batch=4)
+    x = init_input(4, "rand", seed=70).to(cuda)
+    algo1(1)
+    yd = m(x).clone()
+    algo1(2)
+    yw = m(x)
+    torch.testing.assert_close(yw, yd, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode,gold", [("div_n", GOLD_DIV_N_F64), ("raw", GOLD_RAW)])
+def test_conv1_winograd_golden(cuda, algo1, mode, gold):
+    algo1(2)
+    m = AlexNetBlocks(device=cuda, lrn_mode=mode)
+    y = m(init_input(1, "const").to(cuda)).cpu()
+    assert y.flatten()[:5].tolist() == pytest.approx(gold, abs=2e-4)

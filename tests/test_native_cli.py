@@ -90,8 +90,8 @@ def test_native_v3_batch_check(cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize("np_", [2, 3])
 def test_native_v4_shared_gpu(cuda, np_):
-    # direct conv2: every decomposition is bit-identical to the single-GPU run
-    d = ["--conv2-algo", "direct"]
+    # direct conv1/conv2: every decomposition is bit-identical to the single-GPU run
+    d = ["--conv2-algo", "direct", "--conv1-algo", "direct"]
     ref, _ = native(["--version", "v3", "--init", "rand", "--seed", "5", "--batch", "3", *d])
     rec, out = native(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", "--iters", "2", *d], np_)
     assert "Final Output Shape: 13x13x256" in out.stdout

@@ -22,7 +22,7 @@ def test_v3_batch_check(cuda):
 
 @pytest.mark.parametrize("extra", [[], ["--decomp", "per_layer"], ["--strategy", "batch"]])
 def test_v4_two_ranks_one_gpu(cuda, extra):
-    d = ["--conv2-algo", "direct"]  # bit-identical across decompositions (Winograd: ~1e-7)
+    d = ["--conv2-algo", "direct", "--conv1-algo", "direct"]  # bit-identical across decompositions (Winograd: ~1e-7)
     ref, _ = run_cli(["--version", "v3", "--init", "rand", "--seed", "5", "--batch", "3", *d])
     rec, out = run_cli(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", *extra, *d], 2)
     assert "Final Output Shape: 13x13x256" in out
