@@ -120,7 +120,7 @@ void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<floa
 // Tuning (A/B): ring shape 0..3 (conv1_wino.hip default_cfg). -1 on a bad id.
 int conv1_wino_set_cfg(int cfg);
 // Cost probes for profiling only (results become wrong): bit0 skip the output-transform fold,
-// bit1 skip the LDS-DMA refills. 0 = normal.
+// bit1 skip the LDS-DMA refills; bit4 = s_setprio around the MFMA slices (the default, 16).
 int conv1_wino_set_probe(int bits);
 // x: [N, Hin, W, 3] image rows; writes conv1 (+bias, optional ReLU) through `out`.
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,

@@ -127,7 +127,8 @@ struct GemmArgs {
   OutView out;        // conv1 output [N][H1][W1][K] (+ offsets)
   int P, K, H1, W1, ty, tx, relu, n_ptiles, n_ntiles;
   int probe;  // cost probes (wrong results; never set in production): bit0 no fold, bit1 no DMA
-              // refill, bit2 no per-slice barrier (only with bit1), bit3 no epilogue stores
+              // refill, bit2 no per-slice barrier (only with bit1), bit3 no epilogue stores;
+              // bit4: s_setprio(1) around each slice's MFMAs (guide technique T5; on by default)
 };
 
 using lds_f32 = __attribute__((address_space(3))) float;
@@ -280,7 +281,9 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
     if ((a.probe & 6) != 6) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // keep the DMA refill and the ds_reads below the barrier
     if (it + NST - 1 < TOTAL && !(a.probe & 2)) issue(it + NST - 1);
+    if (a.probe & 16) __builtin_amdgcn_s_setprio(1);
     mfma_slice(it, acc);
+    if (a.probe & 16) __builtin_amdgcn_s_setprio(0);
   };
 
 #pragma unroll
@@ -370,7 +373,7 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
 
 int g_probe = [] {
   const char* e = std::getenv("ANX_CONV1_WINO_PROBE");
-  return e ? std::atoi(e) : 0;
+  return e ? std::atoi(e) : 16;  // bit4 (s_setprio around the MFMA slices) on: -1 % at 300 images
 }();
 int conv1_wino_set_probe(int bits) {
   g_probe = bits;

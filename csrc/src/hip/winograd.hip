@@ -141,6 +141,7 @@ struct FusedArgs {
   float* y;            // [N][Ho][Wo][K]
   int P, C, Cg, Kg, K, groups, kpad, kpad_n;
   int N, Ho, Wo, ty, tx, relu, n_ptiles, n_ntiles;
+  int prio;  // A/B: s_setprio(1) around each slice's MFMAs (guide technique T5)
 };
 
 // A^T indexed by the runtime transform point: a copy of wino::kAT in constant memory (scalar loads).
@@ -412,7 +413,9 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // keep the DMA refill and the ds_reads below the barrier
     if (it + 2 < total) issue(it + 2);
+    if (a.prio) __builtin_amdgcn_s_setprio(1);
     mfma_slice(it, acc);
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
   };
 
   issue(0);
@@ -484,6 +487,10 @@ int default_fused_cfg() {
   return v >= 0 && v <= 7 ? v : 7;
 }
 int g_fused_cfg = default_fused_cfg();
+int g_prio = [] {  // default on: -1 % measured at 300 images (ANX_WINO_PRIO=0 disables)
+  const char* e = std::getenv("ANX_WINO_PRIO");
+  return e ? std::atoi(e) : 1;
+}();
 
 template <int BK, bool XCD>
 hipError_t launch_glds(const FusedArgs& a, dim3 grid, hipStream_t s) {
@@ -588,6 +595,7 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
   a.ty = w.ty;
   a.tx = w.tx;
   a.relu = relu ? 1 : 0;
+  a.prio = g_prio;
   a.n_ptiles = (w.P + kFB - 1) / kFB;
   a.n_ntiles = (a.Kg + kFB - 1) / kFB;
   if (a.n_ntiles * kFB > a.kpad_n || a.Cg % 4) return hipErrorInvalidValue;

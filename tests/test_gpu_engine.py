@@ -166,16 +166,17 @@ def test_maxpool(cuda, vec):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-def test_lrn_and_fused_pool_lrn(cuda, mode):
-    x = torch.rand(2, 27, 27, 256, device=cuda) * 4
+@pytest.mark.parametrize("C", [256, 128])  # 256: wave-per-pixel kernel; else the LDS-tile kernel
+def test_lrn_and_fused_pool_lrn(cuda, mode, C):
+    x = torch.rand(2, 27, 27, C, device=cuda) * 4
     pooled = maxpool_nhwc(x, 3, 2)
     ref = lrn_nhwc(pooled.double(), 5, 1e-4, 0.75, 2.0, "div_n" if mode == 0 else "raw")
     y = torch.empty_like(pooled)
-    nat.call("anx_lrn_direct", pooled.data_ptr(), y.data_ptr(), 2, 13, 13, 256, 5, 1e-4, 0.75, 2.0, mode,
+    nat.call("anx_lrn_direct", pooled.data_ptr(), y.data_ptr(), 2, 13, 13, C, 5, 1e-4, 0.75, 2.0, mode,
              nat.stream_ptr(cuda))
     torch.testing.assert_close(y.double(), ref, rtol=1e-6, atol=1e-6)
     y2 = torch.empty_like(pooled)
-    nat.call("anx_maxpool_lrn", x.data_ptr(), y2.data_ptr(), 2, 27, 27, 256, 3, 2, 5, 1e-4, 0.75, 2.0, mode,
+    nat.call("anx_maxpool_lrn", x.data_ptr(), y2.data_ptr(), 2, 27, 27, C, 3, 2, 5, 1e-4, 0.75, 2.0, mode,
              nat.stream_ptr(cuda))
     torch.testing.assert_close(y2.double(), ref, rtol=1e-6, atol=1e-6)
 

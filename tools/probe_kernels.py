@@ -43,7 +43,7 @@ def main():
             e1.record()
             e1.synchronize()
             times[(cfg, probe)].append(e0.elapsed_time(e1) / a.iters)
-    nat.call("anx_conv1_wino_probe", 0)
+    nat.call("anx_conv1_wino_probe", 16)
     nat.call("anx_conv1_wino_cfg", 0)
     for arm, t in times.items():
         t = sorted(t)
