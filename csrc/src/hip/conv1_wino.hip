@@ -52,6 +52,7 @@ constexpr int kBM = 128, kBN = 32;         // tiles x filters per GEMM workgroup
 // of the tile the 12 floats (rw, c) of phase row rh are 3 contiguous float4 units of one image row.
 // Consecutive threads cover consecutive channels, so V rows (48 floats per (p, ab)) are written
 // as whole 192-B runs.
+template <bool NT>
 __global__ void __launch_bounds__(kT) conv1_wino_in_kernel(const float* __restrict__ x, float* __restrict__ V,
                                                            int total, int Hin, int rowf, int ty, int tx) {
   for (int i = blockIdx.x * kT + threadIdx.x; i < total; i += gridDim.x * kT) {
@@ -102,7 +103,10 @@ __global__ void __launch_bounds__(kT) conv1_wino_in_kernel(const float* __restri
 #pragma unroll
         for (int v = 0; v < kN5; ++v)
           if (w33::kBT[b][v] != 0.f) s += w33::kBT[b][v] * t[a][v];
-        *reinterpret_cast<f32x4*>(out + (a * kN5 + b) * kCh) = s;
+        if constexpr (NT)
+          __builtin_nontemporal_store(s, reinterpret_cast<f32x4*>(out + (a * kN5 + b) * kCh));
+        else
+          *reinterpret_cast<f32x4*>(out + (a * kN5 + b) * kCh) = s;
       }
   }
 }
@@ -231,11 +235,13 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
   const int a_row = (wave * 32 + r) * BK, b_row = R::A_FL + r * BK;
 
   // Y[i*3+j][e2] holds output (i, j) of the accumulator rows 2*e2, 2*e2+1 (pairs for v_pk_*_f32)
-  float Y[9][16];
+  // Y[q][e2]: output q of accumulator rows 2*e2 and 2*e2+1 (pairs: one v_pk_fma_f32 per 2 rows)
+  using f32x2 = __attribute__((ext_vector_type(2))) float;
+  f32x2 Y[9][8];
 #pragma unroll
   for (int q = 0; q < 9; ++q)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) Y[q][e] = 0.f;
+    for (int e2 = 0; e2 < 8; ++e2) Y[q][e2] = f32x2{0.f, 0.f};
   f32x16 acc0 = {}, acc1 = {};
 
   // k permutation inside a slice: lane half h at MFMA step s consumes k = h*BK/2 + s (A and B
@@ -264,8 +270,11 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
       for (int j3 = 0; j3 < 3; ++j3) {
         const float c = c_at33.v[i3][aa] * c_at33.v[j3][bb];
         if (c != 0.f) {
+          const f32x2 c2 = {c, c};
 #pragma unroll
-          for (int e = 0; e < 16; ++e) Y[i3 * 3 + j3][e] = fmaf(c, acc[e], Y[i3 * 3 + j3][e]);
+          for (int e2 = 0; e2 < 8; ++e2)
+            Y[i3 * 3 + j3][e2] =
+                __builtin_elementwise_fma(c2, f32x2{acc[2 * e2], acc[2 * e2 + 1]}, Y[i3 * 3 + j3][e2]);
         }
       }
     acc = f32x16{};
@@ -330,7 +339,7 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
   for (int q = 0; q < 9; ++q) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      float v = Y[q][e] + bv;
+      float v = Y[q][e >> 1][e & 1] + bv;
       if (a.relu) v = fmaxf(v, 0.f);
       tr[((e & 3) + 8 * (e >> 2) + 4 * h) * kTS + r] = v;
     }
@@ -446,7 +455,10 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
   const int total = w.P * 12;
   long g = (total + kT - 1) / kT;
   if (g > (1 << 20)) g = 1 << 20;
-  conv1_wino_in_kernel<<<static_cast<unsigned>(g), kT, 0, s>>>(x, V, total, w.Hin, w.W * 3, w.ty, w.tx);
+  if (g_probe & 32)  // A/B: non-temporal V stores
+    conv1_wino_in_kernel<true><<<static_cast<unsigned>(g), kT, 0, s>>>(x, V, total, w.Hin, w.W * 3, w.ty, w.tx);
+  else
+    conv1_wino_in_kernel<false><<<static_cast<unsigned>(g), kT, 0, s>>>(x, V, total, w.Hin, w.W * 3, w.ty, w.tx);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   GemmArgs a{};

@@ -29,6 +29,7 @@ constexpr int kN = wino::kN, kM = wino::kM;
 
 // One thread per (tile, channel): consecutive threads read consecutive channels (coalesced NHWC),
 // the 7x7 patch streams through t = B^T d one input row at a time (t: 49 registers).
+template <bool NT>
 __global__ void __launch_bounds__(kT) wino_in_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
                                                      int Hq, int Wq, int C, int ty, int tx) {
   // 32-bit index math (total < 2^31, checked by the launcher): 64-bit divisions cost more than the loads
@@ -70,7 +71,10 @@ __global__ void __launch_bounds__(kT) wino_in_kernel(const float* __restrict__ x
 #pragma unroll
         for (int v = 0; v < kN; ++v)
           if (wino::kBT[b][v] != 0.f) s2 = fmaf(wino::kBT[b][v], t[a][v], s2);
-        out[static_cast<size_t>(a * kN + b) * C] = s2;
+        if constexpr (NT)
+          __builtin_nontemporal_store(s2, out + static_cast<size_t>(a * kN + b) * C);
+        else
+          out[static_cast<size_t>(a * kN + b) * C] = s2;
       }
   }
 }
@@ -371,11 +375,13 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
   for (int s4 = 0; s4 < BK / 8; ++s4) rd[s4] = 4 * ((h * (BK / 8) + s4) ^ swz);
   const int a_row = (wm * 32 + r) * BK, b_row = TILE + (wn * 32 + r) * BK;
 
-  float Y[9][16];
+  // Y[q][e2]: output q of accumulator rows 2*e2 and 2*e2+1 (pairs: one v_pk_fma_f32 per 2 rows)
+  using f32x2 = __attribute__((ext_vector_type(2))) float;
+  f32x2 Y[9][8];
 #pragma unroll
   for (int q = 0; q < 9; ++q)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) Y[q][e] = 0.f;
+    for (int e2 = 0; e2 < 8; ++e2) Y[q][e2] = f32x2{0.f, 0.f};
   f32x16 acc0 = {}, acc1 = {};
 
   auto mfma_slice = [&](int it, f32x16& acc) {
@@ -398,8 +404,11 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
       for (int j3 = 0; j3 < kM; ++j3) {
         const float c = c_AT[i3][aa] * c_AT[j3][bb];
         if (c != 0.f) {
+          const f32x2 c2 = {c, c};
 #pragma unroll
-          for (int e = 0; e < 16; ++e) Y[i3 * kM + j3][e] = fmaf(c, acc[e], Y[i3 * kM + j3][e]);
+          for (int e2 = 0; e2 < 8; ++e2)
+            Y[i3 * kM + j3][e2] =
+                __builtin_elementwise_fma(c2, f32x2{acc[2 * e2], acc[2 * e2 + 1]}, Y[i3 * kM + j3][e2]);
         }
       }
     acc = f32x16{};
@@ -463,7 +472,7 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
   for (int q = 0; q < kM * kM; ++q) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      float v = Y[q][e] + bv;
+      float v = Y[q][e >> 1][e & 1] + bv;
       if (a.relu) v = fmaxf(v, 0.f);
       tr[((e & 3) + 8 * (e >> 2) + 4 * h) * kTS + r] = v;
     }
@@ -569,8 +578,11 @@ hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s
   const long n = static_cast<long>(w.P) * w.C;
   if (n >= (1L << 31)) return hipErrorInvalidValue;
   const long g = (n + kT - 1) / kT;
-  wino_in_kernel<<<static_cast<unsigned>(g < (1 << 20) ? g : (1 << 20)), kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty,
-                                                                                      w.tx);
+  const unsigned gg = static_cast<unsigned>(g < (1 << 20) ? g : (1 << 20));
+  if (g_prio & 2)  // A/B: non-temporal V stores
+    wino_in_kernel<true><<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
+  else
+    wino_in_kernel<false><<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
   return hipGetLastError();
 }
 
