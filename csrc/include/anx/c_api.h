@@ -100,7 +100,7 @@ int anx_get_conv2_algo(void);
 /* Conv1 (11x11 s4) algorithm on the MFMA path: 0 auto (polyphase Winograd F(3,3) when eligible), 1 direct, 2 Winograd */
 int anx_set_conv1_algo(int algo);
 int anx_get_conv1_algo(void);
-/* conv1 Winograd GEMM ring: 0 BK48 x 2 slots, 1 BK16 x 4, 2 BK16 x 6, 3 BK16 x 8 */
+/* conv1 Winograd GEMM: 0-3 32x32 MFMA rings (BK48 x 2, BK16 x 4/6/8), 4 16x16 MFMA 4 WG/CU (default) */
 int anx_conv1_wino_cfg(int cfg);
 /* profiling probes (wrong results): bit0 skip the output-transform fold, bit1 skip LDS-DMA refills */
 int anx_conv1_wino_probe(int bits);

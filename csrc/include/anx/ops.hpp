@@ -117,7 +117,7 @@ Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F);
 size_t conv1_wino_v_floats(const Conv1WinoPlan& w);  // V workspace [P][25][48]
 size_t conv1_wino_u_floats(int K);                   // transformed weights [25][K][48]
 void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u);
-// Tuning (A/B): ring shape 0..3 (conv1_wino.hip default_cfg). -1 on a bad id.
+// Tuning (A/B): GEMM configuration 0..4 (conv1_wino.hip default_cfg; 4 = default). -1 on a bad id.
 int conv1_wino_set_cfg(int cfg);
 // Cost probes for profiling only (results become wrong): bit0 skip the output-transform fold,
 // bit1 skip the LDS-DMA refills; bit4 = s_setprio around the MFMA slices (the default, 16).

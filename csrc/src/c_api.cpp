@@ -373,7 +373,7 @@ int anx_set_conv1_algo(int algo) {
 int anx_get_conv1_algo(void) { return static_cast<int>(anx::conv1_algo()); }
 int anx_conv1_wino_probe(int bits) { return anx::hip::conv1_wino_set_probe(bits); }
 int anx_conv1_wino_cfg(int cfg) {
-  if (anx::hip::conv1_wino_set_cfg(cfg) != 0) return fail("conv1 winograd cfg must be 0..3");
+  if (anx::hip::conv1_wino_set_cfg(cfg) != 0) return fail("conv1 winograd cfg must be 0..4");
   return 0;
 }
 int anx_wino_fused_cfg(int cfg) {

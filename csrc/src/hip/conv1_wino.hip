@@ -356,14 +356,185 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
   }
 }
 
-// Ring shapes (all fit two workgroups per CU): slices of BK channels x NST slots, NST-2 slices in
-// flight behind the one being consumed. 0: BK 48 x 2 (60 KiB), 1: BK 16 x 4 (40 KiB),
-// 2: BK 16 x 6 (60 KiB), 3: BK 16 x 8 (80 KiB). ANX_CONV1_WINO_CFG overrides (profiling).
-constexpr int kNumCfg = 4;
+
+// ---------------------------------------------------------------------------------------------
+// The same GEMM on v_mfma_f32_16x16x4_f32 for occupancy. A 32x32 wave tile needs 9 x 16 fold
+// registers (Y) and caps the kernel at 2 waves/SIMD; a 16-tile x 32-filter wave tile (two 16x16
+// blocks) needs 9 x 8, so 4 workgroups (16 waves) fit a CU. Workgroup = 64 tiles x 32 filters
+// (4 waves along the tiles), BK = 48 (one slice per point), 2 ring slots of 18 KiB.
+// 16x16x4 operands: lane l holds A[tile l&15][k] and B[k][filter l&15] for the k of lane group
+// g = l>>4; lane group g at MFMA step t (0..11) supplies k = 12g + t, so one ds_read_b128 per
+// operand feeds 4 steps. D: filter l&15, tile 4g + reg. The LDS image rotates the 16-B units of
+// row r by 3*((r>>1)&3) (mod 12): conflict-free for this read pattern (exhaustive check over the
+// four ds_read_b128 lane groups), applied on the DMA's global source address.
+constexpr int kBM16 = 64;
+__device__ __forceinline__ int rot16(int row) { return 3 * ((row >> 1) & 3); }
+
+__global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
+  constexpr int BK = kCh, U4 = BK / 4;            // 48 channels, 12 units per row
+  constexpr int A_PW = kBM16 * U4 / 64 / 4;       // 3 DMA instructions per wave
+  constexpr int B_INS = kBN * U4 / 64;            // 6
+  constexpr int A_FL = kBM16 * BK, B_FL = kBN * BK;
+  constexpr int STAGE = A_FL + B_FL;
+  constexpr int NS_LO = A_PW + B_INS / 4, NS_HI = NS_LO + 1;
+  using f32x2 = __attribute__((ext_vector_type(2))) float;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int nt = jb % a.n_ntiles;
+  const int pt = (jb / a.n_ntiles) * 8 + xcd;
+  if (pt >= a.n_ptiles) return;  // whole workgroup: before any DMA or barrier
+  const int p0 = pt * kBM16, n0 = nt * kBN;
+
+  int aoff[A_PW], boff[2];
+#pragma unroll
+  for (int j = 0; j < A_PW; ++j) {
+    const int U = (j * 4 + wave) * 64 + lane;
+    const int row = U / U4, su = U - row * U4;
+    const int u = (su + U4 - rot16(row)) % U4;  // logical unit stored at slot su
+    const int p = p0 + row;
+    aoff[j] = (p < a.P ? p : 0) * (kPts * kCh) + 4 * u;
+  }
+  const bool b_extra = wave < B_INS % 4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int q = wave + 4 * s;
+    const int U = (q < B_INS ? q : 0) * 64 + lane;
+    const int row = U / U4, su = U - row * U4;
+    boff[s] = (n0 + row) * kCh + 4 * ((su + U4 - rot16(row)) % U4);
+  }
+  lds_f32* lds3 = (lds_f32*)(lds);
+  auto issue = [&](int ab) {
+    const float* va = a.V + ab * kCh;
+    const float* ub = a.U + static_cast<size_t>(ab) * a.K * kCh;
+    lds_f32* st = lds3 + (ab & 1) * STAGE;
+#pragma unroll
+    for (int j = 0; j < A_PW; ++j) glds16(va + aoff[j], st + (j * 4 + wave) * 256);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      if (wave + 4 * s < B_INS) glds16(ub + boff[s], st + A_FL + (wave + 4 * s) * 256);
+  };
+
+  const int r16 = lane & 15, g = lane >> 4;
+  const int a_row = (wave * 16 + r16) * BK, b_row0 = A_FL + r16 * BK, b_row1 = A_FL + (16 + r16) * BK;
+  // slot (in floats) of logical unit 3g + s4 in rows of either rotation (A rows wave*16 + r16 and
+  // B rows r16, 16 + r16 share (row >> 1) & 3)
+  int rd[3];
+#pragma unroll
+  for (int s4 = 0; s4 < 3; ++s4) rd[s4] = 4 * ((3 * g + s4 + rot16(r16)) % U4);
+
+  f32x2 Y[9][2][2];  // [q][block][reg pair]
+#pragma unroll
+  for (int q = 0; q < 9; ++q)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) Y[q][c][0] = Y[q][c][1] = f32x2{0.f, 0.f};
+  f32x4 acc0[2] = {}, acc1[2] = {};
+
+  auto mfma_point = [&](int ab, f32x4 (&acc)[2]) {
+    const float* base = lds + (ab & 1) * STAGE;
+#pragma unroll
+    for (int s4 = 0; s4 < 3; ++s4) {
+      const f32x4 af = *reinterpret_cast<const f32x4*>(base + a_row + rd[s4]);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(base + b_row0 + rd[s4]);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(base + b_row1 + rd[s4]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], b0[s], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], b1[s], acc[1], 0, 0, 0);
+      }
+    }
+  };
+  auto fold = [&](int ab, f32x4 (&acc)[2]) {
+    const int aa = ab / kN5, bb = ab - aa * kN5;
+#pragma unroll
+    for (int i3 = 0; i3 < 3; ++i3)
+#pragma unroll
+      for (int j3 = 0; j3 < 3; ++j3) {
+        const float c = c_at33.v[i3][aa] * c_at33.v[j3][bb];
+        if (c != 0.f) {
+          const f32x2 c2 = {c, c};
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            Y[i3 * 3 + j3][cb][0] = __builtin_elementwise_fma(c2, f32x2{acc[cb][0], acc[cb][1]}, Y[i3 * 3 + j3][cb][0]);
+            Y[i3 * 3 + j3][cb][1] = __builtin_elementwise_fma(c2, f32x2{acc[cb][2], acc[cb][3]}, Y[i3 * 3 + j3][cb][1]);
+          }
+        }
+      }
+    acc[0] = acc[1] = f32x4{};
+  };
+  auto step = [&](int ab, f32x4 (&acc)[2]) {
+    wait_vmcnt<0>();  // this wave's DMA of point ab landed (it was issued one point ago)
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's; every wave is done with slot ab-1
+    asm volatile("" ::: "memory");
+    if (ab + 1 < kPts) issue(ab + 1);
+    if (a.probe & 16) __builtin_amdgcn_s_setprio(1);
+    mfma_point(ab, acc);
+    if (a.probe & 16) __builtin_amdgcn_s_setprio(0);
+  };
+  (void)b_extra;
+  (void)NS_HI;
+
+  issue(0);
+  for (int ab = 0; ab < kPts; ab += 2) {
+    step(ab, acc0);
+    if (ab > 0) fold(ab - 1, acc1);
+    if (ab + 1 < kPts) {
+      step(ab + 1, acc1);
+      fold(ab, acc0);
+    }
+  }
+  fold(kPts - 1, acc0);
+
+  // epilogue: per output position q, transpose the wave's 16 tiles x 32 filters through LDS and
+  // store 16-B filter groups (2 per lane)
+  __syncthreads();
+  constexpr int kTS = kBN + 4;
+  float* tr = lds + wave * 16 * kTS;
+  float bv[2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) bv[cb] = a.bias ? a.bias[n0 + cb * 16 + r16] : 0.f;
+  const OutView o = a.out;
+  int oy0[2], ox0[2], img[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = p0 + wave * 16 + ((k * 64 + lane) >> 3);
+    const int tj = p % a.tx, pq = p / a.tx;
+    oy0[k] = (p < a.P && !(a.probe & 8)) ? (pq % a.ty) * 3 : (1 << 28);
+    ox0[k] = tj * 3;
+    img[k] = pq / a.ty;
+  }
+  const int grp = 4 * (lane & 7);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        float v = Y[q][cb][reg >> 1][reg & 1] + bv[cb];
+        if (a.relu) v = fmaxf(v, 0.f);
+        tr[(4 * g + reg) * kTS + cb * 16 + r16] = v;
+      }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(tr + ((k * 64 + lane) >> 3) * kTS + grp);
+      const int oy = oy0[k] + q / 3, ox = ox0[k] + q % 3;
+      if (oy < a.H1 && ox < a.W1)
+        *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(img[k] * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) *
+                                               o.Cb + o.c_off + n0 + grp) = v4;
+    }
+  }
+}
+
+// GEMM configurations. 0-3: 32x32 MFMA, 128-tile workgroups, 2 per CU, ring of BK channels x NST
+// slots (NST-2 slices in flight behind the one being consumed): 0 BK 48 x 2 (60 KiB), 1 BK 16 x 4
+// (40 KiB), 2 BK 16 x 6 (60 KiB), 3 BK 16 x 8 (80 KiB). 4 (default): 16x16 MFMA, 64-tile
+// workgroups, 4 per CU (conv1_wino_gemm16_kernel; -6 % kernel time at 300 images,
+// profiles/r01_ab_conv1_wino_b300.jsonl). ANX_CONV1_WINO_CFG overrides (profiling).
+constexpr int kNumCfg = 5;
 int default_cfg() {
   const char* e = std::getenv("ANX_CONV1_WINO_CFG");
   const int v = e ? std::atoi(e) : -1;
-  return v >= 0 && v < kNumCfg ? v : 0;
+  return v >= 0 && v < kNumCfg ? v : 4;
 }
 int g_cfg = default_cfg();
 
@@ -480,6 +651,14 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
     case 1: return launch_gemm<16, 4>(a, s);
     case 2: return launch_gemm<16, 6>(a, s);
     case 3: return launch_gemm<16, 8>(a, s);
+    case 4: {  // 16x16 MFMA, 64-tile workgroups, 4 workgroups per CU
+      constexpr size_t lds = 2 * (kBM16 + kBN) * kCh * sizeof(float);
+      GemmArgs b = a;
+      b.n_ptiles = (a.P + kBM16 - 1) / kBM16;
+      const dim3 grid((b.n_ptiles + 7) / 8 * 8 * b.n_ntiles);
+      conv1_wino_gemm16_kernel<<<grid, 256, lds, s>>>(b);
+      return hipGetLastError();
+    }
     default: return launch_gemm<48, 2>(a, s);
   }
 }

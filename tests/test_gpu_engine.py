@@ -247,9 +247,9 @@ def test_conv1_wino_kernel_vs_torch(cuda, shape):
     torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 def test_conv1_wino_ring_configs(cuda, cfg):
-    """Every LDS ring configuration (BK 48 x 2 slots, BK 16 x 4/6/8) gives the same conv1."""
+    """Every GEMM configuration (32x32 MFMA: BK 48 x 2 slots, BK 16 x 4/6/8; 16x16 MFMA) gives the same conv1."""
     torch.manual_seed(5)
     x = torch.rand(4, 227, 227, 3, device=cuda)
     w = (torch.rand(96, 3, 11, 11) - 0.5) * 0.1
@@ -260,7 +260,7 @@ def test_conv1_wino_ring_configs(cuda, cfg):
         nat.call("anx_conv1_wino", x.data_ptr(), 4, 227, 227, w.data_ptr(), 96, 11, b.data_ptr(), y.data_ptr(), 1,
                  nat.stream_ptr(cuda))
     finally:
-        nat.call("anx_conv1_wino_cfg", 0)
+        nat.call("anx_conv1_wino_cfg", 4)
     ref = conv2d_nhwc(x.double(), w.to(cuda).double(), b.double(), 4, 0, relu=True)
     torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
 

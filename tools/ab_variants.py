@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--check", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    defaults = [-1, -1, 0, 7, 0, 0]
+    defaults = [-1, -1, 0, 7, 0, 4]
     arms = []
     for spec in a.arms.split(","):
         f = [int(v) for v in spec.split(":")]

@@ -44,7 +44,7 @@ def main():
             e1.synchronize()
             times[(cfg, probe)].append(e0.elapsed_time(e1) / a.iters)
     nat.call("anx_conv1_wino_probe", 16)
-    nat.call("anx_conv1_wino_cfg", 0)
+    nat.call("anx_conv1_wino_cfg", 4)
     for arm, t in times.items():
         t = sorted(t)
         print(json.dumps({"cfg": arm[0], "probe": arm[1], "batch": N, "ms_median": round(t[len(t) // 2], 4),
