@@ -377,7 +377,7 @@ int anx_conv1_wino_cfg(int cfg) {
   return 0;
 }
 int anx_wino_fused_cfg(int cfg) {
-  if (anx::hip::wino_set_fused_cfg(cfg) != 0) return fail("fused cfg must be 0..7");
+  if (anx::hip::wino_set_fused_cfg(cfg) != 0) return fail("fused cfg must be 0..15");
   return 0;
 }
 

@@ -488,18 +488,224 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same fused GEMM on v_mfma_f32_16x16x4_f32 with 8 waves: the 64-tile x 64-filter workgroup is
+// 4 (tiles) x 2 (filters) waves of 16 tiles x 32 filters (two 16x16 blocks). The fold registers
+// halve (9 x 8 per lane), so two 512-thread workgroups (16 waves, 4 per SIMD) fit a CU at the same
+// bytes per MAC as the 4-wave kernel above. Per K slice (48 channels) the 12 A and 12 B DMA
+// instructions are dealt 3 per wave. 16x16x4 operands: lane l holds A[tile l&15][k], B[k][filter
+// l&15] for its lane group g = l>>4, which at step t supplies k = 12g + t; D: filter l&15, tile
+// 4g + reg. LDS rows rotate their 16-B units by 3*((r>>1)&3) mod 12: conflict-free for these reads
+// (the rotation is applied to the DMA source address, as in conv1_wino.hip).
+__device__ __forceinline__ int rot16(int row) { return 3 * ((row >> 1) & 3); }
+
+template <int WMW, int WNW, bool XCD>
+__global__ void __launch_bounds__(64 * WMW * WNW, 4) wino_fused_glds16_kernel(FusedArgs a) {  // 4 waves/SIMD
+  using f32x2 = __attribute__((ext_vector_type(2))) float;
+  constexpr int NW = WMW * WNW;               // waves per workgroup
+  constexpr int BMT = 16 * WMW, BNT = 32 * WNW;  // tiles x filters per workgroup
+  constexpr int BK = 48, U4 = BK / 4;
+  constexpr int A_INS = BMT * U4 / 64, B_INS = BNT * U4 / 64, INS = A_INS + B_INS;
+  constexpr int PW = (INS + NW - 1) / NW;     // DMA slots per wave (the last may be empty)
+  constexpr int NS_HI = PW, NS_LO = INS % NW ? PW - 1 : PW;  // DMAs per slice: waves < INS % NW / the rest
+  constexpr int A_FL = BMT * BK, B_FL = BNT * BK;
+  constexpr int STAGE = A_FL + B_FL;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WMW, wn = wave / WMW;
+  const int g = blockIdx.z;
+  int pt, nt;
+  if constexpr (XCD) {
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    nt = j % a.n_ntiles;
+    pt = (j / a.n_ntiles) * 8 + xcd;
+    if (pt >= a.n_ptiles) return;  // whole workgroup, before any DMA or barrier
+  } else {
+    pt = blockIdx.x / a.n_ntiles;
+    nt = blockIdx.x - pt * a.n_ntiles;
+  }
+  const int p0 = pt * BMT, n0 = nt * BNT;
+  // DMA instruction q = wave + NW*i of the slice's INS (A_INS for A, then B_INS for B)
+  int off[PW], dst[PW];
+  bool isa[PW], has[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int q = wave + NW * i;
+    has[i] = q < INS;
+    isa[i] = q < A_INS;
+    const int qq = has[i] ? (isa[i] ? q : q - A_INS) : 0;
+    const int U = qq * 64 + lane;
+    const int row = U / U4, su = U - row * U4;
+    const int u = (su + U4 - rot16(row)) % U4;  // logical unit stored at slot su
+    if (isa[i]) {
+      const int p = p0 + row;
+      off[i] = (p < a.P ? p : 0) * (kN * kN) * a.C + 4 * u;
+    } else {
+      off[i] = (n0 + row) * a.kpad + 4 * u;
+    }
+    dst[i] = (isa[i] ? 0 : A_FL) + qq * 256;
+  }
+  const bool hi = wave < INS % NW || INS % NW == 0;
+  const float* Vg = a.V + g * a.Cg;
+  const int ksteps = a.kpad / BK;
+  const int total = kN * kN * ksteps;
+  lds_f32* lds3 = (lds_f32*)(lds);
+  auto issue = [&](int it) {
+    const int ab = it / ksteps, kk = (it - ab * ksteps) * BK;
+    const float* va = Vg + ab * a.C + kk;
+    const float* ub = a.U + static_cast<size_t>(ab * a.groups + g) * a.kpad_n * a.kpad + kk;
+    lds_f32* st = lds3 + (it % 3) * STAGE;
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      if (has[i]) glds16((isa[i] ? va : ub) + off[i], st + dst[i]);
+  };
+
+  const int r16 = lane & 15, lg = lane >> 4;
+  const int a_row = (wm * 16 + r16) * BK, b_row0 = A_FL + (wn * 32 + r16) * BK, b_row1 = b_row0 + 16 * BK;
+  int rd[3];
+#pragma unroll
+  for (int s4 = 0; s4 < 3; ++s4) rd[s4] = 4 * ((3 * lg + s4 + rot16(r16)) % U4);
+
+  f32x2 Y[9][2][2];  // [q][block][register pair]
+#pragma unroll
+  for (int q = 0; q < 9; ++q)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) Y[q][c][0] = Y[q][c][1] = f32x2{0.f, 0.f};
+  f32x4 acc0[2] = {}, acc1[2] = {};
+
+  auto mfma_slice = [&](int it, f32x4 (&acc)[2]) {
+    const float* base = lds + (it % 3) * STAGE;
+#pragma unroll
+    for (int s4 = 0; s4 < 3; ++s4) {
+      const f32x4 af = *reinterpret_cast<const f32x4*>(base + a_row + rd[s4]);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(base + b_row0 + rd[s4]);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(base + b_row1 + rd[s4]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], b0[s], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], b1[s], acc[1], 0, 0, 0);
+      }
+    }
+  };
+  auto fold = [&](int ab, f32x4 (&acc)[2]) {
+    const int aa = ab / kN, bb = ab - aa * kN;
+#pragma unroll
+    for (int i3 = 0; i3 < kM; ++i3)
+#pragma unroll
+      for (int j3 = 0; j3 < kM; ++j3) {
+        const float c = c_AT[i3][aa] * c_AT[j3][bb];
+        if (c != 0.f) {
+          const f32x2 c2 = {c, c};
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            Y[i3 * kM + j3][cb][0] = __builtin_elementwise_fma(c2, f32x2{acc[cb][0], acc[cb][1]}, Y[i3 * kM + j3][cb][0]);
+            Y[i3 * kM + j3][cb][1] = __builtin_elementwise_fma(c2, f32x2{acc[cb][2], acc[cb][3]}, Y[i3 * kM + j3][cb][1]);
+          }
+        }
+      }
+    acc[0] = acc[1] = f32x4{};
+  };
+  auto step = [&](int it, f32x4 (&acc)[2]) {
+    if (it + 1 >= total)
+      wait_vmcnt<0>();
+    else if (hi)
+      wait_vmcnt<NS_HI>();  // slice it+1's DMAs of this wave stay in flight
+    else
+      wait_vmcnt<NS_LO>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + 2 < total) issue(it + 2);
+    if (a.prio) __builtin_amdgcn_s_setprio(1);
+    mfma_slice(it, acc);
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
+  };
+
+  issue(0);
+  if (total > 1) issue(1);
+  int it = 0;
+  for (int ab = 0; ab < kN * kN; ab += 2) {
+    for (int ks = 0; ks < ksteps; ++ks, ++it) {
+      step(it, acc0);
+      if (ks == 0 && ab > 0) fold(ab - 1, acc1);
+    }
+    if (ab + 1 < kN * kN) {
+      for (int ks = 0; ks < ksteps; ++ks, ++it) {
+        step(it, acc1);
+        if (ks == 0) fold(ab, acc0);
+      }
+    }
+  }
+  fold(kN * kN - 1, acc0);
+
+  // epilogue: per output position q, transpose the wave's 16 tiles x 32 filters through LDS and
+  // store 16-B filter groups (2 per lane)
+  __syncthreads();
+  constexpr int kTS = 32 + 4;
+  float* tr = lds + wave * 16 * kTS;
+  const int fb = n0 + wn * 32;
+  float bv[2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) bv[cb] = (a.bias && fb + cb * 16 + r16 < a.Kg) ? a.bias[g * a.Kg + fb + cb * 16 + r16] : 0.f;
+  int oy0[2], ox0[2], img[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = p0 + wm * 16 + ((k * 64 + lane) >> 3);
+    const int tj = p % a.tx, pq = p / a.tx;
+    oy0[k] = p < a.P ? (pq % a.ty) * kM : (1 << 28);  // out of range: never stored
+    ox0[k] = tj * kM;
+    img[k] = pq / a.ty;
+  }
+  const int grp = 4 * (lane & 7);
+  const bool fin = fb + grp < a.Kg;
+#pragma unroll
+  for (int q = 0; q < kM * kM; ++q) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        float v = Y[q][cb][reg >> 1][reg & 1] + bv[cb];
+        if (a.relu) v = fmaxf(v, 0.f);
+        tr[(4 * lg + reg) * kTS + cb * 16 + r16] = v;
+      }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(tr + ((k * 64 + lane) >> 3) * kTS + grp);
+      const int oy = oy0[k] + q / kM, ox = ox0[k] + q % kM;
+      if (fin && oy < a.Ho && ox < a.Wo)
+        *reinterpret_cast<f32x4*>(a.y + ((static_cast<size_t>(img[k]) * a.Ho + oy) * a.Wo + ox) * a.K + g * a.Kg + fb +
+                                  grp) = v4;
+    }
+  }
+}
+
 // fused-kernel configuration: bit0 = BK 48 (else 32), bit1 = XCD-aware block order, bit2 = LDS-DMA
 // ring (when Cg % BK == 0). ANX_WINO_FUSED_CFG overrides the default (profiling).
 int default_fused_cfg() {
   const char* e = std::getenv("ANX_WINO_FUSED_CFG");
   const int v = e ? std::atoi(e) : -1;
-  return v >= 0 && v <= 7 ? v : 7;
+  return v >= 0 && v <= 15 ? v : 7;
 }
 int g_fused_cfg = default_fused_cfg();
 int g_prio = [] {  // default on: -1 % measured at 300 images (ANX_WINO_PRIO=0 disables)
   const char* e = std::getenv("ANX_WINO_PRIO");
   return e ? std::atoi(e) : 1;
 }();
+
+template <int WMW, int WNW, bool XCD>
+hipError_t launch_glds16(FusedArgs a, hipStream_t s) {
+  constexpr int BMT = 16 * WMW, BNT = 32 * WNW;
+  constexpr int kLds = 3 * (BMT + BNT) * 48 * sizeof(float);  // 3-slot ring of A|B tiles
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wino_fused_glds16_kernel<WMW, WNW, XCD>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      kLds);
+  if (attr != hipSuccess) return attr;
+  a.n_ptiles = (a.P + BMT - 1) / BMT;
+  a.n_ntiles = (a.Kg + BNT - 1) / BNT;
+  if (a.n_ntiles * BNT > a.kpad_n) return hipErrorInvalidValue;  // B rows past the packed weights
+  const dim3 grid((XCD ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, a.groups);
+  wino_fused_glds16_kernel<WMW, WNW, XCD><<<grid, 64 * WMW * WNW, kLds, s>>>(a);
+  return hipGetLastError();
+}
 
 template <int BK, bool XCD>
 hipError_t launch_glds(const FusedArgs& a, dim3 grid, hipStream_t s) {
@@ -519,7 +725,7 @@ unsigned grid_for(long n) {
 }  // namespace
 
 int wino_set_fused_cfg(int cfg) {
-  if (cfg < 0 || cfg > 7) return -1;
+  if (cfg < 0 || cfg > 15) return -1;
   g_fused_cfg = cfg;
   return 0;
 }
@@ -612,6 +818,12 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
   a.n_ntiles = (a.Kg + kFB - 1) / kFB;
   if (a.n_ntiles * kFB > a.kpad_n || a.Cg % 4) return hipErrorInvalidValue;
   const bool xcd = (g_fused_cfg & 2) != 0;
+  if ((g_fused_cfg & 8) && a.Cg % 48 == 0 && a.kpad == a.Cg && a.Kg % 32 == 0) {
+    // 16x16 MFMA: bit0 set -> 64 tiles x 64 filters, 8 waves, 2 workgroups/CU; bit0 clear -> 64 tiles
+    // x 128 filters, 16 waves, 1 workgroup/CU (a quarter fewer operand bytes per MAC)
+    if (g_fused_cfg & 1) return xcd ? launch_glds16<4, 2, true>(a, s) : launch_glds16<4, 2, false>(a, s);
+    if (a.Kg % 128 == 0) return xcd ? launch_glds16<4, 4, true>(a, s) : launch_glds16<4, 4, false>(a, s);
+  }
   if (g_fused_cfg & 4) {
     // LDS-DMA ring: BK 48 (72 KiB, 2 workgroups/CU) or BK 32 (48 KiB, 3/CU)
     const int bk = (g_fused_cfg & 1) ? 48 : 32;

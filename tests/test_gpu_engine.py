@@ -305,3 +305,17 @@ def test_conv1_winograd_golden(cuda, algo1, mode, gold):
     m = AlexNetBlocks(device=cuda, lrn_mode=mode)
     y = m(init_input(1, "const").to(cuda)).cpu()
     assert y.flatten()[:5].tolist() == pytest.approx(gold, abs=2e-4)
+
+
+@pytest.mark.parametrize("cfg", [1, 5, 7, 12, 13, 14, 15])  # register ring / LDS-DMA 32x32 / 16x16 64x128, 64x64; +-XCD
+@pytest.mark.parametrize("groups2", [1, 2])
+def test_winograd_fused_configs(cuda, algo, cfg, groups2):
+    algo(2)
+    nat.call("anx_wino_fused_cfg", cfg)
+    try:
+        m = AlexNetBlocks(device=cuda, init="rand", seed=80 + cfg, max_batch=9, groups2=groups2)
+        x = init_input(9, "rand", seed=80 + cfg)
+        y = m(x.to(cuda)).cpu().double()
+    finally:
+        nat.call("anx_wino_fused_cfg", 7)
+    torch.testing.assert_close(y, blocks_forward(x, m.weights, m.b1, m.b2), rtol=2e-5, atol=2e-6)
