@@ -50,6 +50,7 @@ struct Options {
   std::string impl = "mfma";
   std::string conv2_algo = "auto";  // auto | direct | winograd
   std::string conv1_algo = "auto";  // auto | direct | winograd
+  std::string transport = "auto";   // v5 device traffic: auto | rccl | peer (IPC + hipMemcpyPeerAsync)
   bool check = false;
   bool json = true;
   std::string weights;  // directory with raw fp32 w1/b1/w2/b2 .bin (overrides --init for weights)
@@ -60,7 +61,7 @@ struct Options {
                "%s\nusage: anx --version v1|v2.1|v2.2|v3|v4|v5 [--batch N] [--init const|rand] [--seed S]\n"
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
                "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd]\n"
-               "           [--conv1-algo auto|direct|winograd] [--check]\n"
+               "           [--conv1-algo auto|direct|winograd] [--transport auto|rccl|peer] [--check]\n"
                "           [--weights DIR] [--no-json]\n",
                msg);
   std::exit(2);
@@ -85,6 +86,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--impl") o.impl = val();
     else if (a == "--conv2-algo") o.conv2_algo = val();
     else if (a == "--conv1-algo") o.conv1_algo = val();
+    else if (a == "--transport") o.transport = val();
     else if (a == "--check") o.check = true;
     else if (a == "--no-json") o.json = false;
     else if (a == "--weights") o.weights = val();
@@ -542,6 +544,187 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
 }
 
 // ------------------------------------------------------------------------------ V5 (device-resident RCCL)
+// ---- V5 peer transport: every device byte moves by hipMemcpyPeerAsync straight into the
+// destination rank's buffer (scatter rows into its input rows, input halos into its tile, pool1
+// halos into its conv2 window, output rows into rank 0's result), through IPC-mapped allocations
+// (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles exchanged over the host comm). The writer
+// pushes on its own copy stream; a host barrier after each phase orders the pushes against the
+// readers. No host staging and no RCCL, so ranks may also share a GPU (the peer copy is then a
+// same-device copy) — the configuration the one-GPU test box can run.
+struct PeerMap {
+  std::vector<float*> ptr;  // every rank's buffer, mapped into this process (own: the original)
+  std::vector<void*> opened;
+  void close() {
+    for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+    opened.clear();
+  }
+  ~PeerMap() { close(); }
+};
+
+// Share `mine` (a hipMalloc base pointer, or nullptr) of every rank, or only of `root` if >= 0.
+void ipc_share(HostComm& c, float* mine, PeerMap& m, int root = -1) {
+  const int np = c.size(), rank = c.rank();
+  m.ptr.assign(np, nullptr);
+  for (int r = 0; r < np; ++r) {
+    if (root >= 0 && r != root) continue;
+    hipIpcMemHandle_t h{};
+    if (r == rank) hip_check(hipIpcGetMemHandle(&h, mine), "hipIpcGetMemHandle");
+    c.bcast(&h, sizeof h, r);
+    if (r == rank) {
+      m.ptr[r] = mine;
+    } else {
+      void* p = nullptr;
+      hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+      m.opened.push_back(p);
+      m.ptr[r] = static_cast<float*>(p);
+    }
+  }
+}
+
+// Copy `nrows` rows of N images from (src, src_dev) to (dst, dst_dev), row windows as copy_rows():
+// one hipMemcpyPeerAsync per image (the images are strided differently on both sides).
+void peer_rows(float* dst, int dst_dev, int dst_rows, int dst_off, const float* src, int src_dev, int src_rows,
+               int src_off, int nrows, size_t row_floats, int N, hipStream_t s) {
+  if (nrows <= 0 || N <= 0) return;
+  const size_t w = static_cast<size_t>(nrows) * row_floats * sizeof(float);
+  const size_t dp = static_cast<size_t>(dst_rows) * row_floats * sizeof(float);
+  const size_t sp = static_cast<size_t>(src_rows) * row_floats * sizeof(float);
+  char* d = reinterpret_cast<char*>(dst + static_cast<size_t>(dst_off) * row_floats);
+  const char* q = reinterpret_cast<const char*>(src + static_cast<size_t>(src_off) * row_floats);
+  for (int n = 0; n < N; ++n)
+    hip_check(hipMemcpyPeerAsync(d + n * dp, dst_dev, q + n * sp, src_dev, w, s), "hipMemcpyPeerAsync");
+}
+
+int run_v5_peer(Setup& s, HostComm& c, int ndev) {
+  const int N = s.o.batch, rank = c.rank(), np = c.size();
+  const Decomp mode = s.o.decomp == "overlap" ? Decomp::Overlap : Decomp::PerLayer;
+  const DecompPlan plan = make_plan(s.d.H, s.d.W, np, mode, s.b1, s.b2);
+  const TilePlan& t = plan.tiles[rank];
+  const RowRange own = plan.owned_in[rank];
+  const int dev = s.ri.local_rank % ndev;
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  Phases cold, warm;
+  c.barrier();
+  const double t0 = now_ms();
+  double a = now_ms();
+  if (rank == 0) fill_input(s);
+  bcast_weights(c, s.w);
+  std::vector<int> devs(np, 0);
+  for (int r = 0; r < np; ++r) {
+    int d = dev;
+    c.bcast(&d, sizeof d, r);
+    devs[r] = d;
+  }
+  hipStream_t st, cs;
+  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+  hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
+  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma);
+  auto dalloc = [](size_t n) {
+    float* p = nullptr;
+    hip_check(hipMalloc(&p, std::max<size_t>(1, n) * 4), "hipMalloc");
+    return p;
+  };
+  float* d_x = rank == 0 ? dalloc(s.x.size()) : nullptr;
+  float* d_own = dalloc(static_cast<size_t>(N) * std::max(1, own.size()) * s.in_row);
+  float* d_tile = dalloc(static_cast<size_t>(N) * std::max(1, t.in.size()) * s.in_row);
+  float* d_y = dalloc(static_cast<size_t>(N) * std::max(1, t.out.size()) * s.out_row);
+  float* d_yfull = rank == 0 ? dalloc(static_cast<size_t>(N) * s.d.Hp2 * s.out_row) : nullptr;
+  // the conv2 window exists once stage1 has run on this tile geometry: run it once on zeros
+  if (!t.out.empty()) {
+    hip_check(hipMemsetAsync(d_tile, 0, static_cast<size_t>(N) * t.in.size() * s.in_row * 4, st), "memset");
+    hip_check(eng.stage1(d_tile, N, t, st), "stage1");
+  }
+  hip_check(hipStreamSynchronize(st), "sync");
+  PeerMap m_own, m_tile, m_win, m_out;
+  ipc_share(c, d_own, m_own);
+  ipc_share(c, d_tile, m_tile);
+  ipc_share(c, t.out.empty() ? d_tile : eng.q2_row_ptr(t, 0, t.q.lo), m_win);  // window base = allocation base
+  ipc_share(c, d_yfull, m_out, 0);
+  if (rank == 0)
+    hip_check(hipMemcpy(d_x, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice), "H2D input");
+  std::vector<float> y_host(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
+  hip_check(hipDeviceSynchronize(), "sync");
+  c.barrier();
+  cold.add("setup", now_ms() - a);
+  const size_t rowf = eng.q2_row_floats();
+
+  auto phase_end = [&](hipStream_t q) {  // this rank's pushes landed, then everyone's
+    hip_check(hipStreamSynchronize(q), "sync");
+    c.barrier();
+  };
+  auto step = [&](Phases& ph) {
+    // scatter: rank 0 pushes each rank's owned input rows into that rank's d_own
+    double q = now_ms();
+    if (rank == 0)
+      for (int r = 0; r < np; ++r) {
+        const RowRange o = plan.owned_in[r];
+        if (!o.empty())
+          peer_rows(m_own.ptr[r], devs[r], o.size(), 0, d_x, dev, s.d.H, o.lo, o.size(), s.in_row, N, cs);
+      }
+    phase_end(cs);
+    ph.add("scatter", now_ms() - q);
+    // input halos: the owner pushes rows into the neighbour's tile; own rows locally
+    q = now_ms();
+    for (const HaloXfer& h : plan.in_halos)
+      if (h.src == rank) {
+        const TilePlan& td = plan.tiles[h.dst];
+        peer_rows(m_tile.ptr[h.dst], devs[h.dst], td.in.size(), h.rows.lo - td.in.lo, d_own, dev, own.size(),
+                  h.rows.lo - own.lo, h.rows.size(), s.in_row, N, cs);
+      }
+    if (!t.out.empty()) {
+      const int lo = std::max(own.lo, t.in.lo), up = std::min(own.hi, t.in.hi);
+      copy_rows(d_tile, t.in.size(), lo - t.in.lo, d_own, own.size(), lo - own.lo, up - lo, s.in_row, N, true, cs);
+    }
+    phase_end(cs);
+    ph.add("halo_in", now_ms() - q);
+    q = now_ms();
+    if (!t.out.empty()) hip_check(eng.stage1(d_tile, N, t, st), "stage1");
+    phase_end(st);  // every window holds its own pool1 rows before any neighbour writes halos
+    ph.add("compute", now_ms() - q);
+    // pool1 halos: the producer pushes rows from its window into the neighbour's window
+    q = now_ms();
+    if (mode == Decomp::PerLayer) {
+      for (const HaloXfer& h : plan.p1_halos)
+        if (h.src == rank) {
+          const TilePlan& td = plan.tiles[h.dst];
+          peer_rows(m_win.ptr[h.dst], devs[h.dst], td.q.size(), h.rows.lo - td.q.lo, eng.q2_row_ptr(t, 0, t.q.lo),
+                    dev, t.q.size(), h.rows.lo - t.q.lo, h.rows.size(), rowf, N, cs);
+        }
+      phase_end(cs);
+    }
+    ph.add("halo_p1", now_ms() - q);
+    q = now_ms();
+    if (!t.out.empty()) hip_check(eng.stage2(N, t, d_y, st), "stage2");
+    hip_check(hipStreamSynchronize(st), "sync");
+    ph.add("compute", now_ms() - q);
+    // gather: every rank pushes its output rows into rank 0's full result
+    q = now_ms();
+    if (!t.out.empty())
+      peer_rows(m_out.ptr[0], devs[0], s.d.Hp2, t.out.lo, d_y, dev, t.out.size(), 0, t.out.size(), s.out_row, N, cs);
+    phase_end(cs);
+    if (rank == 0) {
+      hip_check(hipMemcpyAsync(y_host.data(), d_yfull, y_host.size() * 4, hipMemcpyDeviceToHost, cs), "D2H");
+      hip_check(hipStreamSynchronize(cs), "sync");
+    }
+    ph.add("gather", now_ms() - q);
+  };
+  step(cold);
+  double cold_ms = now_ms() - t0;
+  for (int i = 0; i < s.o.iters; ++i) step(warm);
+  double tm[2] = {cold_ms, s.o.iters ? warm.total() / s.o.iters : 0};
+  c.allreduce_max(tm, 2);
+  if (rank == 0) report(s, np, y_host, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y_host) : -1);
+  c.barrier();  // nobody writes into a peer's buffers any more: unmap, then free
+  for (PeerMap* m : {&m_own, &m_tile, &m_win, &m_out}) m->close();
+  c.barrier();  // every peer has unmapped this rank's buffers before they are freed
+  for (float* p : {d_x, d_own, d_tile, d_y, d_yfull})
+    if (p) (void)hipFree(p);
+  (void)hipStreamDestroy(st);
+  (void)hipStreamDestroy(cs);
+  c.barrier();
+  return 0;
+}
+
 int run_v5(Setup& s, HostComm& c) {
   const int N = s.o.batch, rank = c.rank(), np = c.size();
   const Decomp mode = s.o.decomp == "overlap" ? Decomp::Overlap : Decomp::PerLayer;
@@ -551,7 +734,10 @@ int run_v5(Setup& s, HostComm& c) {
   int ndev = 0;
   hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
   if (ndev < 1) throw std::runtime_error("v5 needs a GPU");
-  if (np > ndev) throw std::runtime_error("v5 needs one GPU per rank (RCCL rejects shared devices)");
+  const std::string tr = s.o.transport == "auto" ? (np <= ndev ? "rccl" : "peer") : s.o.transport;
+  if (tr == "peer") return run_v5_peer(s, c, ndev);
+  if (tr != "rccl") throw std::runtime_error("--transport must be auto, rccl or peer");
+  if (np > ndev) throw std::runtime_error("v5 over RCCL needs one GPU per rank (use --transport peer to share)");
   const int dev = s.ri.local_rank % ndev;
   Phases cold, warm;
   c.barrier();

@@ -102,6 +102,24 @@ def test_native_v4_shared_gpu(cuda, np_):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("np_,decomp", [(2, "per_layer"), (3, "per_layer"), (4, "per_layer"), (2, "overlap")])
+def test_native_v5_peer_transport(cuda, np_, decomp):
+    """V5 with every device byte moved by hipMemcpyPeerAsync into IPC-mapped neighbour buffers
+    (scatter, input halos, pool1 halos between conv2 windows, gather): ranks share the box's GPU,
+    and the output is bit-identical to the single-GPU run (direct convs)."""
+    d = ["--conv2-algo", "direct", "--conv1-algo", "direct"]
+    ref, _ = native(["--version", "v3", "--init", "rand", "--seed", "6", "--batch", "3", *d])
+    rec, out = native(["--version", "v5", "--transport", "peer", "--decomp", decomp, "--init", "rand", "--seed", "6",
+                       "--batch", "3", "--iters", "2", "--lrn-alpha-mode", "raw", *d], np_)
+    assert "Final Output Shape: 13x13x256" in out.stdout or rec["shape"] == [13, 13, 256]
+    assert rec["checksum"] == ref["checksum"]
+    # default (Winograd) convs: equal to the fp64 oracle within fp32 error
+    rec, _ = native(["--version", "v5", "--transport", "peer", "--init", "rand", "--seed", "6", "--batch", "3",
+                     "--check"], np_)
+    assert rec["max_abs_err"] < 1e-3
+
+
+@pytest.mark.gpu
 def test_native_v5_single_rank(cuda):
     rec, _ = native(["--version", "v5", "--init", "rand", "--batch", "4", "--check", "--iters", "2"], 1)
     assert rec["max_abs_err"] < 1e-3
