@@ -540,12 +540,12 @@ int g_cfg = default_cfg();
 
 template <int BK, int NST>
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
-  constexpr size_t lds = Ring<BK, NST>::kBytes;
+  constexpr size_t lds_bytes = Ring<BK, NST>::kBytes;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_wino_gemm_kernel<BK, NST>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (attr != hipSuccess) return attr;
   const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
-  conv1_wino_gemm_kernel<BK, NST><<<grid, 256, lds, s>>>(a);
+  conv1_wino_gemm_kernel<BK, NST><<<grid, 256, lds_bytes, s>>>(a);
   return hipGetLastError();
 }
 
@@ -652,11 +652,11 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
     case 2: return launch_gemm<16, 6>(a, s);
     case 3: return launch_gemm<16, 8>(a, s);
     case 4: {  // 16x16 MFMA, 64-tile workgroups, 4 workgroups per CU
-      constexpr size_t lds = 2 * (kBM16 + kBN) * kCh * sizeof(float);
+      constexpr size_t lds_bytes = 2 * (kBM16 + kBN) * kCh * sizeof(float);
       GemmArgs b = a;
       b.n_ptiles = (a.P + kBM16 - 1) / kBM16;
       const dim3 grid((b.n_ptiles + 7) / 8 * 8 * b.n_ntiles);
-      conv1_wino_gemm16_kernel<<<grid, 256, lds, s>>>(b);
+      conv1_wino_gemm16_kernel<<<grid, 256, lds_bytes, s>>>(b);
       return hipGetLastError();
     }
     default: return launch_gemm<48, 2>(a, s);
