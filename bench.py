@@ -55,7 +55,8 @@ def parse():
     ap.add_argument("--no-gather", action="store_true", help="leave outputs on their ranks")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu = gloo rehearsal (tests only)")
     ap.add_argument("--graph", type=int, default=0,
-                    help="1-GPU step as one captured HIP graph (replayed each step): 1 on, 0 off (default; measured\n                    "equal to eager launches at 300 images: the step is GPU-bound), -1 auto (on for 1 GPU)")
+                    help="1-GPU step as one captured HIP graph replayed each step: 1 on, 0 off (default; "
+                         "measured equal to eager launches at 300 images, the step is GPU-bound), -1 auto")
     ap.add_argument("--model", default="blocks", choices=["blocks", "full"],
                     help="blocks = the headline AlexNet Blocks1-2 fp32; full = full AlexNet bf16 extension")
     return ap.parse_args()
