@@ -96,6 +96,8 @@ int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff
 int anx_conv_force_variant(int kind, int id);
 /* Conv2 (5x5 s1) algorithm on the MFMA path: 0 auto (Winograd F(3,5) when eligible), 1 direct, 2 Winograd */
 int anx_set_conv2_algo(int algo);
+// images per launch of stage 1 / stage 2 (0 = whole batch); see anx::set_stage_chunks
+int anx_set_stage_chunks(int stage1, int stage2);
 int anx_get_conv2_algo(void);
 /* Conv1 (11x11 s4) algorithm on the MFMA path: 0 auto (polyphase Winograd F(3,3) when eligible), 1 direct, 2 Winograd */
 int anx_set_conv1_algo(int algo);
@@ -110,6 +112,8 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
                    float* y, int relu, void* stream);
 /* fused Winograd kernel tuning: bit0 K-slice 48 (else 32), bit1 XCD-aware order, bit2 LDS-DMA ring (default 7) */
 int anx_wino_fused_cfg(int cfg);
+// Conv2 Winograd kernel flags (anx::hip::wino_set_prio): bit0 setprio, bit1 NT V stores, bits4-7 cost probes
+int anx_wino_prio(int bits);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

@@ -34,6 +34,12 @@ ConvAlgo conv2_algo();
 // row decompositions; Winograd tile origins move with the row split, ~1e-7 relative).
 void set_conv1_algo(ConvAlgo a);
 ConvAlgo conv1_algo();
+// Images per launch of stage 1 (Conv1 + Pool1) and stage 2 (Conv2 + Pool2 + LRN); 0 = the whole
+// batch (up to the 32-bit-index chunk). Smaller chunks reuse one set of transform/conv buffers per
+// chunk, so the Winograd V buffers can stay in the 256 MiB Infinity Cache between the transform that
+// writes them and the GEMM that reads them. Process-wide; env ANX_CHUNK1 / ANX_CHUNK2.
+void set_stage_chunks(int stage1, int stage2);
+int stage_chunk(int stage);
 
 struct HostWeights {
   std::vector<float> w1, b1, w2, b2;  // KCFF weights, biases

@@ -102,6 +102,10 @@ hipError_t wino_output(const WinoPlan& w, const float* Mt, const float* bias, fl
 // Tuning (A/B): bit0 = K-slice 48 instead of 32, bit1 = XCD-aware block order, bit2 = LDS-DMA ring.
 // Default 7 (measured at 300 images: ring +17 %, BK 48 +3 %, XCD order +1 %).
 int wino_set_fused_cfg(int cfg);
+// bit0 s_setprio around MFMA slices, bit8 interleaved output fold (default 257); bit1 non-temporal V
+// stores; bits 4-7 cost probes
+// of the LDS-DMA fused kernel (wrong results): no fold / no refills / no barrier / no stores
+int wino_set_prio(int bits);
 // Batched GEMM + output transform in one kernel (M stays in registers); U packed as for w.gemm.
 hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
                       hipStream_t s);

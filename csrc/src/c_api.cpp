@@ -371,11 +371,17 @@ int anx_set_conv1_algo(int algo) {
   return 0;
 }
 int anx_get_conv1_algo(void) { return static_cast<int>(anx::conv1_algo()); }
+int anx_set_stage_chunks(int stage1, int stage2) {
+  if (stage1 < 0 || stage2 < 0) return fail("stage chunks must be >= 0 (0 = whole batch)");
+  anx::set_stage_chunks(stage1, stage2);
+  return 0;
+}
 int anx_conv1_wino_probe(int bits) { return anx::hip::conv1_wino_set_probe(bits); }
 int anx_conv1_wino_cfg(int cfg) {
   if (anx::hip::conv1_wino_set_cfg(cfg) != 0) return fail("conv1 winograd cfg must be 0..4");
   return 0;
 }
+int anx_wino_prio(int bits) { return anx::hip::wino_set_prio(bits); }
 int anx_wino_fused_cfg(int cfg) {
   if (anx::hip::wino_set_fused_cfg(cfg) != 0) return fail("fused cfg must be 0..15");
   return 0;

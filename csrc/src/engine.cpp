@@ -2,6 +2,7 @@
 #include "anx/engine.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -38,7 +39,17 @@ T* dev_upload(const std::vector<T>& h) {
 namespace {
 ConvAlgo g_conv2_algo = ConvAlgo::Auto;
 ConvAlgo g_conv1_algo = ConvAlgo::Auto;
+int env_int(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? std::max(0, std::atoi(e)) : 0;
+}
+int g_chunk[2] = {env_int("ANX_CHUNK1"), env_int("ANX_CHUNK2")};
 }  // namespace
+void set_stage_chunks(int stage1, int stage2) {
+  g_chunk[0] = std::max(0, stage1);
+  g_chunk[1] = std::max(0, stage2);
+}
+int stage_chunk(int stage) { return g_chunk[stage == 2 ? 1 : 0]; }
 void set_conv2_algo(ConvAlgo a) { g_conv2_algo = a; }
 ConvAlgo conv2_algo() { return g_conv2_algo; }
 void set_conv1_algo(ConvAlgo a) { g_conv1_algo = a; }
@@ -145,8 +156,9 @@ hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStr
   const ConvSpec& k1 = b1_.conv;
   const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
   const size_t q_img = q2_image_stride_floats(t);
-  for (int n0 = 0; n0 < N; n0 += chunk_) {
-    const int n = std::min(chunk_, N - n0);
+  const int chunk = g_chunk[0] > 0 ? std::min(chunk_, g_chunk[0]) : chunk_;
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int n = std::min(chunk, N - n0);
     const float* xc = x + n0 * in_img;
     float* qc = q2_ + n0 * q_img;
     if (impl_ == Impl::Mfma && wv1_ != nullptr && g_conv1_algo != ConvAlgo::Direct) {
@@ -185,8 +197,9 @@ hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t 
   const ConvSpec& k2 = b2_.conv;
   const size_t q_img = q2_image_stride_floats(t);
   const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
-  for (int n0 = 0; n0 < N; n0 += chunk_) {
-    const int n = std::min(chunk_, N - n0);
+  const int chunk = g_chunk[1] > 0 ? std::min(chunk_, g_chunk[1]) : chunk_;
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int n = std::min(chunk, N - n0);
     const float* qc = q2_ + n0 * q_img;
     float* yc = y + n0 * y_img;
     const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && g_conv2_algo != ConvAlgo::Direct;

@@ -123,6 +123,19 @@ constexpr AT33 make_at33() {
   return t;
 }
 __constant__ AT33 c_at33 = make_at33();  // indexed by the runtime point: scalar loads
+// fold coefficients per point: coef[ab][i*3 + j] = A^T[i][a] * A^T[j][b] (the float product the
+// runtime-indexed fold computes)
+struct Coef33 {
+  float v[kPts][9];
+};
+constexpr Coef33 make_coef33() {
+  Coef33 t{};
+  for (int ab = 0; ab < kPts; ++ab)
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) t.v[ab][i * 3 + j] = w33::kAT[i][ab / kN5] * w33::kAT[j][ab % kN5];
+  return t;
+}
+__constant__ Coef33 c_coef33 = make_coef33();
 
 struct GemmArgs {
   const float* V;     // [P][25][48]
@@ -370,6 +383,7 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
 constexpr int kBM16 = 64;
 __device__ __forceinline__ int rot16(int row) { return 3 * ((row >> 1) & 3); }
 
+template <bool IL>
 __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
   constexpr int BK = kCh, U4 = BK / 4;            // 48 channels, 12 units per row
   constexpr int A_PW = kBM16 * U4 / 64 / 4;       // 3 DMA instructions per wave
@@ -471,16 +485,59 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
     mfma_point(ab, acc);
     if (a.probe & 16) __builtin_amdgcn_s_setprio(0);
   };
+  // IL: the fold of point fab rides inside the MFMAs of the next point, branch-free (zero
+  // coefficients included: +0 leaves Y bit-identical), 3 packed FMAs per MFMA pair, so the VALU
+  // work issues while the matrix pipe is busy instead of after it.
+  auto point_fold = [&](int ab, f32x4 (&acc)[2], int fab, f32x4 (&facc)[2]) {
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (ab + 1 < kPts) issue(ab + 1);
+    if (a.probe & 16) __builtin_amdgcn_s_setprio(1);
+    float cq[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) cq[q] = c_coef33.v[fab][q];
+    const float* base = lds + (ab & 1) * STAGE;
+#pragma unroll
+    for (int s4 = 0; s4 < 3; ++s4) {
+      const f32x4 af = *reinterpret_cast<const f32x4*>(base + a_row + rd[s4]);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(base + b_row0 + rd[s4]);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(base + b_row1 + rd[s4]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], b0[s], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], b1[s], acc[1], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int j = (s4 * 4 + s) * 3 + t;  // 0..35 = (q, cb, pair)
+          const int q = j >> 2, cb = (j >> 1) & 1, pr = j & 1;
+          Y[q][cb][pr] = __builtin_elementwise_fma(f32x2{cq[q], cq[q]}, f32x2{facc[cb][2 * pr], facc[cb][2 * pr + 1]},
+                                                   Y[q][cb][pr]);
+        }
+      }
+    }
+    facc[0] = facc[1] = f32x4{};
+    if (a.probe & 16) __builtin_amdgcn_s_setprio(0);
+  };
   (void)b_extra;
   (void)NS_HI;
 
   issue(0);
-  for (int ab = 0; ab < kPts; ab += 2) {
-    step(ab, acc0);
-    if (ab > 0) fold(ab - 1, acc1);
-    if (ab + 1 < kPts) {
-      step(ab + 1, acc1);
-      fold(ab, acc0);
+  if constexpr (IL) {
+    // acc1 is zero before point 1: the first fold adds +0 and changes nothing
+    for (int ab = 0; ab + 1 < kPts; ab += 2) {
+      point_fold(ab, acc0, ab > 0 ? ab - 1 : 0, acc1);
+      point_fold(ab + 1, acc1, ab, acc0);
+    }
+    point_fold(kPts - 1, acc0, kPts - 2, acc1);
+  } else {
+    for (int ab = 0; ab < kPts; ab += 2) {
+      step(ab, acc0);
+      if (ab > 0) fold(ab - 1, acc1);
+      if (ab + 1 < kPts) {
+        step(ab + 1, acc1);
+        fold(ab, acc0);
+      }
     }
   }
   fold(kPts - 1, acc0);
@@ -553,7 +610,9 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
 
 int g_probe = [] {
   const char* e = std::getenv("ANX_CONV1_WINO_PROBE");
-  return e ? std::atoi(e) : 16;  // bit4 (s_setprio around the MFMA slices) on: -1 % at 300 images
+  // bit4 (s_setprio around the MFMA slices) on: -1 % at 300 images. bit6 (interleaved fold,
+  // conv1_wino_gemm16_kernel<true>) is off: +22 us at 300 images (profiles/r01_ab_conv1_ilfold_b300.jsonl)
+  return e ? std::atoi(e) : 16;
 }();
 int conv1_wino_set_probe(int bits) {
   g_probe = bits;
@@ -656,7 +715,10 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
       GemmArgs b = a;
       b.n_ptiles = (a.P + kBM16 - 1) / kBM16;
       const dim3 grid((b.n_ptiles + 7) / 8 * 8 * b.n_ntiles);
-      conv1_wino_gemm16_kernel<<<grid, 256, lds_bytes, s>>>(b);
+      if (g_probe & 64)
+        conv1_wino_gemm16_kernel<true><<<grid, 256, lds_bytes, s>>>(b);
+      else
+        conv1_wino_gemm16_kernel<false><<<grid, 256, lds_bytes, s>>>(b);
       return hipGetLastError();
     }
     default: return launch_gemm<48, 2>(a, s);

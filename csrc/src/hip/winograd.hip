@@ -145,7 +145,9 @@ struct FusedArgs {
   float* y;            // [N][Ho][Wo][K]
   int P, C, Cg, Kg, K, groups, kpad, kpad_n;
   int N, Ho, Wo, ty, tx, relu, n_ptiles, n_ntiles;
-  int prio;  // A/B: s_setprio(1) around each slice's MFMAs (guide technique T5)
+  int prio;  // bit0: s_setprio(1) around each slice's MFMAs (guide technique T5). Cost probes of the
+             // LDS-DMA kernel (wrong results; never set in production): bit4 no fold, bit5 no DMA
+             // refills, bit6 no per-slice barrier (only with bit5), bit7 no epilogue stores
 };
 
 // A^T indexed by the runtime transform point: a copy of wino::kAT in constant memory (scalar loads).
@@ -160,6 +162,20 @@ constexpr ATTable make_at() {
 }
 __constant__ ATTable c_at = make_at();
 #define c_AT c_at.v
+
+// Fold coefficients per transform point: coef[ab][i*kM + j] = A^T[i][a] * A^T[j][b] (float product,
+// the value the runtime-indexed fold computes).
+struct CoefTable {
+  float v[kN * kN][kM * kM];
+};
+constexpr CoefTable make_coef() {
+  CoefTable t{};
+  for (int ab = 0; ab < kN * kN; ++ab)
+    for (int i = 0; i < kM; ++i)
+      for (int j = 0; j < kM; ++j) t.v[ab][i * kM + j] = wino::kAT[i][ab / kN] * wino::kAT[j][ab % kN];
+  return t;
+}
+__constant__ CoefTable c_coef = make_coef();
 
 template <int BK, bool XCD>
 __global__ void __launch_bounds__(256) wino_fused_kernel(FusedArgs a) {
@@ -315,8 +331,8 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BK, bool XCD>
-__global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
+template <int BK, bool XCD, bool IL>
+__global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) {  // 2 waves/SIMD
   using f32x16 = __attribute__((ext_vector_type(16))) float;
   constexpr int U4 = BK / 4;              // 16-B units per row
   constexpr int NI = kFB * U4 / 256;      // DMA instructions per thread per operand
@@ -397,6 +413,11 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
   // coefficients are wave-uniform (scalar registers): a zero one (152 of the 441 coefficient x
   // point pairs) skips its 16 FMAs with a scalar branch
   auto fold = [&](int ab, f32x16& acc) {
+    if (a.prio & 16) {  // probe: keep the accumulator live, skip the output-transform FMAs
+      Y[0][0] += f32x2{acc[0], acc[1]};
+      acc = f32x16{};
+      return;
+    }
     const int aa = ab / kN, bb = ab - aa * kN;
 #pragma unroll
     for (int i3 = 0; i3 < kM; ++i3)
@@ -419,28 +440,93 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
       wait_vmcnt<2 * NI>();
     else
       wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
+    if ((a.prio & 96) != 96) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // keep the DMA refill and the ds_reads below the barrier
-    if (it + 2 < total) issue(it + 2);
-    if (a.prio) __builtin_amdgcn_s_setprio(1);
+    if (it + 2 < total && !(a.prio & 32)) issue(it + 2);
+    if (a.prio & 1) __builtin_amdgcn_s_setprio(1);
     mfma_slice(it, acc);
-    if (a.prio) __builtin_amdgcn_s_setprio(0);
+    if (a.prio & 1) __builtin_amdgcn_s_setprio(0);
+  };
+
+  // IL: the fold of point fab rides inside the first slice of the next point, branch-free (zero
+  // coefficients included: +0 leaves Y bit-identical), 3 packed FMAs after each MFMA, so the VALU
+  // work issues while the wave's MFMAs occupy the matrix pipe instead of after them.
+  // IL (ksteps == 2 only): the fold of point fab rides inside the first slice of the next point,
+  // branch-free (zero coefficients included: +0 leaves Y bit-identical), 3 packed FMAs after each
+  // MFMA, so the VALU work issues while the wave's MFMAs occupy the matrix pipe instead of after
+  // them. Straight-line loop body: in-loop slices always wait vmcnt(2*NI) and always refill.
+  auto slice_fold = [&](int it, f32x16& acc, int fab, f32x16& facc) {
+    float cq[kM * kM];
+#pragma unroll
+    for (int q = 0; q < kM * kM; ++q) cq[q] = c_coef.v[fab][q];
+    const float* base = lds + (it % 3) * STAGE;
+    static_assert(!IL || (BK / 8) * 4 * 3 >= kM * kM * 8, "fold FMAs must fit behind the slice's MFMAs");
+#pragma unroll
+    for (int s4 = 0; s4 < BK / 8; ++s4) {
+      const f32x4 af = *reinterpret_cast<const f32x4*>(base + a_row + rd[s4]);
+      const f32x4 bf = *reinterpret_cast<const f32x4*>(base + b_row + rd[s4]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int j = (s4 * 4 + s) * 3 + t;
+          if (j < kM * kM * 8) {
+            const int q = j >> 3, e2 = j & 7;
+            Y[q][e2] = __builtin_elementwise_fma(f32x2{cq[q], cq[q]}, f32x2{facc[2 * e2], facc[2 * e2 + 1]}, Y[q][e2]);
+          }
+        }
+      }
+    }
+    facc = f32x16{};
+  };
+  auto step_mid = [&](int it, f32x16& acc, int fab, f32x16* facc) {  // it + 2 < total
+    wait_vmcnt<2 * NI>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(it + 2);
+    if (a.prio & 1) __builtin_amdgcn_s_setprio(1);
+    if (facc)
+      slice_fold(it, acc, fab, *facc);
+    else
+      mfma_slice(it, acc);
+    if (a.prio & 1) __builtin_amdgcn_s_setprio(0);
   };
 
   issue(0);
   if (total > 1) issue(1);
-  // ab pairs: even ab accumulate in acc0, odd in acc1; the fold of the previous point is issued
-  // after the first slice of the next one, so the VALU work overlaps in-flight MFMAs.
-  int it = 0;
-  for (int ab = 0; ab < kN * kN; ab += 2) {
-    for (int ks = 0; ks < ksteps; ++ks, ++it) {
-      step(it, acc0);
-      if (ks == 0 && ab > 0) fold(ab - 1, acc1);
+  if constexpr (IL) {
+    // acc1 is zero before point 1: the first fold adds +0 (ab = 0's coefficients) and changes nothing
+    for (int ab = 0; ab + 1 < kN * kN; ab += 2) {
+      const int it = 2 * ab;
+      step_mid(it, acc0, ab > 0 ? ab - 1 : 0, &acc1);
+      step_mid(it + 1, acc0, 0, nullptr);
+      step_mid(it + 2, acc1, ab, &acc0);
+      step_mid(it + 3, acc1, 0, nullptr);
     }
-    if (ab + 1 < kN * kN) {
+    // point 48: slices 96 (fold of 47 inside) and 97 (last: no refill, full drain)
+    wait_vmcnt<2 * NI>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    slice_fold(total - 2, acc0, kN * kN - 2, acc1);
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    mfma_slice(total - 1, acc0);
+  } else {
+    // ab pairs: even ab accumulate in acc0, odd in acc1; the fold of the previous point is issued
+    // after the first slice of the next one, so the VALU work overlaps in-flight MFMAs.
+    int it = 0;
+    for (int ab = 0; ab < kN * kN; ab += 2) {
       for (int ks = 0; ks < ksteps; ++ks, ++it) {
-        step(it, acc1);
-        if (ks == 0) fold(ab, acc0);
+        step(it, acc0);
+        if (ks == 0 && ab > 0) fold(ab - 1, acc1);
+      }
+      if (ab + 1 < kN * kN) {
+        for (int ks = 0; ks < ksteps; ++ks, ++it) {
+          step(it, acc1);
+          if (ks == 0) fold(ab, acc0);
+        }
       }
     }
   }
@@ -462,7 +548,7 @@ __global__ void __launch_bounds__(256) wino_fused_glds_kernel(FusedArgs a) {
   for (int k = 0; k < 4; ++k) {
     const int p = p0 + wm * 32 + ((k * 64 + lane) >> 3);
     const int tj = p % a.tx, pq = p / a.tx;
-    oy0[k] = p < a.P ? (pq % a.ty) * kM : (1 << 28);  // out of range: never stored
+    oy0[k] = (p < a.P && !(a.prio & 128)) ? (pq % a.ty) * kM : (1 << 28);  // out of range: never stored
     ox0[k] = tj * kM;
     img[k] = pq / a.ty;
   }
@@ -615,9 +701,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW, 4) wino_fused_glds16_kernel(Fu
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (it + 2 < total) issue(it + 2);
-    if (a.prio) __builtin_amdgcn_s_setprio(1);
+    if (a.prio & 1) __builtin_amdgcn_s_setprio(1);
     mfma_slice(it, acc);
-    if (a.prio) __builtin_amdgcn_s_setprio(0);
+    if (a.prio & 1) __builtin_amdgcn_s_setprio(0);
   };
 
   issue(0);
@@ -686,9 +772,11 @@ int default_fused_cfg() {
   return v >= 0 && v <= 15 ? v : 7;
 }
 int g_fused_cfg = default_fused_cfg();
-int g_prio = [] {  // default on: -1 % measured at 300 images (ANX_WINO_PRIO=0 disables)
+// bit0 s_setprio (-1 % at 300 images), bit8 interleaved fold (-49 us at 300 images, bit-identical:
+// profiles/r01_ab_wino_ilfold_b300.jsonl); ANX_WINO_PRIO overrides
+int g_prio = [] {
   const char* e = std::getenv("ANX_WINO_PRIO");
-  return e ? std::atoi(e) : 1;
+  return e ? std::atoi(e) : 257;
 }();
 
 template <int WMW, int WNW, bool XCD>
@@ -707,13 +795,14 @@ hipError_t launch_glds16(FusedArgs a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int BK, bool XCD>
+template <int BK, bool XCD, bool IL = false>
 hipError_t launch_glds(const FusedArgs& a, dim3 grid, hipStream_t s) {
   constexpr int kLds = 3 * 2 * kFB * BK * sizeof(float);  // 3-slot ring of A|B tiles
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wino_fused_glds_kernel<BK, XCD>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(wino_fused_glds_kernel<BK, XCD, IL>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      kLds);
   if (attr != hipSuccess) return attr;
-  wino_fused_glds_kernel<BK, XCD><<<grid, 256, kLds, s>>>(a);
+  wino_fused_glds_kernel<BK, XCD, IL><<<grid, 256, kLds, s>>>(a);
   return hipGetLastError();
 }
 
@@ -723,6 +812,11 @@ unsigned grid_for(long n) {
 }
 
 }  // namespace
+
+int wino_set_prio(int bits) {
+  g_prio = bits;
+  return 0;
+}
 
 int wino_set_fused_cfg(int cfg) {
   if (cfg < 0 || cfg > 15) return -1;
@@ -829,7 +923,9 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
     const int bk = (g_fused_cfg & 1) ? 48 : 32;
     if (a.Cg % bk == 0 && a.kpad == a.Cg) {
       const dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
-      if (bk == 48 && xcd) return launch_glds<48, true>(a, grid, s);
+      if (bk == 48 && xcd)  // the interleaved fold needs exactly 2 K slices per point (C = 96)
+        return ((g_prio & 256) && a.kpad == 96) ? launch_glds<48, true, true>(a, grid, s)
+                                                : launch_glds<48, true, false>(a, grid, s);
       if (bk == 48) return launch_glds<48, false>(a, grid, s);
       if (xcd) return launch_glds<32, true>(a, grid, s);
       return launch_glds<32, false>(a, grid, s);

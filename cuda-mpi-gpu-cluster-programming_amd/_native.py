@@ -85,6 +85,7 @@ _SIGS = {
     "anx_conv_pack": (_I, [C.POINTER(_I), _P, _P, _P]),
     "anx_conv_force_variant": (_I, [_I, _I]),
     "anx_set_conv2_algo": (_I, [_I]),
+    "anx_set_stage_chunks": (_I, [_I, _I]),
     "anx_get_conv2_algo": (_I, []),
     "anx_set_conv1_algo": (_I, [_I]),
     "anx_get_conv1_algo": (_I, []),
@@ -92,6 +93,7 @@ _SIGS = {
     "anx_conv1_wino_probe": (_I, [_I]),
     "anx_conv1_wino": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P]),
     "anx_wino_fused_cfg": (_I, [_I]),
+    "anx_wino_prio": (_I, [_I]),
     "anx_conv2d_mfma": (_I, [C.POINTER(_I), _P, _P, _P, _P, _P] + [_I] * 6 + [_I, _P]),
     "anx_cpu_conv2d": (_I, [_P, _P, _P, _P] + [_I] * 10),
     "anx_cpu_maxpool": (_I, [_P, _P] + [_I] * 6),
