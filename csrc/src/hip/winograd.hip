@@ -451,6 +451,22 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
   // IL: the fold of point fab rides inside the first slice of the next point, branch-free (zero
   // coefficients included: +0 leaves Y bit-identical), 3 packed FMAs after each MFMA, so the VALU
   // work issues while the wave's MFMAs occupy the matrix pipe instead of after them.
+  // mfma_slice with the fragments of group s4+1 read while group s4's MFMAs run
+  auto mfma_slice_pf = [&](int it, f32x16& acc) {
+    const float* base = lds + (it % 3) * STAGE;
+    f32x4 af[2], bf[2];
+    af[0] = *reinterpret_cast<const f32x4*>(base + a_row + rd[0]);
+    bf[0] = *reinterpret_cast<const f32x4*>(base + b_row + rd[0]);
+#pragma unroll
+    for (int s4 = 0; s4 < BK / 8; ++s4) {
+      if (s4 + 1 < BK / 8) {
+        af[(s4 + 1) & 1] = *reinterpret_cast<const f32x4*>(base + a_row + rd[s4 + 1]);
+        bf[(s4 + 1) & 1] = *reinterpret_cast<const f32x4*>(base + b_row + rd[s4 + 1]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s4 & 1][s], bf[s4 & 1][s], acc, 0, 0, 0);
+    }
+  };
   // IL (ksteps == 2 only): the fold of point fab rides inside the first slice of the next point,
   // branch-free (zero coefficients included: +0 leaves Y bit-identical), 3 packed FMAs after each
   // MFMA, so the VALU work issues while the wave's MFMAs occupy the matrix pipe instead of after
@@ -461,13 +477,19 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
     for (int q = 0; q < kM * kM; ++q) cq[q] = c_coef.v[fab][q];
     const float* base = lds + (it % 3) * STAGE;
     static_assert(!IL || (BK / 8) * 4 * 3 >= kM * kM * 8, "fold FMAs must fit behind the slice's MFMAs");
+    // fragments of group s4+1 are read while group s4's MFMAs run (two register sets)
+    f32x4 af[2], bf[2];
+    af[0] = *reinterpret_cast<const f32x4*>(base + a_row + rd[0]);
+    bf[0] = *reinterpret_cast<const f32x4*>(base + b_row + rd[0]);
 #pragma unroll
     for (int s4 = 0; s4 < BK / 8; ++s4) {
-      const f32x4 af = *reinterpret_cast<const f32x4*>(base + a_row + rd[s4]);
-      const f32x4 bf = *reinterpret_cast<const f32x4*>(base + b_row + rd[s4]);
+      if (s4 + 1 < BK / 8) {
+        af[(s4 + 1) & 1] = *reinterpret_cast<const f32x4*>(base + a_row + rd[s4 + 1]);
+        bf[(s4 + 1) & 1] = *reinterpret_cast<const f32x4*>(base + b_row + rd[s4 + 1]);
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s4 & 1][s], bf[s4 & 1][s], acc, 0, 0, 0);
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
           const int j = (s4 * 4 + s) * 3 + t;
@@ -489,7 +511,7 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
     if (facc)
       slice_fold(it, acc, fab, *facc);
     else
-      mfma_slice(it, acc);
+      mfma_slice_pf(it, acc);
     if (a.prio & 1) __builtin_amdgcn_s_setprio(0);
   };
 
@@ -512,7 +534,7 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    mfma_slice(total - 1, acc0);
+    mfma_slice_pf(total - 1, acc0);
   } else {
     // ab pairs: even ab accumulate in acc0, odd in acc1; the fold of the previous point is issued
     // after the first slice of the next one, so the VALU work overlaps in-flight MFMAs.
