@@ -24,13 +24,14 @@ enum class Impl : int {
 };
 
 // Algorithm for 5x5 stride-1 convolutions (Conv2) on the Mfma path: Auto picks Winograd
-// F(3x3,5x5) whenever eligible. Process-wide; read when a stage is launched.
+// F(3x3,5x5) when eligible and the launch is larger than 8 images (use_winograd), the direct
+// implicit GEMM below that. Process-wide; read when a stage is launched.
 // WinogradUnfused = input transform + separate batched GEMM (M in HBM) + output transform (A/B).
 enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2, WinogradUnfused = 3 };
 void set_conv2_algo(ConvAlgo a);
 ConvAlgo conv2_algo();
-// Algorithm for Conv1 (stride 4, C = 3) on the Mfma path: Auto / Winograd = polyphase Winograd
-// F(3x3,3x3) (conv1_wino.hip) when eligible, Direct = the implicit-GEMM kernel (bit-identical across
+// Algorithm for Conv1 (stride 4, C = 3) on the Mfma path: Winograd = polyphase Winograd
+// F(3x3,3x3) (conv1_wino.hip) when eligible, Auto = that above 8 images per launch, Direct = the implicit-GEMM kernel (bit-identical across
 // row decompositions; Winograd tile origins move with the row split, ~1e-7 relative).
 void set_conv1_algo(ConvAlgo a);
 ConvAlgo conv1_algo();
@@ -39,6 +40,9 @@ ConvAlgo conv1_algo();
 // chunk, so the Winograd V buffers can stay in the 256 MiB Infinity Cache between the transform that
 // writes them and the GEMM that reads them. Process-wide; env ANX_CHUNK1 / ANX_CHUNK2.
 void set_stage_chunks(int stage1, int stage2);
+// Algorithm actually used by a launch of n images x `rows` output rows of a conv whose full image
+// has `full_rows` rows: Auto = Winograd above 8 full images' worth of rows, direct below.
+bool use_winograd(ConvAlgo a, int n, int rows, int full_rows);
 int stage_chunk(int stage);
 
 struct HostWeights {

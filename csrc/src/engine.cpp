@@ -50,6 +50,17 @@ void set_stage_chunks(int stage1, int stage2) {
   g_chunk[1] = std::max(0, stage2);
 }
 int stage_chunk(int stage) { return g_chunk[stage == 2 ? 1 : 0]; }
+
+// Auto: Winograd once a launch covers more than kAutoDirectImages full-height images' worth of
+// output rows. Below that the Winograd GEMM grids (64 tiles per workgroup) leave most of the 256
+// CUs idle and the direct implicit GEMM wins: 0.081 vs 0.163 ms at batch 1, 0.142 vs 0.169 ms at
+// 8, 0.187 (Winograd) vs 0.217 ms at 16 (profiles/r01_algo_crossover.jsonl).
+constexpr int kAutoDirectImages = 8;
+bool use_winograd(ConvAlgo a, int n, int rows, int full_rows) {
+  if (a == ConvAlgo::Direct) return false;
+  if (a != ConvAlgo::Auto) return true;
+  return static_cast<long>(n) * rows > static_cast<long>(kAutoDirectImages) * full_rows;
+}
 void set_conv2_algo(ConvAlgo a) { g_conv2_algo = a; }
 ConvAlgo conv2_algo() { return g_conv2_algo; }
 void set_conv1_algo(ConvAlgo a) { g_conv1_algo = a; }
@@ -161,7 +172,7 @@ hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStr
     const int n = std::min(chunk, N - n0);
     const float* xc = x + n0 * in_img;
     float* qc = q2_ + n0 * q_img;
-    if (impl_ == Impl::Mfma && wv1_ != nullptr && g_conv1_algo != ConvAlgo::Direct) {
+    if (impl_ == Impl::Mfma && wv1_ != nullptr && use_winograd(g_conv1_algo, n, t.c1.size(), d_.H1)) {
       const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
       if (hip::conv1_wino_v_floats(w) > wv1_cap_) return hipErrorInvalidValue;
       ANX_TRY(hip::conv1_wino(w, xc, wv1_, u1w_, b1d_, hip::OutView{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0}, true,
@@ -202,7 +213,7 @@ hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t 
     const int n = std::min(chunk, N - n0);
     const float* qc = q2_ + n0 * q_img;
     float* yc = y + n0 * y_img;
-    const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && g_conv2_algo != ConvAlgo::Direct;
+    const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(g_conv2_algo, n, t.c2.size(), d_.H2);
     if (wino) {
       const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
       if (hip::wino_v_floats(w) > wv_cap_ || hip::wino_m_floats(w) > wm_cap_) return hipErrorInvalidValue;
