@@ -98,6 +98,8 @@ int anx_conv_force_variant(int kind, int id);
 int anx_set_conv2_algo(int algo);
 // images per launch of stage 1 / stage 2 (0 = whole batch); see anx::set_stage_chunks
 int anx_set_stage_chunks(int stage1, int stage2);
+// pool1 fused into Conv2's Winograd input transform (1) or a separate pool1 pass (0, default)
+int anx_set_fuse_pool1(int on);
 int anx_get_conv2_algo(void);
 /* Conv1 (11x11 s4) algorithm on the MFMA path: 0 auto (polyphase Winograd F(3,3) when eligible), 1 direct, 2 Winograd */
 int anx_set_conv1_algo(int algo);

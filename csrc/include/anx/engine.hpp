@@ -43,6 +43,11 @@ void set_stage_chunks(int stage1, int stage2);
 // Algorithm actually used by a launch of n images x `rows` output rows of a conv whose full image
 // has `full_rows` rows: Auto = Winograd above 8 full images' worth of rows, direct below.
 bool use_winograd(ConvAlgo a, int n, int rows, int full_rows);
+// Pool1 fused into Conv2's Winograd input transform inside forward()/tile_forward() (the split
+// stage1/stage2 path keeps the materialised window for halo exchange). Default off (measured
+// slower); ANX_FUSE_POOL1=1 or anx_set_fuse_pool1 enables it.
+void set_fuse_pool1(bool on);
+bool fuse_pool1();
 int stage_chunk(int stage);
 
 struct HostWeights {
@@ -88,6 +93,8 @@ class BlocksEngine {
 
  private:
   hipError_t ensure_window(const TilePlan& t, int N, hipStream_t s);
+  hipError_t conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s);
+  hipError_t conv2_chunk(int n, const TilePlan& t, const float* qc, float* yc, hipStream_t s);
 
   BlockSpec b1_, b2_;
   BlocksDims d_;

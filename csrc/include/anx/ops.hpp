@@ -98,6 +98,14 @@ size_t wino_m_floats(const WinoPlan& w);
 // U = G g G^T in fp64, laid out as KCFF weights of the grouped 1x1 GEMM ([49*K][C/g]).
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s);
+// Pool1 (3x3 / 2, post-ReLU conv1 input) fused into the input transform: V of the zero-bordered
+// pool1 window without materialising it. Window row r = pool1 row r + q_lo; pool1 rows outside
+// [p1_lo, p1_hi) and columns outside [0, Wp) are the border; conv1 rows [c1_lo, c1_lo + H1) are in
+// `c1` ([N][H1][W1][C]). Bit-identical to maxpool + wino_input.
+struct WinoPoolGeom {
+  int H1, W1, Wp, pad, q_lo, p1_lo, p1_hi, c1_lo;
+};
+hipError_t wino_input_pool(const WinoPlan& w, const float* c1, const WinoPoolGeom& pg, float* V, hipStream_t s);
 hipError_t wino_output(const WinoPlan& w, const float* Mt, const float* bias, float* y, bool relu, hipStream_t s);
 // Tuning (A/B): bit0 = K-slice 48 instead of 32, bit1 = XCD-aware block order, bit2 = LDS-DMA ring.
 // Default 7 (measured at 300 images: ring +17 %, BK 48 +3 %, XCD order +1 %).

@@ -371,6 +371,10 @@ int anx_set_conv1_algo(int algo) {
   return 0;
 }
 int anx_get_conv1_algo(void) { return static_cast<int>(anx::conv1_algo()); }
+int anx_set_fuse_pool1(int on) {
+  anx::set_fuse_pool1(on != 0);
+  return 0;
+}
 int anx_set_stage_chunks(int stage1, int stage2) {
   if (stage1 < 0 || stage2 < 0) return fail("stage chunks must be >= 0 (0 = whole batch)");
   anx::set_stage_chunks(stage1, stage2);

@@ -44,7 +44,16 @@ int env_int(const char* name) {
   return e ? std::max(0, std::atoi(e)) : 0;
 }
 int g_chunk[2] = {env_int("ANX_CHUNK1"), env_int("ANX_CHUNK2")};
+// off: the fused kernel is correct (bit-identical) but slower than maxpool + wino_in at 300 images,
+// +18 us (thread per tile x channel) and +37 us (LDS-staged tile row)
+// (profiles/r01_ab_fuse_pool1_b300.jsonl); the separate passes already run at 4.5-5 TB/s
+int g_fuse_pool1 = [] {
+  const char* e = std::getenv("ANX_FUSE_POOL1");
+  return e ? std::atoi(e) : 0;
+}();
 }  // namespace
+void set_fuse_pool1(bool on) { g_fuse_pool1 = on ? 1 : 0; }
+bool fuse_pool1() { return g_fuse_pool1 != 0; }
 void set_stage_chunks(int stage1, int stage2) {
   g_chunk[0] = std::max(0, stage1);
   g_chunk[1] = std::max(0, stage2);
@@ -160,123 +169,151 @@ float* BlocksEngine::q2_row_ptr(const TilePlan& t, int n, int r) {
   return q2_ + static_cast<size_t>(n) * q2_image_stride_floats(t) + static_cast<size_t>(r - t.q.lo) * q2_row_floats();
 }
 
+hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s) {
+  const ConvSpec& k1 = b1_.conv;
+  const hip::OutView c1v{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0};
+  if (impl_ == Impl::Mfma && wv1_ != nullptr && use_winograd(g_conv1_algo, n, t.c1.size(), d_.H1)) {
+    const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
+    if (hip::conv1_wino_v_floats(w) > wv1_cap_) return hipErrorInvalidValue;
+    return hip::conv1_wino(w, xc, wv1_, u1w_, b1d_, c1v, true, s);
+  }
+  if (impl_ == Impl::Mfma) {
+    const hip::ConvPlan p = hip::make_conv_plan(n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, k1.groups);
+    const int key = p.variant;
+    if (key != plan_key1_) {
+      std::vector<float> packed;
+      std::vector<int> koff;
+      hip::pack_conv_weights_host(p, w1h_.data(), packed, koff);
+      if (w1p_) ANX_TRY(hipFree(w1p_));
+      if (koff1_) ANX_TRY(hipFree(koff1_));
+      w1p_ = dev_upload(packed);
+      koff1_ = dev_upload(koff);
+      plan_key1_ = key;
+    }
+    return hip::conv2d_mfma(p, xc, w1p_, koff1_, b1d_, c1v, true, s);
+  }
+  return hip::conv2d_direct(xc, w1_, b1d_, c1_, n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, 0, k1.groups, true,
+                            s);
+}
+
 hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStream_t s) {
   if (N > max_batch_) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
   ANX_TRY(ensure_window(t, N, s));
-  const ConvSpec& k1 = b1_.conv;
   const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
   const size_t q_img = q2_image_stride_floats(t);
   const int chunk = g_chunk[0] > 0 ? std::min(chunk_, g_chunk[0]) : chunk_;
   for (int n0 = 0; n0 < N; n0 += chunk) {
     const int n = std::min(chunk, N - n0);
-    const float* xc = x + n0 * in_img;
-    float* qc = q2_ + n0 * q_img;
-    if (impl_ == Impl::Mfma && wv1_ != nullptr && use_winograd(g_conv1_algo, n, t.c1.size(), d_.H1)) {
-      const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
-      if (hip::conv1_wino_v_floats(w) > wv1_cap_) return hipErrorInvalidValue;
-      ANX_TRY(hip::conv1_wino(w, xc, wv1_, u1w_, b1d_, hip::OutView{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0}, true,
-                              s));
-    } else if (impl_ == Impl::Mfma) {
-      const hip::ConvPlan p = hip::make_conv_plan(n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, k1.groups);
-      const int key = p.variant;
-      if (key != plan_key1_) {
-        std::vector<float> packed;
-        std::vector<int> koff;
-        hip::pack_conv_weights_host(p, w1h_.data(), packed, koff);
-        if (w1p_) ANX_TRY(hipFree(w1p_));
-        if (koff1_) ANX_TRY(hipFree(koff1_));
-        w1p_ = dev_upload(packed);
-        koff1_ = dev_upload(koff);
-        plan_key1_ = key;
-      }
-      ANX_TRY(hip::conv2d_mfma(p, xc, w1p_, koff1_, b1d_, hip::OutView{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0},
-                               true, s));
-    } else {
-      ANX_TRY(hip::conv2d_direct(xc, w1_, b1d_, c1_, n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, 0, k1.groups,
-                                 true, s));
-    }
+    ANX_TRY(conv1_chunk(x + n0 * in_img, n, t, s));
     ANX_TRY(hip::maxpool(c1_, n, t.c1.size(), d_.W1, d_.C1, b1_.pool.F, b1_.pool.S,
-                         hip::OutView{qc, t.q.size(), wq_, d_.C1, t.p1.lo - t.q.lo, b2_.conv.P, 0}, s));
+                         hip::OutView{q2_ + n0 * q_img, t.q.size(), wq_, d_.C1, t.p1.lo - t.q.lo, b2_.conv.P, 0}, s));
   }
   return hipSuccess;
+}
+
+// Conv2 (+ReLU) and Pool2(+LRN) of n images. qc: their conv2 input window; nullptr = pool1 fused
+// into the Winograd input transform, reading the conv1 rows in c1_ (conv1_chunk just wrote them).
+hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, float* yc, hipStream_t s) {
+  const ConvSpec& k2 = b2_.conv;
+  const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(g_conv2_algo, n, t.c2.size(), d_.H2);
+  if (!qc && !wino) return hipErrorInvalidValue;
+  if (wino) {
+    const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
+    if (hip::wino_v_floats(w) > wv_cap_ || hip::wino_m_floats(w) > wm_cap_) return hipErrorInvalidValue;
+    if (w.gemm.variant != wino_key_) {
+      std::vector<float> u, packed;
+      std::vector<int> koff;
+      hip::wino_transform_weights_host(w, w2h_.data(), u);
+      hip::pack_conv_weights_host(w.gemm, u.data(), packed, koff);
+      if (u2p_) ANX_TRY(hipFree(u2p_));
+      if (ukoff_) ANX_TRY(hipFree(ukoff_));
+      u2p_ = dev_upload(packed);
+      ukoff_ = dev_upload(koff);
+      wino_key_ = w.gemm.variant;
+    }
+    if (qc) {
+      ANX_TRY(hip::wino_input(w, qc, wv_, s));
+    } else {
+      const hip::WinoPoolGeom pg{t.c1.size(), d_.W1, d_.Wp1, k2.P, t.q.lo, t.p1.lo, t.p1.hi, t.c1.lo};
+      ANX_TRY(hip::wino_input_pool(w, c1_, pg, wv_, s));
+    }
+    if (g_conv2_algo == ConvAlgo::WinogradUnfused) {
+      if (!wm_) ANX_TRY(hipMalloc(reinterpret_cast<void**>(&wm_), wm_cap_ * sizeof(float)));
+      ANX_TRY(hip::conv2d_mfma(w.gemm, wv_, u2p_, ukoff_, nullptr, hip::OutView{wm_, 1, 1, w.gemm.K, 0, 0, 0}, false,
+                               s));
+      ANX_TRY(hip::wino_output(w, wm_, b2d_, c2_, true, s));
+    } else {
+      ANX_TRY(hip::wino_fused(w, wv_, u2p_, b2d_, c2_, true, s));
+    }
+  } else if (impl_ == Impl::Mfma) {
+    const hip::ConvPlan p = hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups);
+    const int key = p.variant;
+    if (key != plan_key2_) {
+      std::vector<float> packed;
+      std::vector<int> koff;
+      hip::pack_conv_weights_host(p, w2h_.data(), packed, koff);
+      if (w2p_) ANX_TRY(hipFree(w2p_));
+      if (koff2_) ANX_TRY(hipFree(koff2_));
+      w2p_ = dev_upload(packed);
+      koff2_ = dev_upload(koff);
+      plan_key2_ = key;
+    }
+    ANX_TRY(hip::conv2d_mfma(p, qc, w2p_, koff2_, b2d_, hip::OutView{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0}, true,
+                             s));
+  } else {
+    ANX_TRY(hip::conv2d_direct(qc, w2_, b2d_, c2_, n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, 0, k2.groups, true,
+                               s));
+  }
+  const LrnSpec& l = b2_.lrn;
+  if (b2_.has_lrn) {
+    if (impl_ == Impl::Mfma)
+      return hip::maxpool_lrn(c2_, yc, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S, l.N, l.alpha, l.beta,
+                              l.k, l.mode, s);
+    // oracle path: separate pool and LRN kernels, staged through the conv1 workspace
+    ANX_TRY(hip::maxpool_direct(c2_, c1_, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S, s));
+    return hip::lrn_direct(c1_, yc, n, t.out.size(), d_.Wp2, d_.C2, l.N, l.alpha, l.beta, l.k, l.mode, s);
+  }
+  return hip::maxpool(c2_, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S,
+                      hip::OutView{yc, t.out.size(), d_.Wp2, d_.C2, 0, 0, 0}, s);
 }
 
 hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t s) {
   if (N > max_batch_) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
-  const ConvSpec& k2 = b2_.conv;
   const size_t q_img = q2_image_stride_floats(t);
   const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
   const int chunk = g_chunk[1] > 0 ? std::min(chunk_, g_chunk[1]) : chunk_;
   for (int n0 = 0; n0 < N; n0 += chunk) {
     const int n = std::min(chunk, N - n0);
-    const float* qc = q2_ + n0 * q_img;
-    float* yc = y + n0 * y_img;
-    const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(g_conv2_algo, n, t.c2.size(), d_.H2);
-    if (wino) {
-      const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
-      if (hip::wino_v_floats(w) > wv_cap_ || hip::wino_m_floats(w) > wm_cap_) return hipErrorInvalidValue;
-      if (w.gemm.variant != wino_key_) {
-        std::vector<float> u, packed;
-        std::vector<int> koff;
-        hip::wino_transform_weights_host(w, w2h_.data(), u);
-        hip::pack_conv_weights_host(w.gemm, u.data(), packed, koff);
-        if (u2p_) ANX_TRY(hipFree(u2p_));
-        if (ukoff_) ANX_TRY(hipFree(ukoff_));
-        u2p_ = dev_upload(packed);
-        ukoff_ = dev_upload(koff);
-        wino_key_ = w.gemm.variant;
-      }
-      ANX_TRY(hip::wino_input(w, qc, wv_, s));
-      if (g_conv2_algo == ConvAlgo::WinogradUnfused) {
-        if (!wm_) ANX_TRY(hipMalloc(reinterpret_cast<void**>(&wm_), wm_cap_ * sizeof(float)));
-        ANX_TRY(hip::conv2d_mfma(w.gemm, wv_, u2p_, ukoff_, nullptr,
-                                 hip::OutView{wm_, 1, 1, w.gemm.K, 0, 0, 0}, false, s));
-        ANX_TRY(hip::wino_output(w, wm_, b2d_, c2_, true, s));
-      } else {
-        ANX_TRY(hip::wino_fused(w, wv_, u2p_, b2d_, c2_, true, s));
-      }
-    } else if (impl_ == Impl::Mfma) {
-      const hip::ConvPlan p = hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups);
-      const int key = p.variant;
-      if (key != plan_key2_) {
-        std::vector<float> packed;
-        std::vector<int> koff;
-        hip::pack_conv_weights_host(p, w2h_.data(), packed, koff);
-        if (w2p_) ANX_TRY(hipFree(w2p_));
-        if (koff2_) ANX_TRY(hipFree(koff2_));
-        w2p_ = dev_upload(packed);
-        koff2_ = dev_upload(koff);
-        plan_key2_ = key;
-      }
-      ANX_TRY(hip::conv2d_mfma(p, qc, w2p_, koff2_, b2d_, hip::OutView{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0},
-                               true, s));
-    } else {
-      ANX_TRY(hip::conv2d_direct(qc, w2_, b2d_, c2_, n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, 0, k2.groups,
-                                 true, s));
-    }
-    const LrnSpec& l = b2_.lrn;
-    if (b2_.has_lrn) {
-      if (impl_ == Impl::Mfma) {
-        ANX_TRY(hip::maxpool_lrn(c2_, yc, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S, l.N, l.alpha, l.beta,
-                                 l.k, l.mode, s));
-      } else {
-        // oracle path: separate pool and LRN kernels, staged through the conv1 workspace
-        ANX_TRY(hip::maxpool_direct(c2_, c1_, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S, s));
-        ANX_TRY(hip::lrn_direct(c1_, yc, n, t.out.size(), d_.Wp2, d_.C2, l.N, l.alpha, l.beta, l.k, l.mode, s));
-      }
-    } else {
-      ANX_TRY(hip::maxpool(c2_, n, t.c2.size(), d_.W2, d_.C2, b2_.pool.F, b2_.pool.S,
-                           hip::OutView{yc, t.out.size(), d_.Wp2, d_.C2, 0, 0, 0}, s));
-    }
+    ANX_TRY(conv2_chunk(n, t, q2_ + n0 * q_img, y + n0 * y_img, s));
   }
   return hipSuccess;
 }
 
 hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, float* y, hipStream_t s) {
-  ANX_TRY(stage1(x, N, t, s));
-  return stage2(N, t, y, s);
+  if (N > max_batch_) return hipErrorInvalidValue;
+  if (t.out.empty()) return hipSuccess;
+  // Pool1 fused into Conv2's Winograd input transform when every chunk runs Winograd Conv2 (the
+  // conv2 window is then never written: no memset, no pool1 pass).
+  const int c1c = g_chunk[0] > 0 ? std::min(chunk_, g_chunk[0]) : chunk_;
+  const int c2c = g_chunk[1] > 0 ? std::min(chunk_, g_chunk[1]) : chunk_;
+  const int chunk = std::min(c1c, c2c);
+  const int n_min = N % chunk ? std::min(N % chunk, chunk) : std::min(N, chunk);
+  const bool fuse = g_fuse_pool1 && impl_ == Impl::Mfma && wv_ != nullptr && b1_.pool.F == 3 && b1_.pool.S == 2 &&
+                    g_conv2_algo != ConvAlgo::WinogradUnfused && use_winograd(g_conv2_algo, n_min, t.c2.size(), d_.H2);
+  if (!fuse) {
+    ANX_TRY(stage1(x, N, t, s));
+    return stage2(N, t, y, s);
+  }
+  const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
+  const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int n = std::min(chunk, N - n0);
+    ANX_TRY(conv1_chunk(x + n0 * in_img, n, t, s));
+    ANX_TRY(conv2_chunk(n, t, nullptr, y + n0 * y_img, s));
+  }
+  return hipSuccess;
 }
 
 hipError_t BlocksEngine::forward(const float* x, int N, float* y, hipStream_t s) {

@@ -79,6 +79,98 @@ __global__ void __launch_bounds__(kT) wino_in_kernel(const float* __restrict__ x
   }
 }
 
+struct WinoPoolArgs {
+  int N, Hq, Wq, C, ty, tx;  // window / tile geometry (as wino_in_kernel)
+  int H1, W1, Wp, pad;       // conv1 rows in the buffer, conv1 width, pool1 width, window border
+  int q_lo, p1_lo, p1_hi, c1_lo;
+};
+
+// Pool1 fused into the input transform: the same V as maxpool(c1 -> zero-bordered window) followed
+// by wino_in_kernel, without the window round trip through HBM (84 MB written + 111 MB read per
+// 300 images) and one launch fewer. Window row r is pool1 row pr = r + q_lo (pool rows outside
+// [p1_lo, p1_hi) and columns outside [0, Wp) are the zero border); pool1 row pr is the max over
+// conv1 rows 2pr..2pr+2 (local rows 2pr - c1_lo ...) and columns 2px..2px+2. conv1 outputs are
+// post-ReLU (>= 0) and a max is order-free, so V is bit-identical to the unfused pair.
+// Workgroup = (image, tile row, 32 channels), 320 threads = 10 slots x 32 channels: phase 1 pools
+// the tile row's 7 window rows x Wq columns into LDS (one thread per column walks the 15 conv1
+// rows once, reusing the shared row between window rows); phase 2 transforms one tile per slot
+// from LDS (channel-fastest, conflict-free) and writes V with 128-B coalesced stores.
+constexpr int kPoolCg = 32, kPoolSlots = 10, kPoolThreads = kPoolCg * kPoolSlots, kPoolMaxWq = 40;
+__global__ void __launch_bounds__(kPoolThreads) wino_in_pool_kernel(const float* __restrict__ c1,
+                                                                    float* __restrict__ V, WinoPoolArgs g) {
+  __shared__ float win[kN][kPoolMaxWq][kPoolCg];
+  const int cgs = g.C / kPoolCg;
+  const int cg = blockIdx.x % cgs;
+  const int ti = (blockIdx.x / cgs) % g.ty;
+  const int n = blockIdx.x / (cgs * g.ty);
+  const int c = threadIdx.x % kPoolCg, slot = threadIdx.x / kPoolCg;
+  const int ch = cg * kPoolCg + c;
+  const float* img = c1 + static_cast<size_t>(n) * g.H1 * g.W1 * g.C + ch;
+  // phase 1: window rows ti*3 .. ti*3+6, all Wq columns
+  for (int xx = slot; xx < g.Wq; xx += kPoolSlots) {
+    const int px = xx - g.pad;
+    const bool col_ok = px >= 0 && px < g.Wp;
+    float last = 0.f;
+    bool have_last = false;
+#pragma unroll
+    for (int u = 0; u < kN; ++u) {
+      const int yy = ti * kM + u;
+      const int pr = yy + g.q_lo;
+      float v = 0.f;
+      if (col_ok && yy < g.Hq && pr >= g.p1_lo && pr < g.p1_hi) {
+        const int lr = 2 * pr - g.c1_lo;
+        auto hmax = [&](int r) {
+          const float* q = img + (static_cast<size_t>(r) * g.W1 + 2 * px) * g.C;
+          return fmaxf(fmaxf(q[0], q[g.C]), q[2 * g.C]);
+        };
+        const float h0 = have_last ? last : hmax(lr);
+        const float h1 = hmax(lr + 1), h2 = hmax(lr + 2);
+        v = fmaxf(fmaxf(h0, h1), h2);
+        last = h2;
+        have_last = true;
+      } else {
+        have_last = false;
+      }
+      win[u][xx][c] = v;
+    }
+  }
+  __syncthreads();
+  // phase 2: one tile per slot
+  for (int tj = slot; tj < g.tx; tj += kPoolSlots) {
+    float t[kN][kN];
+#pragma unroll
+    for (int a = 0; a < kN; ++a)
+#pragma unroll
+      for (int v = 0; v < kN; ++v) t[a][v] = 0.f;
+#pragma unroll
+    for (int u = 0; u < kN; ++u) {
+      float row[kN];
+#pragma unroll
+      for (int v = 0; v < kN; ++v) {
+        const int xx = tj * kM + v;
+        row[v] = xx < g.Wq ? win[u][xx][c] : 0.f;
+      }
+#pragma unroll
+      for (int a = 0; a < kN; ++a)
+        if (wino::kBT[a][u] != 0.f)
+#pragma unroll
+          for (int v = 0; v < kN; ++v) t[a][v] = fmaf(wino::kBT[a][u], row[v], t[a][v]);
+    }
+    const int p = (n * g.ty + ti) * g.tx + tj;
+    float* out = V + static_cast<size_t>(p) * (kN * kN) * g.C + ch;
+#pragma unroll
+    for (int a = 0; a < kN; ++a)
+#pragma unroll
+      for (int b = 0; b < kN; ++b) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < kN; ++v)
+          if (wino::kBT[b][v] != 0.f) s2 = fmaf(wino::kBT[b][v], t[a][v], s2);
+        out[static_cast<size_t>(a * kN + b) * g.C] = s2;
+      }
+  }
+}
+
 __global__ void __launch_bounds__(kT) wino_out_kernel(const float* __restrict__ Mt, const float* __restrict__ bias,
                                                       float* __restrict__ y, int N, int Ho, int Wo, int K, int ty,
                                                       int tx, int relu) {
@@ -905,6 +997,35 @@ hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s
     wino_in_kernel<true><<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
   else
     wino_in_kernel<false><<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
+  return hipGetLastError();
+}
+
+hipError_t wino_input_pool(const WinoPlan& w, const float* c1, const WinoPoolGeom& pg, float* V, hipStream_t s) {
+  const long n = static_cast<long>(w.P) * w.C;
+  if (n >= (1L << 31) || static_cast<long>(w.N) * pg.H1 * pg.W1 * w.C >= (1L << 31)) return hipErrorInvalidValue;
+  // every pooled window row must read conv1 rows inside the buffer: 0 <= 2*p1_lo - c1_lo and
+  // 2*(p1_hi - 1) + 2 - c1_lo < H1 (checked on the host: the kernel does not bound-check rows)
+  if (pg.p1_hi > pg.p1_lo && (2 * pg.p1_lo - pg.c1_lo < 0 || 2 * (pg.p1_hi - 1) + 2 - pg.c1_lo >= pg.H1))
+    return hipErrorInvalidValue;
+  WinoPoolArgs g{};
+  g.N = w.N;
+  g.Hq = w.Hq;
+  g.Wq = w.Wq;
+  g.C = w.C;
+  g.ty = w.ty;
+  g.tx = w.tx;
+  g.H1 = pg.H1;
+  g.W1 = pg.W1;
+  g.Wp = pg.Wp;
+  g.pad = pg.pad;
+  g.q_lo = pg.q_lo;
+  g.p1_lo = pg.p1_lo;
+  g.p1_hi = pg.p1_hi;
+  g.c1_lo = pg.c1_lo;
+  if (w.C % kPoolCg || w.Wq > kPoolMaxWq) return hipErrorInvalidValue;
+  const long gb = static_cast<long>(w.N) * w.ty * (w.C / kPoolCg);
+  if (gb >= (1L << 31)) return hipErrorInvalidValue;
+  wino_in_pool_kernel<<<static_cast<unsigned>(gb), kPoolThreads, 0, s>>>(c1, V, g);
   return hipGetLastError();
 }
 

@@ -86,6 +86,7 @@ _SIGS = {
     "anx_conv_force_variant": (_I, [_I, _I]),
     "anx_set_conv2_algo": (_I, [_I]),
     "anx_set_stage_chunks": (_I, [_I, _I]),
+    "anx_set_fuse_pool1": (_I, [_I]),
     "anx_get_conv2_algo": (_I, []),
     "anx_set_conv1_algo": (_I, [_I]),
     "anx_get_conv1_algo": (_I, []),

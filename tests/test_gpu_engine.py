@@ -322,3 +322,37 @@ def test_winograd_fused_configs(cuda, algo, cfg, groups2):
     finally:
         nat.call("anx_wino_fused_cfg", 7)
     torch.testing.assert_close(y, blocks_forward(x, m.weights, m.b1, m.b2), rtol=2e-5, atol=2e-6)
+
+
+@pytest.fixture
+def fuse_pool1():
+    yield lambda on: nat.call("anx_set_fuse_pool1", on)
+    nat.call("anx_set_fuse_pool1", 1)
+
+
+@pytest.mark.parametrize("N", [9, 20])
+def test_fused_pool1_winograd_input_bitwise(cuda, fuse_pool1, N):
+    """Pool1 fused into Conv2's Winograd input transform == maxpool + window + transform, bit for bit
+    (whole images and overlap row tiles), and both match the fp64 oracle."""
+    m = AlexNetBlocks(device=cuda, init="rand", seed=90 + N, max_batch=N)
+    x = init_input(N, "rand", seed=N).to(cuda)
+    fuse_pool1(0)
+    ref = m(x).clone()
+    fuse_pool1(1)
+    got = m(x)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    oracle = blocks_forward(x.cpu(), m.weights, m.b1, m.b2).float()
+    assert (got.cpu() - oracle).abs().max().item() <= 1e-4 * oracle.abs().max().item()
+    for np_ in (2, 3):
+        plan = make_plan(227, 227, np_, OVERLAP)
+        for t in plan.tiles:
+            if t.out.empty:
+                continue
+            xs = x[:, t.inp.lo:t.inp.hi].contiguous()
+            fuse_pool1(0)
+            a = m.tile_forward(xs, t).clone()
+            fuse_pool1(1)
+            b = m.tile_forward(xs, t)
+            torch.cuda.synchronize()
+            assert torch.equal(a, b)

@@ -23,10 +23,10 @@ def main():
     ap.add_argument("--bits", default="1,17,33,97,129,241")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--knob", default="anx_wino_prio", choices=["anx_wino_prio", "anx_conv1_wino_probe"],
+    ap.add_argument("--knob", default="anx_wino_prio", choices=["anx_wino_prio", "anx_conv1_wino_probe", "anx_set_fuse_pool1"],
                     help="which kernel's flag word the arms set (conv1: bit4 setprio, bit6 interleaved fold)")
     a = ap.parse_args()
-    default = {"anx_wino_prio": 257, "anx_conv1_wino_probe": 80}[a.knob]
+    default = {"anx_wino_prio": 257, "anx_conv1_wino_probe": 16, "anx_set_fuse_pool1": 0}[a.knob]
     dev = torch.device("cuda", 0)
     m = AlexNetBlocks(init="rand", device=dev, max_batch=a.batch)
     x = torch.rand(a.batch, 227, 227, 3, device=dev) * 0.1
