@@ -37,6 +37,9 @@ struct SplitK {
   float* ws = nullptr;
 };
 int fc_split_k(const ConvPlanB& p);  // chosen slice count (1 = no split)
+// 128x128 vec8 layers (conv2-5, FC): 2 = LDS-DMA ring of 2 slots (default), 3 = 3 slots, 0 = the
+// register-staged kernel (A/B; env ANX_BF16_GLDS). Returns -1 for another value.
+int bf16_set_glds(int mode);
 hipError_t splitk_reduce_bf16(const float* ws, int ksplit, int M, int K, const float* bias, bool relu, OutViewB out,
                               float* out_f32, hipStream_t s);
 // out_f32 != nullptr: write fp32 (contiguous [M][K]) instead of the bf16 view (final logits).

@@ -116,6 +116,8 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
 int anx_wino_fused_cfg(int cfg);
 // Conv2 Winograd kernel flags (anx::hip::wino_set_prio): bit0 setprio, bit1 NT V stores, bits4-7 cost probes
 int anx_wino_prio(int bits);
+// bf16 128x128 layers: 2 (default) / 3 = LDS-DMA ring slots, 0 = register-staged kernel
+int anx_bf16_glds(int mode);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

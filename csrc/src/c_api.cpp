@@ -386,6 +386,10 @@ int anx_conv1_wino_cfg(int cfg) {
   return 0;
 }
 int anx_wino_prio(int bits) { return anx::hip::wino_set_prio(bits); }
+int anx_bf16_glds(int mode) {
+  if (anx::hip::bf16_set_glds(mode) != 0) return fail("bf16 glds mode must be 0, 2 or 3");
+  return 0;
+}
 int anx_wino_fused_cfg(int cfg) {
   if (anx::hip::wino_set_fused_cfg(cfg) != 0) return fail("fused cfg must be 0..15");
   return 0;

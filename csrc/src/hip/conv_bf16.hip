@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <type_traits>
 #include <vector>
@@ -178,6 +179,145 @@ __global__ void __launch_bounds__(kThreads, VEC8 ? 3 : 2) conv_bf16_kernel(ArgsB
   }
 }
 
+// ---- LDS-DMA ring variant of the 128x128 vec8 kernel (conv2-5, FC) ----
+// The register-staged kernel above pays two __syncthreads per K tile and drains its global loads
+// at each (cdna_hip_programming.md §5: the 2-barrier structure's ceiling). Here operand tiles go
+// global -> LDS by global_load_lds_dwordx4 (per-lane gather addresses: A row = output pixel window
+// origin + koff of the K slice's tap, B row = packed filter) into an NST-deep ring retired by a
+// counted vmcnt and ONE raw barrier per K tile (the fp32 Winograd GEMM's structure, winograd.hip).
+// LDS rows are 64 bf16 = 8 16-B units, unit u of row r stored at u ^ ((r >> 1) & 7): the 16 rows
+// of every ds_read_b128 lane group hit 16 distinct bank quads. No zero-masking: rows past M point
+// at pixel 0 and are never stored; K padding (koff -1 -> 0) meets zero-packed weights.
+using lds_b16 = __attribute__((address_space(3))) bf16;
+__device__ __forceinline__ void glds16_b(const bf16* g, lds_b16* l) { __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0); }
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// WMW waves along M (BM = 64*WMW pixels) x 2 along N (BN = 128 filters), 64x64 per wave.
+template <int NST, int WMW, typename OutT>
+__global__ void __launch_bounds__(128 * WMW) conv_bf16_glds_kernel(ArgsB a) {
+  constexpr int NT = 128 * WMW;                                      // threads
+  constexpr int BM = 64 * WMW, BN = 128, TM = 2, TN = 2, BKU = kBK / 8;  // 8 units per row
+  constexpr int ATILE = BM * kBK, BTILE = BN * kBK;                  // bf16 per operand tile
+  constexpr int STAGE = ATILE + BTILE;
+  constexpr int NA = BM * BKU / NT, NB = BN * BKU / NT;              // DMA per thread per operand
+  static_assert(NA * NT == BM * BKU && NB * NT == BN * BKU && NB >= 1, "tile split");
+  constexpr int RPJ = NT / 8;                                        // rows per DMA round
+  extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
+  int* koff_s = reinterpret_cast<int*>(lds_b + NST * STAGE);
+  int* ooff_s = koff_s + a.kpad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, g = blockIdx.z;
+  const int mt = blockIdx.x / a.n_ntiles, nt = blockIdx.x - mt * a.n_ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const bf16* x = a.x + g * a.Cg;
+  const bf16* wg = a.w + static_cast<size_t>(g) * a.kpad_n * a.kpad;
+  for (int i = tid; i < a.kpad; i += NT) koff_s[i] = a.koff[i];
+  // DMA slot S = j*NT + tid holds row S/8 = j*RPJ + tid/8 (RPJ % 16 == 0), physical unit tid%8 =
+  // logical unit u of that row
+  const int u = (tid & 7) ^ ((tid >> 4) & 7);
+  int aorg[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int m = m0 + j * RPJ + (tid >> 3);
+    aorg[j] = 0;
+    if (m < a.M) {
+      const int n = m / a.HoWo, r = m - n * a.HoWo, oy = r / a.Wo, ox = r - oy * a.Wo;
+      aorg[j] = ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
+    }
+  }
+  if (tid < BM) {
+    const int m = m0 + tid;
+    int oo = -1;
+    if (m < a.M) {
+      const int n = m / a.HoWo, r = m - n * a.HoWo, oy = r / a.Wo, ox = r - oy * a.Wo;
+      oo = ((n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off;
+    }
+    ooff_s[tid] = oo;
+  }
+  const bf16* bsrc = wg + static_cast<size_t>(n0 + (tid >> 3)) * a.kpad + u * 8;
+  __syncthreads();  // koff_s / ooff_s visible
+  lds_b16* lds3 = (lds_b16*)(lds_b);
+  const int kt0 = blockIdx.y * a.kt_per, kt1 = min(a.ktiles, kt0 + a.kt_per);
+  const int total = kt1 > kt0 ? kt1 - kt0 : 0;
+  auto issue = [&](int it) {
+    const int kb = (kt0 + it) * kBK;
+    const int kr = koff_s[kb + u * 8];
+    const int ko = kr >= 0 ? kr : 0;
+    lds_b16* st = lds3 + (it % NST) * STAGE;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) glds16_b(x + aorg[j] + ko, st + (j * NT + wave * 64) * 8);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      glds16_b(bsrc + static_cast<size_t>(j) * RPJ * a.kpad + kb, st + ATILE + (j * NT + wave * 64) * 8);
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+  const int r = lane & 31, h = lane >> 5;
+  int arow[TM], brow[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) arow[i] = wm * 64 + i * 32 + r;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) brow[j] = wn * 64 + j * 32 + r;
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i)
+    if (i < total) issue(i);
+  for (int it = 0; it < total; ++it) {
+    if (it + NST - 2 < total)
+      wait_vm<(NA + NB) * (NST - 2)>();
+    else
+      wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // slice it landed for every wave; slot (it-1) % NST is free
+    asm volatile("" ::: "memory");
+    if (it + NST - 1 < total) issue(it + NST - 1);
+    const bf16* base = lds_b + (it % NST) * STAGE;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < kBK / 16; ++s) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(base + arow[i] * kBK + (((2 * s + h) ^ ((arow[i] >> 1) & 7)) * 8));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(base + ATILE + brow[j] * kBK + (((2 * s + h) ^ ((brow[j] >> 1) & 7)) * 8));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  OutT* out = static_cast<OutT*>(a.out) + blockIdx.y * a.split_stride + g * a.Kg;
+  using i32x4 = __attribute__((ext_vector_type(4))) int;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    i32x4 oo[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) oo[q] = *reinterpret_cast<const i32x4*>(ooff_s + wm * 64 + i * 32 + 8 * q + 4 * h);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int f = n0 + wn * 64 + j * 32 + r;
+      if (f >= a.Kg) continue;
+      const float bv = a.bias ? a.bias[g * a.Kg + f] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int o = oo[e >> 2][e & 3];
+        if (o < 0) continue;
+        float v = acc[i][j][e] + bv;
+        if (a.relu) v = fmaxf(v, 0.f);
+        out[o + f] = static_cast<OutT>(v);
+      }
+    }
+  }
+}
+
 // ---- bf16 max-pool (8 channels per thread) and max-pool + LRN (fp32 math) ----
 __global__ void __launch_bounds__(256) pool_bf16_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
                                                         int F, int S, int Ho, int Wo, OutViewB o) {
@@ -284,6 +424,13 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16* __restrict
        i += static_cast<size_t>(gridDim.x) * blockDim.x)
     y[i] = static_cast<bf16>(x[i]);
 }
+
+// 128x128 vec8 convs / FC: 0 = register-staged kernel, 2 = LDS-DMA ring 2 slots, 3 = 3 slots
+// (ANX_BF16_GLDS; A/B through anx_bf16_glds)
+int g_bf16_glds = [] {
+  const char* e = std::getenv("ANX_BF16_GLDS");
+  return e ? std::atoi(e) : 2;
+}();
 
 struct VariantB {
   int BM, BN;
@@ -429,6 +576,35 @@ hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, c
     else                                                                                              \
       conv_bf16_kernel<BM, BN, WMW, WNW, V8, bf16><<<grid, kThreads, lds, s>>>(a);                    \
   } while (0)
+  if (p.variant == 0 && !p.taps8 && g_bf16_glds > 0) {
+    // LDS-DMA ring: NST slots of (A|B) 128 x 64 bf16 tiles + the koff/ooff tables
+    const int nst = g_bf16_glds == 2 ? 2 : 3;
+    const size_t lds_r = static_cast<size_t>(nst) * 2 * 128 * kBK * 2 + static_cast<size_t>(p.kpad + 128) * 4;
+    if (lds_r <= 160 * 1024) {
+      // dynamic LDS above the 64 KiB default: opt every instantiation in once
+      static const hipError_t attr = [] {
+        const void* ks[] = {reinterpret_cast<const void*>(conv_bf16_glds_kernel<2, 2, float>),
+                            reinterpret_cast<const void*>(conv_bf16_glds_kernel<2, 2, bf16>),
+                            reinterpret_cast<const void*>(conv_bf16_glds_kernel<3, 2, float>),
+                            reinterpret_cast<const void*>(conv_bf16_glds_kernel<3, 2, bf16>)};
+        for (const void* k : ks) {
+          const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+      }();
+      if (attr != hipSuccess) return attr;
+      if (nst == 2 && out_f32)
+        conv_bf16_glds_kernel<2, 2, float><<<grid, kThreads, lds_r, s>>>(a);
+      else if (nst == 2)
+        conv_bf16_glds_kernel<2, 2, bf16><<<grid, kThreads, lds_r, s>>>(a);
+      else if (out_f32)
+        conv_bf16_glds_kernel<3, 2, float><<<grid, kThreads, lds_r, s>>>(a);
+      else
+        conv_bf16_glds_kernel<3, 2, bf16><<<grid, kThreads, lds_r, s>>>(a);
+      return hipGetLastError();
+    }
+  }
   switch (p.variant) {
     case 0: ANX_LAUNCH(128, 128, 2, 2, true); break;
     case 1: ANX_LAUNCH(128, 96, 4, 1, false); break;
@@ -467,6 +643,12 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 }  // namespace
+
+int bf16_set_glds(int mode) {
+  if (mode != 0 && mode != 2 && mode != 3) return -1;
+  g_bf16_glds = mode;
+  return 0;
+}
 
 int fc_split_k(const ConvPlanB& p) {
   if (p.Ho != 1 || p.Wo != 1 || p.groups != 1 || p.Kg % 4) return 1;

@@ -95,6 +95,7 @@ _SIGS = {
     "anx_conv1_wino": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P]),
     "anx_wino_fused_cfg": (_I, [_I]),
     "anx_wino_prio": (_I, [_I]),
+    "anx_bf16_glds": (_I, [_I]),
     "anx_conv2d_mfma": (_I, [C.POINTER(_I), _P, _P, _P, _P, _P] + [_I] * 6 + [_I, _P]),
     "anx_cpu_conv2d": (_I, [_P, _P, _P, _P] + [_I] * 10),
     "anx_cpu_maxpool": (_I, [_P, _P] + [_I] * 6),
