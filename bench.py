@@ -10,9 +10,12 @@ scaling: --batch-per-gpu images per GPU, generated on each rank (--input-source 
 and scatters it every step (prefetched one step ahead); that moves 79 MB per peer per 128 images
 over xGMI, which binds before the compute does, so it is not the throughput configuration.
 
-The default 300 images per GPU is chosen for wave quantization, not memory: both Winograd GEMMs
-then launch whole numbers of 512-workgroup waves (1520 and 2544 workgroups), where 128 images leave
-a 27 % / 30 % tail round (tools/sweep_batch.py: 128 -> 173k, 300 -> 206k images/s).
+The default 600 images per GPU run as 2 lanes of 300 (--lanes: one engine per concurrent HIP stream,
+AlexNetBlocks(lanes=...)). 300 per lane is chosen for wave quantization, not memory: both Winograd
+GEMMs then launch whole numbers of 512-workgroup waves (1520 and 2544 workgroups), where 128 images
+leave a 27 % / 30 % tail round (tools/sweep_batch.py: 128 -> 173k, 300 -> 206k images/s); the second
+lane fills the other's tail waves (profiles/r01_ab_lanes_batch.jsonl: 300 x 1 lane 214k, 300 as
+2 x 150 217k, 600 as 2 x 300 226k images/s).
 
 Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
 bench.py --gpus N``. Rank 0 prints ONE JSON line.
@@ -44,12 +47,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch-per-gpu", type=int, default=300)
+    ap.add_argument("--batch-per-gpu", type=int, default=600)
     # The whole per-rank batch is one launch (fewer, larger launches fill the 256 CUs better); with
     # --no-prefetch, --micro 2 overlaps the second half's scatter with the first half's compute.
     ap.add_argument("--micro", type=int, default=1, help="micro-batches per step for scatter/compute/gather overlap")
     ap.add_argument("--no-prefetch", action="store_true", help="scatter each step's input inside that step only")
     ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="concurrent HIP streams per GPU the batch is split over (one engine each)")
     ap.add_argument("--input-source", default="local", choices=["root", "local"],
                     help="local: per-rank synthetic shard (data-parallel); root: rank 0 scatters the batch (V4/V5)")
     ap.add_argument("--no-gather", action="store_true", help="leave outputs on their ranks")
@@ -86,7 +91,7 @@ def main():
         model = AlexNetFull(seed=1234, device=dev, max_batch=B)
         out_shape, flops = (1000,), FLOPS_PER_IMAGE
     else:
-        model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B)
+        model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B, lanes=a.lanes)
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
     cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather,
                          prefetch=not a.no_prefetch)
@@ -174,6 +179,7 @@ def main():
                 if world > 1 else "single GPU",
                 "input_source": a.input_source,
                 "impl": a.impl,
+                "lanes": a.lanes,
                 "hip_graph": bool(use_graph and world == 1 and dev.type == "cuda"),
                 "gflop_per_image": round(anx.flops_per_image() / 1e9, 4),
                 "tflops": round(imgs * anx.flops_per_image() / 1e12, 2),

@@ -356,3 +356,36 @@ def test_fused_pool1_winograd_input_bitwise(cuda, fuse_pool1, N):
             b = m.tile_forward(xs, t)
             torch.cuda.synchronize()
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("lanes,N", [(2, 150), (3, 200), (2, 100)])
+def test_stream_lanes_bit_identical(cuda, lanes, N):
+    """lanes > 1 splits the batch over concurrent HIP streams (one engine each): every image's output
+    is bit-identical to the one-lane forward (same kernels per image), eager and under graph capture;
+    below lanes * LANE_MIN images the forward stays on one stream."""
+    from anx.models.alexnet_blocks import LANE_MIN
+    x = (init_input(N, "rand", seed=13)).to(cuda)
+    one = AlexNetBlocks(device=cuda, init="rand", seed=13, max_batch=N)
+    many = AlexNetBlocks(one.weights, device=cuda, max_batch=N, lanes=lanes)
+    assert len(many._lanes) == lanes - 1
+    ref = one(x).clone()
+    y = torch.full_like(ref, float("nan"))
+    many(x, out=y)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    # graph capture of the forked/joined lanes, replayed on fresh input
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        many(x, out=y)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        many(x, out=y)
+    x.copy_(init_input(N, "rand", seed=14).to(cuda))
+    y.fill_(float("nan"))
+    g.replay()
+    ref2 = one(x)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref2)
+    assert N >= lanes * LANE_MIN or torch.equal(many(x), ref2)
