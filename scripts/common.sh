@@ -13,7 +13,11 @@ declare -a SUMMARY_ROWS=()
 # here there is exactly one target, gfx950, and its absence is reported, never guessed).
 detect_gpu_arch() {
   if command -v rocminfo >/dev/null 2>&1; then
-    rocminfo 2>/dev/null | grep -o -m1 'gfx[0-9a-f]*' || echo "none"
+    # no `grep -m1`: an early grep exit SIGPIPEs rocminfo and, under pipefail, also printed "none"
+    local a
+    a=$(rocminfo 2>/dev/null | grep -o 'gfx[0-9a-f]*' || true)
+    a=${a%%$'\n'*}
+    echo "${a:-none}"
   else
     echo "none"
   fi
@@ -47,7 +51,8 @@ run_and_classify() {  # logfile, timeout_s, cmd...
   echo 1
 }
 
-# Parse an ANX_JSON record: prints "time_ms shape first5 checksum" (time = warm if present).
+# Parse an ANX_JSON record: prints "time_ms shape first5 checksum max_abs_err" (time = warm if
+# present; max_abs_err vs the fp64 oracle when the run had --check, else NA).
 parse_anx_json() {  # logfile
   python3 - "$1" <<'EOF'
 import json, sys
@@ -56,20 +61,20 @@ for line in open(sys.argv[1], errors="replace"):
     if line.startswith("ANX_JSON "):
         rec = json.loads(line[9:])
 if rec is None:
-    print("NA NA NA NA"); sys.exit(0)
+    print("NA NA NA NA NA"); sys.exit(0)
 t = rec.get("warm_ms") or rec.get("cold_ms")
 first = rec.get("first10") or []
-print(f"{t:.4f} {'x'.join(map(str, rec['shape']))} {'|'.join(str(v) for v in first[:5]) or 'NA'} {rec['checksum']}")
+print(f"{t:.4f} {'x'.join(map(str, rec['shape']))} {'|'.join(str(v) for v in first[:5]) or 'NA'} {rec['checksum']} {rec.get('max_abs_err') if rec.get('max_abs_err') is not None else 'NA'}")
 EOF
 }
 
 summary_add() { SUMMARY_ROWS+=("$*"); }
 
 summary_print() {
-  printf '%-8s %-4s %-6s %-12s %-12s %-10s %s\n' VERSION NP BATCH TIME_MS SHAPE STATUS CHECKSUM
+  printf '%-8s %-4s %-6s %-12s %-12s %-10s %-11s %s\n' VERSION NP BATCH TIME_MS SHAPE STATUS CHECKSUM MAX_ABS_ERR
   printf '%s\n' "-------------------------------------------------------------------------------"
   for r in "${SUMMARY_ROWS[@]}"; do
     # shellcheck disable=SC2086
-    printf '%-8s %-4s %-6s %-12s %-12s %-10s %s\n' $r
+    printf '%-8s %-4s %-6s %-12s %-12s %-10s %-11s %s\n' $r
   done
 }

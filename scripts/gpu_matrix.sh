@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 400 bash scripts/run_matrix.sh --no-build --batch 1 --iters 3 > gpurun_out/matrix_b1.log 2>&1 && \
-timeout -k 10 400 bash scripts/run_matrix.sh --no-build --batch 256 --iters 3 > gpurun_out/matrix_b256.log 2>&1
+timeout -k 10 600 bash scripts/run_matrix.sh --no-build --batch 256 --iters 1 > gpurun_out/matrix_b256.log 2>&1
 rc=$?
 cp -r logs gpurun_out/matrix_logs 2>/dev/null
 [ $rc -ne 0 ] && exit $rc
