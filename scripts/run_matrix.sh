@@ -6,10 +6,11 @@
 # single-process one, and write a session directory with per-run logs, a 20-column CSV and a summary.
 #
 # usage: scripts/run_matrix.sh [--batch N] [--iters K] [--init const|rand] [--no-build] [--cpu-only]
+#                              [--out DIR]   (session directories go under DIR, default logs/)
 set -uo pipefail
 source "$(dirname "$0")/common.sh"
 
-BATCH=1; ITERS=3; INIT=rand; BUILD=1; CPU_ONLY=0
+BATCH=1; ITERS=3; INIT=rand; BUILD=1; CPU_ONLY=0; LOGDIR="$ANX_ROOT/logs"
 while [ $# -gt 0 ]; do
   case "$1" in
     --batch) BATCH="$2"; shift 2 ;;
@@ -17,6 +18,7 @@ while [ $# -gt 0 ]; do
     --init) INIT="$2"; shift 2 ;;
     --no-build) BUILD=0; shift ;;
     --cpu-only) CPU_ONLY=1; shift ;;
+    --out) LOGDIR="$2"; shift 2 ;;
     *) echo "unknown option $1"; exit 2 ;;
   esac
 done
@@ -24,7 +26,7 @@ done
 HOST=$(hostname 2>/dev/null || echo host)
 TS=$(date +%Y%m%d_%H%M%S)
 SESSION="matrix_${TS}_${HOST}"
-OUT="$ANX_ROOT/logs/$SESSION"
+OUT="$LOGDIR/$SESSION"
 mkdir -p "$OUT"
 CSV="$OUT/summary_report_${SESSION}.csv"
 csv_init "$CSV"
