@@ -469,7 +469,12 @@ ConvPlanB make_conv_plan_bf16(int N, int Hp, int Wp, int C, int K, int F, int S,
   }
   p.kpad = (p.kdim + kBK - 1) / kBK * kBK;
   const long M = static_cast<long>(N) * p.Ho * p.Wo;
-  const bool small = M * K < 256L * 128 * 128;
+  // 64x64 tiles below this many outputs (ANX_BF16_SMALL_MK overrides; A/B knob for wave quantization)
+  static const long small_mk = [] {
+    const char* e = std::getenv("ANX_BF16_SMALL_MK");
+    return e ? std::atol(e) : 256L * 128 * 128;
+  }();
+  const bool small = M * K < small_mk;
   const bool fc = Hp == 1 && Wp == 1 && F == 1;  // fully-connected layer: 128x128 tiles + split-K
   if (fc && p.vec8) p.variant = 0;
   else if (p.Kg == 96 && !small) p.variant = p.vec8 ? 5 : 1;
