@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch-per-gpu", type=int, default=600)
+    ap.add_argument("--batch-per-gpu", type=int, default=None,
+                    help="images per GPU (default 600 for blocks; 256 for full = BASELINE's 2048 over 8 GPUs)")
     # The whole per-rank batch is one launch (fewer, larger launches fill the 256 CUs better); with
     # --no-prefetch, --micro 2 overlaps the second half's scatter with the first half's compute.
     ap.add_argument("--micro", type=int, default=1, help="micro-batches per step for scatter/compute/gather overlap")
@@ -84,7 +85,7 @@ def main():
         if world > 1:
             dist.init_process_group("gloo")
 
-    B = a.batch_per_gpu
+    B = a.batch_per_gpu or (256 if a.model == "full" else 600)
     d = anx.blocks_dims()
     if a.model == "full":  # extension config: full AlexNet bf16 (BASELINE.json config 5)
         from anx.models.alexnet_full import FLOPS_PER_IMAGE, AlexNetFull
