@@ -27,6 +27,7 @@ import json
 import os
 import sys
 import time
+from datetime import timedelta
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -79,11 +80,11 @@ def main():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timedelta(seconds=300))  # a hung collective fails in 5 min, not 10
     else:  # CPU rehearsal of the same pipeline over gloo (tests; no GPU)
         dev = torch.device("cpu")
         if world > 1:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timedelta(seconds=300))
 
     B = a.batch_per_gpu or (256 if a.model == "full" else 600)
     d = anx.blocks_dims()
