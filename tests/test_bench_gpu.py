@@ -1,0 +1,38 @@
+"""bench.py's driver contract on one MI355X: one JSON line with the BASELINE metric and config, for
+the headline Blocks 1-2 fp32 step (2 stream lanes) and the full-AlexNet bf16 extension."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config")
+
+
+def bench(args):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", *args],
+                         capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert all(k in rec for k in KEYS) and rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["value"] > 0
+    return rec
+
+
+@pytest.mark.gpu
+def test_bench_blocks_contract():
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        metric = json.load(f)["metric"]
+    rec = bench(["--batch-per-gpu", "64"])
+    assert rec["metric"] == metric and rec["dtype"] == "fp32" and rec["config"]["global_batch"] == 64
+    assert rec["config"]["lanes"] == 2 and rec["vs_baseline"] > 1
+
+
+@pytest.mark.gpu
+def test_bench_full_contract():
+    rec = bench(["--model", "full", "--batch-per-gpu", "32"])
+    assert rec["dtype"] == "bf16" and rec["config"]["global_batch"] == 32
