@@ -49,6 +49,9 @@ hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S,
 hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
                             float beta, float k, LrnMode mode, OutViewB out, hipStream_t s);
 hipError_t f32_to_bf16(const float* x, void* y, size_t n, hipStream_t s);
+// Conv1 polyphase input (space-to-depth by the stride 4) fused with the bf16 conversion:
+// y[n][i][j][(rh*4+rw)*3+c] = x[n][4i+rh][4j+rw][c] (0 past the image), y = [N, ceil(H/4), ceil(W/4), 48].
+hipError_t f32_to_bf16_s2d4(const float* x, void* y, int N, int H, int W, hipStream_t s);
 
 }  // namespace hip
 
@@ -86,6 +89,7 @@ class FullEngine {
   Layer L_[8];
   int classes_, max_batch_, chunk_;
   LrnMode lrn_;
+  bool poly1_ = false;  // Conv1 as a stride-1 3x3 conv over the 48-channel polyphase image (ANX_FULL_CONV1)
   void *xb_ = nullptr, *c1_ = nullptr, *q2_ = nullptr, *c2_ = nullptr, *q3_ = nullptr, *q4_ = nullptr,
        *q5_ = nullptr, *c5_ = nullptr, *f6_ = nullptr, *f7_ = nullptr, *f8_ = nullptr;
   float* ws_ = nullptr;  // split-K partial slabs of the FC layers (sized for every batch <= chunk_)

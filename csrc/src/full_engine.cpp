@@ -2,6 +2,7 @@
 // stay resident; every activation between layers lives in a persistent bf16 workspace, with the
 // padded layers' inputs kept as zero-bordered windows that the producing kernel writes into.
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -55,9 +56,36 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
     L.bias = static_cast<float*>(dalloc(bn[i] * 4));
     check(hipMemcpy(L.bias, w.b[i].data(), bn[i] * 4, hipMemcpyHostToDevice), "H2D bias");
   }
+  // Conv1 polyphase (the fp32 Winograd Conv1's rewrite, conv1_wino.hip): space-to-depth by the stride
+  // turns 11x11/4 over 3 channels into 3x3/1 over 48, so the implicit GEMM's A gathers are aligned
+  // 16-B channel runs instead of taps8's 2-byte-aligned 11-tap rows. Exact: W'[k][(rh*4+rw)*3+c][qh][qw]
+  // = w[k][c][4qh+rh][4qw+rw], 0 past the 11x11 window. ANX_FULL_CONV1=taps8 keeps the direct form.
+  {
+    const char* e = std::getenv("ANX_FULL_CONV1");
+    poly1_ = !(e && std::string(e) == "taps8");
+  }
+  if (poly1_) {
+    Layer& L = L_[0];
+    std::vector<float> wp(static_cast<size_t>(L.K) * 48 * 9, 0.f);
+    for (int k = 0; k < L.K; ++k)
+      for (int rh = 0; rh < 4; ++rh)
+        for (int rw = 0; rw < 4; ++rw)
+          for (int c = 0; c < 3; ++c)
+            for (int qh = 0; qh < 3; ++qh)
+              for (int qw = 0; qw < 3; ++qw) {
+                const int fh = 4 * qh + rh, fw = 4 * qw + rw;
+                if (fh < 11 && fw < 11)
+                  wp[((static_cast<size_t>(k) * 48 + (rh * 4 + rw) * 3 + c) * 3 + qh) * 3 + qw] =
+                      L.host[((static_cast<size_t>(k) * 3 + c) * 11 + fh) * 11 + fw];
+              }
+    L.host = std::move(wp);
+    L.C = 48;
+    L.F = 3;
+    L.S = 1;
+  }
   chunk_ = std::max(1, std::min(max_batch, static_cast<int>(((1UL << 31) - 1) / (55UL * 55 * 96))));
   const size_t n = static_cast<size_t>(chunk_);
-  xb_ = dalloc(n * 227 * 227 * 3 * 2);
+  xb_ = dalloc(n * std::max(227 * 227 * 3, 57 * 57 * 48) * 2);
   c1_ = dalloc(n * 55 * 55 * 96 * 2);
   q2_ = dalloc(n * 31 * 31 * 96 * 2);
   c2_ = dalloc(n * 27 * 27 * 256 * 2);
@@ -119,8 +147,14 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
   auto B = [](void* p) { return static_cast<__bf16*>(p); };
   for (int n0 = 0; n0 < N; n0 += chunk_) {
     const int n = std::min(chunk_, N - n0);
-    ANX_TRY(hip::f32_to_bf16(x + static_cast<size_t>(n0) * 227 * 227 * 3, xb_, static_cast<size_t>(n) * 227 * 227 * 3, s));
-    ANX_TRY(conv(L_[0], n, 227, 227, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
+    const float* xn = x + static_cast<size_t>(n0) * 227 * 227 * 3;
+    if (poly1_) {
+      ANX_TRY(hip::f32_to_bf16_s2d4(xn, xb_, n, 227, 227, s));
+      ANX_TRY(conv(L_[0], n, 57, 57, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
+    } else {
+      ANX_TRY(hip::f32_to_bf16(xn, xb_, static_cast<size_t>(n) * 227 * 227 * 3, s));
+      ANX_TRY(conv(L_[0], n, 227, 227, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
+    }
     ANX_TRY(hip::maxpool_bf16(c1_, n, 55, 55, 96, 3, 2, OutViewB{B(q2_), 31, 31, 96, 2, 2, 0}, s));
     ANX_TRY(conv(L_[1], n, 31, 31, q2_, OutViewB{B(c2_), 27, 27, 256, 0, 0, 0}, nullptr, true, s));
     ANX_TRY(hip::maxpool_lrn_bf16(c2_, n, 27, 27, 256, 3, 2, 5, 1e-4f, 0.75f, 2.0f, lrn_,

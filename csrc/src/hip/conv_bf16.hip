@@ -425,6 +425,37 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16* __restrict
     y[i] = static_cast<bf16>(x[i]);
 }
 
+// Thread = (n, i, j, rh): the 12 floats (rw, c) of polyphase row rh are contiguous in image row
+// 4i+rh, and so are their 12 bf16 outputs (24 B at a 24-B aligned offset: 3 8-byte stores).
+__global__ void __launch_bounds__(256) s2d4_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, int total,
+                                                        int H, int W, int Ho, int Wo) {
+  using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    const int rh = t & 3;
+    const int pix = t >> 2;  // (n, i, j)
+    const int j = pix % Wo;
+    const int ni = pix / Wo;
+    const int i = ni % Ho;
+    const int n = ni / Ho;
+    const int r = 4 * i + rh;
+    float v[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) v[e] = 0.f;
+    if (r < H) {
+      const float* src = x + (static_cast<size_t>(n) * H + r) * W * 3 + 4 * j * 3;
+      const int valid = min(4, W - 4 * j) * 3;
+#pragma unroll
+      for (int e = 0; e < 12; ++e)
+        if (e < valid) v[e] = src[e];
+    }
+    bf16x4* dst = reinterpret_cast<bf16x4*>(y + static_cast<size_t>(pix) * 48 + rh * 12);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      dst[q] = bf16x4{static_cast<bf16>(v[4 * q]), static_cast<bf16>(v[4 * q + 1]), static_cast<bf16>(v[4 * q + 2]),
+                      static_cast<bf16>(v[4 * q + 3])};
+  }
+}
+
 // 128x128 vec8 convs / FC: 0 = register-staged kernel, 2 = LDS-DMA ring 2 slots, 3 = 3 slots
 // (ANX_BF16_GLDS; A/B through anx_bf16_glds)
 int g_bf16_glds = [] {
@@ -699,6 +730,15 @@ hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, in
 hipError_t f32_to_bf16(const float* x, void* y, size_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
   f32_to_bf16_kernel<<<grid1d(static_cast<long>(n)), 256, 0, s>>>(x, static_cast<bf16*>(y), n);
+  return hipGetLastError();
+}
+
+hipError_t f32_to_bf16_s2d4(const float* x, void* y, int N, int H, int W, hipStream_t s) {
+  const int Ho = (H + 3) / 4, Wo = (W + 3) / 4;
+  const long total = static_cast<long>(N) * Ho * Wo * 4;
+  if (total == 0) return hipSuccess;
+  if (total >= (1L << 31)) return hipErrorInvalidValue;
+  s2d4_bf16_kernel<<<grid1d(total), 256, 0, s>>>(x, static_cast<bf16*>(y), static_cast<int>(total), H, W, Ho, Wo);
   return hipGetLastError();
 }
 

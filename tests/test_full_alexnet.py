@@ -51,3 +51,19 @@ def test_bf16_lds_dma_kernel_matches_register_staged(cuda, mode):
     finally:
         nat.call("anx_bf16_glds", 2)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_full_conv1_polyphase_matches_taps8(cuda, monkeypatch):
+    """Conv1 as a 3x3/1 conv over the 48-channel polyphase image (default) against the direct
+    11x11/4 taps8 gathers (ANX_FULL_CONV1=taps8): same products, other bf16 summation order."""
+    N = 16
+    x = (init_input(N, "rand", seed=8) * 10).to(cuda)
+    monkeypatch.setenv("ANX_FULL_CONV1", "taps8")
+    ref = AlexNetFull(seed=8, device=cuda, max_batch=N)(x).clone()
+    monkeypatch.delenv("ANX_FULL_CONV1")
+    got = AlexNetFull(seed=8, device=cuda, max_batch=N)(x)
+    torch.cuda.synchronize()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 1e-2, rel
+    assert (got.argmax(1) == ref.argmax(1)).float().mean() >= 0.9
