@@ -425,6 +425,57 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16* __restrict
     y[i] = static_cast<bf16>(x[i]);
 }
 
+// pool + LRN for C = 256, size 5 (Conv2 -> Pool2 -> LRN2 of the full model): one wave per output
+// pixel, 4 channels per lane (8-B loads and stores), LRN neighbours from the adjacent lanes by
+// ds_bpermute — the fp32 maxpool_lrn256_kernel's scheme (pool_lrn.hip). Same maxima and the same
+// ascending 5-term sums of squares as pool_lrn_bf16_kernel: bit-identical, without the LDS tile.
+template <int F>
+__global__ void __launch_bounds__(256) pool_lrn256_bf16_kernel(const bf16* __restrict__ x, int P, int H, int W,
+                                                               int S, int Ho, int Wo, float a, float beta, float k,
+                                                               OutViewB o) {
+  constexpr int C = 256;
+  using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+  const int lane = threadIdx.x & 63;
+  // a wave loops over pixels when ANX_LRN_WAVE_WGS caps the grid (measured no faster than one wave per pixel)
+  for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < P; p += gridDim.x * 4) {  // wave-uniform
+  const int ox = p % Wo;
+  const int q = p / Wo;
+  const int oy = q % Ho, n = q / Ho;
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int fh = 0; fh < F; ++fh) {
+    const int iy = oy * S + fh;
+    if (iy >= H) break;
+#pragma unroll
+    for (int fw = 0; fw < F; ++fw) {
+      const int ix = ox * S + fw;
+      if (ix >= W) break;
+      const bf16x4 v = *reinterpret_cast<const bf16x4*>(x + ((static_cast<size_t>(n) * H + iy) * W + ix) * C + lane * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], static_cast<float>(v[e]));
+    }
+  }
+  const int left = ((lane + 63) & 63) * 4, right = ((lane + 1) & 63) * 4;
+  float l0 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(m[2])));
+  float l1 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(m[3])));
+  float r0 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(m[0])));
+  float r1 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(m[1])));
+  if (lane == 0) l0 = l1 = 0.f;
+  if (lane == 63) r0 = r1 = 0.f;
+  const float w[8] = {l0, l1, m[0], m[1], m[2], m[3], r0, r1};
+  bf16x4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float s2 = 0.f;
+#pragma unroll
+    for (int u = e; u < e + 5; ++u) s2 = fmaf(w[u], w[u], s2);
+    r[e] = static_cast<bf16>(w[e + 2] / powf(k + a * s2, beta));
+  }
+  *reinterpret_cast<bf16x4*>(o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
+                             o.c_off + lane * 4) = r;
+  }
+}
+
 // Thread = (n, i, j, rh): the 12 floats (rw, c) of polyphase row rh are contiguous in image row
 // 4i+rh, and so are their 12 bf16 outputs (24 B at a 24-B aligned offset: 3 8-byte stores).
 __global__ void __launch_bounds__(256) s2d4_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, int total,
@@ -722,6 +773,15 @@ hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, in
   if (C % 8 || out.Cb % 8 || out.c_off % 8 || C > 8192) return hipErrorInvalidValue;
   const int PP = C >= 4096 ? 1 : 4096 / C;
   const float a = mode == LrnMode::DivN ? alpha / size : alpha;
+  const char* tile = std::getenv("ANX_BF16_LRN_TILE");  // 1: the LDS-tile kernel (A/B, bitwise test)
+  if (C == 256 && size == 5 && F == 3 && P < (1L << 31) && !(tile && tile[0] == '1')) {
+    const char* cap = std::getenv("ANX_LRN_WAVE_WGS");  // grid cap (A/B; 0 = one wave per pixel)
+    const long wgs_cap = cap ? std::atol(cap) : 0;
+    const long wgs = wgs_cap > 0 ? std::min((P + 3) / 4, wgs_cap) : (P + 3) / 4;
+    pool_lrn256_bf16_kernel<3><<<static_cast<unsigned>(wgs), 256, 0, s>>>(
+        static_cast<const bf16*>(x), static_cast<int>(P), H, W, S, Ho, Wo, a, beta, k, out);
+    return hipGetLastError();
+  }
   pool_lrn_bf16_kernel<<<static_cast<unsigned>((P + PP - 1) / PP), 256, PP * C * 4, s>>>(
       static_cast<const bf16*>(x), N, H, W, C, F, S, Ho, Wo, PP, size, a, beta, k, out);
   return hipGetLastError();

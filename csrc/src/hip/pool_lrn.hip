@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 
 #include "anx/ops.hpp"
@@ -178,8 +179,8 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn256_kernel(const float* _
                                                                   float beta, float k) {
   constexpr int C = 256;
   const int lane = threadIdx.x & 63;
-  const int p = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (p >= P) return;  // wave-uniform
+  // a wave loops over pixels when ANX_LRN_WAVE_WGS caps the grid (measured no faster than one wave per pixel)
+  for (int p = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); p < P; p += gridDim.x * (kThreads / 64)) {
   const int ox = p % Wo;
   const int r = p / Wo;
   const int oy = r % Ho;
@@ -203,6 +204,7 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn256_kernel(const float* _
     out[e] = w[e + 2] / powf(k + a * sq, beta);
   }
   *reinterpret_cast<f32x4*>(y + static_cast<size_t>(p) * C + lane * 4) = out;
+  }
 }
 
 }  // namespace
@@ -233,7 +235,10 @@ hipError_t maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int
   const long blocks = (P + PP - 1) / PP;
   const float a = mode == LrnMode::DivN ? alpha / static_cast<float>(size) : alpha;
   if (F == 3 && C == 256 && size == 5) {
-    const unsigned g = static_cast<unsigned>((P + kThreads / 64 - 1) / (kThreads / 64));
+    const char* cap = std::getenv("ANX_LRN_WAVE_WGS");  // grid cap (A/B; 0 = one wave per pixel)
+    const long wgs_cap = cap ? std::atol(cap) : 0;
+    const long all = (P + kThreads / 64 - 1) / (kThreads / 64);
+    const unsigned g = static_cast<unsigned>(wgs_cap > 0 ? std::min(all, wgs_cap) : all);
     maxpool_lrn256_kernel<3><<<g, kThreads, 0, s>>>(x, y, static_cast<int>(P), H, W, S, Ho, Wo, a, beta, k);
     return hipGetLastError();
   }

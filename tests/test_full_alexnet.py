@@ -67,3 +67,19 @@ def test_full_conv1_polyphase_matches_taps8(cuda, monkeypatch):
     rel = ((got - ref).norm() / ref.norm()).item()
     assert rel < 1e-2, rel
     assert (got.argmax(1) == ref.argmax(1)).float().mean() >= 0.9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lrn", ["div_n", "raw"])
+def test_bf16_pool_lrn_wave_kernel_bitwise(cuda, monkeypatch, lrn):
+    """Pool2+LRN2 as one wave per pixel (bpermute neighbours, default) against the LDS-tile kernel
+    (ANX_BF16_LRN_TILE=1): same maxima, same ascending sums -> logits bit-identical."""
+    N = 24
+    x = (init_input(N, "rand", seed=9) * 10).to(cuda)
+    monkeypatch.setenv("ANX_BF16_LRN_TILE", "1")
+    m = AlexNetFull(seed=9, device=cuda, max_batch=N, lrn_mode=lrn)
+    ref = m(x).clone()
+    monkeypatch.delenv("ANX_BF16_LRN_TILE")
+    got = m(x)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
