@@ -7,6 +7,7 @@
 #include <cstring>
 #include <vector>
 
+#include "anx/knobs.hpp"
 #include "anx/shapes.hpp"
 
 namespace anx {
@@ -37,14 +38,13 @@ struct SplitK {
   float* ws = nullptr;
 };
 int fc_split_k(const ConvPlanB& p);  // chosen slice count (1 = no split)
-// 128x128 vec8 layers (conv2-5, FC): 2 = LDS-DMA ring of 2 slots (default), 3 = 3 slots, 0 = the
-// register-staged kernel (A/B; env ANX_BF16_GLDS). Returns -1 for another value.
-int bf16_set_glds(int mode);
 hipError_t splitk_reduce_bf16(const float* ws, int ksplit, int M, int K, const float* bias, bool relu, OutViewB out,
                               float* out_f32, hipStream_t s);
 // out_f32 != nullptr: write fp32 (contiguous [M][K]) instead of the bf16 view (final logits).
+// glds (Knobs::bf16_glds): 128x128 vec8 layers (conv2-5, FC) run the LDS-DMA ring with 2 (default) or
+// 3 slots, 0 = the register-staged kernel (A/B).
 hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, const int* koff, const float* bias,
-                       OutViewB out, float* out_f32, bool relu, hipStream_t s, SplitK split = {});
+                       OutViewB out, float* out_f32, bool relu, hipStream_t s, SplitK split = {}, int glds = 2);
 hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S, OutViewB out, hipStream_t s);
 hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
                             float beta, float k, LrnMode mode, OutViewB out, hipStream_t s);
@@ -66,7 +66,8 @@ void full_weight_shapes(int classes, int groups2, size_t wn[8], size_t bn[8]);
 
 class FullEngine {
  public:
-  FullEngine(const FullWeights& w, int classes, int max_batch, int groups2 = 1, LrnMode lrn = LrnMode::DivN);
+  FullEngine(const FullWeights& w, int classes, int max_batch, int groups2 = 1, LrnMode lrn = LrnMode::DivN,
+             const Knobs& k = default_knobs());
   ~FullEngine();
   FullEngine(const FullEngine&) = delete;
   FullEngine& operator=(const FullEngine&) = delete;
@@ -74,6 +75,7 @@ class FullEngine {
   hipError_t forward(const float* x, int N, float* logits, hipStream_t s);
   int classes() const { return classes_; }
   int max_batch() const { return max_batch_; }
+  Knobs& knobs() { return k_; }  // read at every launch (bf16_glds)
 
  private:
   struct Layer {
@@ -87,6 +89,7 @@ class FullEngine {
   hipError_t conv(Layer& L, int N, int Hp, int Wp, const void* x, hip::OutViewB out, float* out_f32, bool relu,
                   hipStream_t s);
   Layer L_[8];
+  Knobs k_;
   int classes_, max_batch_, chunk_;
   LrnMode lrn_;
   bool poly1_ = false;  // Conv1 as a stride-1 3x3 conv over the 48-channel polyphase image (ANX_FULL_CONV1)

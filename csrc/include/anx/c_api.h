@@ -92,32 +92,19 @@ int anx_maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int F,
 int anx_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups, int* plan_out,
                   size_t* packed_floats, size_t* koff_ints);
 int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff);
-/* tuning: force tile variant `id` for kind 0 (vec4 gather) / 1 (scalar gather); -1 = heuristic */
-int anx_conv_force_variant(int kind, int id);
-/* Conv2 (5x5 s1) algorithm on the MFMA path: 0 auto (Winograd F(3,5) when eligible), 1 direct, 2 Winograd */
-int anx_set_conv2_algo(int algo);
-// images per launch of stage 1 / stage 2 (0 = whole batch); see anx::set_stage_chunks
-int anx_set_stage_chunks(int stage1, int stage2);
-// pool1 fused into Conv2's Winograd input transform (1) or a separate pool1 pass (0, default)
-int anx_set_fuse_pool1(int on);
-int anx_get_conv2_algo(void);
-/* Conv1 (11x11 s4) algorithm on the MFMA path: 0 auto (polyphase Winograd F(3,3) when eligible), 1 direct, 2 Winograd */
-int anx_set_conv1_algo(int algo);
-int anx_get_conv1_algo(void);
-/* conv1 Winograd GEMM: 0-3 32x32 MFMA rings (BK48 x 2, BK16 x 4/6/8), 4 16x16 MFMA 4 WG/CU (default) */
-int anx_conv1_wino_cfg(int cfg);
-/* profiling probes (wrong results): bit0 skip the output-transform fold, bit1 skip LDS-DMA refills */
-int anx_conv1_wino_probe(int bits);
+/* Per-engine kernel knobs (anx/knobs.hpp): names conv1_algo, conv2_algo, conv1_cfg, conv1_probe,
+   wino_cfg, wino_prio, fold_scalar, chunk1, chunk2, fuse_pool1, force_vec4, force_scalar, bf16_glds.
+   set returns non-zero for an unknown name or an out-of-range value. */
+int anx_engine_set_knob(void* engine, const char* name, int value);
+int anx_engine_get_knob(void* engine, const char* name, int* value);
+int anx_full_set_knob(void* engine, const char* name, int value);
+int anx_full_get_knob(void* engine, const char* name, int* value);
+/* the defaults a new engine starts from (built-in values overridden by ANX_* environment variables) */
+int anx_default_knob(const char* name, int* value);
 /* Conv1 by polyphase Winograd on device buffers (test entry; allocates and frees its workspaces,
    synchronises `stream`): x [N,Hin,W,3], KCFF weights on the HOST, y [N,H1,W1,K]. */
 int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, int K, int F, const float* bias,
-                   float* y, int relu, void* stream);
-/* fused Winograd kernel tuning: bit0 K-slice 48 (else 32), bit1 XCD-aware order, bit2 LDS-DMA ring (default 7) */
-int anx_wino_fused_cfg(int cfg);
-// Conv2 Winograd kernel flags (anx::hip::wino_set_prio): bit0 setprio, bit1 NT V stores, bits4-7 cost probes
-int anx_wino_prio(int bits);
-// bf16 128x128 layers: 2 (default) / 3 = LDS-DMA ring slots, 0 = register-staged kernel
-int anx_bf16_glds(int mode);
+                   float* y, int relu, int fold_scalar, void* stream);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

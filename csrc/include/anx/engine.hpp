@@ -12,6 +12,7 @@
 
 #include <vector>
 
+#include "anx/knobs.hpp"
 #include "anx/ops.hpp"
 #include "anx/plan.hpp"
 #include "anx/shapes.hpp"
@@ -22,33 +23,6 @@ enum class Impl : int {
   Mfma = 0,    // MFMA implicit-GEMM convs + fused epilogues (default)
   Direct = 1,  // naive one-thread-per-output kernels (device oracle)
 };
-
-// Algorithm for 5x5 stride-1 convolutions (Conv2) on the Mfma path: Auto picks Winograd
-// F(3x3,5x5) when eligible and the launch is larger than 8 images (use_winograd), the direct
-// implicit GEMM below that. Process-wide; read when a stage is launched.
-// WinogradUnfused = input transform + separate batched GEMM (M in HBM) + output transform (A/B).
-enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2, WinogradUnfused = 3 };
-void set_conv2_algo(ConvAlgo a);
-ConvAlgo conv2_algo();
-// Algorithm for Conv1 (stride 4, C = 3) on the Mfma path: Winograd = polyphase Winograd
-// F(3x3,3x3) (conv1_wino.hip) when eligible, Auto = that above 8 images per launch, Direct = the implicit-GEMM kernel (bit-identical across
-// row decompositions; Winograd tile origins move with the row split, ~1e-7 relative).
-void set_conv1_algo(ConvAlgo a);
-ConvAlgo conv1_algo();
-// Images per launch of stage 1 (Conv1 + Pool1) and stage 2 (Conv2 + Pool2 + LRN); 0 = the whole
-// batch (up to the 32-bit-index chunk). Smaller chunks reuse one set of transform/conv buffers per
-// chunk, so the Winograd V buffers can stay in the 256 MiB Infinity Cache between the transform that
-// writes them and the GEMM that reads them. Process-wide; env ANX_CHUNK1 / ANX_CHUNK2.
-void set_stage_chunks(int stage1, int stage2);
-// Algorithm actually used by a launch of n images x `rows` output rows of a conv whose full image
-// has `full_rows` rows: Auto = Winograd above 8 full images' worth of rows, direct below.
-bool use_winograd(ConvAlgo a, int n, int rows, int full_rows);
-// Pool1 fused into Conv2's Winograd input transform inside forward()/tile_forward() (the split
-// stage1/stage2 path keeps the materialised window for halo exchange). Default off (measured
-// slower); ANX_FUSE_POOL1=1 or anx_set_fuse_pool1 enables it.
-void set_fuse_pool1(bool on);
-bool fuse_pool1();
-int stage_chunk(int stage);
 
 struct HostWeights {
   std::vector<float> w1, b1, w2, b2;  // KCFF weights, biases
@@ -63,8 +37,9 @@ void init_input_random(std::vector<float>& x, size_t n, unsigned seed);
 
 class BlocksEngine {
  public:
+  // k: kernel selection and tuning of this engine (default_knobs(): built-in defaults + ANX_* env).
   BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int W, const HostWeights& w, int max_batch,
-               Impl impl = Impl::Mfma);
+               Impl impl = Impl::Mfma, const Knobs& k = default_knobs());
   ~BlocksEngine();
   BlocksEngine(const BlocksEngine&) = delete;
   BlocksEngine& operator=(const BlocksEngine&) = delete;
@@ -72,6 +47,9 @@ class BlocksEngine {
   const BlocksDims& dims() const { return d_; }
   int max_batch() const { return max_batch_; }
   Impl impl() const { return impl_; }
+  // Read at every launch: changing a knob between calls switches kernels (weights re-pack lazily).
+  Knobs& knobs() { return k_; }
+  const Knobs& knobs() const { return k_; }
 
   // x: [N, H, W, C0] device; y: [N, Hp2, Wp2, C2] device.
   hipError_t forward(const float* x, int N, float* y, hipStream_t s);
@@ -101,6 +79,7 @@ class BlocksEngine {
   int max_batch_;
   int chunk_;  // images per internal launch chunk (32-bit index limits)
   Impl impl_;
+  Knobs k_;
   int wq_;     // padded conv2 input width
   // device buffers
   float *w1_ = nullptr, *b1d_ = nullptr, *w2_ = nullptr, *b2d_ = nullptr;  // KCFF (direct path)

@@ -1,0 +1,50 @@
+// anx/knobs.hpp — per-engine kernel selection and tuning.
+//
+// Every algorithm choice and A/B knob of the compute path lives in one value type that an engine
+// owns (BlocksEngine, FullEngine) and passes to the launchers it calls. Two engines in one process
+// can therefore run different kernels (stream lanes, A/B arms, tests), and nothing a launch reads
+// is process-wide mutable state. Environment variables (ANX_*) only seed default_knobs(), once per
+// engine construction.
+//
+// The reference has no run-time configuration at all: every dim and parameter is hard-coded in each
+// version's main() (v1_serial/src/main.cpp:18-43, v4_mpi_cuda/src/main_mpi_cuda.cpp:146-150).
+#pragma once
+
+namespace anx {
+
+// Algorithm for a convolution on the Mfma path. Auto = Winograd when eligible and the launch is
+// larger than 8 images' worth of output rows (use_winograd), the direct implicit GEMM below that.
+// WinogradUnfused = input transform + separate batched GEMM (M in HBM) + output transform (A/B only).
+enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2, WinogradUnfused = 3 };
+
+struct Knobs {
+  ConvAlgo conv1_algo = ConvAlgo::Auto;  // Conv1: polyphase Winograd F(3x3,3x3) / direct implicit GEMM
+  ConvAlgo conv2_algo = ConvAlgo::Auto;  // Conv2: Winograd F(3x3,5x5) / direct implicit GEMM
+  int conv1_cfg = 4;       // Conv1 Winograd GEMM variant 0..4 (conv1_wino.hip; 4 = 16x16 MFMA, 4 WG/CU)
+  int conv1_probe = 16;    // Conv1 GEMM bits: 4 s_setprio, 5 NT V stores, 6 interleaved fold; 0-3 cost probes
+  int wino_cfg = 7;        // Conv2 fused GEMM: bit0 BK 48, bit1 XCD order, bit2 LDS-DMA ring, bit3 16x16 MFMA
+  int wino_prio = 257;     // Conv2 fused GEMM bits: 0 s_setprio, 1 NT V stores, 8 interleaved fold; 4-7 probes
+  int fold_scalar = 0;     // Winograd output folds as scalar v_fma_f32 instead of packed v_pk_fma_f32: bit0 Conv1, bit1 Conv2
+  int chunk1 = 0;          // images per stage-1 launch (0 = whole batch up to the 32-bit index chunk)
+  int chunk2 = 0;          // images per stage-2 launch
+  int fuse_pool1 = 0;      // pool1 fused into Conv2's Winograd input transform (measured slower: off)
+  int force_vec4 = -1;     // conv_mfma tile variant override for Cg % 4 == 0 convs (-1 = heuristic)
+  int force_scalar = -1;   // conv_mfma tile variant override for scalar-gather convs
+  int bf16_glds = 2;       // bf16 full model: 0 register-staged, 2 / 3 LDS-DMA ring slots
+};
+
+// Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CONV1_WINO_CFG,
+// ANX_CONV1_WINO_PROBE, ANX_WINO_FUSED_CFG, ANX_WINO_PRIO, ANX_FOLD_SCALAR, ANX_CHUNK1, ANX_CHUNK2,
+// ANX_FUSE_POOL1, ANX_BF16_GLDS when set.
+Knobs default_knobs();
+
+// Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for
+// an unknown name or an out-of-range value (the knob is then unchanged).
+int set_knob(Knobs& k, const char* name, int value);
+int get_knob(const Knobs& k, const char* name, int* value);
+
+// Whether a launch of n images x `rows` output rows of a conv whose full image has `full_rows`
+// rows runs Winograd under algorithm a (Auto: above 8 full images' worth of rows).
+bool use_winograd(ConvAlgo a, int n, int rows, int full_rows);
+
+}  // namespace anx

@@ -10,6 +10,7 @@
 
 #include <vector>
 
+#include "anx/knobs.hpp"
 #include "anx/shapes.hpp"
 
 namespace anx {
@@ -70,7 +71,11 @@ struct ConvPlan {
                       // into 4-float units, the last one shifted back to end at F*C (its
                       // overlap gets zero weight) -> kdim = F*4*ceil(F*C/4), 16-B gathers
 };
-ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups);
+// force_vec4 / force_scalar: tile variant override for Cg%4==0 / scalar-gather convs (A/B tuning,
+// Knobs::force_vec4 / force_scalar; -1 or an invalid id = the heuristic).
+ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups, int force_vec4 = -1,
+                        int force_scalar = -1);
+bool conv_variant_valid(int kind, int id);
 // Packed weights: [groups][kpad_n][kpad] with k = (fh*F + fw)*Cg + c (taps4: k = (fh*U + u)*4 + e
 // over the 4-float units u of filter row fh); zero padded.
 size_t packed_weight_floats(const ConvPlan& p);
@@ -79,9 +84,6 @@ size_t koff_ints(const ConvPlan& p);
 // Host-side packing (weights come from the host in KCFF order).
 void pack_conv_weights_host(const ConvPlan& p, const float* w_kcff, std::vector<float>& packed,
                             std::vector<int>& koff);
-// Force a tile variant for subsequent plans (kind 0: Cg%4==0 convs, 1: scalar-gather convs;
-// id -1 restores the heuristic). Tuning/A-B only; returns -1 for an invalid pair.
-int conv_force_variant(int kind, int id);
 hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, const int* koff,
                        const float* bias, OutView out, bool relu, hipStream_t s);
 
@@ -97,7 +99,8 @@ size_t wino_v_floats(const WinoPlan& w);
 size_t wino_m_floats(const WinoPlan& w);
 // U = G g G^T in fp64, laid out as KCFF weights of the grouped 1x1 GEMM ([49*K][C/g]).
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
-hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s);
+// nt: non-temporal V stores (Knobs::wino_prio bit1, A/B).
+hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s, bool nt = false);
 // Pool1 (3x3 / 2, post-ReLU conv1 input) fused into the input transform: V of the zero-bordered
 // pool1 window without materialising it. Window row r = pool1 row r + q_lo; pool1 rows outside
 // [p1_lo, p1_hi) and columns outside [0, Wp) are the border; conv1 rows [c1_lo, c1_lo + H1) are in
@@ -107,16 +110,14 @@ struct WinoPoolGeom {
 };
 hipError_t wino_input_pool(const WinoPlan& w, const float* c1, const WinoPoolGeom& pg, float* V, hipStream_t s);
 hipError_t wino_output(const WinoPlan& w, const float* Mt, const float* bias, float* y, bool relu, hipStream_t s);
-// Tuning (A/B): bit0 = K-slice 48 instead of 32, bit1 = XCD-aware block order, bit2 = LDS-DMA ring.
-// Default 7 (measured at 300 images: ring +17 %, BK 48 +3 %, XCD order +1 %).
-int wino_set_fused_cfg(int cfg);
-// bit0 s_setprio around MFMA slices, bit8 interleaved output fold (default 257); bit1 non-temporal V
-// stores; bits 4-7 cost probes
-// of the LDS-DMA fused kernel (wrong results): no fold / no refills / no barrier / no stores
-int wino_set_prio(int bits);
 // Batched GEMM + output transform in one kernel (M stays in registers); U packed as for w.gemm.
+// Kernel choice from the engine's knobs: wino_cfg bit0 = K-slice 48 instead of 32, bit1 = XCD-aware
+// block order, bit2 = LDS-DMA ring, bit3 = 16x16 MFMA (default 7; measured at 300 images: ring
+// +17 %, BK 48 +3 %, XCD order +1 %); wino_prio bit0 s_setprio around the MFMA slices, bit8
+// interleaved output fold (default 257), bits 4-7 cost probes (wrong results): no fold / no refills
+// / no barrier / no stores; fold_scalar: v_fma_f32 instead of v_pk_fma_f32 folds.
 hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
-                      hipStream_t s);
+                      hipStream_t s, const Knobs& k);
 
 // Conv1 (stride 4, C = 3, 8 < F <= 12, no padding) as Winograd F(3x3,3x3) on the polyphase image
 // (conv1_wino.hip): 48 polyphase channels, 3x3 output tiles, 25 transform points.
@@ -129,14 +130,14 @@ Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F);
 size_t conv1_wino_v_floats(const Conv1WinoPlan& w);  // V workspace [P][25][48]
 size_t conv1_wino_u_floats(int K);                   // transformed weights [25][K][48]
 void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u);
-// Tuning (A/B): GEMM configuration 0..4 (conv1_wino.hip default_cfg; 4 = default). -1 on a bad id.
-int conv1_wino_set_cfg(int cfg);
-// Cost probes for profiling only (results become wrong): bit0 skip the output-transform fold,
-// bit1 skip the LDS-DMA refills; bit4 = s_setprio around the MFMA slices (the default, 16).
-int conv1_wino_set_probe(int bits);
-// x: [N, Hin, W, 3] image rows; writes conv1 (+bias, optional ReLU) through `out`.
+// GEMM configuration ids 0..4 (Knobs::conv1_cfg; 4 = default).
+bool conv1_wino_cfg_valid(int cfg);
+// x: [N, Hin, W, 3] image rows; writes conv1 (+bias, optional ReLU) through `out`. Knobs: conv1_cfg;
+// conv1_probe bit4 s_setprio around the MFMA slices (default 16), bit5 NT V stores, bit6 interleaved
+// fold, bits 0-3 cost probes (wrong results): no fold / no refills / no barrier / no stores;
+// fold_scalar.
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
-                      bool relu, hipStream_t s);
+                      bool relu, hipStream_t s, const Knobs& k);
 
 // Vectorised NHWC max-pool writing through an OutView (C % 4 == 0 required for the fast path).
 hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, OutView out, hipStream_t s);

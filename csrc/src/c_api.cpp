@@ -358,50 +358,34 @@ int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff
   });
 }
 
-int anx_set_conv2_algo(int algo) {
-  if (algo < 0 || algo > 3)
-    return fail("conv2 algo must be 0 (auto), 1 (direct), 2 (winograd) or 3 (winograd, unfused GEMM)");
-  anx::set_conv2_algo(static_cast<anx::ConvAlgo>(algo));
+int anx_engine_set_knob(void* e, const char* name, int value) {
+  if (anx::set_knob(static_cast<anx::BlocksEngine*>(e)->knobs(), name, value) != 0)
+    return fail(std::string("bad knob or value: ") + (name ? name : "(null)"));
   return 0;
 }
-int anx_get_conv2_algo(void) { return static_cast<int>(anx::conv2_algo()); }
-int anx_set_conv1_algo(int algo) {
-  if (algo < 0 || algo > 2) return fail("conv1 algo must be 0 (auto), 1 (direct) or 2 (winograd)");
-  anx::set_conv1_algo(static_cast<anx::ConvAlgo>(algo));
+int anx_engine_get_knob(void* e, const char* name, int* value) {
+  if (anx::get_knob(static_cast<anx::BlocksEngine*>(e)->knobs(), name, value) != 0)
+    return fail(std::string("unknown knob: ") + (name ? name : "(null)"));
   return 0;
 }
-int anx_get_conv1_algo(void) { return static_cast<int>(anx::conv1_algo()); }
-int anx_set_fuse_pool1(int on) {
-  anx::set_fuse_pool1(on != 0);
+int anx_full_set_knob(void* e, const char* name, int value) {
+  if (anx::set_knob(static_cast<anx::FullEngine*>(e)->knobs(), name, value) != 0)
+    return fail(std::string("bad knob or value: ") + (name ? name : "(null)"));
   return 0;
 }
-int anx_set_stage_chunks(int stage1, int stage2) {
-  if (stage1 < 0 || stage2 < 0) return fail("stage chunks must be >= 0 (0 = whole batch)");
-  anx::set_stage_chunks(stage1, stage2);
+int anx_full_get_knob(void* e, const char* name, int* value) {
+  if (anx::get_knob(static_cast<anx::FullEngine*>(e)->knobs(), name, value) != 0)
+    return fail(std::string("unknown knob: ") + (name ? name : "(null)"));
   return 0;
 }
-int anx_conv1_wino_probe(int bits) { return anx::hip::conv1_wino_set_probe(bits); }
-int anx_conv1_wino_cfg(int cfg) {
-  if (anx::hip::conv1_wino_set_cfg(cfg) != 0) return fail("conv1 winograd cfg must be 0..4");
-  return 0;
-}
-int anx_wino_prio(int bits) { return anx::hip::wino_set_prio(bits); }
-int anx_bf16_glds(int mode) {
-  if (anx::hip::bf16_set_glds(mode) != 0) return fail("bf16 glds mode must be 0, 2 or 3");
-  return 0;
-}
-int anx_wino_fused_cfg(int cfg) {
-  if (anx::hip::wino_set_fused_cfg(cfg) != 0) return fail("fused cfg must be 0..15");
-  return 0;
-}
-
-int anx_conv_force_variant(int kind, int id) {
-  if (anx::hip::conv_force_variant(kind, id) != 0) return fail("invalid conv variant");
+int anx_default_knob(const char* name, int* value) {
+  if (anx::get_knob(anx::default_knobs(), name, value) != 0)
+    return fail(std::string("unknown knob: ") + (name ? name : "(null)"));
   return 0;
 }
 
 int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, int K, int F, const float* bias,
-                   float* y, int relu, void* stream) {
+                   float* y, int relu, int fold_scalar, void* stream) {
   return guarded("anx_conv1_wino", [&] {
     if (!anx::hip::conv1_wino_eligible(3, K, F, 4, 0, 1)) return fail("anx_conv1_wino: shape not eligible");
     const auto w = anx::hip::make_conv1_wino_plan(N, Hin, W, K, F);
@@ -415,8 +399,12 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
       return fail("anx_conv1_wino: hipMalloc");
     }
     hipError_t e = hipMemcpy(du, u.data(), u.size() * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-      e = anx::hip::conv1_wino(w, x, dv, du, bias, anx::hip::OutView{y, w.H1, w.W1, K, 0, 0, 0}, relu != 0, S(stream));
+    if (e == hipSuccess) {
+      anx::Knobs kn = anx::default_knobs();
+      kn.fold_scalar = fold_scalar != 0;
+      e = anx::hip::conv1_wino(w, x, dv, du, bias, anx::hip::OutView{y, w.H1, w.W1, K, 0, 0, 0}, relu != 0, S(stream),
+                               kn);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));  // the workspaces are freed below
     (void)hipFree(dv);
     (void)hipFree(du);

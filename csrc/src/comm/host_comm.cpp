@@ -6,6 +6,7 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -88,6 +89,33 @@ int connect_retry(const sockaddr_in& a, double timeout_s) {
   }
 }
 
+// accept() with a deadline: poll the listening socket first, so a rank that never starts or never
+// connects stops the job with a message instead of hanging it (the watchdog only covers wait_all).
+int accept_within(int lfd, double timeout_s, const std::string& what, sockaddr_in* peer = nullptr) {
+  pollfd pf{lfd, POLLIN, 0};
+  const int ms = timeout_s > 0 ? static_cast<int>(timeout_s * 1000) : -1;
+  for (;;) {
+    const int r = poll(&pf, 1, ms);
+    if (r < 0 && errno == EINTR) continue;
+    if (r == 0) die(what + " never joined within " + std::to_string(timeout_s) + " s (ANX_COMM_TIMEOUT)");
+    if (r < 0) die("poll(accept)");
+    break;
+  }
+  socklen_t plen = sizeof(sockaddr_in);
+  const int fd = accept(lfd, reinterpret_cast<sockaddr*>(peer), peer ? &plen : nullptr);
+  if (fd < 0) die("accept");
+  return fd;
+}
+
+// bootstrap reads block at most timeout_s (a peer that connected but never says hello)
+void set_recv_timeout(int fd, double timeout_s) {
+  if (timeout_s <= 0) return;
+  timeval tv{};
+  tv.tv_sec = static_cast<time_t>(timeout_s);
+  tv.tv_usec = static_cast<suseconds_t>((timeout_s - static_cast<double>(tv.tv_sec)) * 1e6);
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+}
+
 void write_all(int fd, const void* p, size_t n) {
   const char* c = static_cast<const char*>(p);
   while (n) {
@@ -137,10 +165,10 @@ HostComm::HostComm(const RankInfo& ri, double timeout_s)
     // star bootstrap: every rank reports (rank, listen port); its address comes from accept()
     for (int i = 1; i < world_; ++i) {
       sockaddr_in peer{};
-      socklen_t plen = sizeof peer;
-      int fd = accept(lfd, reinterpret_cast<sockaddr*>(&peer), &plen);
-      if (fd < 0) die("accept");
+      const int fd = accept_within(lfd, timeout_s_, std::to_string(world_ - i) + " rank(s) of " +
+                                                        std::to_string(world_), &peer);
       set_nodelay(fd);
+      set_recv_timeout(fd, timeout_s_);
       int32_t hdr[2];
       read_all(fd, hdr, sizeof hdr);
       if (hdr[0] <= 0 || hdr[0] >= world_ || fd_[hdr[0]] != -1) die("bad hello");
@@ -151,6 +179,7 @@ HostComm::HostComm(const RankInfo& ri, double timeout_s)
     for (int i = 1; i < world_; ++i) write_all(fd_[i], table.data(), table.size() * sizeof(uint32_t));
   } else {
     int fd = connect_retry(master, timeout_s_);
+    set_recv_timeout(fd, timeout_s_);
     int32_t hdr[2] = {rank_, my_port};
     write_all(fd, hdr, sizeof hdr);
     read_all(fd, table.data(), table.size() * sizeof(uint32_t));
@@ -166,9 +195,9 @@ HostComm::HostComm(const RankInfo& ri, double timeout_s)
       fd_[j] = c;
     }
     for (int k = rank_ + 1; k < world_; ++k) {
-      int c = accept(lfd, nullptr, nullptr);
-      if (c < 0) die("accept");
+      const int c = accept_within(lfd, timeout_s_, "a rank above " + std::to_string(rank_));
       set_nodelay(c);
+      set_recv_timeout(c, timeout_s_);
       int32_t who = -1;
       read_all(c, &who, sizeof who);
       if (who <= rank_ || who >= world_ || fd_[who] != -1) die("bad mesh hello");
@@ -177,7 +206,11 @@ HostComm::HostComm(const RankInfo& ri, double timeout_s)
   }
   close(lfd);
   for (int i = 0; i < world_; ++i)
-    if (fd_[i] >= 0) fcntl(fd_[i], F_SETFL, fcntl(fd_[i], F_GETFL) | O_NONBLOCK);
+    if (fd_[i] >= 0) {
+      timeval none{};
+      setsockopt(fd_[i], SOL_SOCKET, SO_RCVTIMEO, &none, sizeof none);  // wait_all polls with its own watchdog
+      fcntl(fd_[i], F_SETFL, fcntl(fd_[i], F_GETFL) | O_NONBLOCK);
+    }
 }
 
 HostComm::~HostComm() {

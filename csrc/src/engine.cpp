@@ -36,45 +36,6 @@ T* dev_upload(const std::vector<T>& h) {
 }
 }  // namespace
 
-namespace {
-ConvAlgo g_conv2_algo = ConvAlgo::Auto;
-ConvAlgo g_conv1_algo = ConvAlgo::Auto;
-int env_int(const char* name) {
-  const char* e = std::getenv(name);
-  return e ? std::max(0, std::atoi(e)) : 0;
-}
-int g_chunk[2] = {env_int("ANX_CHUNK1"), env_int("ANX_CHUNK2")};
-// off: the fused kernel is correct (bit-identical) but slower than maxpool + wino_in at 300 images,
-// +18 us (thread per tile x channel) and +37 us (LDS-staged tile row)
-// (profiles/r01_ab_fuse_pool1_b300.jsonl); the separate passes already run at 4.5-5 TB/s
-int g_fuse_pool1 = [] {
-  const char* e = std::getenv("ANX_FUSE_POOL1");
-  return e ? std::atoi(e) : 0;
-}();
-}  // namespace
-void set_fuse_pool1(bool on) { g_fuse_pool1 = on ? 1 : 0; }
-bool fuse_pool1() { return g_fuse_pool1 != 0; }
-void set_stage_chunks(int stage1, int stage2) {
-  g_chunk[0] = std::max(0, stage1);
-  g_chunk[1] = std::max(0, stage2);
-}
-int stage_chunk(int stage) { return g_chunk[stage == 2 ? 1 : 0]; }
-
-// Auto: Winograd once a launch covers more than kAutoDirectImages full-height images' worth of
-// output rows. Below that the Winograd GEMM grids (64 tiles per workgroup) leave most of the 256
-// CUs idle and the direct implicit GEMM wins: 0.081 vs 0.163 ms at batch 1, 0.142 vs 0.169 ms at
-// 8, 0.187 (Winograd) vs 0.217 ms at 16 (profiles/r01_algo_crossover.jsonl).
-constexpr int kAutoDirectImages = 8;
-bool use_winograd(ConvAlgo a, int n, int rows, int full_rows) {
-  if (a == ConvAlgo::Direct) return false;
-  if (a != ConvAlgo::Auto) return true;
-  return static_cast<long>(n) * rows > static_cast<long>(kAutoDirectImages) * full_rows;
-}
-void set_conv2_algo(ConvAlgo a) { g_conv2_algo = a; }
-ConvAlgo conv2_algo() { return g_conv2_algo; }
-void set_conv1_algo(ConvAlgo a) { g_conv1_algo = a; }
-ConvAlgo conv1_algo() { return g_conv1_algo; }
-
 void init_const(HostWeights& w, const BlockSpec& b1, const BlockSpec& b2, float wv, float bv) {
   const ConvSpec &c1 = b1.conv, &c2 = b2.conv;
   w.w1.assign(static_cast<size_t>(c1.K) * (c1.C / c1.groups) * c1.F * c1.F, wv);
@@ -98,8 +59,8 @@ void init_input_random(std::vector<float>& x, size_t n, unsigned seed) {
 }
 
 BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int W, const HostWeights& w,
-                           int max_batch, Impl impl)
-    : b1_(b1), b2_(b2), d_(blocks_dims(H, W, b1, b2)), max_batch_(max_batch), impl_(impl) {
+                           int max_batch, Impl impl, const Knobs& k)
+    : b1_(b1), b2_(b2), d_(blocks_dims(H, W, b1, b2)), max_batch_(max_batch), impl_(impl), k_(k) {
   if (b1.conv.P != 0) throw std::invalid_argument("conv1 padding must be 0 (row tiles read raw image rows)");
   if (d_.Hp2 <= 0 || d_.Wp2 <= 0) throw std::invalid_argument("input too small for AlexNet blocks 1-2");
   wq_ = d_.Wp1 + 2 * b2.conv.P;
@@ -172,14 +133,15 @@ float* BlocksEngine::q2_row_ptr(const TilePlan& t, int n, int r) {
 hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s) {
   const ConvSpec& k1 = b1_.conv;
   const hip::OutView c1v{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0};
-  if (impl_ == Impl::Mfma && wv1_ != nullptr && use_winograd(g_conv1_algo, n, t.c1.size(), d_.H1)) {
+  if (impl_ == Impl::Mfma && wv1_ != nullptr && use_winograd(k_.conv1_algo, n, t.c1.size(), d_.H1)) {
     const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
     if (hip::conv1_wino_v_floats(w) > wv1_cap_) return hipErrorInvalidValue;
-    return hip::conv1_wino(w, xc, wv1_, u1w_, b1d_, c1v, true, s);
+    return hip::conv1_wino(w, xc, wv1_, u1w_, b1d_, c1v, true, s, k_);
   }
   if (impl_ == Impl::Mfma) {
-    const hip::ConvPlan p = hip::make_conv_plan(n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, k1.groups);
-    const int key = p.variant;
+    const hip::ConvPlan p =
+        hip::make_conv_plan(n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, k1.groups, k_.force_vec4, k_.force_scalar);
+    const int key = p.variant | (p.taps4 << 8);
     if (key != plan_key1_) {
       std::vector<float> packed;
       std::vector<int> koff;
@@ -199,10 +161,12 @@ hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, 
 hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStream_t s) {
   if (N > max_batch_) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
+  // pool1 rows t.p1 are written into the window t.q at p1.lo - q.lo: they must lie inside it
+  if (t.p1.lo < t.q.lo || t.p1.hi > t.q.hi) return hipErrorInvalidValue;
   ANX_TRY(ensure_window(t, N, s));
   const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
   const size_t q_img = q2_image_stride_floats(t);
-  const int chunk = g_chunk[0] > 0 ? std::min(chunk_, g_chunk[0]) : chunk_;
+  const int chunk = k_.chunk1 > 0 ? std::min(chunk_, k_.chunk1) : chunk_;
   for (int n0 = 0; n0 < N; n0 += chunk) {
     const int n = std::min(chunk, N - n0);
     ANX_TRY(conv1_chunk(x + n0 * in_img, n, t, s));
@@ -216,7 +180,7 @@ hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStr
 // into the Winograd input transform, reading the conv1 rows in c1_ (conv1_chunk just wrote them).
 hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, float* yc, hipStream_t s) {
   const ConvSpec& k2 = b2_.conv;
-  const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(g_conv2_algo, n, t.c2.size(), d_.H2);
+  const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(k_.conv2_algo, n, t.c2.size(), d_.H2);
   if (!qc && !wino) return hipErrorInvalidValue;
   if (wino) {
     const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
@@ -233,22 +197,23 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
       wino_key_ = w.gemm.variant;
     }
     if (qc) {
-      ANX_TRY(hip::wino_input(w, qc, wv_, s));
+      ANX_TRY(hip::wino_input(w, qc, wv_, s, (k_.wino_prio & 2) != 0));
     } else {
       const hip::WinoPoolGeom pg{t.c1.size(), d_.W1, d_.Wp1, k2.P, t.q.lo, t.p1.lo, t.p1.hi, t.c1.lo};
       ANX_TRY(hip::wino_input_pool(w, c1_, pg, wv_, s));
     }
-    if (g_conv2_algo == ConvAlgo::WinogradUnfused) {
+    if (k_.conv2_algo == ConvAlgo::WinogradUnfused) {
       if (!wm_) ANX_TRY(hipMalloc(reinterpret_cast<void**>(&wm_), wm_cap_ * sizeof(float)));
       ANX_TRY(hip::conv2d_mfma(w.gemm, wv_, u2p_, ukoff_, nullptr, hip::OutView{wm_, 1, 1, w.gemm.K, 0, 0, 0}, false,
                                s));
       ANX_TRY(hip::wino_output(w, wm_, b2d_, c2_, true, s));
     } else {
-      ANX_TRY(hip::wino_fused(w, wv_, u2p_, b2d_, c2_, true, s));
+      ANX_TRY(hip::wino_fused(w, wv_, u2p_, b2d_, c2_, true, s, k_));
     }
   } else if (impl_ == Impl::Mfma) {
-    const hip::ConvPlan p = hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups);
-    const int key = p.variant;
+    const hip::ConvPlan p =
+        hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups, k_.force_vec4, k_.force_scalar);
+    const int key = p.variant | (p.taps4 << 8);
     if (key != plan_key2_) {
       std::vector<float> packed;
       std::vector<int> koff;
@@ -283,7 +248,7 @@ hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t 
   if (t.out.empty()) return hipSuccess;
   const size_t q_img = q2_image_stride_floats(t);
   const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
-  const int chunk = g_chunk[1] > 0 ? std::min(chunk_, g_chunk[1]) : chunk_;
+  const int chunk = k_.chunk2 > 0 ? std::min(chunk_, k_.chunk2) : chunk_;
   for (int n0 = 0; n0 < N; n0 += chunk) {
     const int n = std::min(chunk, N - n0);
     ANX_TRY(conv2_chunk(n, t, q2_ + n0 * q_img, y + n0 * y_img, s));
@@ -296,12 +261,12 @@ hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, 
   if (t.out.empty()) return hipSuccess;
   // Pool1 fused into Conv2's Winograd input transform when every chunk runs Winograd Conv2 (the
   // conv2 window is then never written: no memset, no pool1 pass).
-  const int c1c = g_chunk[0] > 0 ? std::min(chunk_, g_chunk[0]) : chunk_;
-  const int c2c = g_chunk[1] > 0 ? std::min(chunk_, g_chunk[1]) : chunk_;
+  const int c1c = k_.chunk1 > 0 ? std::min(chunk_, k_.chunk1) : chunk_;
+  const int c2c = k_.chunk2 > 0 ? std::min(chunk_, k_.chunk2) : chunk_;
   const int chunk = std::min(c1c, c2c);
   const int n_min = N % chunk ? std::min(N % chunk, chunk) : std::min(N, chunk);
-  const bool fuse = g_fuse_pool1 && impl_ == Impl::Mfma && wv_ != nullptr && b1_.pool.F == 3 && b1_.pool.S == 2 &&
-                    g_conv2_algo != ConvAlgo::WinogradUnfused && use_winograd(g_conv2_algo, n_min, t.c2.size(), d_.H2);
+  const bool fuse = k_.fuse_pool1 && impl_ == Impl::Mfma && wv_ != nullptr && b1_.pool.F == 3 && b1_.pool.S == 2 &&
+                    k_.conv2_algo != ConvAlgo::WinogradUnfused && use_winograd(k_.conv2_algo, n_min, t.c2.size(), d_.H2);
   if (!fuse) {
     ANX_TRY(stage1(x, N, t, s));
     return stage2(N, t, y, s);

@@ -39,8 +39,8 @@ void full_weight_shapes(int classes, int groups2, size_t wn[8], size_t bn[8]) {
   }
 }
 
-FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int groups2, LrnMode lrn)
-    : classes_(classes), max_batch_(max_batch), lrn_(lrn) {
+FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int groups2, LrnMode lrn, const Knobs& kn)
+    : k_(kn), classes_(classes), max_batch_(max_batch), lrn_(lrn) {
   size_t wn[8], bn[8];
   full_weight_shapes(classes, groups2, wn, bn);
   for (int i = 0; i < 8; ++i) {
@@ -136,10 +136,10 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
   }
   const int ks = hip::fc_split_k(p);
   if (ks > 1) {  // FC layer at a small batch: K split over ~one workgroup per CU, then a reduce
-    ANX_TRY(hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s, hip::SplitK{ks, ws_}));
+    ANX_TRY(hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s, hip::SplitK{ks, ws_}, k_.bf16_glds));
     return hip::splitk_reduce_bf16(ws_, ks, N, L.K, L.bias, relu, out, out_f32, s);
   }
-  return hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s);
+  return hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s, {}, k_.bf16_glds);
 }
 
 hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t s) {

@@ -155,6 +155,18 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// One fold step on a register pair: y += c * (a0, a1). SF = two scalar v_fma_f32 (this file builds
+// with -fno-slp-vectorize, so they stay scalar), else one v_pk_fma_f32. Bit-identical either way.
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+template <bool SF>
+__device__ __forceinline__ void fma2(f32x2& y, float c, float a0, float a1) {
+  if constexpr (SF) {
+    y.x = fmaf(c, a0, y.x);
+    y.y = fmaf(c, a1, y.y);
+  } else {
+    y = __builtin_elementwise_fma(f32x2{c, c}, f32x2{a0, a1}, y);
+  }
+}
 
 // LDS image per ring slot: [A: 128 rows x BK][B: 32 rows x BK], rows unpadded, the 16-B unit u of
 // row r stored at u ^ ((r >> 2) & 3) (conflict-free ds_read_b128 fragment reads; the swizzle is
@@ -192,7 +204,7 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
   }
 }
 
-template <int BK, int NST>
+template <int BK, int NST, bool SF>
 __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
   using R = Ring<BK, NST>;
   constexpr int KS = kCh / BK;        // slices per transform point
@@ -247,9 +259,7 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
   for (int s4 = 0; s4 < BK / 8; ++s4) rd[s4] = 4 * ((h * (BK / 8) + s4) ^ swz);
   const int a_row = (wave * 32 + r) * BK, b_row = R::A_FL + r * BK;
 
-  // Y[i*3+j][e2] holds output (i, j) of the accumulator rows 2*e2, 2*e2+1 (pairs for v_pk_*_f32)
   // Y[q][e2]: output q of accumulator rows 2*e2 and 2*e2+1 (pairs: one v_pk_fma_f32 per 2 rows)
-  using f32x2 = __attribute__((ext_vector_type(2))) float;
   f32x2 Y[9][8];
 #pragma unroll
   for (int q = 0; q < 9; ++q)
@@ -283,11 +293,8 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
       for (int j3 = 0; j3 < 3; ++j3) {
         const float c = c_at33.v[i3][aa] * c_at33.v[j3][bb];
         if (c != 0.f) {
-          const f32x2 c2 = {c, c};
 #pragma unroll
-          for (int e2 = 0; e2 < 8; ++e2)
-            Y[i3 * 3 + j3][e2] =
-                __builtin_elementwise_fma(c2, f32x2{acc[2 * e2], acc[2 * e2 + 1]}, Y[i3 * 3 + j3][e2]);
+          for (int e2 = 0; e2 < 8; ++e2) fma2<SF>(Y[i3 * 3 + j3][e2], c, acc[2 * e2], acc[2 * e2 + 1]);
         }
       }
     acc = f32x16{};
@@ -383,7 +390,7 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
 constexpr int kBM16 = 64;
 __device__ __forceinline__ int rot16(int row) { return 3 * ((row >> 1) & 3); }
 
-template <bool IL>
+template <bool IL, bool SF>
 __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
   constexpr int BK = kCh, U4 = BK / 4;            // 48 channels, 12 units per row
   constexpr int A_PW = kBM16 * U4 / 64 / 4;       // 3 DMA instructions per wave
@@ -391,7 +398,6 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
   constexpr int A_FL = kBM16 * BK, B_FL = kBN * BK;
   constexpr int STAGE = A_FL + B_FL;
   constexpr int NS_LO = A_PW + B_INS / 4, NS_HI = NS_LO + 1;
-  using f32x2 = __attribute__((ext_vector_type(2))) float;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
@@ -466,11 +472,10 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
       for (int j3 = 0; j3 < 3; ++j3) {
         const float c = c_at33.v[i3][aa] * c_at33.v[j3][bb];
         if (c != 0.f) {
-          const f32x2 c2 = {c, c};
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) {
-            Y[i3 * 3 + j3][cb][0] = __builtin_elementwise_fma(c2, f32x2{acc[cb][0], acc[cb][1]}, Y[i3 * 3 + j3][cb][0]);
-            Y[i3 * 3 + j3][cb][1] = __builtin_elementwise_fma(c2, f32x2{acc[cb][2], acc[cb][3]}, Y[i3 * 3 + j3][cb][1]);
+            fma2<SF>(Y[i3 * 3 + j3][cb][0], c, acc[cb][0], acc[cb][1]);
+            fma2<SF>(Y[i3 * 3 + j3][cb][1], c, acc[cb][2], acc[cb][3]);
           }
         }
       }
@@ -511,8 +516,7 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
         for (int t = 0; t < 3; ++t) {
           const int j = (s4 * 4 + s) * 3 + t;  // 0..35 = (q, cb, pair)
           const int q = j >> 2, cb = (j >> 1) & 1, pr = j & 1;
-          Y[q][cb][pr] = __builtin_elementwise_fma(f32x2{cq[q], cq[q]}, f32x2{facc[cb][2 * pr], facc[cb][2 * pr + 1]},
-                                                   Y[q][cb][pr]);
+          fma2<SF>(Y[q][cb][pr], cq[q], facc[cb][2 * pr], facc[cb][2 * pr + 1]);
         }
       }
     }
@@ -582,48 +586,30 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
   }
 }
 
-// GEMM configurations. 0-3: 32x32 MFMA, 128-tile workgroups, 2 per CU, ring of BK channels x NST
-// slots (NST-2 slices in flight behind the one being consumed): 0 BK 48 x 2 (60 KiB), 1 BK 16 x 4
-// (40 KiB), 2 BK 16 x 6 (60 KiB), 3 BK 16 x 8 (80 KiB). 4 (default): 16x16 MFMA, 64-tile
-// workgroups, 4 per CU (conv1_wino_gemm16_kernel; -6 % kernel time at 300 images,
-// profiles/r01_ab_conv1_wino_b300.jsonl). ANX_CONV1_WINO_CFG overrides (profiling).
+// GEMM configurations (Knobs::conv1_cfg). 0-3: 32x32 MFMA, 128-tile workgroups, 2 per CU, ring of
+// BK channels x NST slots (NST-2 slices in flight behind the one being consumed): 0 BK 48 x 2
+// (60 KiB), 1 BK 16 x 4 (40 KiB), 2 BK 16 x 6 (60 KiB), 3 BK 16 x 8 (80 KiB). 4 (default): 16x16 MFMA,
+// 64-tile workgroups, 4 per CU (conv1_wino_gemm16_kernel; -6 % kernel time at 300 images,
+// profiles/r01_ab_conv1_wino_b300.jsonl).
 constexpr int kNumCfg = 5;
-int default_cfg() {
-  const char* e = std::getenv("ANX_CONV1_WINO_CFG");
-  const int v = e ? std::atoi(e) : -1;
-  return v >= 0 && v < kNumCfg ? v : 4;
-}
-int g_cfg = default_cfg();
 
-template <int BK, int NST>
-hipError_t launch_gemm(const GemmArgs& a, hipStream_t s) {
+template <int BK, int NST, bool SF>
+hipError_t launch_gemm_t(const GemmArgs& a, hipStream_t s) {
   constexpr size_t lds_bytes = Ring<BK, NST>::kBytes;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_wino_gemm_kernel<BK, NST>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(conv1_wino_gemm_kernel<BK, NST, SF>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      lds_bytes);
   if (attr != hipSuccess) return attr;
   const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
-  conv1_wino_gemm_kernel<BK, NST><<<grid, 256, lds_bytes, s>>>(a);
+  conv1_wino_gemm_kernel<BK, NST, SF><<<grid, 256, lds_bytes, s>>>(a);
   return hipGetLastError();
+}
+template <int BK, int NST>
+hipError_t launch_gemm(const GemmArgs& a, hipStream_t s, bool sf) {
+  return sf ? launch_gemm_t<BK, NST, true>(a, s) : launch_gemm_t<BK, NST, false>(a, s);
 }
 
 }  // namespace
-
-int g_probe = [] {
-  const char* e = std::getenv("ANX_CONV1_WINO_PROBE");
-  // bit4 (s_setprio around the MFMA slices) on: -1 % at 300 images. bit6 (interleaved fold,
-  // conv1_wino_gemm16_kernel<true>) is off: +22 us at 300 images (profiles/r01_ab_conv1_ilfold_b300.jsonl)
-  return e ? std::atoi(e) : 16;
-}();
-int conv1_wino_set_probe(int bits) {
-  g_probe = bits;
-  return 0;
-}
-
-int conv1_wino_set_cfg(int cfg) {
-  if (cfg < 0 || cfg >= kNumCfg) return -1;
-  g_cfg = cfg;
-  return 0;
-}
 
 bool conv1_wino_eligible(int C, int K, int F, int S, int P, int groups) {
   // ceil(F/4) == 3 taps per phase axis; 3 input channels -> 48 polyphase channels
@@ -676,8 +662,12 @@ void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<floa
     }
 }
 
+bool conv1_wino_cfg_valid(int cfg) { return cfg >= 0 && cfg < kNumCfg; }
+
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
-                      bool relu, hipStream_t s) {
+                      bool relu, hipStream_t s, const Knobs& kn) {
+  const int probe = kn.conv1_probe;
+  const bool sf = (kn.fold_scalar & 1) != 0;
   if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
   if (w.K % kBN || static_cast<long>(w.P) * kPts * kCh >= (1L << 31) || static_cast<long>(w.P) * 12 >= (1L << 31) ||
       out.Cb % 4 || out.c_off % 4)  // 16-B epilogue stores
@@ -685,7 +675,7 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
   const int total = w.P * 12;
   long g = (total + kT - 1) / kT;
   if (g > (1 << 20)) g = 1 << 20;
-  if (g_probe & 32)  // A/B: non-temporal V stores
+  if (probe & 32)  // A/B: non-temporal V stores
     conv1_wino_in_kernel<true><<<static_cast<unsigned>(g), kT, 0, s>>>(x, V, total, w.Hin, w.W * 3, w.ty, w.tx);
   else
     conv1_wino_in_kernel<false><<<static_cast<unsigned>(g), kT, 0, s>>>(x, V, total, w.Hin, w.W * 3, w.ty, w.tx);
@@ -705,23 +695,30 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
   a.relu = relu ? 1 : 0;
   a.n_ptiles = (w.P + kBM - 1) / kBM;
   a.n_ntiles = w.K / kBN;
-  a.probe = g_probe;
-  switch (g_cfg) {
-    case 1: return launch_gemm<16, 4>(a, s);
-    case 2: return launch_gemm<16, 6>(a, s);
-    case 3: return launch_gemm<16, 8>(a, s);
+  a.probe = probe;
+  switch (kn.conv1_cfg) {
+    case 1: return launch_gemm<16, 4>(a, s, sf);
+    case 2: return launch_gemm<16, 6>(a, s, sf);
+    case 3: return launch_gemm<16, 8>(a, s, sf);
     case 4: {  // 16x16 MFMA, 64-tile workgroups, 4 workgroups per CU
       constexpr size_t lds_bytes = 2 * (kBM16 + kBN) * kCh * sizeof(float);
       GemmArgs b = a;
       b.n_ptiles = (a.P + kBM16 - 1) / kBM16;
       const dim3 grid((b.n_ptiles + 7) / 8 * 8 * b.n_ntiles);
-      if (g_probe & 64)
-        conv1_wino_gemm16_kernel<true><<<grid, 256, lds_bytes, s>>>(b);
-      else
-        conv1_wino_gemm16_kernel<false><<<grid, 256, lds_bytes, s>>>(b);
+      if (probe & 64) {
+        if (sf)
+          conv1_wino_gemm16_kernel<true, true><<<grid, 256, lds_bytes, s>>>(b);
+        else
+          conv1_wino_gemm16_kernel<true, false><<<grid, 256, lds_bytes, s>>>(b);
+      } else {
+        if (sf)
+          conv1_wino_gemm16_kernel<false, true><<<grid, 256, lds_bytes, s>>>(b);
+        else
+          conv1_wino_gemm16_kernel<false, false><<<grid, 256, lds_bytes, s>>>(b);
+      }
       return hipGetLastError();
     }
-    default: return launch_gemm<48, 2>(a, s);
+    default: return launch_gemm<48, 2>(a, s, sf);
   }
 }
 

@@ -507,12 +507,6 @@ __global__ void __launch_bounds__(256) s2d4_bf16_kernel(const float* __restrict_
   }
 }
 
-// 128x128 vec8 convs / FC: 0 = register-staged kernel, 2 = LDS-DMA ring 2 slots, 3 = 3 slots
-// (ANX_BF16_GLDS; A/B through anx_bf16_glds)
-int g_bf16_glds = [] {
-  const char* e = std::getenv("ANX_BF16_GLDS");
-  return e ? std::atoi(e) : 2;
-}();
 
 struct VariantB {
   int BM, BN;
@@ -609,7 +603,7 @@ uint16_t f32_to_bf16_bits(float f) {  // round to nearest even, NaN kept NaN
 }
 
 hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, const int* koff, const float* bias,
-                       OutViewB out, float* out_f32, bool relu, hipStream_t s, SplitK split) {
+                       OutViewB out, float* out_f32, bool relu, hipStream_t s, SplitK split, int glds) {
   const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
   if (M == 0) return hipSuccess;
   if (static_cast<long>(p.N) * p.Hp * p.Wp * p.C >= (1L << 31)) return hipErrorInvalidValue;
@@ -663,9 +657,9 @@ hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, c
     else                                                                                              \
       conv_bf16_kernel<BM, BN, WMW, WNW, V8, bf16><<<grid, kThreads, lds, s>>>(a);                    \
   } while (0)
-  if (p.variant == 0 && !p.taps8 && g_bf16_glds > 0) {
+  if (p.variant == 0 && !p.taps8 && glds > 0) {
     // LDS-DMA ring: NST slots of (A|B) 128 x 64 bf16 tiles + the koff/ooff tables
-    const int nst = g_bf16_glds == 2 ? 2 : 3;
+    const int nst = glds == 2 ? 2 : 3;
     const size_t lds_r = static_cast<size_t>(nst) * 2 * 128 * kBK * 2 + static_cast<size_t>(p.kpad + 128) * 4;
     if (lds_r <= 160 * 1024) {
       // dynamic LDS above the 64 KiB default: opt every instantiation in once
@@ -731,11 +725,6 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 }
 }  // namespace
 
-int bf16_set_glds(int mode) {
-  if (mode != 0 && mode != 2 && mode != 3) return -1;
-  g_bf16_glds = mode;
-  return 0;
-}
 
 int fc_split_k(const ConvPlanB& p) {
   if (p.Ho != 1 || p.Wo != 1 || p.groups != 1 || p.Kg % 4) return 1;

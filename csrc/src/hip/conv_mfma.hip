@@ -267,19 +267,18 @@ constexpr Variant kVariants[] = {
     {256, 96, true, 1},    // 10: = 9 with 64x96 per wave
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-// Tuning override for in-process A/B (anx_conv_force_variant): [0] vec4 convs, [1] scalar convs.
-int g_force[2] = {-1, -1};
-
 }  // namespace
 
-int conv_force_variant(int kind, int id) {
-  if (kind < 0 || kind > 1 || id < -1 || id >= kNumVariants) return -1;
-  if (id >= 0 && kVariants[id].vec4 != (kind == 0)) return -1;
-  g_force[kind] = id;
-  return 0;
+bool conv_variant_valid(int kind, int id) {
+  if (kind < 0 || kind > 1 || id < -1 || id >= kNumVariants) return false;
+  return id < 0 || kVariants[id].vec4 == (kind == 0);
 }
 
-ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups) {
+ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups, int force_vec4,
+                        int force_scalar) {
+  if (!conv_variant_valid(0, force_vec4)) force_vec4 = -1;
+  if (!conv_variant_valid(1, force_scalar)) force_scalar = -1;
+  const int force[2] = {force_vec4, force_scalar};
   ConvPlan p{};
   p.N = N;
   p.Hp = Hp;
@@ -297,7 +296,7 @@ ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int g
   p.vec4 = (p.Cg % 4 == 0 && C % 4 == 0) ? 1 : 0;
   // taps4 needs each filter row's (fw, c) floats contiguous (groups == 1); a forced scalar variant
   // (A/B tuning) keeps the scalar gather.
-  p.taps4 = (!p.vec4 && groups == 1 && F * C >= 4 && g_force[1] < 0) ? 1 : 0;
+  p.taps4 = (!p.vec4 && groups == 1 && F * C >= 4 && force[1] < 0) ? 1 : 0;
   if (p.taps4) {
     p.kdim = F * 4 * ((F * C + 3) / 4);
     p.vec4 = 1;
@@ -311,7 +310,7 @@ ConvPlan make_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int g
     p.variant = p.vec4 ? 2 : 3;
   else
     p.variant = p.vec4 ? 0 : 4;
-  if (g_force[p.vec4 ? 0 : 1] >= 0) p.variant = g_force[p.vec4 ? 0 : 1];
+  if (force[p.vec4 ? 0 : 1] >= 0) p.variant = force[p.vec4 ? 0 : 1];
   const int BN = kVariants[p.variant].BN;
   p.kpad_n = (p.Kg + BN - 1) / BN * BN;
   return p;

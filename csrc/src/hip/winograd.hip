@@ -422,8 +422,20 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// One fold step on a register pair: y += c * (a0, a1). SF = two scalar v_fma_f32 (this file builds
+// with -fno-slp-vectorize, so they stay scalar), else one v_pk_fma_f32. Bit-identical either way.
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+template <bool SF>
+__device__ __forceinline__ void fma2(f32x2& y, float c, float a0, float a1) {
+  if constexpr (SF) {
+    y.x = fmaf(c, a0, y.x);
+    y.y = fmaf(c, a1, y.y);
+  } else {
+    y = __builtin_elementwise_fma(f32x2{c, c}, f32x2{a0, a1}, y);
+  }
+}
 
-template <int BK, bool XCD, bool IL>
+template <int BK, bool XCD, bool IL, bool SF>
 __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) {  // 2 waves/SIMD
   using f32x16 = __attribute__((ext_vector_type(16))) float;
   constexpr int U4 = BK / 4;              // 16-B units per row
@@ -483,8 +495,8 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
   for (int s4 = 0; s4 < BK / 8; ++s4) rd[s4] = 4 * ((h * (BK / 8) + s4) ^ swz);
   const int a_row = (wm * 32 + r) * BK, b_row = TILE + (wn * 32 + r) * BK;
 
-  // Y[q][e2]: output q of accumulator rows 2*e2 and 2*e2+1 (pairs: one v_pk_fma_f32 per 2 rows)
-  using f32x2 = __attribute__((ext_vector_type(2))) float;
+  // Y[q][e2]: output q of accumulator rows 2*e2 and 2*e2+1 (pairs: one v_pk_fma_f32 per 2 rows,
+  // or two v_fma_f32 with SF)
   f32x2 Y[9][8];
 #pragma unroll
   for (int q = 0; q < 9; ++q)
@@ -517,11 +529,8 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
       for (int j3 = 0; j3 < kM; ++j3) {
         const float c = c_AT[i3][aa] * c_AT[j3][bb];
         if (c != 0.f) {
-          const f32x2 c2 = {c, c};
 #pragma unroll
-          for (int e2 = 0; e2 < 8; ++e2)
-            Y[i3 * kM + j3][e2] =
-                __builtin_elementwise_fma(c2, f32x2{acc[2 * e2], acc[2 * e2 + 1]}, Y[i3 * kM + j3][e2]);
+          for (int e2 = 0; e2 < 8; ++e2) fma2<SF>(Y[i3 * kM + j3][e2], c, acc[2 * e2], acc[2 * e2 + 1]);
         }
       }
     acc = f32x16{};
@@ -587,7 +596,7 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
           const int j = (s4 * 4 + s) * 3 + t;
           if (j < kM * kM * 8) {
             const int q = j >> 3, e2 = j & 7;
-            Y[q][e2] = __builtin_elementwise_fma(f32x2{cq[q], cq[q]}, f32x2{facc[2 * e2], facc[2 * e2 + 1]}, Y[q][e2]);
+            fma2<SF>(Y[q][e2], cq[q], facc[2 * e2], facc[2 * e2 + 1]);
           }
         }
       }
@@ -701,7 +710,6 @@ __device__ __forceinline__ int rot16(int row) { return 3 * ((row >> 1) & 3); }
 
 template <int WMW, int WNW, bool XCD>
 __global__ void __launch_bounds__(64 * WMW * WNW, 4) wino_fused_glds16_kernel(FusedArgs a) {  // 4 waves/SIMD
-  using f32x2 = __attribute__((ext_vector_type(2))) float;
   constexpr int NW = WMW * WNW;               // waves per workgroup
   constexpr int BMT = 16 * WMW, BNT = 32 * WNW;  // tiles x filters per workgroup
   constexpr int BK = 48, U4 = BK / 4;
@@ -878,21 +886,6 @@ __global__ void __launch_bounds__(64 * WMW * WNW, 4) wino_fused_glds16_kernel(Fu
   }
 }
 
-// fused-kernel configuration: bit0 = BK 48 (else 32), bit1 = XCD-aware block order, bit2 = LDS-DMA
-// ring (when Cg % BK == 0). ANX_WINO_FUSED_CFG overrides the default (profiling).
-int default_fused_cfg() {
-  const char* e = std::getenv("ANX_WINO_FUSED_CFG");
-  const int v = e ? std::atoi(e) : -1;
-  return v >= 0 && v <= 15 ? v : 7;
-}
-int g_fused_cfg = default_fused_cfg();
-// bit0 s_setprio (-1 % at 300 images), bit8 interleaved fold (-49 us at 300 images, bit-identical:
-// profiles/r01_ab_wino_ilfold_b300.jsonl); ANX_WINO_PRIO overrides
-int g_prio = [] {
-  const char* e = std::getenv("ANX_WINO_PRIO");
-  return e ? std::atoi(e) : 257;
-}();
-
 template <int WMW, int WNW, bool XCD>
 hipError_t launch_glds16(FusedArgs a, hipStream_t s) {
   constexpr int BMT = 16 * WMW, BNT = 32 * WNW;
@@ -909,14 +902,14 @@ hipError_t launch_glds16(FusedArgs a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int BK, bool XCD, bool IL = false>
+template <int BK, bool XCD, bool IL = false, bool SF = false>
 hipError_t launch_glds(const FusedArgs& a, dim3 grid, hipStream_t s) {
   constexpr int kLds = 3 * 2 * kFB * BK * sizeof(float);  // 3-slot ring of A|B tiles
   static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(wino_fused_glds_kernel<BK, XCD, IL>), hipFuncAttributeMaxDynamicSharedMemorySize,
-      kLds);
+      reinterpret_cast<const void*>(wino_fused_glds_kernel<BK, XCD, IL, SF>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
   if (attr != hipSuccess) return attr;
-  wino_fused_glds_kernel<BK, XCD, IL><<<grid, 256, kLds, s>>>(a);
+  wino_fused_glds_kernel<BK, XCD, IL, SF><<<grid, 256, kLds, s>>>(a);
   return hipGetLastError();
 }
 
@@ -926,17 +919,6 @@ unsigned grid_for(long n) {
 }
 
 }  // namespace
-
-int wino_set_prio(int bits) {
-  g_prio = bits;
-  return 0;
-}
-
-int wino_set_fused_cfg(int cfg) {
-  if (cfg < 0 || cfg > 15) return -1;
-  g_fused_cfg = cfg;
-  return 0;
-}
 
 WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups) {
   WinoPlan w{};
@@ -988,12 +970,12 @@ void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::ve
       }
 }
 
-hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s) {
+hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s, bool nt) {
   const long n = static_cast<long>(w.P) * w.C;
   if (n >= (1L << 31)) return hipErrorInvalidValue;
   const long g = (n + kT - 1) / kT;
   const unsigned gg = static_cast<unsigned>(g < (1 << 20) ? g : (1 << 20));
-  if (g_prio & 2)  // A/B: non-temporal V stores
+  if (nt)  // A/B: non-temporal V stores
     wino_in_kernel<true><<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
   else
     wino_in_kernel<false><<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
@@ -1030,7 +1012,9 @@ hipError_t wino_input_pool(const WinoPlan& w, const float* c1, const WinoPoolGeo
 }
 
 hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
-                      hipStream_t s) {
+                      hipStream_t s, const Knobs& kn) {
+  const int cfg = kn.wino_cfg, prio = kn.wino_prio;
+  const bool sf = (kn.fold_scalar & 2) != 0;
   FusedArgs a{};
   a.V = V;
   a.U = U;
@@ -1050,31 +1034,33 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
   a.ty = w.ty;
   a.tx = w.tx;
   a.relu = relu ? 1 : 0;
-  a.prio = g_prio;
+  a.prio = prio;
   a.n_ptiles = (w.P + kFB - 1) / kFB;
   a.n_ntiles = (a.Kg + kFB - 1) / kFB;
   if (a.n_ntiles * kFB > a.kpad_n || a.Cg % 4) return hipErrorInvalidValue;
-  const bool xcd = (g_fused_cfg & 2) != 0;
-  if ((g_fused_cfg & 8) && a.Cg % 48 == 0 && a.kpad == a.Cg && a.Kg % 32 == 0) {
+  const bool xcd = (cfg & 2) != 0;
+  if ((cfg & 8) && a.Cg % 48 == 0 && a.kpad == a.Cg && a.Kg % 32 == 0) {
     // 16x16 MFMA: bit0 set -> 64 tiles x 64 filters, 8 waves, 2 workgroups/CU; bit0 clear -> 64 tiles
     // x 128 filters, 16 waves, 1 workgroup/CU (a quarter fewer operand bytes per MAC)
-    if (g_fused_cfg & 1) return xcd ? launch_glds16<4, 2, true>(a, s) : launch_glds16<4, 2, false>(a, s);
+    if (cfg & 1) return xcd ? launch_glds16<4, 2, true>(a, s) : launch_glds16<4, 2, false>(a, s);
     if (a.Kg % 128 == 0) return xcd ? launch_glds16<4, 4, true>(a, s) : launch_glds16<4, 4, false>(a, s);
   }
-  if (g_fused_cfg & 4) {
+  if (cfg & 4) {
     // LDS-DMA ring: BK 48 (72 KiB, 2 workgroups/CU) or BK 32 (48 KiB, 3/CU)
-    const int bk = (g_fused_cfg & 1) ? 48 : 32;
+    const int bk = (cfg & 1) ? 48 : 32;
     if (a.Cg % bk == 0 && a.kpad == a.Cg) {
       const dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
-      if (bk == 48 && xcd)  // the interleaved fold needs exactly 2 K slices per point (C = 96)
-        return ((g_prio & 256) && a.kpad == 96) ? launch_glds<48, true, true>(a, grid, s)
-                                                : launch_glds<48, true, false>(a, grid, s);
+      if (bk == 48 && xcd) {  // the interleaved fold needs exactly 2 K slices per point (C = 96)
+        if ((prio & 256) && a.kpad == 96)
+          return sf ? launch_glds<48, true, true, true>(a, grid, s) : launch_glds<48, true, true, false>(a, grid, s);
+        return sf ? launch_glds<48, true, false, true>(a, grid, s) : launch_glds<48, true, false, false>(a, grid, s);
+      }
       if (bk == 48) return launch_glds<48, false>(a, grid, s);
       if (xcd) return launch_glds<32, true>(a, grid, s);
       return launch_glds<32, false>(a, grid, s);
     }
   }
-  const int bk = (a.kpad % 48 == 0 && g_fused_cfg & 1) ? 48 : 32;
+  const int bk = (a.kpad % 48 == 0 && cfg & 1) ? 48 : 32;
   dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
   if (bk == 48 && xcd)
     wino_fused_kernel<48, true><<<grid, 256, 0, s>>>(a);

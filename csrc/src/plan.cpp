@@ -132,6 +132,12 @@ const char* check_plan(const DecompPlan& p) {
       std::snprintf(buf, sizeof buf, "rank %d pool1 window mismatch", t);
       return (msg = buf).c_str();
     }
+    // stage1 writes the pool1 rows it computes into the conv2 input window at p1.lo - q.lo
+    if (tp.p1.lo < tp.q.lo || tp.p1.hi > tp.q.hi) {
+      std::snprintf(buf, sizeof buf, "rank %d pool1 rows [%d,%d) outside its conv2 window [%d,%d)", t, tp.p1.lo,
+                    tp.p1.hi, tp.q.lo, tp.q.hi);
+      return (msg = buf).c_str();
+    }
     if (conv_out_dim(tp.q.size(), k2.F, k2.S, 0) != tp.c2.size()) {
       std::snprintf(buf, sizeof buf, "rank %d conv2 window mismatch", t);
       return (msg = buf).c_str();

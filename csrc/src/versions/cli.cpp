@@ -173,6 +173,7 @@ void copy_rows(float* dst, int dst_rows, int dst_off, const float* src, int src_
 
 struct Setup {
   Options o;
+  Knobs k;  // engine kernel knobs (--conv1-algo / --conv2-algo over default_knobs())
   RankInfo ri;
   BlockSpec b1, b2;
   BlocksDims d;
@@ -185,6 +186,15 @@ Setup make_setup(const Options& o, const RankInfo& ri) {
   Setup s;
   s.o = o;
   s.ri = ri;
+  s.k = default_knobs();
+  // Winograd conv2 sums in a different order per row tile (tile origins move with the decomposition):
+  // results match to ~1e-7 relative, not bitwise; `direct` makes every decomposition bit-identical.
+  // Conv1 likewise: polyphase Winograd by default, `direct` for bit-identical decompositions.
+  auto algo = [](const std::string& a, ConvAlgo dflt) {
+    return a == "direct" ? ConvAlgo::Direct : a == "winograd" ? ConvAlgo::Winograd : dflt;
+  };
+  s.k.conv2_algo = algo(o.conv2_algo, s.k.conv2_algo);
+  s.k.conv1_algo = algo(o.conv1_algo, s.k.conv1_algo);
   s.b1 = kBlock1;
   s.b2 = kBlock2;
   s.b2.conv.groups = o.groups;
@@ -321,7 +331,7 @@ int run_single(Setup& s) {
     hip_check(hipSetDevice(s.ri.local_rank % ndev), "hipSetDevice");
     hipStream_t st;
     hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
-    BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma);
+    BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
     float *dx, *dy;
     hip_check(hipMalloc(&dx, s.x.size() * 4), "hipMalloc");
     hip_check(hipMalloc(&dy, y.size() * 4), "hipMalloc");
@@ -413,7 +423,7 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
     hip_check(hipSetDevice(s.ri.local_rank % ndev), "hipSetDevice");  // fixes reference D4
     hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
     geng = std::make_unique<BlocksEngine>(s.b1, s.b2, s.d.H, s.d.W, s.w, N,
-                                          s.o.impl == "direct" ? Impl::Direct : Impl::Mfma);
+                                          s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
     hip_check(hipMalloc(&d_in, std::max<size_t>(1, tile_in.size()) * 4), "hipMalloc");
     hip_check(hipMalloc(&d_y, std::max<size_t>(1, y_loc.size()) * 4), "hipMalloc");
     hip_check(hipHostMalloc(&h_in, std::max<size_t>(1, tile_in.size()) * 4, hipHostMallocDefault), "pinned");
@@ -618,7 +628,7 @@ int run_v5_peer(Setup& s, HostComm& c, int ndev) {
   hipStream_t st, cs;
   hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
   hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
-  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma);
+  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
   auto dalloc = [](size_t n) {
     float* p = nullptr;
     hip_check(hipMalloc(&p, std::max<size_t>(1, n) * 4), "hipMalloc");
@@ -748,7 +758,7 @@ int run_v5(Setup& s, HostComm& c) {
   DeviceComm dc(c, dev);
   hipStream_t st;
   hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
-  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma);
+  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
   auto dalloc = [](size_t n) {
     float* p = nullptr;
     hip_check(hipMalloc(&p, std::max<size_t>(1, n) * 4), "hipMalloc");
@@ -922,15 +932,6 @@ int run_v5(Setup& s, HostComm& c) {
 
 int main(int argc, char** argv) {
   const Options o = parse(argc, argv);
-  // Winograd conv2 sums in a different order per row tile (tile origins move with the decomposition):
-  // results match to ~1e-7 relative, not bitwise; `direct` makes every decomposition bit-identical.
-  set_conv2_algo(o.conv2_algo == "direct"     ? ConvAlgo::Direct
-                 : o.conv2_algo == "winograd" ? ConvAlgo::Winograd
-                                              : ConvAlgo::Auto);
-  // Conv1 likewise: polyphase Winograd by default, `direct` for bit-identical decompositions.
-  set_conv1_algo(o.conv1_algo == "direct"     ? ConvAlgo::Direct
-                 : o.conv1_algo == "winograd" ? ConvAlgo::Winograd
-                                              : ConvAlgo::Auto);
   const RankInfo ri = rank_info_from_env();
   try {
     Setup s = make_setup(o, ri);

@@ -107,7 +107,7 @@ int main(int argc, char** argv) {
     auto run = [&]() {
       if (wino) {
         ck(hip::wino_input(wp, dxp, dv, s), "wino_input");
-        ck(hip::wino_fused(wp, dv, dpk, db, dy, false, s), "wino_fused");
+        ck(hip::wino_fused(wp, dv, dpk, db, dy, false, s, default_knobs()), "wino_fused");
       } else {
         ck(hip::conv2d_mfma(p, dxp, dpk, dko, db, hip::OutView{dy, Ho, Wo, L.K, 0, 0, 0}, false, s), "mfma");
       }

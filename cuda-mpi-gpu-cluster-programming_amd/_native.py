@@ -83,19 +83,12 @@ _SIGS = {
     "anx_maxpool_lrn": (_I, [_P, _P] + [_I] * 6 + [_I, _F, _F, _F, _I, _P]),
     "anx_conv_plan": (_I, [_I] * 8 + [C.POINTER(_I), C.POINTER(_SZ), C.POINTER(_SZ)]),
     "anx_conv_pack": (_I, [C.POINTER(_I), _P, _P, _P]),
-    "anx_conv_force_variant": (_I, [_I, _I]),
-    "anx_set_conv2_algo": (_I, [_I]),
-    "anx_set_stage_chunks": (_I, [_I, _I]),
-    "anx_set_fuse_pool1": (_I, [_I]),
-    "anx_get_conv2_algo": (_I, []),
-    "anx_set_conv1_algo": (_I, [_I]),
-    "anx_get_conv1_algo": (_I, []),
-    "anx_conv1_wino_cfg": (_I, [_I]),
-    "anx_conv1_wino_probe": (_I, [_I]),
-    "anx_conv1_wino": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P]),
-    "anx_wino_fused_cfg": (_I, [_I]),
-    "anx_wino_prio": (_I, [_I]),
-    "anx_bf16_glds": (_I, [_I]),
+    "anx_conv1_wino": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P, _I, _I, _P]),
+    "anx_engine_set_knob": (_I, [_P, C.c_char_p, _I]),
+    "anx_engine_get_knob": (_I, [_P, C.c_char_p, C.POINTER(_I)]),
+    "anx_full_set_knob": (_I, [_P, C.c_char_p, _I]),
+    "anx_full_get_knob": (_I, [_P, C.c_char_p, C.POINTER(_I)]),
+    "anx_default_knob": (_I, [C.c_char_p, C.POINTER(_I)]),
     "anx_conv2d_mfma": (_I, [C.POINTER(_I), _P, _P, _P, _P, _P] + [_I] * 6 + [_I, _P]),
     "anx_cpu_conv2d": (_I, [_P, _P, _P, _P] + [_I] * 10),
     "anx_cpu_maxpool": (_I, [_P, _P] + [_I] * 6),

@@ -29,6 +29,7 @@ from .. import _native as nat
 from ..config import IN_H, IN_W, BlockSpec, blocks, blocks_dims
 from ..parallel.plan import TilePlan, full_plan
 from ..utils.init import init_weights
+from ..utils.tuning import apply_knobs, knob_value, read_knob
 
 IMPLS = {"mfma": 0, "direct": 1}
 LANE_MIN = 64  # images per lane below which a forward stays on one stream
@@ -42,7 +43,8 @@ def _tile_c(t: TilePlan) -> nat.TileC:
 class AlexNetBlocks:
     def __init__(self, weights: dict | None = None, *, init: str = "const", seed: int = 0, lrn_mode: str = "div_n",
                  groups2: int = 1, H: int = IN_H, W: int = IN_W, device="cuda", impl: str = "mfma",
-                 max_batch: int = 1, specs: tuple[BlockSpec, BlockSpec] | None = None, lanes: int = 1):
+                 max_batch: int = 1, specs: tuple[BlockSpec, BlockSpec] | None = None, lanes: int = 1,
+                 knobs: dict | None = None):
         self.b1, self.b2 = specs if specs is not None else blocks(lrn_mode, groups2)
         if self.b1.has_lrn:
             raise ValueError("the native engine implements LRN after block 2 only (the reference's topology)")
@@ -58,6 +60,8 @@ class AlexNetBlocks:
         if impl not in IMPLS:
             raise ValueError(f"impl must be one of {sorted(IMPLS)}")
         self.impl = impl
+        # kernel knobs of this model's engines (anx.utils.tuning): applied at every engine creation
+        self.knobs = {k: knob_value(k, v) for k, v in (knobs or {}).items()}
         self._engine = None
         self._cap = 0
         self._ensure(max_batch)
@@ -70,12 +74,27 @@ class AlexNetBlocks:
             per_lane = -(-max(1, max_batch) // lanes)
             for _ in range(lanes - 1):
                 self._lanes.append(AlexNetBlocks(self.weights, specs=(self.b1, self.b2), H=H, W=W, device=self.device,
-                                                 impl=impl, max_batch=per_lane))
+                                                 impl=impl, max_batch=per_lane, knobs=self.knobs))
                 self._lane_streams.append(torch.cuda.Stream(self.device))
 
     @property
     def is_cuda(self) -> bool:
         return self.device.type == "cuda"
+
+    def set_knob(self, name: str, value) -> None:
+        """Change one kernel knob of this model (every lane); later forwards use it."""
+        v = knob_value(name, value)
+        if self.is_cuda and self._engine is not None:
+            apply_knobs(self._engine, {name: v})
+        self.knobs[name] = v
+        for m in self._lanes:
+            m.set_knob(name, v)
+
+    def get_knob(self, name: str) -> int:
+        """The value the GPU engine launches with."""
+        if not self.is_cuda:
+            raise ValueError("kernel knobs belong to the GPU engine")
+        return read_knob(self._engine, name)
 
     # ------------------------------------------------------------------ engine lifetime
     def _ensure(self, n: int) -> None:
@@ -89,6 +108,11 @@ class AlexNetBlocks:
         if self.is_cuda:
             with torch.cuda.device(self.device):
                 nat.call("anx_engine_create", C.byref(h), *args, max(1, n), IMPLS[self.impl])
+            try:
+                apply_knobs(h, self.knobs)
+            except Exception:
+                nat.lib().anx_engine_destroy(h)
+                raise
         else:
             nat.call("anx_cpu_engine_create", C.byref(h), *args)
         self._engine, self._cap = h, max(1, n)

@@ -16,6 +16,7 @@ import torch.nn.functional as F
 
 from .. import _native as nat
 from ..utils.init import STREAM_EXTRA, uniform
+from ..utils.tuning import apply_knobs, knob_value
 
 LAYERS = ("conv1", "conv2", "conv3", "conv4", "conv5", "fc6", "fc7", "fc8")
 FLOPS_PER_IMAGE = 2.0 * (55 * 55 * 96 * 363 + 27 * 27 * 256 * 2400 + 13 * 13 * 384 * 2304 + 13 * 13 * 384 * 3456 +
@@ -47,8 +48,9 @@ def init_full_weights(seed: int = 0, classes: int = 1000, groups2: int = 1) -> d
 
 class AlexNetFull:
     def __init__(self, weights: dict | None = None, *, seed: int = 0, classes: int = 1000, device="cuda",
-                 max_batch: int = 1, groups2: int = 1, lrn_mode: str = "div_n"):
+                 max_batch: int = 1, groups2: int = 1, lrn_mode: str = "div_n", knobs: dict | None = None):
         self.classes, self.groups2, self.lrn_mode = classes, groups2, lrn_mode
+        self.knobs = {k: knob_value(k, v) for k, v in (knobs or {}).items()}  # e.g. {"bf16_glds": 3}
         self.weights = {k: v.detach().to("cpu", torch.float32).contiguous()
                         for k, v in (weights or init_full_weights(seed, classes, groups2)).items()}
         self.device = torch.device(device)
@@ -68,7 +70,17 @@ class AlexNetFull:
         with torch.cuda.device(self.device):
             nat.call("anx_full_create", C.byref(h), ws, bs, self.classes, max(1, n), self.groups2,
                      0 if self.lrn_mode == "div_n" else 1)
+        try:
+            apply_knobs(h, self.knobs, full=True)
+        except Exception:
+            nat.lib().anx_full_destroy(h)
+            raise
         self._h, self._cap = h, max(1, n)
+
+    def set_knob(self, name: str, value) -> None:
+        v = knob_value(name, value)
+        apply_knobs(self._h, {name: v}, full=True)
+        self.knobs[name] = v
 
     def close(self):
         if self._h is not None:

@@ -12,8 +12,11 @@ per-layer kernels:
 
 How the GPU versions differ:
 
-* ``conv2d`` is the MFMA implicit GEMM: packed weights are cached per (weight tensor, version, plan);
-  ``impl="direct"`` selects the one-thread-per-output oracle kernel.
+* ``conv2d`` is the MFMA implicit GEMM: packed weights are cached per (weight tensor, version, plan).
+  The cache entry holds a reference to the weight tensor, so its storage (and address) cannot be
+  reused by another tensor while the entry exists; in-place edits through ``w.data`` do not bump
+  ``w._version`` — call :func:`clear_cache` after them. ``impl="direct"`` selects the
+  one-thread-per-output oracle kernel.
 * ``maxpool`` uses float4 channels.
 * ``maxpool_lrn`` is the fused pool+LRN kernel.
 * ``conv2d`` can write into a channel slice of a preallocated output (``out`` / ``c_off``), which
@@ -45,10 +48,10 @@ def _check(x: torch.Tensor, name: str) -> None:
 
 
 def _packed(w: torch.Tensor, plan, sizes: tuple[int, int], dev: torch.device):
-    key = (w.data_ptr(), w._version, tuple(w.shape), tuple(plan), str(dev))
+    key = (w.data_ptr(), w._version, tuple(w.shape), w.stride(), str(w.device), tuple(plan), str(dev))
     hit = _pack_cache.get(key)
-    if hit is not None:
-        return hit
+    if hit is not None and hit[0] is w:
+        return hit[1], hit[2]
     wc = w.detach().to("cpu", torch.float32).contiguous()
     packed = torch.empty(sizes[0], dtype=torch.float32)
     koff = torch.empty(sizes[1], dtype=torch.int32)
@@ -56,9 +59,11 @@ def _packed(w: torch.Tensor, plan, sizes: tuple[int, int], dev: torch.device):
              C.c_void_p(koff.data_ptr()))
     if len(_pack_cache) > 64:
         _pack_cache.clear()
-    hit = (packed.to(dev), koff.to(dev))
+    # keep `w` alive with the entry: a freed temporary's address could otherwise be handed to the
+    # next temporary of the same shape (e.g. equal-size filter shards) and hit this entry
+    hit = (w, packed.to(dev), koff.to(dev))
     _pack_cache[key] = hit
-    return hit
+    return hit[1], hit[2]
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, stride: int = 1, pad: int = 0,

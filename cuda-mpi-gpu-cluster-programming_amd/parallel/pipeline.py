@@ -15,6 +15,13 @@ batch scale and MI355X-first:
   two input buffers while step k computes, so the root's xGMI egress (world-1 links, each carrying
   one peer's shard) overlaps the compute instead of preceding it. Every step still scatters,
   computes and gathers its full batch; only the order changes.
+
+Input semantics with prefetch: ``step()`` snapshots ``x_global`` as it is at the call (the scatter
+for the NEXT step is issued from it) and computes the batch snapshotted by the previous call (the
+first call computes its own snapshot). Writes to ``x_global`` after ``step()`` returns are safe when
+they are stream-ordered on the current stream (any torch op or copy): each step makes the current
+stream wait for the scatter it issued before returning, so a later write cannot overtake that read.
+Host code writing ``x_global`` through a raw pointer must synchronise the stream first.
 """
 from __future__ import annotations
 
@@ -97,6 +104,11 @@ class ScatterComputeGather:
                 dst = [self.y_global[r, lo:hi] for r in range(self.world)] if self.rank == 0 else None
                 gw.append(dist.gather(y[lo:hi], dst, dst=0, group=self.group, async_op=True))
         self._gather_pending[cur] = gw
+        # Order the prefetch's read of x_global before anything the caller enqueues next (e.g. writing
+        # the following batch into x_global). Enqueued after this step's compute, so it delays
+        # nothing: step k+1's compute needs that scatter anyway.
+        for w in self._scatter_pending or []:
+            w.wait()
         self.x, self.y = x, y
         self._k += 1
 

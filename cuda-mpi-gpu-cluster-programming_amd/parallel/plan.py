@@ -153,18 +153,27 @@ def full_plan(H: int, W: int, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) ->
 
 
 def check_plan(p: DecompPlan, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> None:
+    """Raise ValueError unless the tiles partition the output rows and every layer window matches the
+    layer algebra (the C++ check_plan's contract; no ``assert``, so ``python -O`` keeps the checks)."""
     d = blocks_dims(p.H, p.W, b1, b2)
     nxt = 0
+
+    def need(ok: bool, msg: str) -> None:
+        if not ok:
+            raise ValueError(msg)
+
     for r, t in enumerate(p.tiles):
         if t.out.empty:
             continue
-        assert t.out.lo == nxt, f"rank {r}: output rows start at {t.out.lo}, expected {nxt}"
+        need(t.out.lo == nxt, f"rank {r}: output rows start at {t.out.lo}, expected {nxt}")
         nxt = t.out.hi
-        assert t.inp.lo == t.c1.lo * b1.conv.S and conv_out_dim(t.inp.size, b1.conv.F, b1.conv.S, 0) == t.c1.size, \
-            f"rank {r}: conv1 window"
-        assert t.c1.lo == t.p1.lo * b1.pool.S and pool_out_dim(t.c1.size, b1.pool.F, b1.pool.S) == t.p1.size, \
-            f"rank {r}: pool1 window"
-        assert conv_out_dim(t.q.size, b2.conv.F, b2.conv.S, 0) == t.c2.size, f"rank {r}: conv2 window"
-        assert t.c2.lo == t.out.lo * b2.pool.S and pool_out_dim(t.c2.size, b2.pool.F, b2.pool.S) == t.out.size, \
-            f"rank {r}: pool2 window"
-    assert nxt == d.Hp2, "output rows do not cover the image"
+        need(t.inp.lo == t.c1.lo * b1.conv.S and conv_out_dim(t.inp.size, b1.conv.F, b1.conv.S, 0) == t.c1.size,
+             f"rank {r}: conv1 window")
+        need(t.c1.lo == t.p1.lo * b1.pool.S and pool_out_dim(t.c1.size, b1.pool.F, b1.pool.S) == t.p1.size,
+             f"rank {r}: pool1 window")
+        # the pool1 rows a rank computes land inside its conv2 input window (stage1 writes them there)
+        need(t.q.lo <= t.p1.lo and t.p1.hi <= t.q.hi, f"rank {r}: pool1 rows outside the conv2 window")
+        need(conv_out_dim(t.q.size, b2.conv.F, b2.conv.S, 0) == t.c2.size, f"rank {r}: conv2 window")
+        need(t.c2.lo == t.out.lo * b2.pool.S and pool_out_dim(t.c2.size, b2.pool.F, b2.pool.S) == t.out.size,
+             f"rank {r}: pool2 window")
+    need(nxt == d.Hp2, "output rows do not cover the image")

@@ -1,66 +1,56 @@
-"""Process-wide kernel selection knobs of the native engine (read at launch time).
+"""Kernel selection knobs of the native engines (anx/knobs.hpp), per engine.
 
-* ``set_conv2_algo``: Conv2 (5x5, stride 1) on the MFMA path — ``auto`` (Winograd F(3x3,5x5) when
-  eligible), ``direct`` (implicit-GEMM; bit-identical across any row decomposition), ``winograd``,
-  ``winograd_unfused`` (separate batched GEMM + output transform; A/B only).
-* ``set_conv1_algo``: Conv1 (11x11, stride 4) on the MFMA path — ``auto``/``winograd`` (polyphase
-  Winograd F(3x3,3x3)) or ``direct`` (implicit GEMM; bit-identical across any row decomposition).
-* ``force_conv_variant``: pin an implicit-GEMM tile variant (A/B tuning; ``None`` = heuristic).
+Every :class:`~anx.models.alexnet_blocks.AlexNetBlocks` / :class:`~anx.models.alexnet_full.AlexNetFull`
+owns its knobs (``knobs={...}`` at construction, ``set_knob`` later); nothing here is process-wide.
+Names and values:
+
+* ``conv2_algo``: Conv2 (5x5, stride 1) on the MFMA path — ``auto`` (Winograd F(3x3,5x5) when
+  eligible and the launch exceeds 8 images), ``direct`` (implicit GEMM; bit-identical across any row
+  decomposition), ``winograd``, ``winograd_unfused`` (separate batched GEMM + output transform; A/B).
+* ``conv1_algo``: Conv1 (11x11, stride 4) — ``auto``/``winograd`` (polyphase Winograd F(3x3,3x3)) or
+  ``direct``.
+* integer knobs: ``conv1_cfg``, ``conv1_probe``, ``wino_cfg``, ``wino_prio``, ``fold_scalar``,
+  ``chunk1``, ``chunk2``, ``fuse_pool1``, ``force_vec4``, ``force_scalar``, ``bf16_glds``.
 """
 from __future__ import annotations
 
-from contextlib import contextmanager
+import ctypes as C
 
 from .. import _native as nat
 
-_ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd_unfused": 3}
+ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd_unfused": 3}
+KNOBS = ("conv1_algo", "conv2_algo", "conv1_cfg", "conv1_probe", "wino_cfg", "wino_prio", "fold_scalar",
+         "chunk1", "chunk2", "fuse_pool1", "force_vec4", "force_scalar", "bf16_glds")
 
 
-def set_conv2_algo(name: str) -> None:
-    if name not in _ALGOS:
-        raise ValueError(f"conv2 algo must be one of {sorted(_ALGOS)}")
-    nat.call("anx_set_conv2_algo", _ALGOS[name])
+def knob_value(name: str, value) -> int:
+    """Normalise a knob value: algorithm names for ``conv*_algo``, ints (or bools) otherwise."""
+    if name not in KNOBS:
+        raise ValueError(f"unknown knob {name!r}; known: {', '.join(KNOBS)}")
+    if name.endswith("_algo") and isinstance(value, str):
+        if value not in ALGOS or (name == "conv1_algo" and value == "winograd_unfused"):
+            raise ValueError(f"{name} must be one of {sorted(ALGOS)}")
+        return ALGOS[value]
+    return int(value)
 
 
-def get_conv2_algo() -> str:
-    v = nat.lib().anx_get_conv2_algo()
-    return {i: k for k, i in _ALGOS.items()}[v]
+def default_knob(name: str) -> int:
+    """The value a new engine starts from (built-in default or its ANX_* environment override)."""
+    knob_value(name, 0)
+    v = C.c_int()
+    nat.call("anx_default_knob", name.encode(), C.byref(v))
+    return v.value
 
 
-@contextmanager
-def conv2_algo(name: str):
-    old = get_conv2_algo()
-    set_conv2_algo(name)
-    try:
-        yield
-    finally:
-        set_conv2_algo(old)
+def apply_knobs(handle, knobs: dict | None, full: bool = False) -> None:
+    """Set ``knobs`` on one native engine handle (BlocksEngine, or FullEngine with ``full``)."""
+    fn = "anx_full_set_knob" if full else "anx_engine_set_knob"
+    for k, v in (knobs or {}).items():
+        nat.call(fn, handle, k.encode(), knob_value(k, v))
 
 
-_ALGOS1 = {"auto": 0, "direct": 1, "winograd": 2}
-
-
-def set_conv1_algo(name: str) -> None:
-    if name not in _ALGOS1:
-        raise ValueError(f"conv1 algo must be one of {sorted(_ALGOS1)}")
-    nat.call("anx_set_conv1_algo", _ALGOS1[name])
-
-
-def get_conv1_algo() -> str:
-    v = nat.lib().anx_get_conv1_algo()
-    return {i: k for k, i in _ALGOS1.items()}[v]
-
-
-@contextmanager
-def conv1_algo(name: str):
-    old = get_conv1_algo()
-    set_conv1_algo(name)
-    try:
-        yield
-    finally:
-        set_conv1_algo(old)
-
-
-def force_conv_variant(vec4: int | None = None, scalar: int | None = None) -> None:
-    nat.call("anx_conv_force_variant", 0, -1 if vec4 is None else vec4)
-    nat.call("anx_conv_force_variant", 1, -1 if scalar is None else scalar)
+def read_knob(handle, name: str, full: bool = False) -> int:
+    v = C.c_int()
+    knob_value(name, 0)
+    nat.call("anx_full_get_knob" if full else "anx_engine_get_knob", handle, name.encode(), C.byref(v))
+    return v.value

@@ -134,10 +134,8 @@ def run(cfg: RunConfig) -> RunResult | None:
         w = init_weights(cfg.init, cfg.seed, b1, b2) if rank == 0 else \
             {k: torch.empty_like(v) for k, v in init_weights("const", 0, b1, b2).items()}
         w = comm.bcast_weights(w, device=comm_dev)
-        from .utils.tuning import set_conv1_algo, set_conv2_algo
-        set_conv2_algo(cfg.conv2_algo)
-        set_conv1_algo(cfg.conv1_algo)
-        model = AlexNetBlocks(w, specs=(b1, b2), device=device, impl=cfg.impl, max_batch=cfg.batch)
+        model = AlexNetBlocks(w, specs=(b1, b2), device=device, impl=cfg.impl, max_batch=cfg.batch,
+                              knobs={"conv1_algo": cfg.conv1_algo, "conv2_algo": cfg.conv2_algo} if gpu else None)
         x = init_input(cfg.batch, cfg.init, cfg.seed) if rank == 0 else None
         if cfg.version == "v2.1" or (cfg.strategy == "filter" and cfg.version in ("v2.2", "v4", "v5")):
             # broadcast-all: every rank receives the whole input (M3, main.cpp:71); the filter

@@ -68,6 +68,57 @@ def test_scatter_compute_gather_gloo(prefetch):
     torch.testing.assert_close(y.view_as(ref), ref, rtol=0, atol=0)
 
 
+def _prefetch_changing_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import anx  # noqa: F401
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.parallel.pipeline import PipelineConfig, ScatterComputeGather
+    from anx.utils.init import init_input
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    d = anx.blocks_dims()
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    pipe = ScatterComputeGather(m, PipelineConfig(1, micro=1, prefetch=True), (d.H, d.W, d.C0),
+                                (d.Hp2, d.Wp2, d.C2), "cpu")
+    outs = []
+    for k in range(4):  # a new batch written into x_global after every step
+        if rank == 0:
+            pipe.x_global.copy_(init_input(world, "rand", seed=10 + k).view(world, 1, d.H, d.W, d.C0))
+        pipe.step()
+        pipe.drain()
+        if rank == 0:
+            outs.append(pipe.y_global.clone())
+    if rank == 0:
+        q.put(torch.stack(outs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_prefetch_pipeline_input_semantics():
+    """With prefetch, step k computes the batch x_global held when step k-1 was called (step 0 its
+    own): inputs rewritten between steps are never mixed or lost."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_prefetch_changing_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ys = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, ROOT)
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.utils.init import init_input
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    for k in range(4):
+        src = max(k - 1, 0)
+        ref = m(init_input(world, "rand", seed=10 + src))
+        torch.testing.assert_close(ys[k].view_as(ref), ref, rtol=0, atol=0)
+
+
 def test_bench_contract_gloo():
     """bench.py under torch.distributed.run (gloo/CPU rehearsal) prints ONE valid JSON line on rank 0."""
     port = free_port()

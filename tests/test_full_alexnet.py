@@ -39,17 +39,11 @@ def test_full_alexnet_vs_torch(cuda, N, groups2):
 def test_bf16_lds_dma_kernel_matches_register_staged(cuda, mode):
     """The LDS-DMA ring kernel (128x128 vec8 layers: conv2-5 at this batch, FC6-8) sums the same
     products in the same order as the register-staged kernel: logits bit-identical."""
-    from anx import _native as nat
     N = 160
     x = (init_input(N, "rand", seed=6) * 10).to(cuda)
-    try:
-        nat.call("anx_bf16_glds", 0)
-        ref = AlexNetFull(seed=6, device=cuda, max_batch=N)(x).clone()
-        nat.call("anx_bf16_glds", mode)
-        got = AlexNetFull(seed=6, device=cuda, max_batch=N)(x)
-        torch.cuda.synchronize()
-    finally:
-        nat.call("anx_bf16_glds", 2)
+    ref = AlexNetFull(seed=6, device=cuda, max_batch=N, knobs={"bf16_glds": 0})(x).clone()
+    got = AlexNetFull(seed=6, device=cuda, max_batch=N, knobs={"bf16_glds": mode})(x)
+    torch.cuda.synchronize()
     assert torch.equal(got, ref)
 
 

@@ -182,17 +182,14 @@ def test_lrn_and_fused_pool_lrn(cuda, mode, C):
 
 
 # ---------------------------------------------------------------- Winograd F(3x3,5x5) conv2
-@pytest.fixture
-def algo():
-    yield lambda a: nat.call("anx_set_conv2_algo", a)
-    nat.call("anx_set_conv2_algo", 0)
+WINO2 = {"conv2_algo": "winograd"}
+WINO1 = {"conv1_algo": "winograd"}
 
 
 @pytest.mark.parametrize("N", [1, 5, 64])
 @pytest.mark.parametrize("groups2", [1, 2])
-def test_winograd_engine_vs_oracle(cuda, algo, N, groups2):
-    algo(2)
-    m = AlexNetBlocks(device=cuda, init="rand", seed=31 + N, max_batch=N, groups2=groups2)
+def test_winograd_engine_vs_oracle(cuda, N, groups2):
+    m = AlexNetBlocks(device=cuda, init="rand", seed=31 + N, max_batch=N, groups2=groups2, knobs=WINO2)
     x = init_input(N, "rand", seed=31 + N)
     y = m(x.to(cuda)).cpu().double()
     ref = blocks_forward(x, m.weights, m.b1, m.b2)
@@ -200,10 +197,9 @@ def test_winograd_engine_vs_oracle(cuda, algo, N, groups2):
 
 
 @pytest.mark.parametrize("np_", [2, 3, 4, 8])
-def test_winograd_row_tiles_partial(cuda, algo, np_):
+def test_winograd_row_tiles_partial(cuda, np_):
     """Row tiles give conv2 heights that are not multiples of 3 (partial Winograd tiles)."""
-    algo(2)
-    m = AlexNetBlocks(device=cuda, init="rand", seed=40, max_batch=2)
+    m = AlexNetBlocks(device=cuda, init="rand", seed=40, max_batch=2, knobs=WINO2)
     x = init_input(2, "rand", seed=40)
     ref = blocks_forward(x, m.weights, m.b1, m.b2)
     xd = x.to(cuda)
@@ -212,20 +208,13 @@ def test_winograd_row_tiles_partial(cuda, algo, np_):
     torch.testing.assert_close(torch.cat(parts, dim=1).cpu().double(), ref, rtol=2e-5, atol=2e-6)
 
 
-def test_winograd_golden(cuda, algo):
-    algo(2)
-    m = AlexNetBlocks(device=cuda, lrn_mode="raw")
+def test_winograd_golden(cuda):
+    m = AlexNetBlocks(device=cuda, lrn_mode="raw", knobs=WINO2)
     y = m(init_input(1, "const").to(cuda)).cpu()
     assert y.flatten()[:5].tolist() == pytest.approx(GOLD_RAW, abs=2e-4)
 
 
 # ---------------------------------------------------------------- polyphase Winograd F(3x3,3x3) conv1
-@pytest.fixture
-def algo1():
-    yield lambda a: nat.call("anx_set_conv1_algo", a)
-    nat.call("anx_set_conv1_algo", 0)
-
-
 @pytest.mark.parametrize("shape", [
     # N, Hin, W, K, F
     (1, 227, 227, 96, 11),
@@ -242,33 +231,47 @@ def test_conv1_wino_kernel_vs_torch(cuda, shape):
     H1, W1 = (H - F) // 4 + 1, (W - F) // 4 + 1
     y = torch.full((N, H1, W1, K), float("nan"), device=cuda)
     nat.call("anx_conv1_wino", x.data_ptr(), N, H, W, w.contiguous().data_ptr(), K, F, b.data_ptr(), y.data_ptr(), 0,
-             nat.stream_ptr(cuda))
+             0, nat.stream_ptr(cuda))
     ref = conv2d_nhwc(x.double(), w.to(cuda).double(), b.double(), 4, 0)
     torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
-def test_conv1_wino_ring_configs(cuda, cfg):
-    """Every GEMM configuration (32x32 MFMA: BK 48 x 2 slots, BK 16 x 4/6/8; 16x16 MFMA) gives the same conv1."""
-    torch.manual_seed(5)
-    x = torch.rand(4, 227, 227, 3, device=cuda)
-    w = (torch.rand(96, 3, 11, 11) - 0.5) * 0.1
-    b = torch.zeros(96, device=cuda)
-    y = torch.empty(4, 55, 55, 96, device=cuda)
-    nat.call("anx_conv1_wino_cfg", cfg)
-    try:
-        nat.call("anx_conv1_wino", x.data_ptr(), 4, 227, 227, w.data_ptr(), 96, 11, b.data_ptr(), y.data_ptr(), 1,
-                 nat.stream_ptr(cuda))
-    finally:
-        nat.call("anx_conv1_wino_cfg", 4)
-    ref = conv2d_nhwc(x.double(), w.to(cuda).double(), b.double(), 4, 0, relu=True)
-    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
+@pytest.mark.parametrize("fold_scalar", [0, 1])
+def test_conv1_wino_ring_configs(cuda, cfg, fold_scalar):
+    """Every Conv1 GEMM configuration (32x32 MFMA: BK 48 x 2 slots, BK 16 x 4/6/8; 16x16 MFMA) and
+    both fold forms (packed / scalar FMAs) give the same Blocks 1-2 output, bitwise across the folds."""
+    x = init_input(9, "rand", seed=5).to(cuda)
+    knobs = {**WINO1, "conv1_cfg": cfg, "fold_scalar": fold_scalar}
+    m = AlexNetBlocks(device=cuda, init="rand", seed=5, max_batch=9, knobs=knobs)
+    y = m(x)
+    assert m.get_knob("conv1_cfg") == cfg and m.get_knob("fold_scalar") == fold_scalar
+    m.set_knob("fold_scalar", 1 - fold_scalar)
+    assert torch.equal(m(x), y)
+    ref = blocks_forward(x.cpu(), m.weights, m.b1, m.b2)
+    torch.testing.assert_close(y.cpu().double(), ref, rtol=2e-5, atol=2e-6)
+
+
+def test_knobs_are_per_engine(cuda):
+    """Two models in one process run different kernels at the same time; unknown knobs and bad
+    values are rejected without changing the engine."""
+    x = init_input(12, "rand", seed=8).to(cuda)
+    a = AlexNetBlocks(device=cuda, init="rand", seed=8, max_batch=12, knobs={"conv2_algo": "direct"})
+    b = AlexNetBlocks(device=cuda, init="rand", seed=8, max_batch=12, knobs={"conv2_algo": "winograd"})
+    assert a.get_knob("conv2_algo") == 1 and b.get_knob("conv2_algo") == 2
+    ya, yb = a(x), b(x)
+    assert not torch.equal(ya, yb)  # different summation orders
+    torch.testing.assert_close(ya, yb, rtol=1e-5, atol=1e-6)
+    with pytest.raises(ValueError):
+        a.set_knob("no_such_knob", 1)
+    with pytest.raises(nat.NativeError):
+        a.set_knob("wino_cfg", 99)
+    assert a.get_knob("wino_cfg") == 7
 
 
 @pytest.mark.parametrize("N", [1, 7, 128])
-def test_conv1_winograd_engine_vs_oracle(cuda, algo1, N):
-    algo1(2)
-    m = AlexNetBlocks(device=cuda, init="rand", seed=50 + N, max_batch=N)
+def test_conv1_winograd_engine_vs_oracle(cuda, N):
+    m = AlexNetBlocks(device=cuda, init="rand", seed=50 + N, max_batch=N, knobs=WINO1)
     x = init_input(N, "rand", seed=50 + N)
     y = m(x.to(cuda)).cpu().double()
     idx = torch.arange(N) if N <= 8 else torch.tensor([0, 1, 63, 64, 126, 127])
@@ -277,10 +280,9 @@ def test_conv1_winograd_engine_vs_oracle(cuda, algo1, N):
 
 
 @pytest.mark.parametrize("np_", [2, 3, 4, 8])
-def test_conv1_winograd_row_tiles(cuda, algo1, np_):
+def test_conv1_winograd_row_tiles(cuda, np_):
     """Row tiles start conv1's 3x3 Winograd tiles at the tile's own first row (partial tiles)."""
-    algo1(2)
-    m = AlexNetBlocks(device=cuda, init="rand", seed=60, max_batch=2)
+    m = AlexNetBlocks(device=cuda, init="rand", seed=60, max_batch=2, knobs=WINO1)
     x = init_input(2, "rand", seed=60)
     ref = blocks_forward(x, m.weights, m.b1, m.b2)
     xd = x.to(cuda)
@@ -289,53 +291,54 @@ def test_conv1_winograd_row_tiles(cuda, algo1, np_):
     torch.testing.assert_close(torch.cat(parts, dim=1).cpu().double(), ref, rtol=2e-5, atol=2e-6)
 
 
-def test_conv1_direct_and_winograd_agree(cuda, algo1):
+def test_conv1_direct_and_winograd_agree(cuda):
     m = AlexNetBlocks(device=cuda, init="rand", seed=70, max_batch=4)
     x = init_input(4, "rand", seed=70).to(cuda)
-    algo1(1)
+    m.set_knob("conv1_algo", "direct")
     yd = m(x).clone()
-    algo1(2)
+    m.set_knob("conv1_algo", "winograd")
     yw = m(x)
     torch.testing.assert_close(yw, yd, rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("mode,gold", [("div_n", GOLD_DIV_N_F64), ("raw", GOLD_RAW)])
-def test_conv1_winograd_golden(cuda, algo, algo1, mode, gold):
+def test_conv1_winograd_golden(cuda, mode, gold):
     # both convs Winograd (batch 1 would otherwise run conv2 direct: Auto picks direct below 9
     # images, whose 2400-term fp32 chains sit 1e-5 off the fp64 golden values)
-    algo(2)
-    algo1(2)
-    m = AlexNetBlocks(device=cuda, lrn_mode=mode)
+    m = AlexNetBlocks(device=cuda, lrn_mode=mode, knobs={**WINO1, **WINO2})
     y = m(init_input(1, "const").to(cuda)).cpu()
     assert y.flatten()[:5].tolist() == pytest.approx(gold, abs=2e-4)
 
 
 @pytest.mark.parametrize("cfg", [1, 5, 7, 12, 13, 14, 15])  # register ring / LDS-DMA 32x32 / 16x16 64x128, 64x64; +-XCD
 @pytest.mark.parametrize("groups2", [1, 2])
-def test_winograd_fused_configs(cuda, algo, cfg, groups2):
-    algo(2)
-    nat.call("anx_wino_fused_cfg", cfg)
-    try:
-        m = AlexNetBlocks(device=cuda, init="rand", seed=80 + cfg, max_batch=9, groups2=groups2)
-        x = init_input(9, "rand", seed=80 + cfg)
-        y = m(x.to(cuda)).cpu().double()
-    finally:
-        nat.call("anx_wino_fused_cfg", 7)
+def test_winograd_fused_configs(cuda, cfg, groups2):
+    m = AlexNetBlocks(device=cuda, init="rand", seed=80 + cfg, max_batch=9, groups2=groups2,
+                      knobs={**WINO2, "wino_cfg": cfg})
+    x = init_input(9, "rand", seed=80 + cfg)
+    y = m(x.to(cuda)).cpu().double()
     torch.testing.assert_close(y, blocks_forward(x, m.weights, m.b1, m.b2), rtol=2e-5, atol=2e-6)
 
 
-@pytest.fixture
-def fuse_pool1():
-    yield lambda on: nat.call("anx_set_fuse_pool1", on)
-    nat.call("anx_set_fuse_pool1", 1)
+@pytest.mark.parametrize("prio", [1, 257])  # the plain and the interleaved-fold LDS-DMA kernel
+def test_winograd_scalar_fold_bitwise(cuda, prio):
+    """Scalar (v_fma_f32) and packed (v_pk_fma_f32) Conv2 output folds compute the same FMAs."""
+    x = init_input(20, "rand", seed=81).to(cuda)
+    m = AlexNetBlocks(device=cuda, init="rand", seed=81, max_batch=20, knobs={**WINO2, "wino_prio": prio})
+    y = m(x).clone()
+    m.set_knob("fold_scalar", 2)
+    assert torch.equal(m(x), y)
+
+
 
 
 @pytest.mark.parametrize("N", [9, 20])
-def test_fused_pool1_winograd_input_bitwise(cuda, fuse_pool1, N):
+def test_fused_pool1_winograd_input_bitwise(cuda, N):
     """Pool1 fused into Conv2's Winograd input transform == maxpool + window + transform, bit for bit
     (whole images and overlap row tiles), and both match the fp64 oracle."""
     m = AlexNetBlocks(device=cuda, init="rand", seed=90 + N, max_batch=N)
     x = init_input(N, "rand", seed=N).to(cuda)
+    fuse_pool1 = lambda on: m.set_knob("fuse_pool1", on)  # noqa: E731
     fuse_pool1(0)
     ref = m(x).clone()
     fuse_pool1(1)

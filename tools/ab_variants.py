@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
-"""In-process A/B of conv tile variants on the full Blocks 1-2 forward (CDNA guide §5.4 rule 24:
+"""In-process A/B of engine kernel knobs on the full Blocks 1-2 forward (CDNA guide §5.4 rule 24:
 interleaved rounds in ONE process, report median and min).
 
-usage: tools/ab_variants.py --arms "0:1,5:6,7:8" --batch 128
-each arm = <vec4 variant>:<scalar variant>[:<conv2 algo 0 auto|1 direct|2 winograd>[:<wino fused cfg>
-[:<conv1 algo 0 auto|1 direct|2 winograd>[:<conv1 winograd ring cfg 0..2>]]]] (-1 = heuristic)."""
+Every arm is its own model (own engine, own knobs: anx/knobs.hpp), so arms never touch shared state.
+
+usage: tools/ab_variants.py --arms "fold_scalar=0|fold_scalar=1" --batch 300
+       tools/ab_variants.py --arms "|wino_prio=17|wino_prio=33" --batch 300   # cost probes (wrong results)
+An arm is ';'-separated name=value pairs over the defaults (empty arm = defaults); '|' separates
+arms. Names: anx.utils.tuning.KNOBS (algorithm knobs take auto/direct/winograd). --lanes L runs
+every arm as L stream lanes. Probe arms (bits 0-3 of conv1_probe, 4-7 of wino_prio) give wrong
+outputs by design: only their times matter; max_abs_diff_vs_arm0 says which arms are exact."""
 import argparse
 import json
 import os
@@ -14,50 +19,39 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import anx  # noqa: E402
-from anx import _native as nat  # noqa: E402
 from anx.models.alexnet_blocks import AlexNetBlocks  # noqa: E402
+
+
+def parse_arm(spec: str) -> dict:
+    out = {}
+    for kv in filter(None, (p.strip() for p in spec.split(";"))):
+        k, v = kv.split("=", 1)
+        out[k.strip()] = v.strip() if k.strip().endswith("_algo") and not v.strip().lstrip("-").isdigit() else int(v)
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--arms", default="-1:-1:1,-1:-1:2")
-    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--arms", default="|fold_scalar=1")
+    ap.add_argument("--batch", type=int, default=300)
+    ap.add_argument("--lanes", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--check", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    defaults = [-1, -1, 0, 7, 0, 4]
-    arms = []
-    for spec in a.arms.split(","):
-        f = [int(v) for v in spec.split(":")]
-        arms.append(tuple(f + defaults[len(f):]))
-
-    def force(arm):
-        v4, sc, al, fc, c1, c1c = arm
-        nat.call("anx_conv_force_variant", 0, v4)
-        nat.call("anx_conv_force_variant", 1, sc)
-        nat.call("anx_set_conv2_algo", al)
-        nat.call("anx_wino_fused_cfg", fc)
-        nat.call("anx_set_conv1_algo", c1)
-        nat.call("anx_conv1_wino_cfg", c1c)
-    models = []
+    arms = [parse_arm(s) for s in a.arms.split("|")]
     x = torch.rand(a.batch, 227, 227, 3, device=dev) * 0.1
-    ref = None
-    for arm in arms:
-        force(arm)
-        m = AlexNetBlocks(init="rand", device=dev, max_batch=a.batch)
-        y = m(x)  # packs weights for the forced variants
+    models, ref = [], None
+    for knobs in arms:
+        m = AlexNetBlocks(init="rand", device=dev, max_batch=a.batch, lanes=a.lanes, knobs=knobs)
+        y = m(x)
         torch.cuda.synchronize()
         if ref is None:
             ref = y.clone()
-        err = (y - ref).abs().max().item()
-        models.append((m, torch.empty_like(y), err))
+        models.append((m, torch.empty_like(y), (y - ref).abs().max().item()))
     times = [[] for _ in arms]
     for _ in range(a.rounds):
         for i, (m, y, _) in enumerate(models):
-            # the variant is chosen at plan time (every call): force it for this arm's launches
-            force(arms[i])
             m(x, out=y)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -66,13 +60,13 @@ def main():
             e1.record()
             e1.synchronize()
             times[i].append(e0.elapsed_time(e1) / a.iters)
-    force(tuple(defaults))
     f = anx.flops_per_image()
-    for arm, t, (_, _, err) in zip(arms, times, models):
+    for knobs, t, (_, _, err) in zip(arms, times, models):
         med = sorted(t)[len(t) // 2]
-        print(json.dumps({"arm": ":".join(str(v) for v in arm), "batch": a.batch, "ms_median": round(med, 4), "ms_min": round(min(t), 4),
-                          "img_per_s": round(a.batch / med * 1e3, 1), "tflops": round(a.batch * f / med / 1e9, 2),
-                          "max_abs_diff_vs_arm0": err}))
+        print(json.dumps({"arm": knobs, "batch": a.batch, "lanes": a.lanes, "ms_median": round(med, 4),
+                          "ms_min": round(min(t), 4), "img_per_s": round(a.batch / med * 1e3, 1),
+                          "direct_equiv_tflops": round(a.batch * f / med / 1e9, 2), "max_abs_diff_vs_arm0": err}),
+              flush=True)
 
 
 if __name__ == "__main__":
