@@ -40,6 +40,13 @@ int anx_make_plan(int H, int W, int np, int mode, const anx_block_c* b1, const a
                   int* n_p1_halos, int cap);
 
 /* ---- engine (Blocks 1-2) ---- */
+/* Hybrid batch x rows plan (anx/plan.hpp make_hybrid_plan). Per rank r (arrays of np):
+   group[r], index[r] (position in its group), img[2r..2r+1] (its image range), tile[r] (its rows);
+   per group g (arrays of np, first `*groups` used): gsize[g]. redundancy: conv1 rows computed over
+   one device's, minus 1. */
+int anx_make_hybrid_plan(int H, int W, int np, int batch, int row_ways, int mode, const anx_block_c* b1,
+                         const anx_block_c* b2, int* groups, int* group, int* index, int* img, int* gsize,
+                         anx_tile_c* tile, double* redundancy);
 int anx_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,
                       const float* bias1, const float* w2, const float* bias2, int max_batch, int impl);
 int anx_engine_destroy(void* e);

@@ -73,4 +73,36 @@ DecompPlan make_plan(int H, int W, int np, Decomp mode, const BlockSpec& b1 = kB
 // consistent with the layer algebra. Returns an empty string when valid, else a message.
 const char* check_plan(const DecompPlan& p);
 
+// Redundant Conv1 work of a row decomposition: sum over ranks of the conv1 rows each computes,
+// divided by the image's conv1 rows, minus 1 (0 = no row is computed twice). Overlap tiles
+// recompute their neighbours' rows (np = 8: 1.38); per-layer tiles only at the pool1 seams.
+double conv1_redundancy(const DecompPlan& p);
+
+// Hybrid batch x rows decomposition. The reference only splits image rows
+// (v2_mpi_only/2.2_scatter_halo/src/main.cpp:100-249); images are independent, so the batch is split
+// first and rows only where there are fewer images than ranks (or when asked):
+//   row_ways == 0 (auto): batch >= np -> np groups of 1 rank, images split over them (pure batch);
+//                         batch <  np -> `batch` groups of one image each, the ranks split over the
+//                         groups as evenly as possible (sizes differ by at most one), rows inside.
+//   row_ways == r > 0   : np / r groups of r ranks (np % r == 0), images split over the groups,
+//                         each group row-decomposes its images r ways (r == np: the reference's
+//                         pure row split of the whole batch).
+// Every rank computes images `images[group_of[rank]]` x tile rows_plan(rank).
+struct HybridPlan {
+  int np = 1, batch = 1, groups = 1;
+  std::vector<RowRange> images;      // per group: its image range (empty when batch < groups)
+  std::vector<int> group_first;      // per group: its first rank (ranks of a group are contiguous)
+  std::vector<int> group_size;       // per group: its number of ranks
+  std::vector<int> group_of, index_in_group;  // per rank
+  std::vector<DecompPlan> row_plans;  // per group: the row plan over group_size[g] ranks
+  const TilePlan& tile(int rank) const { return row_plans[group_of[rank]].tiles[index_in_group[rank]]; }
+};
+// Returns false (plan untouched) for an invalid request (np < 1, batch < 1, row_ways > np or not
+// dividing np).
+bool make_hybrid_plan(int H, int W, int np, int batch, int row_ways, Decomp mode, HybridPlan& out,
+                      const BlockSpec& b1 = kBlock1, const BlockSpec& b2 = kBlock2);
+// Conv1 rows computed by all ranks over the batch, relative to one device computing it: 0 for a
+// pure batch split.
+double conv1_redundancy(const HybridPlan& p);
+
 }  // namespace anx

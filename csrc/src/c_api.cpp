@@ -152,6 +152,32 @@ int anx_make_plan(int H, int W, int np, int mode, const anx_block_c* b1, const a
   });
 }
 
+int anx_make_hybrid_plan(int H, int W, int np, int batch, int row_ways, int mode, const anx_block_c* b1,
+                         const anx_block_c* b2, int* groups, int* group, int* index, int* img, int* gsize,
+                         anx_tile_c* tile, double* redundancy) {
+  return guarded("anx_make_hybrid_plan", [&] {
+    anx::HybridPlan p;
+    if (!anx::make_hybrid_plan(H, W, np, batch, row_ways, static_cast<anx::Decomp>(mode), p, from_c(*b1),
+                               from_c(*b2)))
+      return fail("invalid hybrid plan request (np >= 1, batch >= 1, row_ways dividing np)");
+    for (int g = 0; g < p.groups; ++g) {
+      const char* err = anx::check_plan(p.row_plans[g]);
+      if (err[0]) return fail(err);
+      gsize[g] = p.group_size[g];
+    }
+    *groups = p.groups;
+    for (int r = 0; r < np; ++r) {
+      group[r] = p.group_of[r];
+      index[r] = p.index_in_group[r];
+      img[2 * r] = p.images[p.group_of[r]].lo;
+      img[2 * r + 1] = p.images[p.group_of[r]].hi;
+      tile[r] = tile_to_c(p.tile(r));
+    }
+    *redundancy = anx::conv1_redundancy(p);
+    return 0;
+  });
+}
+
 int anx_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,
                       const float* bias1, const float* w2, const float* bias2, int max_batch, int impl) {
   return guarded("anx_engine_create", [&] {

@@ -153,4 +153,49 @@ const char* check_plan(const DecompPlan& p) {
   return "";
 }
 
+double conv1_redundancy(const DecompPlan& p) {
+  long rows = 0;
+  for (const TilePlan& t : p.tiles) rows += t.c1.size();
+  return p.dims.H1 > 0 ? static_cast<double>(rows) / p.dims.H1 - 1.0 : 0.0;
+}
+
+bool make_hybrid_plan(int H, int W, int np, int batch, int row_ways, Decomp mode, HybridPlan& out,
+                      const BlockSpec& b1, const BlockSpec& b2) {
+  if (np < 1 || batch < 1 || row_ways < 0 || row_ways > np || (row_ways > 0 && np % row_ways)) return false;
+  HybridPlan p;
+  p.np = np;
+  p.batch = batch;
+  if (row_ways > 0) {
+    p.groups = np / row_ways;
+    p.group_size.assign(p.groups, row_ways);
+    p.images = split_rows(batch, p.groups);
+  } else if (batch >= np) {
+    p.groups = np;
+    p.group_size.assign(np, 1);
+    p.images = split_rows(batch, np);
+  } else {
+    p.groups = batch;
+    p.images = split_rows(batch, batch);  // one image per group
+    for (const RowRange& r : split_rows(np, batch)) p.group_size.push_back(r.size());
+  }
+  int first = 0;
+  for (int g = 0; g < p.groups; ++g) {
+    p.group_first.push_back(first);
+    for (int j = 0; j < p.group_size[g]; ++j) {
+      p.group_of.push_back(g);
+      p.index_in_group.push_back(j);
+    }
+    first += p.group_size[g];
+    p.row_plans.push_back(make_plan(H, W, p.group_size[g], mode, b1, b2));
+  }
+  out = std::move(p);
+  return true;
+}
+
+double conv1_redundancy(const HybridPlan& p) {
+  double rows = 0;
+  for (int g = 0; g < p.groups; ++g) rows += (conv1_redundancy(p.row_plans[g]) + 1.0) * p.images[g].size();
+  return rows / p.batch - 1.0;
+}
+
 }  // namespace anx

@@ -80,8 +80,18 @@ def cmd_launch(a, rest):
 
 
 def cmd_plan(a):
-    from .parallel.plan import make_plan
+    from .parallel.plan import conv1_redundancy, hybrid_conv1_redundancy, make_hybrid_plan, make_plan
+    if a.batch is not None:  # hybrid batch x rows plan
+        hp = make_hybrid_plan(227, 227, a.np, a.batch, a.row_ways, a.decomp)
+        print(f"np {a.np} batch {a.batch}: {hp.groups} group(s); redundant conv1 rows "
+              f"{100 * hybrid_conv1_redundancy(hp):.1f}% of one device's")
+        for r in range(a.np):
+            t, im = hp.tile(r), hp.images_of(r)
+            print(f"rank {r}: group {hp.group_of[r]} ({hp.group_size[hp.group_of[r]]} ranks) images "
+                  f"{im.lo}..{im.hi - 1}  out rows {t.out.lo}..{t.out.hi - 1}  input rows {t.inp.lo}..{t.inp.hi - 1}")
+        return
     p = make_plan(227, 227, a.np, a.decomp)
+    print(f"redundant conv1 rows: {100 * conv1_redundancy(p):.1f}% of one device's")
     for r, t in enumerate(p.tiles):
         print(f"rank {r}: out {t.out.lo}..{t.out.hi - 1}  pool1 {t.p1.lo}..{t.p1.hi - 1}  conv1 {t.c1.lo}..{t.c1.hi - 1}"
               f"  input {t.inp.lo}..{t.inp.hi - 1}  owned input {p.owned_in[r].lo}..{p.owned_in[r].hi - 1}")
@@ -102,6 +112,8 @@ def main(argv=None):
     pp = sub.add_parser("plan")
     pp.add_argument("--np", "-n", type=int, default=4)
     pp.add_argument("--decomp", default="overlap", choices=["overlap", "per_layer"])
+    pp.add_argument("--batch", "-b", type=int, default=None, help="hybrid batch x rows plan for this many images")
+    pp.add_argument("--row-ways", type=int, default=0, help="ranks per image group (0 = auto: batch first)")
     sub.add_parser("bench")
     if argv and argv[0] == "launch":
         a, rest = ap.parse_known_args(argv)

@@ -56,6 +56,9 @@ _SIGS = {
     "anx_default_blocks": (None, [C.POINTER(BlockC), C.POINTER(BlockC)]),
     "anx_make_plan": (_I, [_I, _I, _I, _I, C.POINTER(BlockC), C.POINTER(BlockC), C.POINTER(TileC), C.POINTER(_I),
                            C.POINTER(_I), C.POINTER(XferC), C.POINTER(_I), C.POINTER(XferC), C.POINTER(_I), _I]),
+    "anx_make_hybrid_plan": (_I, [_I, _I, _I, _I, _I, _I, C.POINTER(BlockC), C.POINTER(BlockC), C.POINTER(_I),
+                                  C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), C.POINTER(TileC),
+                                  C.POINTER(C.c_double)]),
     "anx_engine_create": (_I, [C.POINTER(_P), C.POINTER(BlockC), C.POINTER(BlockC), _I, _I, _P, _P, _P, _P, _I, _I]),
     "anx_engine_destroy": (_I, [_P]),
     "anx_engine_forward": (_I, [_P, _P, _I, _P, _P]),

@@ -148,6 +148,67 @@ def make_plan(H: int, W: int, np_: int, mode: str = OVERLAP, b1: BlockSpec = BLO
     return p
 
 
+def conv1_redundancy(p: DecompPlan, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> float:
+    """Conv1 rows computed by all ranks / the image's conv1 rows - 1 (0 = nothing recomputed)."""
+    d = blocks_dims(p.H, p.W, b1, b2)
+    return sum(t.c1.size for t in p.tiles) / d.H1 - 1.0
+
+
+@dataclass
+class HybridPlan:
+    """Batch x rows decomposition (mirror of anx::make_hybrid_plan, csrc/src/plan.cpp): ``groups``
+    groups of contiguous ranks; group g computes images ``images[g]`` row-decomposed over its
+    ``group_size[g]`` ranks by ``row_plans[g]``."""
+    np: int
+    batch: int
+    groups: int
+    images: list
+    group_size: list
+    group_of: list
+    index_in_group: list
+    row_plans: list
+
+    def tile(self, rank: int) -> TilePlan:
+        return self.row_plans[self.group_of[rank]].tiles[self.index_in_group[rank]]
+
+    def images_of(self, rank: int) -> Rows:
+        return self.images[self.group_of[rank]]
+
+    def group_ranks(self, g: int) -> list[int]:
+        first = sum(self.group_size[:g])
+        return list(range(first, first + self.group_size[g]))
+
+
+def make_hybrid_plan(H: int, W: int, np_: int, batch: int, row_ways: int = 0, mode: str = OVERLAP,
+                     b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> HybridPlan:
+    """Split the batch across ranks first, rows only where there are fewer images than ranks
+    (``row_ways=0``), or ``row_ways`` ranks per image group when asked (``row_ways=np``: the
+    reference's pure row split, v2_mpi_only/2.2_scatter_halo/src/main.cpp:100-249)."""
+    if np_ < 1 or batch < 1 or row_ways < 0 or row_ways > np_ or (row_ways and np_ % row_ways):
+        raise ValueError(f"invalid hybrid plan: np={np_} batch={batch} row_ways={row_ways}")
+    if row_ways:
+        groups = np_ // row_ways
+        sizes = [row_ways] * groups
+        images = split_rows(batch, groups)
+    elif batch >= np_:
+        groups, sizes, images = np_, [1] * np_, split_rows(batch, np_)
+    else:
+        groups = batch
+        images = split_rows(batch, batch)
+        sizes = [r.size for r in split_rows(np_, batch)]
+    group_of, index = [], []
+    for g, n in enumerate(sizes):
+        group_of += [g] * n
+        index += list(range(n))
+    plans = [make_plan(H, W, n, mode, b1, b2) for n in sizes]
+    return HybridPlan(np_, batch, groups, images, sizes, group_of, index, plans)
+
+
+def hybrid_conv1_redundancy(p: HybridPlan, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> float:
+    rows = sum((conv1_redundancy(rp, b1, b2) + 1.0) * im.size for rp, im in zip(p.row_plans, p.images))
+    return rows / p.batch - 1.0
+
+
 def full_plan(H: int, W: int, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> TilePlan:
     return make_plan(H, W, 1, OVERLAP, b1, b2).tiles[0]
 

@@ -9,7 +9,8 @@ import torch
 from anx import _native as nat
 from anx.config import blocks
 from anx.models.alexnet_blocks import AlexNetBlocks
-from anx.parallel.plan import OVERLAP, PER_LAYER, Rows, make_plan
+from anx.parallel.plan import (OVERLAP, PER_LAYER, Rows, conv1_redundancy, hybrid_conv1_redundancy,
+                               make_hybrid_plan, make_plan)
 from anx.utils.init import init_input
 
 # pool2 rows -> conv1 input rows (inclusive)
@@ -95,3 +96,80 @@ def test_cpu_per_layer_halo_exchange(np_):
         engines[h.dst].window_put(p.tiles[h.dst], h.rows.lo, rows)
     parts = [engines[r].stage2(1, t) for r, t in enumerate(p.tiles) if not t.out.empty]
     torch.testing.assert_close(torch.cat(parts, dim=1), full, rtol=0, atol=0)
+
+
+# ---------------------------------------------------------------- hybrid batch x rows
+def _native_hybrid(np_, batch, row_ways, mode):
+    b1, b2 = blocks()
+    I = C.c_int
+    groups = I()
+    group, index, gsize = (I * np_)(), (I * np_)(), (I * np_)()
+    img = (I * (2 * np_))()
+    tiles = (nat.TileC * np_)()
+    red = C.c_double()
+    nat.call("anx_make_hybrid_plan", 227, 227, np_, batch, row_ways, 0 if mode == OVERLAP else 1,
+             C.byref(nat.block_c(b1)), C.byref(nat.block_c(b2)), C.byref(groups), group, index, img, gsize, tiles,
+             C.byref(red))
+    return groups.value, list(group), list(index), list(img), list(gsize[:groups.value]), tiles, red.value
+
+
+@pytest.mark.parametrize("mode", [OVERLAP, PER_LAYER])
+@pytest.mark.parametrize("batch", [1, 3, 256, 1024])
+@pytest.mark.parametrize("np_", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_hybrid_plan(np_, batch, mode):
+    """Every image goes to exactly one group, every group's rows cover the image, ranks are used
+    whenever there is work for them, the batch is split before rows, and C++ == Python."""
+    p = make_hybrid_plan(227, 227, np_, batch, 0, mode)
+    assert sum(p.group_size) == np_ and p.groups == min(np_, batch)
+    covered = sorted(i for im in p.images for i in range(im.lo, im.hi))
+    assert covered == list(range(batch))
+    if batch >= np_:
+        assert all(n == 1 for n in p.group_size) and hybrid_conv1_redundancy(p) == 0.0
+        sizes = [im.size for im in p.images]
+        assert max(sizes) - min(sizes) <= 1
+    else:
+        assert all(im.size == 1 for im in p.images) and max(p.group_size) - min(p.group_size) <= 1
+    for g, rp in enumerate(p.row_plans):
+        outs = [t.out for t in rp.tiles if not t.out.empty]
+        assert outs[0].lo == 0 and outs[-1].hi == 13 and all(a.hi == b.lo for a, b in zip(outs, outs[1:]))
+    groups, group, index, img, gsize, tiles, red = _native_hybrid(np_, batch, 0, mode)
+    assert groups == p.groups and gsize == p.group_size and group == p.group_of and index == p.index_in_group
+    for r in range(np_):
+        t, c = p.tile(r), tiles[r]
+        assert (p.images_of(r).lo, p.images_of(r).hi) == (img[2 * r], img[2 * r + 1])
+        assert (t.inp.lo, t.inp.hi, t.out.lo, t.out.hi) == (c.in_lo, c.in_hi, c.out_lo, c.out_hi)
+    assert red == pytest.approx(hybrid_conv1_redundancy(p))
+
+
+@pytest.mark.parametrize("np_,row_ways", [(4, 4), (8, 2), (8, 4), (6, 3)])
+def test_hybrid_forced_row_ways(np_, row_ways):
+    p = make_hybrid_plan(227, 227, np_, 256, row_ways)
+    assert p.groups == np_ // row_ways and set(p.group_size) == {row_ways}
+    assert hybrid_conv1_redundancy(p) == pytest.approx(conv1_redundancy(make_plan(227, 227, row_ways)))
+    with pytest.raises(ValueError):
+        make_hybrid_plan(227, 227, 8, 16, 3)
+
+
+def test_redundancy_values():
+    """Overlap tiles recompute conv1 rows under the halos: 0 at np=1, growing with np."""
+    r = [conv1_redundancy(make_plan(227, 227, n)) for n in (1, 2, 4, 8)]
+    assert r[0] == 0.0 and r[1] < r[2] < r[3]
+    assert conv1_redundancy(make_plan(227, 227, 8, PER_LAYER)) < r[3]
+
+
+@pytest.mark.parametrize("np_,batch", [(3, 2), (8, 3), (5, 7)])
+def test_cpu_hybrid_reproduces_single_device(np_, batch):
+    """Every rank's (images x rows) part, computed on the host engine and assembled, equals the
+    single-device output bit for bit."""
+    m = AlexNetBlocks(device="cpu", init="rand", seed=13)
+    x = init_input(batch, "rand", seed=13)
+    full = m(x)
+    p = make_hybrid_plan(227, 227, np_, batch)
+    out = torch.full_like(full, float("nan"))
+    for r in range(np_):
+        t, im = p.tile(r), p.images_of(r)
+        if t.out.empty or im.empty:
+            continue
+        y = m.tile_forward(x[im.lo:im.hi, t.inp.lo:t.inp.hi].contiguous(), t)
+        out[im.lo:im.hi, t.out.lo:t.out.hi] = y
+    torch.testing.assert_close(out, full, rtol=0, atol=0)
