@@ -31,6 +31,8 @@ struct Knobs {
   int force_vec4 = -1;     // conv_mfma tile variant override for Cg % 4 == 0 convs (-1 = heuristic)
   int force_scalar = -1;   // conv_mfma tile variant override for scalar-gather convs
   int bf16_glds = 2;       // bf16 full model: 0 register-staged, 2 / 3 LDS-DMA ring slots
+  int conv1_occ = 0;       // cap on Conv1 Winograd GEMM workgroups per CU (0 = natural: 4), by LDS padding,
+  int conv2_occ = 0;       // ... and Conv2's (natural 2): leaves room for a concurrent lane's kernels
 };
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CONV1_WINO_CFG,

@@ -139,6 +139,10 @@ bool conv1_wino_cfg_valid(int cfg);
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
                       bool relu, hipStream_t s, const Knobs& k);
 
+// Dynamic LDS bytes that cap a kernel at `wgs` workgroups per CU (160 KiB LDS per CU): the larger of
+// `natural` and just over 160 KiB / (wgs + 1). wgs <= 0: `natural`.
+size_t occupancy_lds(size_t natural, int wgs);
+
 // Vectorised NHWC max-pool writing through an OutView (C % 4 == 0 required for the fast path).
 hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, OutView out, hipStream_t s);
 // Fused max-pool + cross-channel LRN (block 2 tail).

@@ -701,7 +701,18 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
     case 2: return launch_gemm<16, 6>(a, s, sf);
     case 3: return launch_gemm<16, 8>(a, s, sf);
     case 4: {  // 16x16 MFMA, 64-tile workgroups, 4 workgroups per CU
-      constexpr size_t lds_bytes = 2 * (kBM16 + kBN) * kCh * sizeof(float);
+      const size_t lds_bytes = occupancy_lds(2 * (kBM16 + kBN) * kCh * sizeof(float), kn.conv1_occ);
+      static const hipError_t attr = [] {
+        for (const void* f : {reinterpret_cast<const void*>(conv1_wino_gemm16_kernel<true, true>),
+                              reinterpret_cast<const void*>(conv1_wino_gemm16_kernel<true, false>),
+                              reinterpret_cast<const void*>(conv1_wino_gemm16_kernel<false, true>),
+                              reinterpret_cast<const void*>(conv1_wino_gemm16_kernel<false, false>)}) {
+          const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+      }();
+      if (attr != hipSuccess) return attr;
       GemmArgs b = a;
       b.n_ptiles = (a.P + kBM16 - 1) / kBM16;
       const dim3 grid((b.n_ptiles + 7) / 8 * 8 * b.n_ntiles);

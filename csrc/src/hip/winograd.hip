@@ -903,13 +903,13 @@ hipError_t launch_glds16(FusedArgs a, hipStream_t s) {
 }
 
 template <int BK, bool XCD, bool IL = false, bool SF = false>
-hipError_t launch_glds(const FusedArgs& a, dim3 grid, hipStream_t s) {
-  constexpr int kLds = 3 * 2 * kFB * BK * sizeof(float);  // 3-slot ring of A|B tiles
+hipError_t launch_glds(const FusedArgs& a, dim3 grid, hipStream_t s, int occ) {
+  const size_t lds = occupancy_lds(3 * 2 * kFB * BK * sizeof(float), occ);  // 3-slot ring of A|B tiles
   static const hipError_t attr = hipFuncSetAttribute(
       reinterpret_cast<const void*>(wino_fused_glds_kernel<BK, XCD, IL, SF>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
-  wino_fused_glds_kernel<BK, XCD, IL, SF><<<grid, 256, kLds, s>>>(a);
+  wino_fused_glds_kernel<BK, XCD, IL, SF><<<grid, 256, lds, s>>>(a);
   return hipGetLastError();
 }
 
@@ -1013,7 +1013,7 @@ hipError_t wino_input_pool(const WinoPlan& w, const float* c1, const WinoPoolGeo
 
 hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
                       hipStream_t s, const Knobs& kn) {
-  const int cfg = kn.wino_cfg, prio = kn.wino_prio;
+  const int cfg = kn.wino_cfg, prio = kn.wino_prio, occ = kn.conv2_occ;
   const bool sf = (kn.fold_scalar & 2) != 0;
   FusedArgs a{};
   a.V = V;
@@ -1052,12 +1052,14 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
       const dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
       if (bk == 48 && xcd) {  // the interleaved fold needs exactly 2 K slices per point (C = 96)
         if ((prio & 256) && a.kpad == 96)
-          return sf ? launch_glds<48, true, true, true>(a, grid, s) : launch_glds<48, true, true, false>(a, grid, s);
-        return sf ? launch_glds<48, true, false, true>(a, grid, s) : launch_glds<48, true, false, false>(a, grid, s);
+          return sf ? launch_glds<48, true, true, true>(a, grid, s, occ)
+                    : launch_glds<48, true, true, false>(a, grid, s, occ);
+        return sf ? launch_glds<48, true, false, true>(a, grid, s, occ)
+                  : launch_glds<48, true, false, false>(a, grid, s, occ);
       }
-      if (bk == 48) return launch_glds<48, false>(a, grid, s);
-      if (xcd) return launch_glds<32, true>(a, grid, s);
-      return launch_glds<32, false>(a, grid, s);
+      if (bk == 48) return launch_glds<48, false>(a, grid, s, occ);
+      if (xcd) return launch_glds<32, true>(a, grid, s, occ);
+      return launch_glds<32, false>(a, grid, s, occ);
     }
   }
   const int bk = (a.kpad % 48 == 0 && cfg & 1) ? 48 : 32;

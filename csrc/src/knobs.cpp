@@ -32,6 +32,8 @@ const Field kFields[] = {
     {"force_vec4", &Knobs::force_vec4, nullptr, -1, 255, nullptr},
     {"force_scalar", &Knobs::force_scalar, nullptr, -1, 255, nullptr},
     {"bf16_glds", &Knobs::bf16_glds, nullptr, 0, 3, "ANX_BF16_GLDS"},
+    {"conv1_occ", &Knobs::conv1_occ, nullptr, 0, 8, "ANX_CONV1_OCC"},
+    {"conv2_occ", &Knobs::conv2_occ, nullptr, 0, 8, "ANX_CONV2_OCC"},
 };
 
 const Field* find(const char* name) {
@@ -88,5 +90,13 @@ bool use_winograd(ConvAlgo a, int n, int rows, int full_rows) {
   if (a != ConvAlgo::Auto) return true;
   return static_cast<long>(n) * rows > static_cast<long>(kAutoDirectImages) * full_rows;
 }
+
+namespace hip {
+size_t occupancy_lds(size_t natural, int wgs) {
+  if (wgs <= 0) return natural;
+  const size_t cap = 160 * 1024 / static_cast<size_t>(wgs + 1) + 1024;
+  return natural > cap ? natural : cap;
+}
+}  // namespace hip
 
 }  // namespace anx

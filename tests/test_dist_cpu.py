@@ -119,6 +119,67 @@ def test_prefetch_pipeline_input_semantics():
         torch.testing.assert_close(ys[k].view_as(ref), ref, rtol=0, atol=0)
 
 
+def _workload_worker(rank, world, port, q, version, decomp, batch):
+    sys.path.insert(0, ROOT)
+    import anx  # noqa: F401
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.parallel.workloads import RowsWorkload
+    from anx.utils.init import init_input
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    m = AlexNetBlocks(init="rand", seed=4, device="cpu")
+    wl = RowsWorkload(m, batch, version, decomp, device="cpu")
+    wl.fill(init_input(batch, "rand", seed=4))
+    wl.step()
+    wl.step()  # steady state: buffers reused
+    if rank == 0:
+        q.put(wl.output().clone())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("version,decomp,world,batch", [
+    ("v5", "rows", 2, 2), ("v5", "rows", 3, 1), ("v5", "hybrid", 4, 3), ("v4", "rows", 2, 2),
+    ("v4", "hybrid", 3, 2), ("v5", "batch", 2, 3)])
+def test_rows_workload_gloo(version, decomp, world, batch):
+    """bench.py's V4/V5 workloads (scatter -> tiles [-> pool1 halos] -> gather) on CPU ranks
+    reproduce the single-process output bit for bit (host engine: direct convolutions)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_workload_worker, args=(r, world, port, q, version, decomp, batch))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    y = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, ROOT)
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.utils.init import init_input
+    ref = AlexNetBlocks(init="rand", seed=4, device="cpu")(init_input(batch, "rand", seed=4))
+    torch.testing.assert_close(y, ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("workload", ["v4", "v5"])
+def test_bench_workload_contract_gloo(workload):
+    """bench.py --workload v4|v5 at N=2 (gloo/CPU rehearsal): one JSON line, strong scaling, phases."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "1", "--warmup", "0", "--workload", workload, "--batch", "2", "--device", "cpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["scaling"] == "strong" and rec["config"]["global_batch"] == 2 and rec["value"] > 0
+    assert rec["config"]["workload"] == workload and rec["config"]["parallelism"] == f"{workload}-rows2"
+
+
 def test_bench_contract_gloo():
     """bench.py under torch.distributed.run (gloo/CPU rehearsal) prints ONE valid JSON line on rank 0."""
     port = free_port()
