@@ -8,6 +8,7 @@
 #include <string>
 
 #include "anx/rng.hpp"
+#include "anx/trace.hpp"
 
 #define ANX_TRY(expr)                          \
   do {                                         \
@@ -131,6 +132,7 @@ float* BlocksEngine::q2_row_ptr(const TilePlan& t, int n, int r) {
 }
 
 hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s) {
+  RoctxRange rx("anx conv1");
   const ConvSpec& k1 = b1_.conv;
   const hip::OutView c1v{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0};
   if (impl_ == Impl::Mfma && wv1_ != nullptr && use_winograd(k_.conv1_algo, n, t.c1.size(), d_.H1)) {
@@ -170,6 +172,7 @@ hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStr
   for (int n0 = 0; n0 < N; n0 += chunk) {
     const int n = std::min(chunk, N - n0);
     ANX_TRY(conv1_chunk(x + n0 * in_img, n, t, s));
+    RoctxRange rx("anx pool1");
     ANX_TRY(hip::maxpool(c1_, n, t.c1.size(), d_.W1, d_.C1, b1_.pool.F, b1_.pool.S,
                          hip::OutView{q2_ + n0 * q_img, t.q.size(), wq_, d_.C1, t.p1.lo - t.q.lo, b2_.conv.P, 0}, s));
   }
@@ -179,6 +182,7 @@ hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStr
 // Conv2 (+ReLU) and Pool2(+LRN) of n images. qc: their conv2 input window; nullptr = pool1 fused
 // into the Winograd input transform, reading the conv1 rows in c1_ (conv1_chunk just wrote them).
 hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, float* yc, hipStream_t s) {
+  RoctxRange rx("anx conv2+pool2+lrn");
   const ConvSpec& k2 = b2_.conv;
   const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(k_.conv2_algo, n, t.c2.size(), d_.H2);
   if (!qc && !wino) return hipErrorInvalidValue;

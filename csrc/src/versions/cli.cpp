@@ -33,6 +33,8 @@
 #include "anx/engine.hpp"
 #include "anx/plan.hpp"
 #include "anx/rng.hpp"
+#include "anx/schedule.hpp"
+#include "anx/trace.hpp"
 
 using namespace anx;
 
@@ -50,7 +52,9 @@ struct Options {
   std::string impl = "mfma";
   std::string conv2_algo = "auto";  // auto | direct | winograd
   std::string conv1_algo = "auto";  // auto | direct | winograd
-  std::string transport = "auto";   // v5 device traffic: auto | rccl | peer (IPC + hipMemcpyPeerAsync)
+  std::string transport = "auto";   // v5 device traffic: auto | rccl | peer (IPC + hipMemcpy2DAsync)
+  std::string split = "rows";       // v5 decomposition: rows (reference) | hybrid (batch first) | batch
+  bool dry_run = false;             // v5: print the transfer schedule (record-only transports, no GPU)
   bool check = false;
   bool json = true;
   std::string weights;  // directory with raw fp32 w1/b1/w2/b2 .bin (overrides --init for weights)
@@ -62,7 +66,7 @@ struct Options {
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
                "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd]\n"
                "           [--conv1-algo auto|direct|winograd] [--transport auto|rccl|peer] [--check]\n"
-               "           [--weights DIR] [--no-json]\n",
+               "           [--split rows|hybrid|batch] [--dry-run] [--weights DIR] [--no-json]\n",
                msg);
   std::exit(2);
 }
@@ -87,6 +91,8 @@ Options parse(int argc, char** argv) {
     else if (a == "--conv2-algo") o.conv2_algo = val();
     else if (a == "--conv1-algo") o.conv1_algo = val();
     else if (a == "--transport") o.transport = val();
+    else if (a == "--split") o.split = val();
+    else if (a == "--dry-run") o.dry_run = true;
     else if (a == "--check") o.check = true;
     else if (a == "--no-json") o.json = false;
     else if (a == "--weights") o.weights = val();
@@ -98,6 +104,7 @@ Options parse(int argc, char** argv) {
   if (o.lrn.empty()) o.lrn = (o.version == "v1" || o.version == "v2.1" || o.version == "v2.2") ? "div_n" : "raw";
   if (o.decomp.empty()) o.decomp = o.version == "v5" ? "per_layer" : "overlap";
   if (o.batch < 1) usage("--batch must be >= 1");
+  if (o.split != "rows" && o.split != "hybrid" && o.split != "batch") usage("bad --split");
   return o;
 }
 
@@ -439,6 +446,7 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
   auto step = [&](Phases& ph) {
     // scatter owned input rows (Scatterv, M9)
     double q = now_ms();
+    roctx_push("v4 scatter");
     if (rank == 0) {
       for (int r = 0; r < np; ++r) {
         const RowRange o = plan.owned_in[r];
@@ -452,9 +460,11 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
       c.irecv(own_buf.data(), own_buf.size() * 4, 0);
     }
     c.wait_all();
+    roctx_pop();
     ph.add("scatter", now_ms() - q);
     // input halo exchange (M10/M12) — planner transfers, both directions in one group
     q = now_ms();
+    roctx_push("v4 halo_in");
     hbufs.clear();
     std::vector<std::pair<RowRange, float*>> recvs;
     for (const HaloXfer& h : plan.in_halos) {
@@ -483,10 +493,12 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
         copy_rows(tile_in.data(), t.in.size(), rv.first.lo - t.in.lo, rv.second, rv.first.size(), 0,
                   rv.first.size(), s.in_row, N, false, nullptr);
     }
+    roctx_pop();
     ph.add("halo", now_ms() - q);
     // compute (V4: host -> device -> host around the tile, pinned buffers)
     if (!t.out.empty()) {
       if (gpu) {
+        RoctxRange rc("v4 h2d+compute+d2h");
         q = now_ms();
         std::memcpy(h_in, tile_in.data(), tile_in.size() * 4);
         hip_check(hipMemcpyAsync(d_in, h_in, tile_in.size() * 4, hipMemcpyHostToDevice, st), "H2D");
@@ -517,6 +529,7 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
     }
     // gather output rows (Gatherv, M16)
     q = now_ms();
+    RoctxRange rg("v4 gather");
     if (rank == 0) {
       for (int r = 1; r < np; ++r) {
         const RowRange o = plan.tiles[r].out;
@@ -553,65 +566,54 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
   return 0;
 }
 
-// ------------------------------------------------------------------------------ V5 (device-resident RCCL)
-// ---- V5 peer transport: every device byte moves by hipMemcpyPeerAsync straight into the
-// destination rank's buffer (scatter rows into its input rows, input halos into its tile, pool1
-// halos into its conv2 window, output rows into rank 0's result), through IPC-mapped allocations
-// (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles exchanged over the host comm). The writer
-// pushes on its own copy stream; a host barrier after each phase orders the pushes against the
-// readers. No host staging and no RCCL, so ranks may also share a GPU (the peer copy is then a
-// same-device copy) — the configuration the one-GPU test box can run.
-struct PeerMap {
-  std::vector<float*> ptr;  // every rank's buffer, mapped into this process (own: the original)
-  std::vector<void*> opened;
-  void close() {
-    for (void* p : opened) (void)hipIpcCloseMemHandle(p);
-    opened.clear();
-  }
-  ~PeerMap() { close(); }
-};
-
-// Share `mine` (a hipMalloc base pointer, or nullptr) of every rank, or only of `root` if >= 0.
-void ipc_share(HostComm& c, float* mine, PeerMap& m, int root = -1) {
-  const int np = c.size(), rank = c.rank();
-  m.ptr.assign(np, nullptr);
-  for (int r = 0; r < np; ++r) {
-    if (root >= 0 && r != root) continue;
-    hipIpcMemHandle_t h{};
-    if (r == rank) hip_check(hipIpcGetMemHandle(&h, mine), "hipIpcGetMemHandle");
-    c.bcast(&h, sizeof h, r);
-    if (r == rank) {
-      m.ptr[r] = mine;
-    } else {
-      void* p = nullptr;
-      hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-      m.opened.push_back(p);
-      m.ptr[r] = static_cast<float*>(p);
-    }
-  }
-}
-
-// Copy `nrows` rows of N images from (src, src_dev) to (dst, dst_dev), row windows as copy_rows():
-// one hipMemcpyPeerAsync per image (the images are strided differently on both sides).
-void peer_rows(float* dst, int dst_dev, int dst_rows, int dst_off, const float* src, int src_dev, int src_rows,
-               int src_off, int nrows, size_t row_floats, int N, hipStream_t s) {
-  if (nrows <= 0 || N <= 0) return;
-  const size_t w = static_cast<size_t>(nrows) * row_floats * sizeof(float);
-  const size_t dp = static_cast<size_t>(dst_rows) * row_floats * sizeof(float);
-  const size_t sp = static_cast<size_t>(src_rows) * row_floats * sizeof(float);
-  char* d = reinterpret_cast<char*>(dst + static_cast<size_t>(dst_off) * row_floats);
-  const char* q = reinterpret_cast<const char*>(src + static_cast<size_t>(src_off) * row_floats);
-  for (int n = 0; n < N; ++n)
-    hip_check(hipMemcpyPeerAsync(d + n * dp, dst_dev, q + n * sp, src_dev, w, s), "hipMemcpyPeerAsync");
-}
-
-int run_v5_peer(Setup& s, HostComm& c, int ndev) {
+// ------------------------------------------------------------------------------ V5 (device-resident)
+// One transfer schedule per step (anx/schedule.hpp: scatter of images x input rows, pool1 halos
+// inside each row group, gather of output rows), executed by a pluggable transport:
+//   rccl  grouped ncclSend/ncclRecv over xGMI (one GPU per rank),
+//   peer  one hipMemcpy2DAsync per transfer into the receiver's IPC-mapped buffer, IPC events for
+//         ordering (ranks may share a GPU: the configuration the one-GPU test box can run).
+// Steady-state steps never synchronise a stream with the host: compute, copies and RCCL are
+// ordered by events; Tile / Y / YFull alternate by step parity so a step's pushes never land in a
+// buffer the previous step still reads. Phase times come from events on the compute stream (the
+// time that stream spent in or waiting for each phase). --dry-run prints the schedule each rank's
+// transport would execute (record-only, no GPU) as ANX_SCHEDULE lines.
+int run_v5(Setup& s, HostComm& c, bool dry) {
   const int N = s.o.batch, rank = c.rank(), np = c.size();
   const Decomp mode = s.o.decomp == "overlap" ? Decomp::Overlap : Decomp::PerLayer;
-  const DecompPlan plan = make_plan(s.d.H, s.d.W, np, mode, s.b1, s.b2);
-  const TilePlan& t = plan.tiles[rank];
-  const RowRange own = plan.owned_in[rank];
-  const int dev = s.ri.local_rank % ndev;
+  const int row_ways = s.o.split == "rows" ? np : s.o.split == "batch" ? 1 : 0;
+  HybridPlan hp;
+  if (!make_hybrid_plan(s.d.H, s.d.W, np, N, row_ways, mode, hp, s.b1, s.b2))
+    throw std::runtime_error("invalid plan for --split " + s.o.split);
+  const TilePlan& t = hp.tile(rank);
+  const RowRange im = hp.images[hp.group_of[rank]];
+  const int n = t.out.empty() ? 0 : im.size();
+  const size_t win_row = static_cast<size_t>(s.d.Wp1 + 2 * s.b2.conv.P) * s.d.C1 * 4;
+  const Schedule sched = make_step_schedule(hp, {s.in_row * 4, s.out_row * 4, win_row, s.d.H, s.d.Hp2});
+  int ndev = 0;
+  if (!dry) {
+    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (ndev < 1) throw std::runtime_error("v5 needs a GPU");
+  }
+  const std::string tr = s.o.transport == "auto" ? (!dry && np > ndev ? "peer" : "rccl") : s.o.transport;
+  if (tr != "rccl" && tr != "peer") throw std::runtime_error("--transport must be auto, rccl or peer");
+  if (tr == "rccl" && !dry && np > ndev)
+    throw std::runtime_error("v5 over RCCL needs one GPU per rank (use --transport peer to share)");
+  const int dev = dry ? 0 : s.ri.local_rank % ndev;
+  std::unique_ptr<Transport> x = tr == "rccl" ? make_rccl_transport(c, dev, rank) : make_peer_transport(c, dev, rank);
+  constexpr int kB = static_cast<int>(BufId::kCount);
+  if (dry) {  // the schedule this rank's transport would execute, one step
+    x->record_only = true;
+    void* none[2][kB] = {};
+    x->bind(sched, none, nullptr);
+    for (int ph = 0; ph < 3; ++ph) x->run_phase(static_cast<Phase>(ph), sched.phase[ph], nullptr, 0);
+    for (int r = 0; r < np; ++r) {
+      if (r == rank)
+        for (const std::string& l : x->log()) std::printf("ANX_SCHEDULE %s rank %d: %s\n", x->name(), rank, l.c_str());
+      std::fflush(stdout);
+      c.barrier();
+    }
+    return 0;
+  }
   hip_check(hipSetDevice(dev), "hipSetDevice");
   Phases cold, warm;
   c.barrier();
@@ -619,310 +621,121 @@ int run_v5_peer(Setup& s, HostComm& c, int ndev) {
   double a = now_ms();
   if (rank == 0) fill_input(s);
   bcast_weights(c, s.w);
-  std::vector<int> devs(np, 0);
-  for (int r = 0; r < np; ++r) {
-    int d = dev;
-    c.bcast(&d, sizeof d, r);
-    devs[r] = d;
-  }
-  hipStream_t st, cs;
-  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
-  hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
-  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
-  auto dalloc = [](size_t n) {
-    float* p = nullptr;
-    hip_check(hipMalloc(&p, std::max<size_t>(1, n) * 4), "hipMalloc");
-    return p;
-  };
-  float* d_x = rank == 0 ? dalloc(s.x.size()) : nullptr;
-  float* d_own = dalloc(static_cast<size_t>(N) * std::max(1, own.size()) * s.in_row);
-  float* d_tile = dalloc(static_cast<size_t>(N) * std::max(1, t.in.size()) * s.in_row);
-  float* d_y = dalloc(static_cast<size_t>(N) * std::max(1, t.out.size()) * s.out_row);
-  float* d_yfull = rank == 0 ? dalloc(static_cast<size_t>(N) * s.d.Hp2 * s.out_row) : nullptr;
-  // the conv2 window exists once stage1 has run on this tile geometry: run it once on zeros
-  if (!t.out.empty()) {
-    hip_check(hipMemsetAsync(d_tile, 0, static_cast<size_t>(N) * t.in.size() * s.in_row * 4, st), "memset");
-    hip_check(eng.stage1(d_tile, N, t, st), "stage1");
-  }
-  hip_check(hipStreamSynchronize(st), "sync");
-  PeerMap m_own, m_tile, m_win, m_out;
-  ipc_share(c, d_own, m_own);
-  ipc_share(c, d_tile, m_tile);
-  ipc_share(c, t.out.empty() ? d_tile : eng.q2_row_ptr(t, 0, t.q.lo), m_win);  // window base = allocation base
-  ipc_share(c, d_yfull, m_out, 0);
-  if (rank == 0)
-    hip_check(hipMemcpy(d_x, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice), "H2D input");
-  std::vector<float> y_host(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
-  hip_check(hipDeviceSynchronize(), "sync");
-  c.barrier();
-  cold.add("setup", now_ms() - a);
-  const size_t rowf = eng.q2_row_floats();
-
-  auto phase_end = [&](hipStream_t q) {  // this rank's pushes landed, then everyone's
-    hip_check(hipStreamSynchronize(q), "sync");
-    c.barrier();
-  };
-  auto step = [&](Phases& ph) {
-    // scatter: rank 0 pushes each rank's owned input rows into that rank's d_own
-    double q = now_ms();
-    if (rank == 0)
-      for (int r = 0; r < np; ++r) {
-        const RowRange o = plan.owned_in[r];
-        if (!o.empty())
-          peer_rows(m_own.ptr[r], devs[r], o.size(), 0, d_x, dev, s.d.H, o.lo, o.size(), s.in_row, N, cs);
-      }
-    phase_end(cs);
-    ph.add("scatter", now_ms() - q);
-    // input halos: the owner pushes rows into the neighbour's tile; own rows locally
-    q = now_ms();
-    for (const HaloXfer& h : plan.in_halos)
-      if (h.src == rank) {
-        const TilePlan& td = plan.tiles[h.dst];
-        peer_rows(m_tile.ptr[h.dst], devs[h.dst], td.in.size(), h.rows.lo - td.in.lo, d_own, dev, own.size(),
-                  h.rows.lo - own.lo, h.rows.size(), s.in_row, N, cs);
-      }
-    if (!t.out.empty()) {
-      const int lo = std::max(own.lo, t.in.lo), up = std::min(own.hi, t.in.hi);
-      copy_rows(d_tile, t.in.size(), lo - t.in.lo, d_own, own.size(), lo - own.lo, up - lo, s.in_row, N, true, cs);
-    }
-    phase_end(cs);
-    ph.add("halo_in", now_ms() - q);
-    q = now_ms();
-    if (!t.out.empty()) hip_check(eng.stage1(d_tile, N, t, st), "stage1");
-    phase_end(st);  // every window holds its own pool1 rows before any neighbour writes halos
-    ph.add("compute", now_ms() - q);
-    // pool1 halos: the producer pushes rows from its window into the neighbour's window
-    q = now_ms();
-    if (mode == Decomp::PerLayer) {
-      for (const HaloXfer& h : plan.p1_halos)
-        if (h.src == rank) {
-          const TilePlan& td = plan.tiles[h.dst];
-          peer_rows(m_win.ptr[h.dst], devs[h.dst], td.q.size(), h.rows.lo - td.q.lo, eng.q2_row_ptr(t, 0, t.q.lo),
-                    dev, t.q.size(), h.rows.lo - t.q.lo, h.rows.size(), rowf, N, cs);
-        }
-      phase_end(cs);
-    }
-    ph.add("halo_p1", now_ms() - q);
-    q = now_ms();
-    if (!t.out.empty()) hip_check(eng.stage2(N, t, d_y, st), "stage2");
-    hip_check(hipStreamSynchronize(st), "sync");
-    ph.add("compute", now_ms() - q);
-    // gather: every rank pushes its output rows into rank 0's full result
-    q = now_ms();
-    if (!t.out.empty())
-      peer_rows(m_out.ptr[0], devs[0], s.d.Hp2, t.out.lo, d_y, dev, t.out.size(), 0, t.out.size(), s.out_row, N, cs);
-    phase_end(cs);
-    if (rank == 0) {
-      hip_check(hipMemcpyAsync(y_host.data(), d_yfull, y_host.size() * 4, hipMemcpyDeviceToHost, cs), "D2H");
-      hip_check(hipStreamSynchronize(cs), "sync");
-    }
-    ph.add("gather", now_ms() - q);
-  };
-  step(cold);
-  double cold_ms = now_ms() - t0;
-  for (int i = 0; i < s.o.iters; ++i) step(warm);
-  double tm[2] = {cold_ms, s.o.iters ? warm.total() / s.o.iters : 0};
-  c.allreduce_max(tm, 2);
-  if (rank == 0) report(s, np, y_host, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y_host) : -1);
-  c.barrier();  // nobody writes into a peer's buffers any more: unmap, then free
-  for (PeerMap* m : {&m_own, &m_tile, &m_win, &m_out}) m->close();
-  c.barrier();  // every peer has unmapped this rank's buffers before they are freed
-  for (float* p : {d_x, d_own, d_tile, d_y, d_yfull})
-    if (p) (void)hipFree(p);
-  (void)hipStreamDestroy(st);
-  (void)hipStreamDestroy(cs);
-  c.barrier();
-  return 0;
-}
-
-int run_v5(Setup& s, HostComm& c) {
-  const int N = s.o.batch, rank = c.rank(), np = c.size();
-  const Decomp mode = s.o.decomp == "overlap" ? Decomp::Overlap : Decomp::PerLayer;
-  const DecompPlan plan = make_plan(s.d.H, s.d.W, np, mode, s.b1, s.b2);
-  const TilePlan& t = plan.tiles[rank];
-  const RowRange own = plan.owned_in[rank];
-  int ndev = 0;
-  hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
-  if (ndev < 1) throw std::runtime_error("v5 needs a GPU");
-  const std::string tr = s.o.transport == "auto" ? (np <= ndev ? "rccl" : "peer") : s.o.transport;
-  if (tr == "peer") return run_v5_peer(s, c, ndev);
-  if (tr != "rccl") throw std::runtime_error("--transport must be auto, rccl or peer");
-  if (np > ndev) throw std::runtime_error("v5 over RCCL needs one GPU per rank (use --transport peer to share)");
-  const int dev = s.ri.local_rank % ndev;
-  Phases cold, warm;
-  c.barrier();
-  const double t0 = now_ms();
-  double a = now_ms();
-  if (rank == 0) fill_input(s);
-  bcast_weights(c, s.w);
-  DeviceComm dc(c, dev);
   hipStream_t st;
   hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
-  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
-  auto dalloc = [](size_t n) {
+  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, std::max(1, n), s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
+  auto dalloc = [](size_t floats) {
     float* p = nullptr;
-    hip_check(hipMalloc(&p, std::max<size_t>(1, n) * 4), "hipMalloc");
+    hip_check(hipMalloc(&p, std::max<size_t>(1, floats) * 4), "hipMalloc");
     return p;
   };
   float* d_x = rank == 0 ? dalloc(s.x.size()) : nullptr;
-  float* d_own = dalloc(static_cast<size_t>(N) * own.size() * s.in_row);
-  float* d_tile = dalloc(static_cast<size_t>(N) * t.in.size() * s.in_row);
-  float* d_y = dalloc(static_cast<size_t>(N) * t.out.size() * s.out_row);
-  float* d_yfull = rank == 0 ? dalloc(static_cast<size_t>(N) * s.d.Hp2 * s.out_row) : nullptr;
-  std::vector<float*> d_stage(np, nullptr);
-  if (rank == 0)
-    for (int r = 1; r < np; ++r) {
-      const size_t in_n = static_cast<size_t>(N) * plan.owned_in[r].size() * s.in_row;
-      const size_t out_n = static_cast<size_t>(N) * plan.tiles[r].out.size() * s.out_row;
-      d_stage[r] = dalloc(std::max(in_n, out_n));
-    }
-  // halo buffers (input rows and pool1 window rows), sized for the largest transfer
-  size_t hmax = 1;
-  for (auto& h : plan.in_halos) hmax = std::max(hmax, static_cast<size_t>(N) * h.rows.size() * s.in_row);
-  for (auto& h : plan.p1_halos) hmax = std::max(hmax, static_cast<size_t>(N) * h.rows.size() * eng.q2_row_floats());
-  std::vector<float*> d_halo;
-  for (size_t i = 0; i < plan.in_halos.size() + plan.p1_halos.size(); ++i) d_halo.push_back(dalloc(hmax));
-  if (rank == 0)
-    hip_check(hipMemcpy(d_x, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice), "H2D input");
-  std::vector<float> y_host(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
+  float *d_tile[2], *d_y[2], *d_yfull[2] = {nullptr, nullptr};
+  for (int p = 0; p < 2; ++p) {
+    d_tile[p] = dalloc(static_cast<size_t>(n) * t.in.size() * s.in_row);
+    d_y[p] = dalloc(static_cast<size_t>(n) * t.out.size() * s.out_row);
+    if (rank == 0) d_yfull[p] = dalloc(static_cast<size_t>(N) * s.d.Hp2 * s.out_row);
+  }
+  // the conv2 window exists once stage1 has run on this tile geometry: run it once on zeros
+  float* d_win = nullptr;
+  if (n) {
+    hip_check(hipMemsetAsync(d_tile[0], 0, static_cast<size_t>(n) * t.in.size() * s.in_row * 4, st), "memset");
+    hip_check(eng.stage1(d_tile[0], n, t, st), "stage1");
+    d_win = eng.q2_row_ptr(t, 0, t.q.lo);
+  }
+  if (rank == 0) hip_check(hipMemcpy(d_x, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice), "H2D input");
   hip_check(hipDeviceSynchronize(), "sync");
+  void* bufs[2][kB];
+  for (int p = 0; p < 2; ++p) {
+    bufs[p][static_cast<int>(BufId::X)] = d_x;
+    bufs[p][static_cast<int>(BufId::Tile)] = d_tile[p];
+    bufs[p][static_cast<int>(BufId::Win)] = d_win;
+    bufs[p][static_cast<int>(BufId::Y)] = d_y[p];
+    bufs[p][static_cast<int>(BufId::YFull)] = d_yfull[p];
+  }
+  x->bind(sched, bufs, st);
+  c.barrier();
   cold.add("setup", now_ms() - a);
-  hipStream_t cs = dc.stream();
-
-  auto sync_all = [&]() {
-    hip_check(hipStreamSynchronize(cs), "sync");
-    hip_check(hipStreamSynchronize(st), "sync");
+  std::vector<float> y_host(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
+  const char* names[5] = {"scatter", "compute", "halo_p1", "compute", "gather"};
+  constexpr int kEv = 6;
+  auto step = [&](int k, hipEvent_t* ev) {
+    const int par = k & 1;
+    hip_check(hipEventRecord(ev[0], st), "event");
+    RoctxRange r0("v5 scatter");
+    x->run_phase(Phase::Scatter, sched.phase[0], st, par);
+    hip_check(hipEventRecord(ev[1], st), "event");
+    if (n && mode == Decomp::PerLayer) {
+      RoctxRange r1("v5 stage1");
+      hip_check(eng.stage1(d_tile[par], n, t, st), "stage1");
+    }
+    hip_check(hipEventRecord(ev[2], st), "event");
+    {
+      RoctxRange r2("v5 halo_p1");
+      x->run_phase(Phase::P1Halo, sched.phase[1], st, par);
+    }
+    hip_check(hipEventRecord(ev[3], st), "event");
+    if (n) {
+      RoctxRange r3("v5 stage2");
+      if (mode == Decomp::PerLayer)
+        hip_check(eng.stage2(n, t, d_y[par], st), "stage2");
+      else
+        hip_check(eng.tile_forward(d_tile[par], n, t, d_y[par], st), "tile_forward");
+    }
+    hip_check(hipEventRecord(ev[4], st), "event");
+    {
+      RoctxRange r4("v5 gather");
+      x->run_phase(Phase::Gather, sched.phase[2], st, par);
+    }
+    hip_check(hipEventRecord(ev[5], st), "event");
+    x->end_step(st);
   };
-  auto step = [&](Phases& ph) {
-    // scatter owned rows: root packs per destination on device, grouped ncclSend/Recv
-    double q = now_ms();
-    dc.after(st);
-    if (rank == 0) {
-      for (int r = 0; r < np; ++r) {
-        const RowRange o = plan.owned_in[r];
-        if (o.empty()) continue;
-        copy_rows(r == 0 ? d_own : d_stage[r], o.size(), 0, d_x, s.d.H, o.lo, o.size(), s.in_row, N, true, cs);
-      }
-    }
-    dc.group_start();
-    if (rank == 0) {
-      for (int r = 1; r < np; ++r)
-        if (!plan.owned_in[r].empty())
-          dc.send(d_stage[r], static_cast<size_t>(N) * plan.owned_in[r].size() * s.in_row * 4, r);
-    } else if (!own.empty()) {
-      dc.recv(d_own, static_cast<size_t>(N) * own.size() * s.in_row * 4, 0);
-    }
-    dc.group_end();
-    sync_all();
-    ph.add("scatter", now_ms() - q);
-    // input halos, device to device
-    q = now_ms();
-    size_t hi = 0;
-    std::vector<std::pair<RowRange, float*>> recvs;
-    for (const HaloXfer& h : plan.in_halos) {
-      if (h.src == rank)
-        copy_rows(d_halo[hi], h.rows.size(), 0, d_own, own.size(), h.rows.lo - own.lo, h.rows.size(), s.in_row, N,
-                  true, cs);
-      if (h.src == rank || h.dst == rank) ++hi;
-    }
-    hi = 0;
-    dc.group_start();
-    for (const HaloXfer& h : plan.in_halos) {
-      const size_t bytes = static_cast<size_t>(N) * h.rows.size() * s.in_row * 4;
-      if (h.src == rank) dc.send(d_halo[hi++], bytes, h.dst);
-      else if (h.dst == rank) {
-        dc.recv(d_halo[hi], bytes, h.src);
-        recvs.push_back({h.rows, d_halo[hi++]});
-      }
-    }
-    dc.group_end();
-    if (!t.out.empty()) {
-      const int lo = std::max(own.lo, t.in.lo), up = std::min(own.hi, t.in.hi);
-      copy_rows(d_tile, t.in.size(), lo - t.in.lo, d_own, own.size(), lo - own.lo, up - lo, s.in_row, N, true, cs);
-      for (auto& rv : recvs)
-        copy_rows(d_tile, t.in.size(), rv.first.lo - t.in.lo, rv.second, rv.first.size(), 0, rv.first.size(),
-                  s.in_row, N, true, cs);
-    }
-    dc.before(st);
-    sync_all();
-    ph.add("halo_in", now_ms() - q);
-    // conv1 + pool1 on the compute stream
-    q = now_ms();
-    if (!t.out.empty()) hip_check(eng.stage1(d_tile, N, t, st), "stage1");
-    hip_check(hipStreamSynchronize(st), "sync");
-    ph.add("compute", now_ms() - q);
-    // pool1 halos straight between the conv2 input windows of neighbouring GPUs
-    q = now_ms();
-    if (mode == Decomp::PerLayer) {
-      dc.after(st);
-      const size_t rowf = eng.q2_row_floats();
-      const int qrows = t.q.size();
-      std::vector<std::pair<RowRange, float*>> prv;
-      size_t pi = plan.in_halos.size();
-      size_t pk = pi;
-      for (const HaloXfer& h : plan.p1_halos)
-        if (h.src == rank) {
-          copy_rows(d_halo[pk], h.rows.size(), 0, eng.q2_row_ptr(t, 0, t.q.lo), qrows, h.rows.lo - t.q.lo,
-                    h.rows.size(), rowf, N, true, cs);
-          ++pk;
-        } else if (h.dst == rank) {
-          ++pk;
-        }
-      dc.group_start();
-      for (const HaloXfer& h : plan.p1_halos) {
-        const size_t bytes = static_cast<size_t>(N) * h.rows.size() * rowf * 4;
-        if (h.src == rank) dc.send(d_halo[pi++], bytes, h.dst);
-        else if (h.dst == rank) {
-          dc.recv(d_halo[pi], bytes, h.src);
-          prv.push_back({h.rows, d_halo[pi++]});
-        }
-      }
-      dc.group_end();
-      for (auto& rv : prv)
-        copy_rows(eng.q2_row_ptr(t, 0, t.q.lo), qrows, rv.first.lo - t.q.lo, rv.second, rv.first.size(), 0,
-                  rv.first.size(), rowf, N, true, cs);
-      dc.before(st);
-      sync_all();
-    }
-    ph.add("halo_p1", now_ms() - q);
-    q = now_ms();
-    if (!t.out.empty()) hip_check(eng.stage2(N, t, d_y, st), "stage2");
-    hip_check(hipStreamSynchronize(st), "sync");
-    ph.add("compute", now_ms() - q);
-    // gather to rank 0 over RCCL, then one D2H of the full output
-    q = now_ms();
-    dc.after(st);
-    dc.group_start();
-    if (rank == 0) {
-      for (int r = 1; r < np; ++r)
-        if (!plan.tiles[r].out.empty())
-          dc.recv(d_stage[r], static_cast<size_t>(N) * plan.tiles[r].out.size() * s.out_row * 4, r);
-    } else if (!t.out.empty()) {
-      dc.send(d_y, static_cast<size_t>(N) * t.out.size() * s.out_row * 4, 0);
-    }
-    dc.group_end();
-    if (rank == 0) {
-      for (int r = 0; r < np; ++r) {
-        const RowRange o = plan.tiles[r].out;
-        if (o.empty()) continue;
-        copy_rows(d_yfull, s.d.Hp2, o.lo, r == 0 ? d_y : d_stage[r], o.size(), 0, o.size(), s.out_row, N, true, cs);
-      }
-      hip_check(hipMemcpyAsync(y_host.data(), d_yfull, y_host.size() * 4, hipMemcpyDeviceToHost, cs), "D2H");
-    }
-    sync_all();
-    ph.add("gather", now_ms() - q);
+  auto make_events = [](int count) {
+    std::vector<hipEvent_t> v(count);
+    for (auto& e : v) hip_check(hipEventCreate(&e), "hipEventCreate");
+    return v;
   };
-  step(cold);
+  auto add_phases = [&](Phases& ph, hipEvent_t* ev) {
+    for (int i = 0; i < kEv - 1; ++i) {
+      float ms = 0;
+      hip_check(hipEventElapsedTime(&ms, ev[i], ev[i + 1]), "elapsed");
+      ph.add(names[i], ms);
+    }
+  };
+  std::vector<hipEvent_t> ev0 = make_events(kEv);
+  step(0, ev0.data());
+  if (rank == 0)
+    hip_check(hipMemcpyAsync(y_host.data(), d_yfull[0], y_host.size() * 4, hipMemcpyDeviceToHost, st), "D2H");
+  hip_check(hipStreamSynchronize(st), "sync");
+  add_phases(cold, ev0.data());
   double cold_ms = now_ms() - t0;
-  for (int i = 0; i < s.o.iters; ++i) step(warm);
-  double tm[2] = {cold_ms, s.o.iters ? warm.total() / s.o.iters : 0};
+  std::vector<hipEvent_t> evw = make_events(kEv * std::max(1, s.o.iters));
+  double wall = 0;
+  if (s.o.iters > 0) {
+    c.barrier();
+    const double w0 = now_ms();
+    for (int i = 0; i < s.o.iters; ++i) step(1 + i, evw.data() + kEv * i);  // no host sync inside
+    hip_check(hipStreamSynchronize(st), "sync");
+    c.barrier();
+    wall = (now_ms() - w0) / s.o.iters;
+    for (int i = 0; i < s.o.iters; ++i) add_phases(warm, evw.data() + kEv * i);
+    if (rank == 0) {  // the last warm step's output (parity of step iters)
+      hip_check(hipMemcpy(y_host.data(), d_yfull[s.o.iters & 1], y_host.size() * 4, hipMemcpyDeviceToHost), "D2H");
+    }
+  }
+  for (auto e : ev0) (void)hipEventDestroy(e);
+  for (auto e : evw) (void)hipEventDestroy(e);
+  double tm[2] = {cold_ms, wall};
   c.allreduce_max(tm, 2);
-  if (rank == 0) report(s, np, y_host, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y_host) : -1);
-  for (float* p : {d_x, d_own, d_tile, d_y, d_yfull})
+  if (rank == 0) {
+    std::printf("ANX_TRANSPORT %s transfers %zu\n", x->name(), x->log().size());
+    report(s, np, y_host, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y_host) : -1);
+  }
+  c.barrier();  // nobody pushes into a peer's buffers any more: unmap, then free
+  x->close();
+  c.barrier();  // every peer has unmapped this rank's buffers before they are freed
+  for (float* p : {d_x, d_tile[0], d_tile[1], d_y[0], d_y[1], d_yfull[0], d_yfull[1]})
     if (p) (void)hipFree(p);
-  for (float* p : d_stage)
-    if (p) (void)hipFree(p);
-  for (float* p : d_halo) (void)hipFree(p);
   (void)hipStreamDestroy(st);
   c.barrier();
   return 0;
@@ -956,7 +769,7 @@ int main(int argc, char** argv) {
       if (o.version == "v2.1") return run_v21(s, c);
       if (o.version == "v2.2") return run_rows_host(s, c, false);
       if (o.version == "v4") return run_rows_host(s, c, true);
-      return run_v5(s, c);
+      return run_v5(s, c, o.dry_run);
     } catch (const std::exception& e) {
       c.abort(e.what());  // coordinated fail-stop (the reference's CUDA_CHECK -> MPI_Abort, N29)
     }

@@ -57,12 +57,19 @@ class RowsWorkload:
         self.n = self.im.size if not self.tile.out.empty else 0
         dev = self.device
         t = self.tile
-        self.x_loc = torch.empty((self.n, t.inp.size, model.W, d.C0), device=dev)
-        self.y_loc = torch.empty((self.n, t.out.size, d.Wp2, d.C2), device=dev)
         self.root = r == 0
+        # whole-image tiles (a row group of one rank) need no stage1/halo/stage2 split: the plain
+        # forward (stream lanes, fused path) computes them
+        self.whole = t.inp.size == model.H and t.out.size == d.Hp2
         if self.root:
             self.x_dev = torch.empty((batch, *self.in_shape), device=dev)
             self.y_dev = torch.empty((batch, *self.out_shape), device=dev)
+        if self.root and self.whole:  # the root computes its images in place: no local copies
+            self.x_loc, self.y_loc = self.x_dev[self.im.lo:self.im.lo + self.n], self.y_dev[self.im.lo:self.im.lo + self.n]
+        else:
+            self.x_loc = torch.empty((self.n, t.inp.size, model.W, d.C0), device=dev)
+            self.y_loc = torch.empty((self.n, t.out.size, d.Wp2, d.C2), device=dev)
+        if self.root:
             pin = dev.type == "cuda"
             self.x_host = torch.empty((batch, *self.in_shape), pin_memory=pin) if version == "v4" else None
             self.y_host = torch.empty((batch, *self.out_shape), pin_memory=pin) if version == "v4" else None
@@ -123,7 +130,8 @@ class RowsWorkload:
                     continue
                 src = self.x_dev[iq.lo:iq.hi, tq.inp.lo:tq.inp.hi]
                 if q == 0:
-                    self.x_loc.copy_(src)
+                    if not self.whole:
+                        self.x_loc.copy_(src)
                     continue
                 buf = self.x_stage.get(q)
                 if buf is not None:
@@ -136,7 +144,7 @@ class RowsWorkload:
         for w in _p2p(ops):
             w.wait()
         self._mark(rec)
-        if self.layer == PER_LAYER:
+        if self.layer == PER_LAYER and not self.whole:
             if self.n:
                 m.stage1(self.x_loc, t)
             self._mark(rec)
@@ -174,7 +182,8 @@ class RowsWorkload:
                     continue
                 dst = self.y_dev[iq.lo:iq.hi, tq.out.lo:tq.out.hi]
                 if q == 0:
-                    dst.copy_(self.y_loc)
+                    if not self.whole:
+                        dst.copy_(self.y_loc)
                     continue
                 buf = self.y_stage.get(q)
                 if buf is None:

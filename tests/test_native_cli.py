@@ -101,16 +101,37 @@ def test_native_v4_shared_gpu(cuda, np_):
     assert rec["max_abs_err"] < 1e-3
 
 
+def _schedule(np_, transport, split, batch=3, decomp="per_layer"):
+    _, out = native(["--version", "v5", "--dry-run", "--transport", transport, "--split", split, "--batch",
+                     str(batch), "--decomp", decomp], np_)
+    return sorted(l.split(" ", 2)[2] for l in out.stdout.splitlines() if l.startswith("ANX_SCHEDULE "))
+
+
+@pytest.mark.parametrize("np_,split", [(2, "rows"), (3, "rows"), (4, "rows"), (4, "hybrid"), (3, "batch")])
+def test_v5_transports_issue_identical_transfers(np_, split):
+    """The RCCL and peer transports execute the same transfer list (record-only dry run: each logs
+    every transfer at the point it would issue it), so the shared-GPU peer tests cover the RCCL
+    schedule."""
+    rccl, peer = _schedule(np_, "rccl", split), _schedule(np_, "peer", split)
+    assert rccl == peer and len(rccl) > 0
+    phases = {l.split(" ")[2] for l in rccl}
+    assert {"scatter", "gather"} <= phases
+    assert ("halo_p1" in phases) == (split == "rows" or np_ > 3)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("np_,decomp", [(2, "per_layer"), (3, "per_layer"), (4, "per_layer"), (2, "overlap")])
-def test_native_v5_peer_transport(cuda, np_, decomp):
-    """V5 with every device byte moved by hipMemcpyPeerAsync into IPC-mapped neighbour buffers
-    (scatter, input halos, pool1 halos between conv2 windows, gather): ranks share the box's GPU,
-    and the output is bit-identical to the single-GPU run (direct convs)."""
+@pytest.mark.parametrize("np_,decomp,split", [(2, "per_layer", "rows"), (3, "per_layer", "rows"),
+                                              (4, "per_layer", "rows"), (2, "overlap", "rows"),
+                                              (4, "per_layer", "hybrid"), (3, "per_layer", "batch")])
+def test_native_v5_peer_transport(cuda, np_, decomp, split):
+    """V5 on the schedule runtime with the peer transport (one hipMemcpy2DAsync per transfer into
+    IPC-mapped receiver buffers, IPC-event ordering, no host stream sync in steady state): ranks
+    share the box's GPU, and the output is bit-identical to the single-GPU run (direct convs)."""
     d = ["--conv2-algo", "direct", "--conv1-algo", "direct"]
     ref, _ = native(["--version", "v3", "--init", "rand", "--seed", "6", "--batch", "3", *d])
-    rec, out = native(["--version", "v5", "--transport", "peer", "--decomp", decomp, "--init", "rand", "--seed", "6",
-                       "--batch", "3", "--iters", "2", "--lrn-alpha-mode", "raw", *d], np_)
+    rec, out = native(["--version", "v5", "--transport", "peer", "--decomp", decomp, "--split", split, "--init",
+                       "rand", "--seed", "6", "--batch", "3", "--iters", "3", "--lrn-alpha-mode", "raw", *d], np_)
+    assert set(rec["phases_warm"]) >= {"scatter", "halo_p1", "compute", "gather"}
     assert "Final Output Shape: 13x13x256" in out.stdout or rec["shape"] == [13, 13, 256]
     assert rec["checksum"] == ref["checksum"]
     # default (Winograd) convs: equal to the fp64 oracle within fp32 error
