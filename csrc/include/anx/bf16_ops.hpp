@@ -76,6 +76,12 @@ class FullEngine {
   int classes() const { return classes_; }
   int max_batch() const { return max_batch_; }
   Knobs& knobs() { return k_; }  // read at every launch (bf16_glds)
+  // Debug / numerics taps: copy the bf16 activation buffer `i` of the last forward (images of its
+  // last chunk; N <= chunk) to dst on stream s. i: 0 conv1 [N,55,55,96], 1 pool1 window
+  // [N,31,31,96], 2 conv2 [N,27,27,256], 3 pool2+LRN window [N,15,15,256], 4 conv3 window
+  // [N,15,15,384], 5 conv4 window [N,15,15,384], 6 conv5 [N,13,13,256], 7 pool5 [N,9216],
+  // 8 fc6 [N,4096], 9 fc7 [N,4096]. Returns the element count per image (0 for a bad i).
+  size_t tap(int i, int N, void* dst, hipStream_t s) const;
 
  private:
   struct Layer {

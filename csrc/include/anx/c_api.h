@@ -104,6 +104,8 @@ int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff
    set returns non-zero for an unknown name or an out-of-range value. */
 int anx_engine_set_knob(void* engine, const char* name, int value);
 int anx_engine_get_knob(void* engine, const char* name, int* value);
+/* bf16 activation tap `i` of the last forward (FullEngine::tap) into dst; *elems = per-image count */
+int anx_full_tap(void* engine, int i, int N, void* dst, size_t* elems, void* stream);
 int anx_full_set_knob(void* engine, const char* name, int value);
 int anx_full_get_knob(void* engine, const char* name, int* value);
 /* the defaults a new engine starts from (built-in values overridden by ANX_* environment variables) */
@@ -112,6 +114,11 @@ int anx_default_knob(const char* name, int* value);
    synchronises `stream`): x [N,Hin,W,3], KCFF weights on the HOST, y [N,H1,W1,K]. */
 int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, int K, int F, const float* bias,
                    float* y, int relu, int fold_scalar, void* stream);
+/* Conv2-shaped 5x5/1 conv by Winograd F(3x3,5x5) on device buffers (test entry; allocates, syncs):
+   x [N,Hq,Wq,C] (padding already in the window), KCFF weights on the HOST, y [N,Hq-4,Wq-4,K].
+   wino_cfg -1 = the default fused kernel. */
+int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
+                   const float* bias, float* y, int relu, int wino_cfg, void* stream);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

@@ -394,6 +394,10 @@ int anx_engine_get_knob(void* e, const char* name, int* value) {
     return fail(std::string("unknown knob: ") + (name ? name : "(null)"));
   return 0;
 }
+int anx_full_tap(void* e, int i, int N, void* dst, size_t* elems, void* stream) {
+  *elems = static_cast<anx::FullEngine*>(e)->tap(i, N, dst, S(stream));
+  return *elems ? 0 : fail("anx_full_tap: bad tap index or batch");
+}
 int anx_full_set_knob(void* e, const char* name, int value) {
   if (anx::set_knob(static_cast<anx::FullEngine*>(e)->knobs(), name, value) != 0)
     return fail(std::string("bad knob or value: ") + (name ? name : "(null)"));
@@ -435,6 +439,34 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
     (void)hipFree(dv);
     (void)hipFree(du);
     return hip_status(e, "conv1_wino");
+  });
+}
+
+int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
+                   const float* bias, float* y, int relu, int wino_cfg, void* stream) {
+  return guarded("anx_conv2_wino", [&] {
+    if (!anx::hip::wino_eligible(5, 1, C, K, groups)) return fail("anx_conv2_wino: shape not eligible");
+    const auto w = anx::hip::make_wino_plan(N, Hq, Wq, C, K, groups);
+    std::vector<float> u, packed;
+    std::vector<int> koff;
+    anx::hip::wino_transform_weights_host(w, w_kcff, u);
+    anx::hip::pack_conv_weights_host(w.gemm, u.data(), packed, koff);
+    float *dv = nullptr, *du = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&dv), std::max<size_t>(anx::hip::wino_v_floats(w), 1) * 4) != hipSuccess)
+      return fail("anx_conv2_wino: hipMalloc");
+    if (hipMalloc(reinterpret_cast<void**>(&du), packed.size() * 4) != hipSuccess) {
+      (void)hipFree(dv);
+      return fail("anx_conv2_wino: hipMalloc");
+    }
+    hipError_t e = hipMemcpy(du, packed.data(), packed.size() * 4, hipMemcpyHostToDevice);
+    anx::Knobs kn = anx::default_knobs();
+    if (wino_cfg >= 0) kn.wino_cfg = wino_cfg;
+    if (e == hipSuccess) e = anx::hip::wino_input(w, x, dv, S(stream));
+    if (e == hipSuccess) e = anx::hip::wino_fused(w, dv, du, bias, y, relu != 0, S(stream), kn);
+    if (e == hipSuccess) e = hipStreamSynchronize(S(stream));  // the workspaces are freed below
+    (void)hipFree(dv);
+    (void)hipFree(du);
+    return hip_status(e, "conv2_wino");
   });
 }
 

@@ -171,4 +171,13 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
   return hipSuccess;
 }
 
+size_t FullEngine::tap(int i, int N, void* dst, hipStream_t s) const {
+  static const size_t kElems[10] = {55 * 55 * 96,   31 * 31 * 96,   27 * 27 * 256, 15 * 15 * 256, 15 * 15 * 384,
+                                    15 * 15 * 384, 13 * 13 * 256, 9216,          4096,          4096};
+  void* const bufs[10] = {c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_};
+  if (i < 0 || i >= 10 || N < 1 || N > chunk_) return 0;
+  if (hipMemcpyAsync(dst, bufs[i], kElems[i] * N * 2, hipMemcpyDeviceToDevice, s) != hipSuccess) return 0;
+  return kElems[i];
+}
+
 }  // namespace anx

@@ -1,0 +1,86 @@
+"""fp32 Winograd kernels at realistic dynamic range (randn activations, He-init weights), with the
+error bounded relative to the sum of absolute products Σ|x·w| of each output — the scale of fp32
+accumulation error itself (a direct fp32 conv sits at ~1e-7 of it). The reference-init tests (inputs
+U[0,0.1), weights ±0.01) exercise a narrow range only; these pin the transforms' cancellation error.
+Also: the exact bench.py step (stream lanes) against the fp64 oracle, images of every lane."""
+import math
+
+import pytest
+import torch
+
+from anx import _native as nat
+from anx.models.alexnet_blocks import AlexNetBlocks
+from anx.models.reference import blocks_forward, conv2d_nhwc
+
+pytestmark = pytest.mark.gpu
+BOUND = 2e-6  # of Σ|x·w|; measured ~3e-7 (Conv1) and ~6e-7 (Conv2), tools/winograd_numerics.py
+
+
+def _rel_to_terms(y, x, w, b, S, P, groups=1):
+    ref = conv2d_nhwc(x.double(), w.double(), b.double(), S, P, groups)
+    terms = conv2d_nhwc(x.double().abs(), w.double().abs(), b.double().abs(), S, P, groups)
+    return ((y.double() - ref).abs() / (terms + 1e-30)).max().item()
+
+
+@pytest.mark.parametrize("N,groups,cfg", [(12, 1, -1), (12, 2, -1), (9, 1, 15), (9, 1, 1)])
+def test_conv2_winograd_randn_he(cuda, N, groups, cfg):
+    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights."""
+    torch.manual_seed(21 + N)
+    C, K = 96, 256
+    x = torch.randn(N, 31, 31, C, device=cuda)
+    x[:, :2] = 0
+    x[:, -2:] = 0
+    x[:, :, :2] = 0
+    x[:, :, -2:] = 0  # the zero border of the conv2 window
+    w = torch.randn(K, C // groups, 5, 5) * math.sqrt(2.0 / (C // groups * 25))
+    b = torch.randn(K, device=cuda) * 0.1
+    y = torch.full((N, 27, 27, K), float("nan"), device=cuda)
+    nat.call("anx_conv2_wino", x.data_ptr(), N, 31, 31, C, w.contiguous().data_ptr(), K, groups, b.data_ptr(),
+             y.data_ptr(), 0, cfg, nat.stream_ptr(cuda))
+    assert torch.isfinite(y).all()
+    assert _rel_to_terms(y, x, w.to(cuda), b, 1, 0, groups) < BOUND
+
+
+@pytest.mark.parametrize("N", [5, 70])
+def test_conv1_polyphase_winograd_randn_he(cuda, N):
+    """Conv1 (227x227x3, 11x11/4, 96 filters) on the polyphase Winograd path: randn inputs."""
+    torch.manual_seed(31 + N)
+    x = torch.randn(N, 227, 227, 3, device=cuda)
+    w = torch.randn(96, 3, 11, 11) * math.sqrt(2.0 / (3 * 121))
+    b = torch.randn(96, device=cuda) * 0.1
+    y = torch.full((N, 55, 55, 96), float("nan"), device=cuda)
+    nat.call("anx_conv1_wino", x.data_ptr(), N, 227, 227, w.contiguous().data_ptr(), 96, 11, b.data_ptr(),
+             y.data_ptr(), 0, 0, nat.stream_ptr(cuda))
+    assert torch.isfinite(y).all()
+    assert _rel_to_terms(y, x, w.to(cuda), b, 4, 0) < BOUND
+
+
+def test_full_blocks_randn_he_vs_oracle(cuda):
+    """The whole Blocks 1-2 engine (both Winograd convs, pools, LRN) at randn/He scale."""
+    torch.manual_seed(5)
+    w1 = torch.randn(96, 3, 11, 11) * math.sqrt(2.0 / 363)
+    w2 = torch.randn(256, 96, 5, 5) * math.sqrt(2.0 / 2400)
+    ws = {"w1": w1, "b1": torch.randn(96) * 0.1, "w2": w2, "b2": torch.randn(256) * 0.1}
+    m = AlexNetBlocks(ws, device=cuda, max_batch=24)
+    x = torch.randn(24, 227, 227, 3)
+    y = m(x.to(cuda)).cpu().double()
+    ref = blocks_forward(x, m.weights, m.b1, m.b2)
+    assert (y - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_bench_step_vs_oracle(cuda):
+    """bench.py's default step: 128 images as 2 stream lanes of 64 (one engine per HIP stream),
+    checked against the fp64 oracle on images from both lanes including the first and last."""
+    B = 128
+    m = AlexNetBlocks(init="rand", seed=1234, device=cuda, max_batch=B, lanes=2)
+    g = torch.Generator(device=cuda)
+    g.manual_seed(1234)
+    x = torch.rand((B, 227, 227, 3), device=cuda, generator=g) * 0.1
+    y = m(x)
+    idx = torch.tensor([0, 1, 63, 64, 65, 126, 127])
+    ref = blocks_forward(x[idx.to(cuda)].cpu(), m.weights, m.b1, m.b2)
+    got = y[idx.to(cuda)].cpu().double()
+    assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    # the second lane's half is bitwise what one engine computes for it alone
+    solo = AlexNetBlocks(init="rand", seed=1234, device=cuda, max_batch=B // 2)
+    assert torch.equal(solo(x[B // 2:].contiguous()), y[B // 2:])
