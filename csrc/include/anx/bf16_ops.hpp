@@ -45,6 +45,16 @@ hipError_t splitk_reduce_bf16(const float* ws, int ksplit, int M, int K, const f
 // 3 slots, 0 = the register-staged kernel (A/B).
 hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, const int* koff, const float* bias,
                        OutViewB out, float* out_f32, bool relu, hipStream_t s, SplitK split = {}, int glds = 2);
+// Wide-tile kernel (conv_bf16_big.hip): 1 workgroup per CU, 8 waves over a 256-row tile, LDS-DMA
+// double buffer, 16x16x32 MFMA, LDS-transposed epilogue with 16-B stores. Same packed weights / koff
+// as conv2d_bf16 (vec8, non-taps8 plans); bf16 output only. cfg: 0 = 256x256, 1 = 256x128,
+// 2 = 256x96, 3 = 128x128 (4 waves), 4 = 128x96 (4 waves).
+int conv_bf16_big_cfgs();
+bool conv_bf16_big_ok(const ConvPlanB& p, int cfg, const OutViewB& out);
+// The config a cost model of wave quantization picks for this launch (-1: none applies).
+int pick_bf16_big_cfg(const ConvPlanB& p, const OutViewB& out, int cus = 256);
+hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const void* wpacked, const int* koff,
+                           const float* bias, OutViewB out, bool relu, hipStream_t s);
 hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S, OutViewB out, hipStream_t s);
 hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
                             float beta, float k, LrnMode mode, OutViewB out, hipStream_t s);
@@ -75,7 +85,7 @@ class FullEngine {
   hipError_t forward(const float* x, int N, float* logits, hipStream_t s);
   int classes() const { return classes_; }
   int max_batch() const { return max_batch_; }
-  Knobs& knobs() { return k_; }  // read at every launch (bf16_glds)
+  Knobs& knobs() { return k_; }  // read at every launch (bf16_glds, bf16_big)
   // Debug / numerics taps: copy the bf16 activation buffer `i` of the last forward (images of its
   // last chunk; N <= chunk) to dst on stream s. i: 0 conv1 [N,55,55,96], 1 pool1 window
   // [N,31,31,96], 2 conv2 [N,27,27,256], 3 pool2+LRN window [N,15,15,256], 4 conv3 window
@@ -97,6 +107,7 @@ class FullEngine {
   Layer L_[8];
   Knobs k_;
   int classes_, max_batch_, chunk_;
+  int cus_ = 256;  // compute units (the wide-tile kernel's cost model)
   LrnMode lrn_;
   bool poly1_ = false;  // Conv1 as a stride-1 3x3 conv over the 48-channel polyphase image (ANX_FULL_CONV1)
   void *xb_ = nullptr, *c1_ = nullptr, *q2_ = nullptr, *c2_ = nullptr, *q3_ = nullptr, *q4_ = nullptr,

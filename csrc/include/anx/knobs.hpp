@@ -31,13 +31,15 @@ struct Knobs {
   int force_vec4 = -1;     // conv_mfma tile variant override for Cg % 4 == 0 convs (-1 = heuristic)
   int force_scalar = -1;   // conv_mfma tile variant override for scalar-gather convs
   int bf16_glds = 2;       // bf16 full model: 0 register-staged, 2 / 3 LDS-DMA ring slots
+  int bf16_big = -1;       // bf16 conv layers on the wide-tile kernel (conv_bf16_big.hip): -1 cost model
+                           // picks the config, -2 off (the 128x128 kernels above), 0.. force that config
   int conv1_occ = 0;       // cap on Conv1 Winograd GEMM workgroups per CU (0 = natural: 4), by LDS padding,
   int conv2_occ = 0;       // ... and Conv2's (natural 2): leaves room for a concurrent lane's kernels
 };
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CONV1_WINO_CFG,
 // ANX_CONV1_WINO_PROBE, ANX_WINO_FUSED_CFG, ANX_WINO_PRIO, ANX_FOLD_SCALAR, ANX_CHUNK1, ANX_CHUNK2,
-// ANX_FUSE_POOL1, ANX_BF16_GLDS when set.
+// ANX_FUSE_POOL1, ANX_BF16_GLDS, ANX_BF16_BIG when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

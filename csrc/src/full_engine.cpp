@@ -83,6 +83,11 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
     L.F = 3;
     L.S = 1;
   }
+  {
+    int dev = 0;
+    check(hipGetDevice(&dev), "hipGetDevice");
+    check(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+  }
   chunk_ = std::max(1, std::min(max_batch, static_cast<int>(((1UL << 31) - 1) / (55UL * 55 * 96))));
   const size_t n = static_cast<size_t>(chunk_);
   xb_ = dalloc(n * std::max(227 * 227 * 3, 57 * 57 * 48) * 2);
@@ -138,6 +143,11 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
   if (ks > 1) {  // FC layer at a small batch: K split over ~one workgroup per CU, then a reduce
     ANX_TRY(hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s, hip::SplitK{ks, ws_}, k_.bf16_glds));
     return hip::splitk_reduce_bf16(ws_, ks, N, L.K, L.bias, relu, out, out_f32, s);
+  }
+  if (!out_f32 && k_.bf16_big != -2) {  // wide-tile kernel: forced config if it applies, else the cost model
+    const int cfg = k_.bf16_big >= 0 && hip::conv_bf16_big_ok(p, k_.bf16_big, out) ? k_.bf16_big
+                                                                                    : hip::pick_bf16_big_cfg(p, out, cus_);
+    if (cfg >= 0) return hip::conv2d_bf16_big(p, cfg, x, L.wp, L.koff, L.bias, out, relu, s);
   }
   return hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s, {}, k_.bf16_glds);
 }

@@ -1,0 +1,305 @@
+// Wide-tile bf16 implicit-GEMM convolution for the full-AlexNet extension (conv1-polyphase, conv2-5).
+//
+// The 128x128 4-wave kernels of conv_bf16.hip run 2-3 workgroups per CU and measured 0.55-0.70
+// PFLOP/s on conv2-5 (profiles/r01_full_bf16_glds_kernels_latest.md): the 128^2 structure's ceiling
+// (cdna_hip_programming.md §5, "the step-3 structure"). This kernel is the 1-workgroup-per-CU
+// shape: a BM=256-row output tile over 8 waves, operands staged global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, per-lane gather addresses: A row = the output pixel's input-window
+// origin + koff of the K slice's tap, B row = packed filter row) into two K=64 buffers, a counted
+// vmcnt and one raw barrier per K tile, 16x16x32 bf16 MFMAs in between (setprio-fenced clusters).
+//
+//   LDS image: rows of 64 bf16 = 8 16-B chunks; chunk c of row r is stored at c ^ ((r >> 1) & 7)
+//   (the swizzle lives on the DMA SOURCE address — the DMA destination is lane-linear — and on the
+//   fragment reads), so every ds_read_b128 lane group of a 16x16x32 fragment hits 16 distinct bank
+//   quads.
+//   Tile order: blockIdx -> tile is XCD-aware and bijective (each XCD walks a contiguous run of
+//   M tiles: neighbouring output rows share input rows in its L2).
+//   Epilogue: bias + ReLU + bf16 into an LDS image of the whole output tile (chunk-XOR swizzled),
+//   then 16-B row-contiguous stores — the MFMA C layout (one column per lane) would otherwise
+//   store 2 bytes per lane.
+//
+// Conv reference: final_project/v3_cuda_only/src/layers_cuda.cu:20-62 (one thread per output,
+// fp32); the AlexNet tail (conv3-5) is the extension's own (BASELINE.json config 5).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "anx/bf16_ops.hpp"
+
+namespace anx::hip {
+namespace {
+
+using bf16 = __bf16;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+using lds_b16 = __attribute__((address_space(3))) bf16;
+
+constexpr int kBK = 64;  // bf16 per staged row = 8 chunks of 16 B
+
+struct ArgsW {
+  const bf16* x;
+  const bf16* w;
+  const int* koff;
+  const float* bias;
+  bf16* out;
+  int M, HoWo, Wo, Hp, Wp, C, S, Cg, Kg, kpad, kpad_n, ktiles, n_ntiles, m_tiles;
+  int Hb, Wb, Cb, h_off, w_off, c_off, relu;
+};
+
+__device__ __forceinline__ void glds16(const bf16* g, lds_b16* l) { __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0); }
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// BM x BN output tile, WGM x WGN waves (WM = BM/WGM rows, WN = BN/WGN columns per wave).
+template <int BM, int BN, int WGM, int WGN>
+__global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) {
+  constexpr int NW = WGM * WGN, NT = 64 * NW;
+  constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && BM % 16 == 0, "tile split");
+  constexpr int UNITS = (BM + BN) * 8;              // 16-B DMA units per stage (A rows, then B rows)
+  constexpr int NJ = (UNITS + NT - 1) / NT;         // DMA instructions per lane per stage
+  static_assert(UNITS % 64 == 0, "a DMA instruction never straddles A and B");
+  constexpr int STAGE = (BM + BN) * kBK;            // bf16 per stage
+  constexpr int CH = BN / 8;                        // 16-B chunks per epilogue row
+  constexpr int XM = (CH % 8 == 0) ? 7 : (CH % 4 == 0) ? 3 : (CH % 2 == 0) ? 1 : 0;
+  static_assert(BM * BN <= 2 * STAGE, "the epilogue image fits in the two stages");
+  extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
+  int* koff_s = reinterpret_cast<int*>(lds_b + 2 * STAGE);
+  int* ooff_s = koff_s + a.kpad;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, g = blockIdx.z;
+  // XCD-aware bijective remap: dispatch round-robins blocks over the 8 XCDs; give each XCD a
+  // contiguous run of tiles (m-major, n inner) so neighbouring tiles share its L2.
+  int tile;
+  {
+    const int nwg = gridDim.x, b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int mt = tile / a.n_ntiles, nt = tile - mt * a.n_ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const bf16* x = a.x + g * a.Cg;
+  const bf16* wg = a.w + static_cast<size_t>(g) * a.kpad_n * a.kpad;
+  for (int i = tid; i < a.kpad; i += NT) koff_s[i] = a.koff[i];
+  for (int i = tid; i < BM; i += NT) {
+    const int m = m0 + i;
+    int oo = -1;
+    if (m < a.M) {
+      const int n = m / a.HoWo, rr = m - n * a.HoWo, oy = rr / a.Wo, ox = rr - oy * a.Wo;
+      oo = ((n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off;
+    }
+    ooff_s[i] = oo;
+  }
+  // DMA unit q = j*NT + tid: row q/8 (rows < BM are A rows), physical chunk tid&7 holding logical
+  // chunk u (the row-swizzle involution; (row >> 1) & 7 depends on tid only since NT/8 % 16 == 0)
+  static_assert((NT / 8) % 16 == 0, "swizzle phase is per-lane");
+  const int u = (tid & 7) ^ ((tid >> 4) & 7);
+  const bf16* src[NJ];
+  bool isA[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int row = j * (NT / 8) + (tid >> 3);
+    isA[j] = row < BM;
+    if (row < BM) {
+      const int m = m0 + row;
+      int o = 0;
+      if (m < a.M) {
+        const int n = m / a.HoWo, rr = m - n * a.HoWo, oy = rr / a.Wo, ox = rr - oy * a.Wo;
+        o = ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
+      }
+      src[j] = x + o;  // + koff of (K tile, u) per stage
+    } else {
+      const int n = min(n0 + row - BM, a.kpad_n - 1);  // rows past the packed filters: never stored
+      src[j] = wg + static_cast<size_t>(n) * a.kpad + u * 8;  // + kb per stage
+    }
+  }
+  __syncthreads();  // koff_s / ooff_s visible
+  lds_b16* lds3 = (lds_b16*)(lds_b);
+  auto issue = [&](int kt, int st) {
+    const int kb = kt * kBK;
+    const int kr = koff_s[kb + u * 8];
+    const int ko = kr >= 0 ? kr : 0;  // K padding: zero-packed weights meet pixel data
+    lds_b16* dst = lds3 + st * STAGE;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int q0 = j * NT + wave * 64;
+      if (UNITS % NT != 0 && q0 >= UNITS) break;  // wave-uniform
+      glds16(src[j] + (isA[j] ? ko : kb), dst + q0 * 8);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fragment reads: lane row (lane & 15) of each 16-row block, k chunk 4s + (lane >> 4); every
+  // block starts at a multiple of 16 rows, so the swizzle phase is ((lane & 15) >> 1) & 7
+  const int hq = lane >> 4, sw = (lane >> 1) & 7;
+  const int arow = (wm * WM + (lane & 15)) * kBK, brow = (BM + wn * WN + (lane & 15)) * kBK;
+  const int total = a.ktiles;
+  issue(0, 0);
+  for (int it = 0; it < total; ++it) {
+    wait_vm<0>();                  // this lane's DMA pieces of tile it landed
+    __builtin_amdgcn_s_barrier();  // ... every lane's; and every wave is done reading tile it-1
+    asm volatile("" ::: "memory");
+    if (it + 1 < total) issue(it + 1, (it + 1) & 1);
+    const bf16* base = lds_b + (it & 1) * STAGE;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < kBK / 32; ++s) {
+      const int ca = ((4 * s + hq) ^ sw) * 8;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(base + arow + i * 16 * kBK + ca);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(base + brow + j * 16 * kBK + ca);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  // epilogue: the tile through LDS (all DMA retired above; wait for every wave's last reads)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16* E = lds_b;
+  const int ncol = lane & 15;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * WN + j * 16 + ncol, f = n0 + nl;
+    const float bv = (a.bias && f < a.Kg) ? a.bias[g * a.Kg + f] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ml = wm * WM + i * 16 + hq * 4 + e;
+        float v = acc[i][j][e] + bv;
+        if (a.relu) v = fmaxf(v, 0.f);
+        E[ml * BN + (((nl >> 3) ^ (ml & XM)) << 3) + (nl & 7)] = static_cast<bf16>(v);
+      }
+  }
+  __syncthreads();
+  bf16* out = a.out + g * a.Kg;
+  for (int q = tid; q < BM * CH; q += NT) {
+    const int ml = q / CH, c = q - ml * CH;
+    const int o = ooff_s[ml], f = n0 + c * 8;
+    if (o >= 0 && f < a.Kg)
+      *reinterpret_cast<u32x4*>(out + o + f) = *reinterpret_cast<const u32x4*>(E + ml * BN + ((c ^ (ml & XM)) << 3));
+  }
+}
+
+struct BigCfg {
+  int BM, BN, threads;
+  int wgs_per_cu;  // co-resident workgroups (LDS / registers) at AlexNet's kpad
+  float eff;       // relative per-CU MFMA efficiency (anx_bf16bench, 256 images)
+};
+constexpr BigCfg kCfg[] = {{256, 256, 512, 1, 1.0f},
+                           {256, 128, 512, 1, 0.86f},
+                           {256, 96, 512, 1, 0.8f},
+                           {128, 128, 256, 2, 0.92f},
+                           {128, 96, 256, 2, 0.85f}};
+constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
+
+size_t lds_bytes(const BigCfg& c, int kpad) {
+  return static_cast<size_t>(2) * (c.BM + c.BN) * kBK * 2 + static_cast<size_t>(kpad + c.BM) * 4;
+}
+
+}  // namespace
+
+int conv_bf16_big_cfgs() { return kNumCfg; }
+
+bool conv_bf16_big_ok(const ConvPlanB& p, int cfg, const OutViewB& out) {
+  if (cfg < 0 || cfg >= kNumCfg) return false;
+  return p.vec8 && !p.taps8 && p.Kg % 8 == 0 && out.Cb % 8 == 0 && out.c_off % 8 == 0 && out.base &&
+         lds_bytes(kCfg[cfg], p.kpad) <= 160 * 1024 && static_cast<long>(p.N) * p.Hp * p.Wp * p.C < (1L << 31) &&
+         static_cast<long>(p.N) * out.Hb * out.Wb * out.Cb < (1L << 31);
+}
+
+// Wave-quantization cost model: a config's time ~ rounds of co-resident workgroups x tile area x
+// workgroups per CU / efficiency (ceil, so a 1.3-round launch costs 2 rounds); ties keep the
+// lower config index.
+int pick_bf16_big_cfg(const ConvPlanB& p, const OutViewB& out, int cus) {
+  const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
+  int best = -1;
+  double best_cost = 0;
+  for (int c = 0; c < kNumCfg; ++c) {
+    if (!conv_bf16_big_ok(p, c, out)) continue;
+    const BigCfg& k = kCfg[c];
+    const long tiles = (M + k.BM - 1) / k.BM * ((p.Kg + k.BN - 1) / k.BN) * p.groups;
+    const long slots = static_cast<long>(cus) * k.wgs_per_cu;
+    const long rounds = (tiles + slots - 1) / slots;
+    const double cost = static_cast<double>(rounds) * k.BM * k.BN * k.wgs_per_cu / k.eff;
+    if (best < 0 || cost < best_cost * 0.999) {
+      best = c;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const void* wpacked, const int* koff,
+                           const float* bias, OutViewB out, bool relu, hipStream_t s) {
+  if (!conv_bf16_big_ok(p, cfg, out)) return hipErrorInvalidValue;
+  const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
+  if (M == 0) return hipSuccess;
+  const BigCfg c = kCfg[cfg];
+  ArgsW a{};
+  a.x = static_cast<const bf16*>(x);
+  a.w = static_cast<const bf16*>(wpacked);
+  a.koff = koff;
+  a.bias = bias;
+  a.out = out.base;
+  a.M = static_cast<int>(M);
+  a.HoWo = p.Ho * p.Wo;
+  a.Wo = p.Wo;
+  a.Hp = p.Hp;
+  a.Wp = p.Wp;
+  a.C = p.C;
+  a.S = p.S;
+  a.Cg = p.Cg;
+  a.Kg = p.Kg;
+  a.kpad = p.kpad;
+  a.kpad_n = p.kpad_n;
+  a.ktiles = p.kpad / kBK;
+  a.n_ntiles = (p.Kg + c.BN - 1) / c.BN;
+  a.m_tiles = static_cast<int>((M + c.BM - 1) / c.BM);
+  a.Hb = out.Hb;
+  a.Wb = out.Wb;
+  a.Cb = out.Cb;
+  a.h_off = out.h_off;
+  a.w_off = out.w_off;
+  a.c_off = out.c_off;
+  a.relu = relu ? 1 : 0;
+  const dim3 grid(static_cast<unsigned>(a.m_tiles * a.n_ntiles), 1, p.groups);
+  const size_t lds = lds_bytes(c, p.kpad);
+  static const hipError_t attr = [] {
+    const void* ks[] = {reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 256, 2, 4>),
+                        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 128, 4, 2>),
+                        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 96, 4, 2>),
+                        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 128, 2, 2>),
+                        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 96, 2, 2>)};
+    for (const void* k : ks) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }();
+  if (attr != hipSuccess) return attr;
+  switch (cfg) {
+    case 0: conv_bf16_big_kernel<256, 256, 2, 4><<<grid, c.threads, lds, s>>>(a); break;
+    case 1: conv_bf16_big_kernel<256, 128, 4, 2><<<grid, c.threads, lds, s>>>(a); break;
+    case 2: conv_bf16_big_kernel<256, 96, 4, 2><<<grid, c.threads, lds, s>>>(a); break;
+    case 3: conv_bf16_big_kernel<128, 128, 2, 2><<<grid, c.threads, lds, s>>>(a); break;
+    case 4: conv_bf16_big_kernel<128, 96, 2, 2><<<grid, c.threads, lds, s>>>(a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace anx::hip

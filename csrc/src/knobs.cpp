@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "anx/bf16_ops.hpp"
 #include "anx/ops.hpp"
 
 namespace anx {
@@ -32,6 +33,7 @@ const Field kFields[] = {
     {"force_vec4", &Knobs::force_vec4, nullptr, -1, 255, nullptr},
     {"force_scalar", &Knobs::force_scalar, nullptr, -1, 255, nullptr},
     {"bf16_glds", &Knobs::bf16_glds, nullptr, 0, 3, "ANX_BF16_GLDS"},
+    {"bf16_big", &Knobs::bf16_big, nullptr, -2, 15, "ANX_BF16_BIG"},
     {"conv1_occ", &Knobs::conv1_occ, nullptr, 0, 8, "ANX_CONV1_OCC"},
     {"conv2_occ", &Knobs::conv2_occ, nullptr, 0, 8, "ANX_CONV2_OCC"},
 };
@@ -46,6 +48,7 @@ const Field* find(const char* name) {
 bool valid(const Field& f, int v) {
   if (v < f.lo || v > f.hi) return false;
   if (std::strcmp(f.name, "bf16_glds") == 0) return v == 0 || v == 2 || v == 3;
+  if (std::strcmp(f.name, "bf16_big") == 0) return v < hip::conv_bf16_big_cfgs();
   if (std::strcmp(f.name, "force_vec4") == 0) return hip::conv_variant_valid(0, v);
   if (std::strcmp(f.name, "force_scalar") == 0) return hip::conv_variant_valid(1, v);
   return true;
