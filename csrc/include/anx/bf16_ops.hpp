@@ -53,11 +53,20 @@ int conv_bf16_big_cfgs();
 bool conv_bf16_big_ok(const ConvPlanB& p, int cfg, const OutViewB& out);
 // The config a cost model of wave quantization picks for this launch (-1: none applies).
 int pick_bf16_big_cfg(const ConvPlanB& p, const OutViewB& out, int cus = 256);
+// split.ws set (groups == 1): fp32 partial slabs [ksplit][M][Kg] into split.ws, K split ksplit ways
+// (no bias / ReLU; then splitk_reduce_bf16, which also serves an fp32 result at ksplit 1). `out` is
+// then only validated.
 hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const void* wpacked, const int* koff,
-                           const float* bias, OutViewB out, bool relu, hipStream_t s);
+                           const float* bias, OutViewB out, bool relu, hipStream_t s, SplitK split = {});
+// Fully-connected layer plan on the wide-tile kernel (cfg -1: not applicable).
+struct BigFc {
+  int cfg, ksplit;
+};
+BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus = 256);
 hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S, OutViewB out, hipStream_t s);
+// tile (Knobs::bf16_lrn_tile): 1 = the generic LDS-tile kernel even where the C = 256 wave kernel applies (A/B).
 hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
-                            float beta, float k, LrnMode mode, OutViewB out, hipStream_t s);
+                            float beta, float k, LrnMode mode, OutViewB out, hipStream_t s, int tile = 0);
 hipError_t f32_to_bf16(const float* x, void* y, size_t n, hipStream_t s);
 // Conv1 polyphase input (space-to-depth by the stride 4) fused with the bf16 conversion:
 // y[n][i][j][(rh*4+rw)*3+c] = x[n][4i+rh][4j+rw][c] (0 past the image), y = [N, ceil(H/4), ceil(W/4), 48].

@@ -112,6 +112,8 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
       const hip::ConvPlanB p = hip::make_conv_plan_bf16(b, 1, 1, L_[i].C, L_[i].K, 1, 1, 1);
       const int ks = hip::fc_split_k(p);
       if (ks > 1) ws = std::max(ws, static_cast<size_t>(ks) * b * L_[i].K);
+      const hip::BigFc f = hip::pick_bf16_big_fc(p, cus_);  // wide-tile FC slabs (at ksplit 1 for fp32 logits)
+      if (f.cfg >= 0) ws = std::max(ws, static_cast<size_t>(f.ksplit) * b * L_[i].K);
     }
   if (ws) ws_ = static_cast<float*>(dalloc(ws * 4));
 }
@@ -126,6 +128,7 @@ FullEngine::~FullEngine() {
 
 hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip::OutViewB out, float* out_f32,
                             bool relu, hipStream_t s) {
+  auto B = [](void* q) { return static_cast<__bf16*>(q); };
   const hip::ConvPlanB p = hip::make_conv_plan_bf16(N, Hp, Wp, L.C, L.K, L.F, L.S, L.groups);
   if (p.variant != L.key) {  // pack for this tile variant (first use / batch-size class change)
     std::vector<uint16_t> pk;
@@ -139,12 +142,24 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
     ANX_TRY(hipMemcpy(L.koff, ko.data(), ko.size() * 4, hipMemcpyHostToDevice));
     L.key = p.variant;
   }
+  const bool fc = p.Hp == 1 && p.Wp == 1 && p.F == 1;
+  if (fc && k_.bf16_big != -2) {  // wide-tile FC: one 256-row tile of the batch, K split over the CUs
+    hip::BigFc f = hip::pick_bf16_big_fc(p, cus_);
+    if (f.cfg >= 0 && k_.bf16_big >= 0 && hip::conv_bf16_big_ok(p, k_.bf16_big, hip::OutViewB{B(ws_), 1, 1, p.Kg, 0, 0, 0}))
+      f.cfg = k_.bf16_big;
+    if (f.cfg >= 0 && (f.ksplit > 1 || out_f32)) {
+      ANX_TRY(hip::conv2d_bf16_big(p, f.cfg, x, L.wp, L.koff, L.bias, hip::OutViewB{B(ws_), 1, 1, p.Kg, 0, 0, 0}, relu,
+                                   s, hip::SplitK{f.ksplit, ws_}));
+      return hip::splitk_reduce_bf16(ws_, f.ksplit, N, L.K, L.bias, relu, out, out_f32, s);
+    }
+    if (f.cfg >= 0) return hip::conv2d_bf16_big(p, f.cfg, x, L.wp, L.koff, L.bias, out, relu, s);
+  }
   const int ks = hip::fc_split_k(p);
   if (ks > 1) {  // FC layer at a small batch: K split over ~one workgroup per CU, then a reduce
     ANX_TRY(hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s, hip::SplitK{ks, ws_}, k_.bf16_glds));
     return hip::splitk_reduce_bf16(ws_, ks, N, L.K, L.bias, relu, out, out_f32, s);
   }
-  if (!out_f32 && k_.bf16_big != -2) {  // wide-tile kernel: forced config if it applies, else the cost model
+  if (!fc && !out_f32 && k_.bf16_big != -2) {  // wide-tile kernel: forced config if it applies, else the cost model
     const int cfg = k_.bf16_big >= 0 && hip::conv_bf16_big_ok(p, k_.bf16_big, out) ? k_.bf16_big
                                                                                     : hip::pick_bf16_big_cfg(p, out, cus_);
     if (cfg >= 0) return hip::conv2d_bf16_big(p, cfg, x, L.wp, L.koff, L.bias, out, relu, s);
@@ -168,7 +183,7 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
     ANX_TRY(hip::maxpool_bf16(c1_, n, 55, 55, 96, 3, 2, OutViewB{B(q2_), 31, 31, 96, 2, 2, 0}, s));
     ANX_TRY(conv(L_[1], n, 31, 31, q2_, OutViewB{B(c2_), 27, 27, 256, 0, 0, 0}, nullptr, true, s));
     ANX_TRY(hip::maxpool_lrn_bf16(c2_, n, 27, 27, 256, 3, 2, 5, 1e-4f, 0.75f, 2.0f, lrn_,
-                                  OutViewB{B(q3_), 15, 15, 256, 1, 1, 0}, s));
+                                  OutViewB{B(q3_), 15, 15, 256, 1, 1, 0}, s, k_.bf16_lrn_tile));
     ANX_TRY(conv(L_[2], n, 15, 15, q3_, OutViewB{B(q4_), 15, 15, 384, 1, 1, 0}, nullptr, true, s));
     ANX_TRY(conv(L_[3], n, 15, 15, q4_, OutViewB{B(q5_), 15, 15, 384, 1, 1, 0}, nullptr, true, s));
     ANX_TRY(conv(L_[4], n, 15, 15, q5_, OutViewB{B(c5_), 13, 13, 256, 0, 0, 0}, nullptr, true, s));

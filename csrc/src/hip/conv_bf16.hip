@@ -425,54 +425,68 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16* __restrict
     y[i] = static_cast<bf16>(x[i]);
 }
 
-// pool + LRN for C = 256, size 5 (Conv2 -> Pool2 -> LRN2 of the full model): one wave per output
-// pixel, 4 channels per lane (8-B loads and stores), LRN neighbours from the adjacent lanes by
-// ds_bpermute — the fp32 maxpool_lrn256_kernel's scheme (pool_lrn.hip). Same maxima and the same
-// ascending 5-term sums of squares as pool_lrn_bf16_kernel: bit-identical, without the LDS tile.
-template <int F>
+// pool + LRN for C = 256, size 5 (Conv2 -> Pool2 -> LRN2 of the full model). A half-wave owns one
+// output pixel, 8 channels per lane (16-B loads and stores), and a wave walks U pixel pairs per
+// step with all 9U loads in flight (one wave per 4-channel pixel was latency-bound: 74 us at 256
+// images for 124 MB). LRN neighbours c-2, c-1 / c+8, c+9 come from the adjacent lanes' maxima by
+// ds_bpermute, zero past each pixel's channel ends. Same maxima and the same ascending 5-term sums
+// of squares as pool_lrn_bf16_kernel: bit-identical, without the LDS tile.
+template <int F, int U>
 __global__ void __launch_bounds__(256) pool_lrn256_bf16_kernel(const bf16* __restrict__ x, int P, int H, int W,
                                                                int S, int Ho, int Wo, float a, float beta, float k,
                                                                OutViewB o) {
   constexpr int C = 256;
-  using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
-  const int lane = threadIdx.x & 63;
-  // a wave loops over pixels when ANX_LRN_WAVE_WGS caps the grid (measured no faster than one wave per pixel)
-  for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < P; p += gridDim.x * 4) {  // wave-uniform
-  const int ox = p % Wo;
-  const int q = p / Wo;
-  const int oy = q % Ho, n = q / Ho;
-  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  const int lane = threadIdx.x & 63, half = lane >> 5, cl = lane & 31;
+  const int nw = gridDim.x * 4;
+  for (int base = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 * U; base < P; base += nw * 2 * U) {  // wave-uniform
+    float m[U][8];
+    int pix[U];
 #pragma unroll
-  for (int fh = 0; fh < F; ++fh) {
-    const int iy = oy * S + fh;
-    if (iy >= H) break;
+    for (int u = 0; u < U; ++u) {
+      const int p = base + 2 * u + half;
+      pix[u] = p;
 #pragma unroll
-    for (int fw = 0; fw < F; ++fw) {
-      const int ix = ox * S + fw;
-      if (ix >= W) break;
-      const bf16x4 v = *reinterpret_cast<const bf16x4*>(x + ((static_cast<size_t>(n) * H + iy) * W + ix) * C + lane * 4);
+      for (int e = 0; e < 8; ++e) m[u][e] = -INFINITY;
+      if (p >= P) continue;
+      const int ox = p % Wo, q = p / Wo, oy = q % Ho, n = q / Ho;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], static_cast<float>(v[e]));
+      for (int fh = 0; fh < F; ++fh) {
+        const int iy = oy * S + fh;
+#pragma unroll
+        for (int fw = 0; fw < F; ++fw) {
+          const int ix = ox * S + fw;
+          if (iy < H && ix < W) {
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((static_cast<size_t>(n) * H + iy) * W + ix) * C + cl * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m[u][e] = fmaxf(m[u][e], static_cast<float>(v[e]));
+          }
+        }
+      }
     }
-  }
-  const int left = ((lane + 63) & 63) * 4, right = ((lane + 1) & 63) * 4;
-  float l0 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(m[2])));
-  float l1 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(m[3])));
-  float r0 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(m[0])));
-  float r1 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(m[1])));
-  if (lane == 0) l0 = l1 = 0.f;
-  if (lane == 63) r0 = r1 = 0.f;
-  const float w[8] = {l0, l1, m[0], m[1], m[2], m[3], r0, r1};
-  bf16x4 r;
+    const int left = ((lane + 63) & 63) * 4, right = ((lane + 1) & 63) * 4;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float s2 = 0.f;
+    for (int u = 0; u < U; ++u) {
+      float l0 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(m[u][6])));
+      float l1 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(m[u][7])));
+      float r0 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(m[u][0])));
+      float r1 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(m[u][1])));
+      if (cl == 0) l0 = l1 = 0.f;
+      if (cl == 31) r0 = r1 = 0.f;
+      const int p = pix[u];
+      if (p >= P) continue;
+      const float w[12] = {l0, l1, m[u][0], m[u][1], m[u][2], m[u][3], m[u][4], m[u][5], m[u][6], m[u][7], r0, r1};
+      bf16x8 r;
 #pragma unroll
-    for (int u = e; u < e + 5; ++u) s2 = fmaf(w[u], w[u], s2);
-    r[e] = static_cast<bf16>(w[e + 2] / powf(k + a * s2, beta));
-  }
-  *reinterpret_cast<bf16x4*>(o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
-                             o.c_off + lane * 4) = r;
+      for (int e = 0; e < 8; ++e) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int t = e; t < e + 5; ++t) s2 = fmaf(w[t], w[t], s2);
+        r[e] = static_cast<bf16>(w[e + 2] / powf(k + a * s2, beta));
+      }
+      const int ox = p % Wo, q = p / Wo, oy = q % Ho, n = q / Ho;
+      *reinterpret_cast<bf16x8*>(o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
+                                 o.c_off + cl * 8) = r;
+    }
   }
 }
 
@@ -755,19 +769,17 @@ hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S,
 }
 
 hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
-                            float beta, float k, LrnMode mode, OutViewB out, hipStream_t s) {
+                            float beta, float k, LrnMode mode, OutViewB out, hipStream_t s, int tile) {
   const int Ho = pool_out_dim(H, F, S), Wo = pool_out_dim(W, F, S);
   const long P = static_cast<long>(N) * Ho * Wo;
   if (P == 0) return hipSuccess;
   if (C % 8 || out.Cb % 8 || out.c_off % 8 || C > 8192) return hipErrorInvalidValue;
   const int PP = C >= 4096 ? 1 : 4096 / C;
   const float a = mode == LrnMode::DivN ? alpha / size : alpha;
-  const char* tile = std::getenv("ANX_BF16_LRN_TILE");  // 1: the LDS-tile kernel (A/B, bitwise test)
-  if (C == 256 && size == 5 && F == 3 && P < (1L << 31) && !(tile && tile[0] == '1')) {
-    const char* cap = std::getenv("ANX_LRN_WAVE_WGS");  // grid cap (A/B; 0 = one wave per pixel)
-    const long wgs_cap = cap ? std::atol(cap) : 0;
-    const long wgs = wgs_cap > 0 ? std::min((P + 3) / 4, wgs_cap) : (P + 3) / 4;
-    pool_lrn256_bf16_kernel<3><<<static_cast<unsigned>(wgs), 256, 0, s>>>(
+  if (C == 256 && size == 5 && F == 3 && P < (1L << 31) && !tile) {
+    constexpr int U = 2;  // pixel pairs per wave step
+    const long waves = (P + 2 * U - 1) / (2 * U);
+    pool_lrn256_bf16_kernel<3, U><<<static_cast<unsigned>((waves + 3) / 4), 256, 0, s>>>(
         static_cast<const bf16*>(x), static_cast<int>(P), H, W, S, Ho, Wo, a, beta, k, out);
     return hipGetLastError();
   }

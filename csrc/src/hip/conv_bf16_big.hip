@@ -45,6 +45,8 @@ struct ArgsW {
   bf16* out;
   int M, HoWo, Wo, Hp, Wp, C, S, Cg, Kg, kpad, kpad_n, ktiles, n_ntiles, m_tiles;
   int Hb, Wb, Cb, h_off, w_off, c_off, relu;
+  int kt_per;  // K tiles per blockIdx.y slice (split-K; = ktiles when not split)
+  float* ws;   // split-K: fp32 partial slabs [gridDim.y][M][Kg] (no bias / ReLU)
 };
 
 __device__ __forceinline__ void glds16(const bf16* g, lds_b16* l) { __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0); }
@@ -53,8 +55,10 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// BM x BN output tile, WGM x WGN waves (WM = BM/WGM rows, WN = BN/WGN columns per wave).
-template <int BM, int BN, int WGM, int WGN>
+// BM x BN output tile, WGM x WGN waves (WM = BM/WGM rows, WN = BN/WGN columns per wave). SLAB:
+// split-K partial (K tiles [y*kt_per, (y+1)*kt_per) of slice y = blockIdx.y) stored as fp32 straight
+// from the accumulators into slab y (groups == 1; the reduce adds bias and ReLU).
+template <int BM, int BN, int WGM, int WGN, bool SLAB>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
@@ -140,13 +144,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   // block starts at a multiple of 16 rows, so the swizzle phase is ((lane & 15) >> 1) & 7
   const int hq = lane >> 4, sw = (lane >> 1) & 7;
   const int arow = (wm * WM + (lane & 15)) * kBK, brow = (BM + wn * WN + (lane & 15)) * kBK;
-  const int total = a.ktiles;
-  issue(0, 0);
+  const int kt0 = blockIdx.y * a.kt_per, total = min(a.ktiles - kt0, a.kt_per);
+  if (total > 0) issue(kt0, 0);
   for (int it = 0; it < total; ++it) {
     wait_vm<0>();                  // this lane's DMA pieces of tile it landed
     __builtin_amdgcn_s_barrier();  // ... every lane's; and every wave is done reading tile it-1
     asm volatile("" ::: "memory");
-    if (it + 1 < total) issue(it + 1, (it + 1) & 1);
+    if (it + 1 < total) issue(kt0 + it + 1, (it + 1) & 1);
     const bf16* base = lds_b + (it & 1) * STAGE;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -165,11 +169,27 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
     }
     __builtin_amdgcn_s_setprio(0);
   }
+  const int ncol = lane & 15;
+  if constexpr (SLAB) {  // 16 consecutive fp32 columns x 4 rows per store instruction
+    float* ws = a.ws + static_cast<size_t>(blockIdx.y) * a.M * a.Kg;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int f = n0 + wn * WN + j * 16 + ncol;
+      if (f >= a.Kg) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wm * WM + i * 16 + hq * 4 + e;
+          if (m < a.M) ws[static_cast<size_t>(m) * a.Kg + f] = acc[i][j][e];
+        }
+    }
+    return;
+  }
   // epilogue: the tile through LDS (all DMA retired above; wait for every wave's last reads)
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   bf16* E = lds_b;
-  const int ncol = lane & 15;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int nl = wn * WN + j * 16 + ncol, f = n0 + nl;
@@ -243,9 +263,29 @@ int pick_bf16_big_cfg(const ConvPlanB& p, const OutViewB& out, int cus) {
   return best;
 }
 
+// Fully-connected layers (M = batch, 1x1): one M tile of 256 rows when it holds the batch (each
+// weight tile streamed once), 128 columns per tile, and K split so that tiles x slices fill the CUs
+// with >= 4 K tiles per slice.
+BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus) {
+  BigFc r{-1, 1};
+  if (p.Ho != 1 || p.Wo != 1 || p.groups != 1 || p.Kg % 8) return r;
+  const OutViewB probe{reinterpret_cast<__bf16*>(16), 1, 1, p.Kg, 0, 0, 0};
+  r.cfg = p.N <= 128 ? 3 : 1;
+  if (!conv_bf16_big_ok(p, r.cfg, probe)) return BigFc{-1, 1};
+  const BigCfg& c = kCfg[r.cfg];
+  const long tiles = (p.N + c.BM - 1) / c.BM * ((p.Kg + c.BN - 1) / c.BN);
+  const int ktiles = p.kpad / kBK;
+  const long want = (static_cast<long>(cus) * c.wgs_per_cu + tiles - 1) / tiles;
+  r.ksplit = static_cast<int>(std::max<long>(1, std::min<long>(want, ktiles / 4)));
+  return r;
+}
+
 hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const void* wpacked, const int* koff,
-                           const float* bias, OutViewB out, bool relu, hipStream_t s) {
+                           const float* bias, OutViewB out, bool relu, hipStream_t s, SplitK split) {
   if (!conv_bf16_big_ok(p, cfg, out)) return hipErrorInvalidValue;
+  const int ksplit = std::max(1, split.ksplit);
+  const bool slab = split.ws != nullptr;  // fp32 slabs (also at ksplit 1: an fp32 result via the reduce)
+  if ((ksplit > 1 && !slab) || (slab && p.groups != 1)) return hipErrorInvalidValue;
   const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
   if (M == 0) return hipSuccess;
   const BigCfg c = kCfg[cfg];
@@ -276,14 +316,22 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   a.w_off = out.w_off;
   a.c_off = out.c_off;
   a.relu = relu ? 1 : 0;
-  const dim3 grid(static_cast<unsigned>(a.m_tiles * a.n_ntiles), 1, p.groups);
+  a.kt_per = (a.ktiles + ksplit - 1) / ksplit;
+  a.ws = split.ws;
+  const dim3 grid(static_cast<unsigned>(a.m_tiles * a.n_ntiles), ksplit, p.groups);
   const size_t lds = lds_bytes(c, p.kpad);
   static const hipError_t attr = [] {
-    const void* ks[] = {reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 256, 2, 4>),
-                        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 128, 4, 2>),
-                        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 96, 4, 2>),
-                        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 128, 2, 2>),
-                        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 96, 2, 2>)};
+    const void* ks[] = {
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 256, 2, 4, false>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 128, 4, 2, false>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 96, 4, 2, false>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 128, 2, 2, false>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 96, 2, 2, false>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 256, 2, 4, true>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 128, 4, 2, true>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 96, 4, 2, true>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 128, 2, 2, true>),
+        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 96, 2, 2, true>)};
     for (const void* k : ks) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
@@ -291,14 +339,22 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
     return hipSuccess;
   }();
   if (attr != hipSuccess) return attr;
+#define ANX_BIG(BM, BN, WGM, WGN)                                                           \
+  do {                                                                                      \
+    if (slab)                                                                               \
+      conv_bf16_big_kernel<BM, BN, WGM, WGN, true><<<grid, c.threads, lds, s>>>(a);         \
+    else                                                                                    \
+      conv_bf16_big_kernel<BM, BN, WGM, WGN, false><<<grid, c.threads, lds, s>>>(a);        \
+  } while (0)
   switch (cfg) {
-    case 0: conv_bf16_big_kernel<256, 256, 2, 4><<<grid, c.threads, lds, s>>>(a); break;
-    case 1: conv_bf16_big_kernel<256, 128, 4, 2><<<grid, c.threads, lds, s>>>(a); break;
-    case 2: conv_bf16_big_kernel<256, 96, 4, 2><<<grid, c.threads, lds, s>>>(a); break;
-    case 3: conv_bf16_big_kernel<128, 128, 2, 2><<<grid, c.threads, lds, s>>>(a); break;
-    case 4: conv_bf16_big_kernel<128, 96, 2, 2><<<grid, c.threads, lds, s>>>(a); break;
+    case 0: ANX_BIG(256, 256, 2, 4); break;
+    case 1: ANX_BIG(256, 128, 4, 2); break;
+    case 2: ANX_BIG(256, 96, 4, 2); break;
+    case 3: ANX_BIG(128, 128, 2, 2); break;
+    case 4: ANX_BIG(128, 96, 2, 2); break;
     default: return hipErrorInvalidValue;
   }
+#undef ANX_BIG
   return hipGetLastError();
 }
 

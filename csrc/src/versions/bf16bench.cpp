@@ -34,7 +34,10 @@ const Layer kLayers[] = {{"conv1p", 57, 57, 48, 96, 3},
                          {"conv2", 31, 31, 96, 256, 5},
                          {"conv3", 15, 15, 256, 384, 3},
                          {"conv4", 15, 15, 384, 384, 3},
-                         {"conv5", 15, 15, 384, 256, 3}};
+                         {"conv5", 15, 15, 384, 256, 3},
+                         {"fc6", 1, 1, 9216, 4096, 1},
+                         {"fc7", 1, 1, 4096, 4096, 1},
+                         {"fc8", 1, 1, 4096, 1000, 1}};
 float bf2f(uint16_t b) {
   const uint32_t u = static_cast<uint32_t>(b) << 16;
   float f;
@@ -91,15 +94,45 @@ int main(int argc, char** argv) {
     ck(hipMemcpy(db, hb.data(), L.K * 4, hipMemcpyHostToDevice), "H2D");
     const hip::OutViewB o0{static_cast<__bf16*>(dy0), p.Ho, p.Wo, L.K, 0, 0, 0};
     const hip::OutViewB o1{static_cast<__bf16*>(dy1), p.Ho, p.Wo, L.K, 0, 0, 0};
-    // arms: -2 register-staged 128x128, -1 LDS-DMA ring 128x128, 0.. wide-tile configs
+    // arms: -2 register-staged 128x128 (unsplit), -1 LDS-DMA ring 128x128 (the legacy FC split-K),
+    // c = wide-tile config c; FC layers: 100*ks + c = config c with K split ks ways (+ reduce)
+    const bool fc = L.Hp == 1;
     std::vector<int> arms = {-2, -1};
-    for (int c = 0; c < hip::conv_bf16_big_cfgs(); ++c)
-      if (hip::conv_bf16_big_ok(p, c, o1)) arms.push_back(c);
+    for (int c = 0; c < hip::conv_bf16_big_cfgs(); ++c) {
+      if (!hip::conv_bf16_big_ok(p, c, o1)) continue;
+      if (!fc) {
+        arms.push_back(c);
+        continue;
+      }
+      for (int ks : {1, 2, 4, 8, 16})
+        if (ks * 4 <= p.kpad / 64 && (c == 0 || c == 1 || c == 3)) arms.push_back(100 * ks + c);
+    }
+    float* dws = nullptr;
+    if (fc) ck(hipMalloc(&dws, static_cast<size_t>(16) * N * L.K * 4), "malloc ws");
+    const int ks_legacy = hip::fc_split_k(p);
     auto run = [&](int arm) {
-      if (arm == -2) ck(hip::conv2d_bf16(p, dx, dw, dko, db, o0, nullptr, true, s, {}, 0), "conv2d_bf16");
-      else if (arm == -1) ck(hip::conv2d_bf16(p, dx, dw, dko, db, o1, nullptr, true, s, {}, 2), "conv2d_bf16 glds");
-      else ck(hip::conv2d_bf16_big(p, arm, dx, dw, dko, db, o1, true, s), "conv2d_bf16_big");
+      if (arm == -2) {
+        ck(hip::conv2d_bf16(p, dx, dw, dko, db, o0, nullptr, true, s, {}, 0), "conv2d_bf16");
+      } else if (arm == -1) {
+        if (fc && ks_legacy > 1) {
+          ck(hip::conv2d_bf16(p, dx, dw, dko, db, o1, nullptr, true, s, hip::SplitK{ks_legacy, dws}, 2), "legacy split");
+          ck(hip::splitk_reduce_bf16(dws, ks_legacy, N, L.K, db, true, o1, nullptr, s), "reduce");
+        } else {
+          ck(hip::conv2d_bf16(p, dx, dw, dko, db, o1, nullptr, true, s, {}, 2), "conv2d_bf16 glds");
+        }
+      } else if (arm >= 100) {
+        const int ks = arm / 100, c = arm % 100;
+        ck(hip::conv2d_bf16_big(p, c, dx, dw, dko, db, o1, true, s, hip::SplitK{ks, dws}), "big split");
+        ck(hip::splitk_reduce_bf16(dws, ks, N, L.K, db, true, o1, nullptr, s), "reduce");
+      } else {
+        ck(hip::conv2d_bf16_big(p, arm, dx, dw, dko, db, o1, true, s), "conv2d_bf16_big");
+      }
     };
+    if (fc) {
+      const hip::BigFc f = hip::pick_bf16_big_fc(p);
+      std::printf("%s: legacy ksplit %d, picker cfg %d ksplit %d (arm %d)\n", L.name, ks_legacy, f.cfg, f.ksplit,
+                  100 * f.ksplit + f.cfg);
+    }
     std::vector<uint16_t> y0(ny), y1(ny);
     run(-2);
     ck(hipMemcpy(y0.data(), dy0, ny * 2, hipMemcpyDeviceToHost), "D2H");
@@ -139,7 +172,8 @@ int main(int argc, char** argv) {
       std::printf("{\"layer\": \"%s\", \"batch\": %d, \"arm\": %d, \"ms_median\": %.4f, \"ms_min\": %.4f, \"tflops\": %.1f}\n",
                   L.name, N, arms[a], med, ms[a][0], flop / med / 1e9);
     }
-    for (void* q : {dx, dw, static_cast<void*>(dko), static_cast<void*>(db), dy0, dy1}) (void)hipFree(q);
+    for (void* q : {dx, dw, static_cast<void*>(dko), static_cast<void*>(db), dy0, dy1, static_cast<void*>(dws)})
+      if (q) (void)hipFree(q);
   }
   return 0;
 }

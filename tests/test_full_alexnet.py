@@ -89,10 +89,32 @@ def test_bf16_lds_dma_kernel_matches_register_staged(cuda, mode):
     products in the same order as the register-staged kernel: logits bit-identical."""
     N = 160
     x = (init_input(N, "rand", seed=6) * 10).to(cuda)
-    ref = AlexNetFull(seed=6, device=cuda, max_batch=N, knobs={"bf16_glds": 0})(x).clone()
-    got = AlexNetFull(seed=6, device=cuda, max_batch=N, knobs={"bf16_glds": mode})(x)
+    ref = AlexNetFull(seed=6, device=cuda, max_batch=N, knobs={"bf16_glds": 0, "bf16_big": -2})(x).clone()
+    got = AlexNetFull(seed=6, device=cuda, max_batch=N, knobs={"bf16_glds": mode, "bf16_big": -2})(x)
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4])
+def test_bf16_wide_tile_kernel_matches_register_staged(cuda, cfg):
+    """The wide-tile kernel (conv_bf16_big.hip; -1 = the cost model's per-layer pick, else that
+    config forced wherever it fits) sums each output's products in the register-staged kernel's
+    order: conv1..pool5 activations bit-identical. FC6-8 run K split another number of ways, so
+    they agree to summation order only."""
+    N = 37  # partial M tiles everywhere
+    x = (init_input(N, "rand", seed=12) * 10).to(cuda)
+    ref_m = AlexNetFull(seed=12, device=cuda, max_batch=N, knobs={"bf16_glds": 0, "bf16_big": -2})
+    ref = ref_m(x).double()
+    ref_taps = [ref_m.tap(i, N) for i in range(10)]
+    m = AlexNetFull(seed=12, device=cuda, max_batch=N, knobs={"bf16_big": cfg})
+    got = m(x).double()
+    for i in range(8):
+        assert torch.equal(m.tap(i, N), ref_taps[i]), i
+    for i in (8, 9):
+        t, r = m.tap(i, N).double(), ref_taps[i].double()
+        assert ((t - r).norm() / r.norm()).item() < 1e-2, i
+    assert ((got - ref).norm() / ref.norm()).item() < 1e-2
 
 
 @pytest.mark.gpu
@@ -113,15 +135,14 @@ def test_full_conv1_polyphase_matches_taps8(cuda, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("lrn", ["div_n", "raw"])
-def test_bf16_pool_lrn_wave_kernel_bitwise(cuda, monkeypatch, lrn):
-    """Pool2+LRN2 as one wave per pixel (bpermute neighbours, default) against the LDS-tile kernel
-    (ANX_BF16_LRN_TILE=1): same maxima, same ascending sums -> logits bit-identical."""
-    N = 24
+def test_bf16_pool_lrn_wave_kernel_bitwise(cuda, lrn):
+    """Pool2+LRN2 as half-wave pixels (bpermute neighbours, default) against the LDS-tile kernel
+    (knob bf16_lrn_tile=1): same maxima, same ascending sums -> logits bit-identical."""
+    N = 25  # odd pixel count: the last wave step holds a lone pixel
     x = (init_input(N, "rand", seed=9) * 10).to(cuda)
-    monkeypatch.setenv("ANX_BF16_LRN_TILE", "1")
-    m = AlexNetFull(seed=9, device=cuda, max_batch=N, lrn_mode=lrn)
+    m = AlexNetFull(seed=9, device=cuda, max_batch=N, lrn_mode=lrn, knobs={"bf16_lrn_tile": 1})
     ref = m(x).clone()
-    monkeypatch.delenv("ANX_BF16_LRN_TILE")
+    m.set_knob("bf16_lrn_tile", 0)
     got = m(x)
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
