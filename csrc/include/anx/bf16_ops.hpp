@@ -47,8 +47,10 @@ hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, c
                        OutViewB out, float* out_f32, bool relu, hipStream_t s, SplitK split = {}, int glds = 2);
 // Wide-tile kernel (conv_bf16_big.hip): 1 workgroup per CU, 8 waves over a 256-row tile, LDS-DMA
 // double buffer, 16x16x32 MFMA, LDS-transposed epilogue with 16-B stores. Same packed weights / koff
-// as conv2d_bf16 (vec8, non-taps8 plans); bf16 output only. cfg: 0 = 256x256, 1 = 256x128,
-// 2 = 256x96, 3 = 128x128 (4 waves), 4 = 128x96 (4 waves).
+// as conv2d_bf16 (vec8, non-taps8 plans; the koff table is recomputed in arithmetic); bf16 output
+// only. cfg (BM x BN, waves, LDS stages): 0 = 256x256 8w 2, 1 = 256x128 8w 2, 2 = 256x96 8w 2,
+// 3 = 128x128 4w 2, 4 = 128x96 4w 2, 5 = 256x128 8w 3, 6 = 128x128 4w 3, 7 = 128x96 4w 3,
+// 8 = 256x64 8w 3 (FC).
 int conv_bf16_big_cfgs();
 bool conv_bf16_big_ok(const ConvPlanB& p, int cfg, const OutViewB& out);
 // The config a cost model of wave quantization picks for this launch (-1: none applies).

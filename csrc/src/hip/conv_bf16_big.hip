@@ -43,7 +43,7 @@ struct ArgsW {
   const int* koff;
   const float* bias;
   bf16* out;
-  int M, HoWo, Wo, Hp, Wp, C, S, Cg, Kg, kpad, kpad_n, ktiles, n_ntiles, m_tiles;
+  int M, HoWo, Wo, Hp, Wp, C, S, F, Cg, Kg, kpad, kpad_n, ktiles, n_ntiles, m_tiles;
   int Hb, Wb, Cb, h_off, w_off, c_off, relu;
   int kt_per;  // K tiles per blockIdx.y slice (split-K; = ktiles when not split)
   float* ws;   // split-K: fp32 partial slabs [gridDim.y][M][Kg] (no bias / ReLU)
@@ -55,10 +55,11 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// BM x BN output tile, WGM x WGN waves (WM = BM/WGM rows, WN = BN/WGN columns per wave). SLAB:
-// split-K partial (K tiles [y*kt_per, (y+1)*kt_per) of slice y = blockIdx.y) stored as fp32 straight
-// from the accumulators into slab y (groups == 1; the reduce adds bias and ReLU).
-template <int BM, int BN, int WGM, int WGN, bool SLAB>
+// BM x BN output tile, WGM x WGN waves (WM = BM/WGM rows, WN = BN/WGN columns per wave), NST LDS
+// stages (NST - 1 K tiles in flight behind the one being multiplied). SLAB: split-K partial (K tiles
+// [y*kt_per, (y+1)*kt_per) of slice y = blockIdx.y) stored as fp32 straight from the accumulators
+// into slab y (groups == 1; the reduce adds bias and ReLU).
+template <int BM, int BN, int WGM, int WGN, int NST, bool SLAB>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
@@ -69,10 +70,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   constexpr int STAGE = (BM + BN) * kBK;            // bf16 per stage
   constexpr int CH = BN / 8;                        // 16-B chunks per epilogue row
   constexpr int XM = (CH % 8 == 0) ? 7 : (CH % 4 == 0) ? 3 : (CH % 2 == 0) ? 1 : 0;
-  static_assert(BM * BN <= 2 * STAGE, "the epilogue image fits in the two stages");
+  static_assert(BM * BN <= NST * STAGE, "the epilogue image fits in the stages");
+  static_assert(NST == 2 || UNITS % NT == 0, "counted vmcnt: every wave issues NJ pieces per stage");
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
-  int* koff_s = reinterpret_cast<int*>(lds_b + 2 * STAGE);
-  int* ooff_s = koff_s + a.kpad;
+  int* ooff_s = reinterpret_cast<int*>(lds_b + NST * STAGE);  // output offset per tile row (-1 past M)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, g = blockIdx.z;
@@ -87,7 +88,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   const int m0 = mt * BM, n0 = nt * BN;
   const bf16* x = a.x + g * a.Cg;
   const bf16* wg = a.w + static_cast<size_t>(g) * a.kpad_n * a.kpad;
-  for (int i = tid; i < a.kpad; i += NT) koff_s[i] = a.koff[i];
   for (int i = tid; i < BM; i += NT) {
     const int m = m0 + i;
     int oo = -1;
@@ -120,12 +120,31 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
       src[j] = wg + static_cast<size_t>(n) * a.kpad + u * 8;  // + kb per stage
     }
   }
-  __syncthreads();  // koff_s / ooff_s visible
+  __syncthreads();  // ooff_s visible
   lds_b16* lds3 = (lds_b16*)(lds_b);
+  const int kt0 = blockIdx.y * a.kt_per, total = min(a.ktiles - kt0, a.kt_per);
+  // This lane's K unit k = kt*64 + 8u as (filter row fh, column fw, channel c): the packer's k order
+  // (fh*F + fw)*Cg + c, so its input offset is (fh*Wp + fw)*C + c — the koff table in arithmetic,
+  // advanced by one K tile per issue (the issues run in K order). fh == F: K padding (zero-packed
+  // weights then meet pixel data at offset 0).
+  int uc, ufw, ufh;
+  {
+    const int k = kt0 * kBK + u * 8, tap = k / a.Cg;
+    uc = k - tap * a.Cg;
+    ufh = tap / a.F;
+    ufw = tap - ufh * a.F;
+  }
   auto issue = [&](int kt, int st) {
     const int kb = kt * kBK;
-    const int kr = koff_s[kb + u * 8];
-    const int ko = kr >= 0 ? kr : 0;  // K padding: zero-packed weights meet pixel data
+    const int ko = ufh < a.F ? (ufh * a.Wp + ufw) * a.C + uc : 0;
+    uc += kBK;
+    while (uc >= a.Cg) {
+      uc -= a.Cg;
+      if (++ufw == a.F) {
+        ufw = 0;
+        ++ufh;
+      }
+    }
     lds_b16* dst = lds3 + st * STAGE;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -144,14 +163,21 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   // block starts at a multiple of 16 rows, so the swizzle phase is ((lane & 15) >> 1) & 7
   const int hq = lane >> 4, sw = (lane >> 1) & 7;
   const int arow = (wm * WM + (lane & 15)) * kBK, brow = (BM + wn * WN + (lane & 15)) * kBK;
-  const int kt0 = blockIdx.y * a.kt_per, total = min(a.ktiles - kt0, a.kt_per);
-  if (total > 0) issue(kt0, 0);
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i)
+    if (i < total) issue(kt0 + i, i);
+  int st = 0, st_free = NST - 1;  // stage of tile it; stage of tile it-1 (free once all waves pass)
   for (int it = 0; it < total; ++it) {
-    wait_vm<0>();                  // this lane's DMA pieces of tile it landed
+    if (it + NST - 2 < total)
+      wait_vm<NJ * (NST - 2)>();   // this lane's pieces of tile it landed (later tiles may fly)
+    else
+      wait_vm<0>();
     __builtin_amdgcn_s_barrier();  // ... every lane's; and every wave is done reading tile it-1
     asm volatile("" ::: "memory");
-    if (it + 1 < total) issue(kt0 + it + 1, (it + 1) & 1);
-    const bf16* base = lds_b + (it & 1) * STAGE;
+    if (it + NST - 1 < total) issue(kt0 + it + NST - 1, st_free);
+    st_free = st_free + 1 == NST ? 0 : st_free + 1;
+    const bf16* base = lds_b + st * STAGE;
+    st = st + 1 == NST ? 0 : st + 1;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < kBK / 32; ++s) {
@@ -215,19 +241,20 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
 }
 
 struct BigCfg {
-  int BM, BN, threads;
-  int wgs_per_cu;  // co-resident workgroups (LDS / registers) at AlexNet's kpad
+  int BM, BN, threads, nst;
+  int wgs_per_cu;  // co-resident workgroups (LDS / registers)
   float eff;       // relative per-CU MFMA efficiency (anx_bf16bench, 256 images)
 };
-constexpr BigCfg kCfg[] = {{256, 256, 512, 1, 1.0f},
-                           {256, 128, 512, 1, 0.86f},
-                           {256, 96, 512, 1, 0.8f},
-                           {128, 128, 256, 2, 0.92f},
-                           {128, 96, 256, 2, 0.85f}};
+// eff of the 3-stage configs: 0.55-0.8 of cfg 0 on conv2-5 (deeper prefetch does not pay where a
+// K tile's MFMA work already covers the DMA; it takes LDS the 2-stage 128-row configs use for a
+// second workgroup per CU) - they serve the FC layers.
+constexpr BigCfg kCfg[] = {{256, 256, 512, 2, 1, 1.0f},  {256, 128, 512, 2, 1, 0.86f}, {256, 96, 512, 2, 1, 0.8f},
+                           {128, 128, 256, 2, 2, 0.92f}, {128, 96, 256, 2, 2, 0.85f},  {256, 128, 512, 3, 1, 0.7f},
+                           {128, 128, 256, 3, 1, 0.6f},  {128, 96, 256, 3, 1, 0.5f},   {256, 64, 512, 3, 1, 0.6f}};
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 
-size_t lds_bytes(const BigCfg& c, int kpad) {
-  return static_cast<size_t>(2) * (c.BM + c.BN) * kBK * 2 + static_cast<size_t>(kpad + c.BM) * 4;
+size_t lds_bytes(const BigCfg& c) {
+  return static_cast<size_t>(c.nst) * (c.BM + c.BN) * kBK * 2 + static_cast<size_t>(c.BM) * 4;
 }
 
 }  // namespace
@@ -237,7 +264,7 @@ int conv_bf16_big_cfgs() { return kNumCfg; }
 bool conv_bf16_big_ok(const ConvPlanB& p, int cfg, const OutViewB& out) {
   if (cfg < 0 || cfg >= kNumCfg) return false;
   return p.vec8 && !p.taps8 && p.Kg % 8 == 0 && out.Cb % 8 == 0 && out.c_off % 8 == 0 && out.base &&
-         lds_bytes(kCfg[cfg], p.kpad) <= 160 * 1024 && static_cast<long>(p.N) * p.Hp * p.Wp * p.C < (1L << 31) &&
+         lds_bytes(kCfg[cfg]) <= 160 * 1024 && static_cast<long>(p.N) * p.Hp * p.Wp * p.C < (1L << 31) &&
          static_cast<long>(p.N) * out.Hb * out.Wb * out.Cb < (1L << 31);
 }
 
@@ -263,14 +290,16 @@ int pick_bf16_big_cfg(const ConvPlanB& p, const OutViewB& out, int cus) {
   return best;
 }
 
-// Fully-connected layers (M = batch, 1x1): one M tile of 256 rows when it holds the batch (each
-// weight tile streamed once), 128 columns per tile, and K split so that tiles x slices fill the CUs
-// with >= 4 K tiles per slice.
+// Fully-connected layers (M = batch, 1x1): 256-row tiles (the whole batch at 256: each weight tile
+// streamed once) x 64 columns over 8 waves with 3 LDS stages (cfg 8), K split so that tiles x
+// slices ~ one workgroup per CU with >= 4 K tiles per slice. Measured at 256 images
+// (profiles/r02_bf16bench_b256.txt): FC6 36 us, FC7 23 us, FC8 18 us with the reduce, against 43 /
+// 28 / 24 us for the 128x128 split-K path.
 BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus) {
   BigFc r{-1, 1};
   if (p.Ho != 1 || p.Wo != 1 || p.groups != 1 || p.Kg % 8) return r;
   const OutViewB probe{reinterpret_cast<__bf16*>(16), 1, 1, p.Kg, 0, 0, 0};
-  r.cfg = p.N <= 128 ? 3 : 1;
+  r.cfg = 8;
   if (!conv_bf16_big_ok(p, r.cfg, probe)) return BigFc{-1, 1};
   const BigCfg& c = kCfg[r.cfg];
   const long tiles = (p.N + c.BM - 1) / c.BM * ((p.Kg + c.BN - 1) / c.BN);
@@ -302,6 +331,7 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   a.Wp = p.Wp;
   a.C = p.C;
   a.S = p.S;
+  a.F = p.F;
   a.Cg = p.Cg;
   a.Kg = p.Kg;
   a.kpad = p.kpad;
@@ -319,42 +349,43 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   a.kt_per = (a.ktiles + ksplit - 1) / ksplit;
   a.ws = split.ws;
   const dim3 grid(static_cast<unsigned>(a.m_tiles * a.n_ntiles), ksplit, p.groups);
-  const size_t lds = lds_bytes(c, p.kpad);
+  const size_t lds = lds_bytes(c);
+#define ANX_BIG_CFGS(X)         \
+  X(0, 256, 256, 2, 4, 2)       \
+  X(1, 256, 128, 4, 2, 2)       \
+  X(2, 256, 96, 4, 2, 2)        \
+  X(3, 128, 128, 2, 2, 2)       \
+  X(4, 128, 96, 2, 2, 2)        \
+  X(5, 256, 128, 4, 2, 3)       \
+  X(6, 128, 128, 2, 2, 3)       \
+  X(7, 128, 96, 2, 2, 3)        \
+  X(8, 256, 64, 8, 1, 3)
   static const hipError_t attr = [] {
-    const void* ks[] = {
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 256, 2, 4, false>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 128, 4, 2, false>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 96, 4, 2, false>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 128, 2, 2, false>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 96, 2, 2, false>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 256, 2, 4, true>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 128, 4, 2, true>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<256, 96, 4, 2, true>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 128, 2, 2, true>),
-        reinterpret_cast<const void*>(conv_bf16_big_kernel<128, 96, 2, 2, true>)};
-    for (const void* k : ks) {
-      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      if (e != hipSuccess) return e;
-    }
+#define ANX_ATTR(I, BM, BN, WGM, WGN, NST)                                                                    \
+  for (const void* k : {reinterpret_cast<const void*>(conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, false>),   \
+                        reinterpret_cast<const void*>(conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, true>)}) { \
+    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
+    if (e != hipSuccess) return e;                                                                            \
+  }
+    ANX_BIG_CFGS(ANX_ATTR)
+#undef ANX_ATTR
     return hipSuccess;
   }();
   if (attr != hipSuccess) return attr;
-#define ANX_BIG(BM, BN, WGM, WGN)                                                           \
-  do {                                                                                      \
-    if (slab)                                                                               \
-      conv_bf16_big_kernel<BM, BN, WGM, WGN, true><<<grid, c.threads, lds, s>>>(a);         \
-    else                                                                                    \
-      conv_bf16_big_kernel<BM, BN, WGM, WGN, false><<<grid, c.threads, lds, s>>>(a);        \
-  } while (0)
   switch (cfg) {
-    case 0: ANX_BIG(256, 256, 2, 4); break;
-    case 1: ANX_BIG(256, 128, 4, 2); break;
-    case 2: ANX_BIG(256, 96, 4, 2); break;
-    case 3: ANX_BIG(128, 128, 2, 2); break;
-    case 4: ANX_BIG(128, 96, 2, 2); break;
-    default: return hipErrorInvalidValue;
+#define ANX_CASE(I, BM, BN, WGM, WGN, NST)                                                   \
+  case I:                                                                                    \
+    if (slab)                                                                                \
+      conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, true><<<grid, c.threads, lds, s>>>(a);     \
+    else                                                                                     \
+      conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, false><<<grid, c.threads, lds, s>>>(a);    \
+    break;
+    ANX_BIG_CFGS(ANX_CASE)
+#undef ANX_CASE
+    default:
+      return hipErrorInvalidValue;
   }
-#undef ANX_BIG
+#undef ANX_BIG_CFGS
   return hipGetLastError();
 }
 

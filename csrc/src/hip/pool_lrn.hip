@@ -168,42 +168,54 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __re
   }
 }
 
-// Pool2 + LRN for C = 256 (AlexNet): one wave per pooled pixel, lane i owns channels 4i..4i+3.
-// The 9 window loads of a lane are 16 B each and the wave's loads are whole 1-KiB pixel rows; the
-// LRN neighbours (channels 4i-2, 4i-1, 4i+4, 4i+5) come from lanes i-1 / i+1 by ds_bpermute, so
-// there is no LDS tile, no barrier, and no bank conflicts. The squared-sum order is that of
-// maxpool_lrn_kernel (left to right), so both kernels give bitwise equal results.
-template <int F>
+// Pool2 + LRN for C = 256 (AlexNet): a wave owns a pooled pixel per step, lane i channels
+// 4i..4i+3, and takes U consecutive pixels per step with all 9U window loads in flight (U = 1 was
+// latency-bound at 3.7 TB/s). The 9 loads of a lane are 16 B each and a wave's loads are whole
+// 1-KiB pixel rows; the LRN neighbours (channels 4i-2, 4i-1, 4i+4, 4i+5) come from lanes i-1 / i+1
+// by ds_bpermute, so there is no LDS tile, no barrier, and no bank conflicts. The squared-sum order
+// is that of maxpool_lrn_kernel (left to right), so both kernels give bitwise equal results.
+template <int F, int U>
 __global__ void __launch_bounds__(kThreads) maxpool_lrn256_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                                   int P, int H, int W, int S, int Ho, int Wo, float a,
                                                                   float beta, float k) {
   constexpr int C = 256;
   const int lane = threadIdx.x & 63;
-  // a wave loops over pixels when ANX_LRN_WAVE_WGS caps the grid (measured no faster than one wave per pixel)
-  for (int p = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); p < P; p += gridDim.x * (kThreads / 64)) {
-  const int ox = p % Wo;
-  const int r = p / Wo;
-  const int oy = r % Ho;
-  const int n = r / Ho;
-  const f32x4 own = window_max<F>(x + nhwc(n, oy * S, ox * S, lane * 4, H, W, C), W, C);
-  // neighbours: left pair = (z, w) of lane-1, right pair = (x, y) of lane+1; zero past the edges
-  const int left = ((lane + 63) & 63) * 4, right = ((lane + 1) & 63) * 4;
-  float l0 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(own.z)));
-  float l1 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(own.w)));
-  float r0 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(own.x)));
-  float r1 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(own.y)));
-  if (lane == 0) l0 = l1 = 0.f;
-  if (lane == 63) r0 = r1 = 0.f;
-  const float w[8] = {l0, l1, own.x, own.y, own.z, own.w, r0, r1};
-  f32x4 out;
+  const int nw = gridDim.x * (kThreads / 64);
+  for (int base = (blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * U; base < P; base += nw * U) {  // wave-uniform
+    f32x4 own[U];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float sq = 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int p = base + u;
+      if (p < P) {
+        const int ox = p % Wo, r = p / Wo, oy = r % Ho, n = r / Ho;
+        own[u] = window_max<F>(x + nhwc(n, oy * S, ox * S, lane * 4, H, W, C), W, C);
+      } else {
+        own[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    // neighbours: left pair = (z, w) of lane-1, right pair = (x, y) of lane+1; zero past the edges
+    const int left = ((lane + 63) & 63) * 4, right = ((lane + 1) & 63) * 4;
 #pragma unroll
-    for (int u = e; u < e + 5; ++u) sq = fmaf(w[u], w[u], sq);
-    out[e] = w[e + 2] / powf(k + a * sq, beta);
-  }
-  *reinterpret_cast<f32x4*>(y + static_cast<size_t>(p) * C + lane * 4) = out;
+    for (int u = 0; u < U; ++u) {
+      float l0 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(own[u].z)));
+      float l1 = __int_as_float(__builtin_amdgcn_ds_bpermute(left, __float_as_int(own[u].w)));
+      float r0 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(own[u].x)));
+      float r1 = __int_as_float(__builtin_amdgcn_ds_bpermute(right, __float_as_int(own[u].y)));
+      if (lane == 0) l0 = l1 = 0.f;
+      if (lane == 63) r0 = r1 = 0.f;
+      const int p = base + u;
+      if (p >= P) continue;
+      const float w[8] = {l0, l1, own[u].x, own[u].y, own[u].z, own[u].w, r0, r1};
+      f32x4 out;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float sq = 0.f;
+#pragma unroll
+        for (int t = e; t < e + 5; ++t) sq = fmaf(w[t], w[t], sq);
+        out[e] = w[e + 2] / powf(k + a * sq, beta);
+      }
+      *reinterpret_cast<f32x4*>(y + static_cast<size_t>(p) * C + lane * 4) = out;
+    }
   }
 }
 
@@ -235,11 +247,10 @@ hipError_t maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int
   const long blocks = (P + PP - 1) / PP;
   const float a = mode == LrnMode::DivN ? alpha / static_cast<float>(size) : alpha;
   if (F == 3 && C == 256 && size == 5) {
-    const char* cap = std::getenv("ANX_LRN_WAVE_WGS");  // grid cap (A/B; 0 = one wave per pixel)
-    const long wgs_cap = cap ? std::atol(cap) : 0;
-    const long all = (P + kThreads / 64 - 1) / (kThreads / 64);
-    const unsigned g = static_cast<unsigned>(wgs_cap > 0 ? std::min(all, wgs_cap) : all);
-    maxpool_lrn256_kernel<3><<<g, kThreads, 0, s>>>(x, y, static_cast<int>(P), H, W, S, Ho, Wo, a, beta, k);
+    constexpr int U = 2;  // pixels per wave step
+    const long waves = (P + U - 1) / U;
+    const unsigned g = static_cast<unsigned>((waves + kThreads / 64 - 1) / (kThreads / 64));
+    maxpool_lrn256_kernel<3, U><<<g, kThreads, 0, s>>>(x, y, static_cast<int>(P), H, W, S, Ho, Wo, a, beta, k);
     return hipGetLastError();
   }
   if (F == 3)

@@ -105,7 +105,7 @@ int main(int argc, char** argv) {
         continue;
       }
       for (int ks : {1, 2, 4, 8, 16})
-        if (ks * 4 <= p.kpad / 64 && (c == 0 || c == 1 || c == 3)) arms.push_back(100 * ks + c);
+        if (ks * 4 <= p.kpad / 64 && ks > 1 && (c == 1 || c == 3 || c >= 5)) arms.push_back(100 * ks + c);
     }
     float* dws = nullptr;
     if (fc) ck(hipMalloc(&dws, static_cast<size_t>(16) * N * L.K * 4), "malloc ws");
