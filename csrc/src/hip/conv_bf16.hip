@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "anx/bf16_ops.hpp"
+#include "anx/lrn_math.hpp"
 
 namespace anx::hip {
 namespace {
@@ -400,7 +401,7 @@ __global__ void __launch_bounds__(256) pool_lrn_bf16_kernel(const bf16* __restri
         float s2 = 0.f;
 #pragma unroll
         for (int u = e; u < e + 5; ++u) s2 = fmaf(w[u], w[u], s2);
-        r[e] = static_cast<bf16>(w[e + 2] / powf(k + a * s2, beta));
+        r[e] = static_cast<bf16>(w[e + 2] * lrn_scale(s2, k, a, beta));
       }
     } else {
       for (int e = 0; e < 8; ++e) {
@@ -408,7 +409,7 @@ __global__ void __launch_bounds__(256) pool_lrn_bf16_kernel(const bf16* __restri
         float s2 = 0.f;
         for (int j = c - half < 0 ? 0 : c - half; j <= (c + half >= C ? C - 1 : c + half); ++j)
           s2 = fmaf(row[j], row[j], s2);
-        r[e] = static_cast<bf16>(row[c] / powf(k + a * s2, beta));
+        r[e] = static_cast<bf16>(row[c] * lrn_scale(s2, k, a, beta));
       }
     }
     const int ox = static_cast<int>(p % Wo);
@@ -481,7 +482,7 @@ __global__ void __launch_bounds__(256) pool_lrn256_bf16_kernel(const bf16* __res
         float s2 = 0.f;
 #pragma unroll
         for (int t = e; t < e + 5; ++t) s2 = fmaf(w[t], w[t], s2);
-        r[e] = static_cast<bf16>(w[e + 2] / powf(k + a * s2, beta));
+        r[e] = static_cast<bf16>(w[e + 2] * lrn_scale(s2, k, a, beta));
       }
       const int ox = p % Wo, q = p / Wo, oy = q % Ho, n = q / Ho;
       *reinterpret_cast<bf16x8*>(o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +

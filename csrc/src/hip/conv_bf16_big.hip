@@ -59,7 +59,10 @@ __device__ __forceinline__ void wait_vm() {
 // stages (NST - 1 K tiles in flight behind the one being multiplied). SLAB: split-K partial (K tiles
 // [y*kt_per, (y+1)*kt_per) of slice y = blockIdx.y) stored as fp32 straight from the accumulators
 // into slab y (groups == 1; the reduce adds bias and ReLU).
-template <int BM, int BN, int WGM, int WGN, int NST, bool SLAB>
+// PIPE: both k-steps' fragments are read up front (k-step 1's behind the next tile's DMA issue) and
+// the 2 x TM x TN MFMAs run on registers already loaded (sched_barrier-fenced), instead of the
+// compiler's read-2-wait-8-MFMA interleave that stalls both waves of a SIMD on LDS latency together.
+template <int BM, int BN, int WGM, int WGN, int NST, bool SLAB, bool PIPE = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
@@ -174,10 +177,40 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
       wait_vm<0>();
     __builtin_amdgcn_s_barrier();  // ... every lane's; and every wave is done reading tile it-1
     asm volatile("" ::: "memory");
-    if (it + NST - 1 < total) issue(kt0 + it + NST - 1, st_free);
-    st_free = st_free + 1 == NST ? 0 : st_free + 1;
     const bf16* base = lds_b + st * STAGE;
     st = st + 1 == NST ? 0 : st + 1;
+    if constexpr (PIPE) {
+      bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(base + arow + i * 16 * kBK + (hq ^ sw) * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(base + brow + j * 16 * kBK + (hq ^ sw) * 8);
+      __builtin_amdgcn_sched_barrier(0);
+      if (it + NST - 1 < total) issue(kt0 + it + NST - 1, st_free);
+      st_free = st_free + 1 == NST ? 0 : st_free + 1;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        a1[i] = *reinterpret_cast<const bf16x8*>(base + arow + i * 16 * kBK + ((4 + hq) ^ sw) * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b1[j] = *reinterpret_cast<const bf16x8*>(base + brow + j * 16 * kBK + ((4 + hq) ^ sw) * 8);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      continue;
+    }
+    if (it + NST - 1 < total) issue(kt0 + it + NST - 1, st_free);
+    st_free = st_free + 1 == NST ? 0 : st_free + 1;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < kBK / 32; ++s) {
@@ -191,24 +224,25 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
   }
-  const int ncol = lane & 15;
-  if constexpr (SLAB) {  // 16 consecutive fp32 columns x 4 rows per store instruction
+  // The MFMAs take the filters as the A operand and the pixels as B, so acc[i][j] is the 16x16 tile
+  // transposed: lane holds pixel m = ... + (lane & 15), channels n = ... + 4 * (lane >> 4) + e,
+  // e = 0..3 — four consecutive channels of one pixel (one 8-B / 16-B write instead of four).
+  const int mcol = lane & 15;
+  if constexpr (SLAB) {  // 16 pixels x 16 channels per store instruction, 16 B per lane
     float* ws = a.ws + static_cast<size_t>(blockIdx.y) * a.M * a.Kg;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int f = n0 + wn * WN + j * 16 + ncol;
-      if (f >= a.Kg) continue;
+      const int f = n0 + wn * WN + j * 16 + hq * 4;
+      if (f >= a.Kg) continue;  // Kg % 8 == 0: a 4-channel group is wholly in or out
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + wm * WM + i * 16 + hq * 4 + e;
-          if (m < a.M) ws[static_cast<size_t>(m) * a.Kg + f] = acc[i][j][e];
-        }
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * WM + i * 16 + mcol;
+        if (m < a.M) *reinterpret_cast<f32x4*>(ws + static_cast<size_t>(m) * a.Kg + f) = acc[i][j];
+      }
     }
     return;
   }
@@ -216,19 +250,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   bf16* E = lds_b;
+  using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int nl = wn * WN + j * 16 + ncol, f = n0 + nl;
-    const float bv = (a.bias && f < a.Kg) ? a.bias[g * a.Kg + f] : 0.f;
+    const int nl = wn * WN + j * 16 + hq * 4, f = n0 + nl;
+    const f32x4 bv = (a.bias && f < a.Kg) ? *reinterpret_cast<const f32x4*>(a.bias + g * a.Kg + f) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ml = wm * WM + i * 16 + hq * 4 + e;
-        float v = acc[i][j][e] + bv;
-        if (a.relu) v = fmaxf(v, 0.f);
-        E[ml * BN + (((nl >> 3) ^ (ml & XM)) << 3) + (nl & 7)] = static_cast<bf16>(v);
-      }
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * WM + i * 16 + mcol;
+      f32x4 v = acc[i][j] + bv;
+      if (a.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+      *reinterpret_cast<bf16x4*>(E + ml * BN + (((nl >> 3) ^ (ml & XM)) << 3) + (nl & 7)) =
+          bf16x4{static_cast<bf16>(v.x), static_cast<bf16>(v.y), static_cast<bf16>(v.z), static_cast<bf16>(v.w)};
+    }
   }
   __syncthreads();
   bf16* out = a.out + g * a.Kg;
@@ -245,12 +279,15 @@ struct BigCfg {
   int wgs_per_cu;  // co-resident workgroups (LDS / registers)
   float eff;       // relative per-CU MFMA efficiency (anx_bf16bench, 256 images)
 };
-// eff of the 3-stage configs: 0.55-0.8 of cfg 0 on conv2-5 (deeper prefetch does not pay where a
-// K tile's MFMA work already covers the DMA; it takes LDS the 2-stage 128-row configs use for a
-// second workgroup per CU) - they serve the FC layers.
-constexpr BigCfg kCfg[] = {{256, 256, 512, 2, 1, 1.0f},  {256, 128, 512, 2, 1, 0.86f}, {256, 96, 512, 2, 1, 0.8f},
-                           {128, 128, 256, 2, 2, 0.92f}, {128, 96, 256, 2, 2, 0.85f},  {256, 128, 512, 3, 1, 0.7f},
-                           {128, 128, 256, 3, 1, 0.6f},  {128, 96, 256, 3, 1, 0.5f},   {256, 64, 512, 3, 1, 0.6f}};
+// eff: cfg 2 vs 4 and 0 vs 4 are set so the ceil-rounds model ranks them as measured (conv1p:
+// 128x96 ahead of 256x96; conv5, 169 256x256 tiles in one partial round: 256x256 ahead of 1014
+// 128x96 tiles in two). The 3-stage configs ran 0.55-0.8 of cfg 0 on conv2-5 (deeper prefetch does
+// not pay where a K tile's MFMA work already covers the DMA, and it takes the LDS a second 128-row
+// workgroup per CU would use): they serve the FC layers. 9-11: cfgs 0, 3, 4 without PIPE (A/B).
+constexpr BigCfg kCfg[] = {{256, 256, 512, 2, 1, 1.0f},  {256, 128, 512, 2, 1, 0.86f}, {256, 96, 512, 2, 1, 0.7f},
+                           {128, 128, 256, 2, 2, 0.92f}, {128, 96, 256, 2, 2, 0.74f},  {256, 128, 512, 3, 1, 0.7f},
+                           {128, 128, 256, 3, 1, 0.6f},  {128, 96, 256, 3, 1, 0.5f},   {256, 64, 512, 3, 1, 0.6f},
+                           {256, 256, 512, 2, 1, 0.5f},  {128, 128, 256, 2, 2, 0.5f},  {128, 96, 256, 2, 2, 0.5f}};
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 
 size_t lds_bytes(const BigCfg& c) {
@@ -351,19 +388,22 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   const dim3 grid(static_cast<unsigned>(a.m_tiles * a.n_ntiles), ksplit, p.groups);
   const size_t lds = lds_bytes(c);
 #define ANX_BIG_CFGS(X)         \
-  X(0, 256, 256, 2, 4, 2)       \
-  X(1, 256, 128, 4, 2, 2)       \
-  X(2, 256, 96, 4, 2, 2)        \
-  X(3, 128, 128, 2, 2, 2)       \
-  X(4, 128, 96, 2, 2, 2)        \
-  X(5, 256, 128, 4, 2, 3)       \
-  X(6, 128, 128, 2, 2, 3)       \
-  X(7, 128, 96, 2, 2, 3)        \
-  X(8, 256, 64, 8, 1, 3)
+  X(0, 256, 256, 2, 4, 2, true)        \
+  X(1, 256, 128, 4, 2, 2, false)       \
+  X(2, 256, 96, 4, 2, 2, false)        \
+  X(3, 128, 128, 2, 2, 2, true)        \
+  X(4, 128, 96, 2, 2, 2, true)         \
+  X(5, 256, 128, 4, 2, 3, false)       \
+  X(6, 128, 128, 2, 2, 3, false)       \
+  X(7, 128, 96, 2, 2, 3, false)        \
+  X(8, 256, 64, 8, 1, 3, false)     \
+  X(9, 256, 256, 2, 4, 2, false)    \
+  X(10, 128, 128, 2, 2, 2, false)   \
+  X(11, 128, 96, 2, 2, 2, false)
   static const hipError_t attr = [] {
-#define ANX_ATTR(I, BM, BN, WGM, WGN, NST)                                                                    \
-  for (const void* k : {reinterpret_cast<const void*>(conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, false>),   \
-                        reinterpret_cast<const void*>(conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, true>)}) { \
+#define ANX_ATTR(I, BM, BN, WGM, WGN, NST, P)                                                                     \
+  for (const void* k : {reinterpret_cast<const void*>(conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, false, P>),    \
+                        reinterpret_cast<const void*>(conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, true, P>)}) {  \
     const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
     if (e != hipSuccess) return e;                                                                            \
   }
@@ -373,12 +413,12 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   }();
   if (attr != hipSuccess) return attr;
   switch (cfg) {
-#define ANX_CASE(I, BM, BN, WGM, WGN, NST)                                                   \
+#define ANX_CASE(I, BM, BN, WGM, WGN, NST, P)                                                \
   case I:                                                                                    \
     if (slab)                                                                                \
-      conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, true><<<grid, c.threads, lds, s>>>(a);     \
+      conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, true, P><<<grid, c.threads, lds, s>>>(a);  \
     else                                                                                     \
-      conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, false><<<grid, c.threads, lds, s>>>(a);    \
+      conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, false, P><<<grid, c.threads, lds, s>>>(a); \
     break;
     ANX_BIG_CFGS(ANX_CASE)
 #undef ANX_CASE

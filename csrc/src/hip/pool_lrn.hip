@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cmath>
 
+#include "anx/lrn_math.hpp"
 #include "anx/ops.hpp"
 
 namespace anx::hip {
@@ -151,7 +152,7 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __re
         float s = 0.f;
 #pragma unroll
         for (int u = e; u < e + 5; ++u) s = fmaf(w[u], w[u], s);
-        out[e] = w[e + 2] / powf(k + a * s, beta);
+        out[e] = w[e + 2] * lrn_scale(s, k, a, beta);
       }
     } else {
 #pragma unroll
@@ -161,7 +162,7 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __re
         const int hi = c + half >= C ? C - 1 : c + half;
         float s = 0.f;
         for (int j = lo; j <= hi; ++j) s = fmaf(row[j], row[j], s);
-        out[e] = row[c] / powf(k + a * s, beta);
+        out[e] = row[c] * lrn_scale(s, k, a, beta);
       }
     }
     *reinterpret_cast<f32x4*>(y + static_cast<size_t>(p) * C + c4 * 4) = out;
@@ -212,7 +213,7 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn256_kernel(const float* _
         float sq = 0.f;
 #pragma unroll
         for (int t = e; t < e + 5; ++t) sq = fmaf(w[t], w[t], sq);
-        out[e] = w[e + 2] / powf(k + a * sq, beta);
+        out[e] = w[e + 2] * lrn_scale(sq, k, a, beta);
       }
       *reinterpret_cast<f32x4*>(y + static_cast<size_t>(p) * C + lane * 4) = out;
     }
