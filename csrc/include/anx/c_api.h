@@ -116,9 +116,9 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
                    float* y, int relu, int fold_scalar, void* stream);
 /* Conv2-shaped 5x5/1 conv by Winograd F(3x3,5x5) on device buffers (test entry; allocates, syncs):
    x [N,Hq,Wq,C] (padding already in the window), KCFF weights on the HOST, y [N,Hq-4,Wq-4,K].
-   wino_cfg -1 = the default fused kernel. */
+   wino_cfg -1 = the default fused kernel; wino_split -1 = the default (auto tail split), 0 off. */
 int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
-                   const float* bias, float* y, int relu, int wino_cfg, void* stream);
+                   const float* bias, float* y, int relu, int wino_cfg, int wino_split, void* stream);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

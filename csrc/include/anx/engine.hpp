@@ -92,6 +92,7 @@ class BlocksEngine {
   int plan_key1_ = -1, plan_key2_ = -1;
   // Winograd conv2: transformed weights packed for the batched GEMM + V / M workspaces
   float *u2p_ = nullptr, *wv_ = nullptr, *wm_ = nullptr;
+  float* wsplit_ = nullptr;  // Conv2 fused GEMM tail-split slabs (hip::wino_split_ws_floats)
   int* ukoff_ = nullptr;
   int wino_key_ = -1;
   // Winograd conv1: transformed polyphase weights + V workspace (full-height tiles of chunk_ images)

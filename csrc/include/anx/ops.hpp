@@ -116,8 +116,20 @@ hipError_t wino_output(const WinoPlan& w, const float* Mt, const float* bias, fl
 // +17 %, BK 48 +3 %, XCD order +1 %); wino_prio bit0 s_setprio around the MFMA slices, bit8
 // interleaved output fold (default 257), bits 4-7 cost probes (wrong results): no fold / no refills
 // / no barrier / no stores; fold_scalar: v_fma_f32 instead of v_pk_fma_f32 folds.
+// split_ws (wino_split_ws_floats() floats, or nullptr = never split): when the launch's last round of
+// workgroups would leave CUs idle (wave quantization: 648 workgroups on 512 slots at 128 images),
+// the whole rounds run as usual and the tail point tiles run their 49 transform points split
+// nsplit ways (Knobs::wino_split: 0 off, 1 auto by a cost model, 2-7 forced where the workspace
+// allows), writing raw folds to split_ws, then a reduce adds them in slice order with bias / ReLU.
+// Deterministic for a given launch size; the summation order (hence the last bits) depends on
+// whether a tile was split.
 hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
-                      hipStream_t s, const Knobs& k);
+                      hipStream_t s, const Knobs& k, float* split_ws = nullptr);
+struct WinoSplit {
+  int pt_full, tail_pt, nsplit;  // whole point tiles, split tail tiles, slices (1: no split)
+};
+WinoSplit plan_wino_split(const WinoPlan& w, const Knobs& k);
+size_t wino_split_ws_floats();  // workspace: two rounds of workgroups (2 per CU) x 9 x 64 x 64 fold floats
 
 // Conv1 (stride 4, C = 3, 8 < F <= 12, no padding) as Winograd F(3x3,3x3) on the polyphase image
 // (conv1_wino.hip): 48 polyphase channels, 3x3 output tiles, 25 transform points.

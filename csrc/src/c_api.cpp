@@ -443,7 +443,7 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
 }
 
 int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
-                   const float* bias, float* y, int relu, int wino_cfg, void* stream) {
+                   const float* bias, float* y, int relu, int wino_cfg, int wino_split, void* stream) {
   return guarded("anx_conv2_wino", [&] {
     if (!anx::hip::wino_eligible(5, 1, C, K, groups)) return fail("anx_conv2_wino: shape not eligible");
     const auto w = anx::hip::make_wino_plan(N, Hq, Wq, C, K, groups);
@@ -451,21 +451,25 @@ int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_
     std::vector<int> koff;
     anx::hip::wino_transform_weights_host(w, w_kcff, u);
     anx::hip::pack_conv_weights_host(w.gemm, u.data(), packed, koff);
-    float *dv = nullptr, *du = nullptr;
+    float *dv = nullptr, *du = nullptr, *ws = nullptr;
     if (hipMalloc(reinterpret_cast<void**>(&dv), std::max<size_t>(anx::hip::wino_v_floats(w), 1) * 4) != hipSuccess)
       return fail("anx_conv2_wino: hipMalloc");
-    if (hipMalloc(reinterpret_cast<void**>(&du), packed.size() * 4) != hipSuccess) {
+    if (hipMalloc(reinterpret_cast<void**>(&du), packed.size() * 4) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&ws), anx::hip::wino_split_ws_floats() * 4) != hipSuccess) {
       (void)hipFree(dv);
+      (void)hipFree(du);
       return fail("anx_conv2_wino: hipMalloc");
     }
     hipError_t e = hipMemcpy(du, packed.data(), packed.size() * 4, hipMemcpyHostToDevice);
     anx::Knobs kn = anx::default_knobs();
     if (wino_cfg >= 0) kn.wino_cfg = wino_cfg;
+    if (wino_split >= 0) kn.wino_split = wino_split;
     if (e == hipSuccess) e = anx::hip::wino_input(w, x, dv, S(stream));
-    if (e == hipSuccess) e = anx::hip::wino_fused(w, dv, du, bias, y, relu != 0, S(stream), kn);
+    if (e == hipSuccess) e = anx::hip::wino_fused(w, dv, du, bias, y, relu != 0, S(stream), kn, ws);
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));  // the workspaces are freed below
     (void)hipFree(dv);
     (void)hipFree(du);
+    (void)hipFree(ws);
     return hip_status(e, "conv2_wino");
   });
 }

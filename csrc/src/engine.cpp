@@ -102,6 +102,7 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
       wv_cap_ = hip::wino_v_floats(wp);
       wm_cap_ = hip::wino_m_floats(wp);
       wv_ = dev_alloc<float>(wv_cap_);
+      wsplit_ = dev_alloc<float>(hip::wino_split_ws_floats());
     }
   }
 }
@@ -112,7 +113,7 @@ BlocksEngine::~BlocksEngine() {
                   static_cast<void*>(koff1_), static_cast<void*>(koff2_), static_cast<void*>(c1_),
                   static_cast<void*>(q2_), static_cast<void*>(c2_), static_cast<void*>(u2p_),
                   static_cast<void*>(ukoff_), static_cast<void*>(wv_), static_cast<void*>(wm_),
-                  static_cast<void*>(u1w_), static_cast<void*>(wv1_)})
+                  static_cast<void*>(u1w_), static_cast<void*>(wv1_), static_cast<void*>(wsplit_)})
     if (p) (void)hipFree(p);
 }
 
@@ -212,7 +213,7 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
                                s));
       ANX_TRY(hip::wino_output(w, wm_, b2d_, c2_, true, s));
     } else {
-      ANX_TRY(hip::wino_fused(w, wv_, u2p_, b2d_, c2_, true, s, k_));
+      ANX_TRY(hip::wino_fused(w, wv_, u2p_, b2d_, c2_, true, s, k_, wsplit_));
     }
   } else if (impl_ == Impl::Mfma) {
     const hip::ConvPlan p =

@@ -240,6 +240,12 @@ struct FusedArgs {
   int prio;  // bit0: s_setprio(1) around each slice's MFMAs (guide technique T5). Cost probes of the
              // LDS-DMA kernel (wrong results; never set in production): bit4 no fold, bit5 no DMA
              // refills, bit6 no per-slice barrier (only with bit5), bit7 no epilogue stores
+  // Tail split (LDS-DMA kernel, non-IL): this launch covers point tiles [pt_base, pt_base +
+  // n_ptiles); with nsplit > 1, blockIdx.y = s takes transform points [49 s / nsplit, 49 (s+1) /
+  // nsplit) and stores its raw fold Y (no bias / ReLU) to slab s of `slab`, summed by
+  // wino_split_reduce_kernel.
+  int pt_base, nsplit;
+  float* slab;
 };
 
 // A^T indexed by the runtime transform point: a copy of wino::kAT in constant memory (scalar loads).
@@ -458,7 +464,12 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
     pt = blockIdx.x / a.n_ntiles;
     nt = blockIdx.x - pt * a.n_ntiles;
   }
+  const int ptl = pt;  // point tile within this launch (slab index)
+  pt += a.pt_base;
   const int p0 = pt * kFB, n0 = nt * kFB;
+  // transform points of this workgroup: all 49, or slice blockIdx.y of a tail split
+  const int nsplit = a.nsplit > 1 ? a.nsplit : 1, sidx = nsplit > 1 ? blockIdx.y : 0;
+  const int pb = kN * kN * sidx / nsplit, pe = kN * kN * (sidx + 1) / nsplit;
 
   // per-lane source offsets of this thread's NI A units and NI B units (swizzled unit order)
   int aoff[NI], boff[NI];
@@ -473,7 +484,7 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
   }
   const float* Vg = a.V + g * a.Cg;
   const int ksteps = a.kpad / BK;
-  const int total = kN * kN * ksteps;
+  const int it0 = pb * ksteps, total = pe * ksteps;  // K slices [it0, total) (all 49 points unless split)
   lds_f32* lds3 = (lds_f32*)(lds);  // generic -> LDS address space (C-style cast required)
 
   auto issue = [&](int it) {
@@ -616,8 +627,8 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
     if (a.prio & 1) __builtin_amdgcn_s_setprio(0);
   };
 
-  issue(0);
-  if (total > 1) issue(1);
+  issue(it0);
+  if (it0 + 1 < total) issue(it0 + 1);
   if constexpr (IL) {
     // acc1 is zero before point 1: the first fold adds +0 (ab = 0's coefficients) and changes nothing
     for (int ab = 0; ab + 1 < kN * kN; ab += 2) {
@@ -637,15 +648,21 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
     asm volatile("" ::: "memory");
     mfma_slice_pf(total - 1, acc0);
   } else {
-    // ab pairs: even ab accumulate in acc0, odd in acc1; the fold of the previous point is issued
-    // after the first slice of the next one, so the VALU work overlaps in-flight MFMAs.
-    int it = 0;
-    for (int ab = 0; ab < kN * kN; ab += 2) {
+    // ab pairs: the last point pe-1 and every second one before it accumulate in acc0, the others
+    // in acc1 (an even count starts with a lone point in acc1, so acc1 is dead after the loop); the
+    // fold of the previous point is issued after the first slice of the next one, so the VALU work
+    // overlaps in-flight MFMAs. All 49 points: the original order (pb = 0 in acc0).
+    int it = it0, ab0 = pb;
+    if (((pe - pb) & 1) == 0) {
+      for (int ks = 0; ks < ksteps; ++ks, ++it) step(it, acc1);
+      ab0 = pb + 1;
+    }
+    for (int ab = ab0; ab < pe; ab += 2) {
       for (int ks = 0; ks < ksteps; ++ks, ++it) {
         step(it, acc0);
-        if (ks == 0 && ab > 0) fold(ab - 1, acc1);
+        if (ks == 0 && ab > pb) fold(ab - 1, acc1);
       }
-      if (ab + 1 < kN * kN) {
+      if (ab + 1 < pe) {
         for (int ks = 0; ks < ksteps; ++ks, ++it) {
           step(it, acc1);
           if (ks == 0) fold(ab, acc0);
@@ -653,8 +670,19 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
       }
     }
   }
-  // kN*kN is odd: the last point (48, even) is still in acc0
-  fold(kN * kN - 1, acc0);
+  // the last point is still unfolded, in acc0
+  fold(pe - 1, acc0);
+
+  if (a.slab) {  // tail split: raw Y of this point range, [q][tile][filter] per (s, tile block)
+    float* sl = a.slab + ((((static_cast<size_t>(g) * nsplit + sidx) * a.n_ptiles + ptl) * a.n_ntiles + nt) * kM * kM) *
+                             (kFB * kFB);
+#pragma unroll
+    for (int q = 0; q < kM * kM; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        sl[(q * kFB + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * kFB + wn * 32 + r] = Y[q][e >> 1][e & 1];
+    return;
+  }
 
   // Epilogue: bias + ReLU, then one LDS transpose per output position q so each lane stores whole
   // 16-B filter groups (4 dwordx4 per lane per q instead of 16 single-dword stores, which were
@@ -913,6 +941,57 @@ hipError_t launch_glds(const FusedArgs& a, dim3 grid, hipStream_t s, int occ) {
   return hipGetLastError();
 }
 
+// Tail-split fixup: y = act(sum_s slab[s] + bias) for the split point tiles, slabs summed in slice
+// order (deterministic); 4 filters per thread (16-B loads / store), the fused epilogue's NHWC store.
+struct SplitReduceArgs {
+  const float* slab;
+  const float* bias;
+  float* y;
+  int nsplit, n_ptiles, n_ntiles, pt_base, groups;
+  int P, Kg, K, Ho, Wo, ty, tx, relu;
+};
+__global__ void __launch_bounds__(256) wino_split_reduce_kernel(SplitReduceArgs r) {
+  constexpr int F4 = kFB / 4;
+  const long total = static_cast<long>(r.groups) * r.n_ptiles * r.n_ntiles * kM * kM * kFB * F4;
+  const size_t sstride = static_cast<size_t>(r.n_ptiles) * r.n_ntiles * kM * kM * kFB * kFB;  // between slices
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
+    long t = i;
+    const int f4 = static_cast<int>(t % F4);
+    t /= F4;
+    const int tl = static_cast<int>(t % kFB);
+    t /= kFB;
+    const int q = static_cast<int>(t % (kM * kM));
+    t /= kM * kM;
+    const int nt = static_cast<int>(t % r.n_ntiles);
+    t /= r.n_ntiles;
+    const int ptl = static_cast<int>(t % r.n_ptiles);
+    const int g = static_cast<int>(t / r.n_ptiles);
+    const int f = nt * kFB + f4 * 4;
+    const int p = (r.pt_base + ptl) * kFB + tl;
+    if (f >= r.Kg || p >= r.P) continue;
+    const int tj = p % r.tx, pq = p / r.tx, ti = pq % r.ty, n = pq / r.ty;
+    const int oy = ti * kM + q / kM, ox = tj * kM + q % kM;
+    if (oy >= r.Ho || ox >= r.Wo) continue;
+    const float* src = r.slab + (((static_cast<size_t>(g) * r.nsplit * r.n_ptiles + ptl) * r.n_ntiles + nt) * kM * kM + q) *
+                                    (kFB * kFB) + tl * kFB + f4 * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < r.nsplit; ++sl) v += *reinterpret_cast<const f32x4*>(src + sl * sstride);
+    if (r.bias) v += *reinterpret_cast<const f32x4*>(r.bias + g * r.Kg + f);
+    if (r.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+    *reinterpret_cast<f32x4*>(r.y + ((static_cast<size_t>(n) * r.Ho + oy) * r.Wo + ox) * r.K + g * r.Kg + f) = v;
+  }
+}
+
+int device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
 unsigned grid_for(long n) {
   long g = (n + kT - 1) / kT;
   return static_cast<unsigned>(g > 65535 ? 65535 : (g < 1 ? 1 : g));
@@ -1011,8 +1090,51 @@ hipError_t wino_input_pool(const WinoPlan& w, const float* c1, const WinoPoolGeo
   return hipGetLastError();
 }
 
+// two rounds of co-resident workgroups' worth of 9 x 64 x 64 fold slabs (~150 MB at 256 CUs)
+size_t wino_split_ws_floats() { return static_cast<size_t>(4) * device_cus() * kM * kM * kFB * kFB; }
+
+// Tail split: whole rounds of workgroups run as usual; the point tiles of the last, partial round
+// are split S ways by transform point. A CU's throughput is the same with one resident workgroup as
+// with two (128 images: 512 workgroups in 253 us, then the 160-workgroup tail in 122 us), so a
+// round is one workgroup per CU. In units of one workgroup's whole-tile time the tail then costs
+// ceil(S * tail / CUs) / S, plus ~0.09 per CU-round of slabs written and summed (a 147 KB slab
+// round trip per split workgroup); S = 1 costs 1. S is the cheapest of 1..7 within the workspace:
+// 3 at 128 images, 7 at 256 (16 tail workgroups), none at 300 (the tail round is 94 % full).
+WinoSplit plan_wino_split(const WinoPlan& w, const Knobs& kn) {
+  WinoSplit sp{0, 0, 1};
+  const int n_ptiles = (w.P + kFB - 1) / kFB, per_pt = (w.K / w.groups + kFB - 1) / kFB * w.groups;  // WGs per point tile
+  sp.pt_full = n_ptiles;
+  if (kn.wino_split == 0 || (kn.wino_cfg & 15) != 7 || (kn.wino_prio & ~257) != 0) return sp;
+  const long slots = device_cus();  // throughput rounds (see above)
+  const long wgs = static_cast<long>(n_ptiles) * per_pt;
+  const long full_rounds = wgs / slots;
+  int pt_full = static_cast<int>(full_rounds * slots / per_pt / 8 * 8);  // whole XCD groups of 8 point tiles
+  if (pt_full > n_ptiles) pt_full = n_ptiles;
+  const int tail_pt = n_ptiles - pt_full;
+  if (tail_pt == 0) return sp;
+  const long tail_wgs = static_cast<long>((tail_pt + 7) / 8 * 8) * per_pt;
+  const long cap = static_cast<long>(wino_split_ws_floats() / (kM * kM * kFB * kFB));  // slabs
+  int best = 1;
+  double best_cost = 1.0;
+  for (int S = 2; S <= 7; ++S) {
+    if (S * tail_wgs > cap) break;
+    const double cost = static_cast<double>((S * tail_wgs + slots - 1) / slots) / S +
+                        0.09 * static_cast<double>(S * tail_wgs) / static_cast<double>(slots);
+    if (kn.wino_split == S || (kn.wino_split == 1 && cost < best_cost * 0.97)) {
+      best = S;
+      best_cost = cost;
+      if (kn.wino_split == S) break;
+    }
+  }
+  if (best < 2) return sp;
+  sp.pt_full = pt_full;
+  sp.tail_pt = tail_pt;
+  sp.nsplit = best;
+  return sp;
+}
+
 hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
-                      hipStream_t s, const Knobs& kn) {
+                      hipStream_t s, const Knobs& kn, float* split_ws) {
   const int cfg = kn.wino_cfg, prio = kn.wino_prio, occ = kn.conv2_occ;
   const bool sf = (kn.fold_scalar & 2) != 0;
   FusedArgs a{};
@@ -1050,6 +1172,38 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
     const int bk = (cfg & 1) ? 48 : 32;
     if (a.Cg % bk == 0 && a.kpad == a.Cg) {
       const dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
+      const WinoSplit sp = split_ws ? plan_wino_split(w, kn) : WinoSplit{a.n_ptiles, 0, 1};
+      if (bk == 48 && xcd && sp.nsplit > 1 &&
+          static_cast<size_t>(sp.nsplit) * ((sp.tail_pt + 7) / 8 * 8) * a.n_ntiles * w.groups * kM * kM * kFB * kFB <=
+              wino_split_ws_floats()) {
+        // whole rounds of point tiles as usual, then the tail tiles' 49 points split nsplit ways
+        // over the CUs the tail round would leave idle, then the slab sum (deterministic order)
+        if (sp.pt_full > 0) {
+          FusedArgs f = a;
+          f.n_ptiles = sp.pt_full;
+          const dim3 gf(sp.pt_full * a.n_ntiles, 1, w.groups);
+          const hipError_t e = ((prio & 256) && a.kpad == 96)
+                                   ? (sf ? launch_glds<48, true, true, true>(f, gf, s, occ)
+                                         : launch_glds<48, true, true, false>(f, gf, s, occ))
+                                   : (sf ? launch_glds<48, true, false, true>(f, gf, s, occ)
+                                         : launch_glds<48, true, false, false>(f, gf, s, occ));
+          if (e != hipSuccess) return e;
+        }
+        FusedArgs t = a;
+        t.n_ptiles = sp.tail_pt;
+        t.pt_base = sp.pt_full;
+        t.nsplit = sp.nsplit;
+        t.slab = split_ws;
+        const dim3 gt((sp.tail_pt + 7) / 8 * 8 * a.n_ntiles, sp.nsplit, w.groups);
+        const hipError_t e = sf ? launch_glds<48, true, false, true>(t, gt, s, occ)
+                                : launch_glds<48, true, false, false>(t, gt, s, occ);
+        if (e != hipSuccess) return e;
+        SplitReduceArgs r{split_ws, bias, y, sp.nsplit, sp.tail_pt, a.n_ntiles, sp.pt_full, w.groups,
+                          w.P,      a.Kg, w.K, w.Ho,      w.Wo,       w.ty,     w.tx,     relu ? 1 : 0};
+        const long n = static_cast<long>(w.groups) * sp.tail_pt * a.n_ntiles * kM * kM * kFB * (kFB / 4);
+        wino_split_reduce_kernel<<<grid_for(n), 256, 0, s>>>(r);
+        return hipGetLastError();
+      }
       if (bk == 48 && xcd) {  // the interleaved fold needs exactly 2 K slices per point (C = 96)
         if ((prio & 256) && a.kpad == 96)
           return sf ? launch_glds<48, true, true, true>(a, grid, s, occ)

@@ -28,9 +28,11 @@ def _rel_to_terms(y, x, w, b, S, P, groups=1):
     return rel.max().item()
 
 
-@pytest.mark.parametrize("N,groups,cfg", [(12, 1, -1), (12, 2, -1), (9, 1, 15), (9, 1, 1)])
-def test_conv2_winograd_randn_he(cuda, N, groups, cfg):
-    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights."""
+@pytest.mark.parametrize("N,groups,cfg,split", [(12, 1, -1, -1), (12, 2, -1, -1), (9, 1, 15, -1), (9, 1, 1, -1),
+                                               (128, 1, -1, -1), (140, 2, -1, -1), (128, 1, -1, 0)])
+def test_conv2_winograd_randn_he(cuda, N, groups, cfg, split):
+    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights. At 128 / 140
+    images the default launch splits its tail point tiles' 49 points 3 / 2 ways (plan_wino_split)."""
     torch.manual_seed(21 + N)
     C, K = 96, 256
     x = torch.randn(N, 31, 31, C, device=cuda)
@@ -42,7 +44,7 @@ def test_conv2_winograd_randn_he(cuda, N, groups, cfg):
     b = torch.randn(K, device=cuda) * 0.1
     y = torch.full((N, 27, 27, K), float("nan"), device=cuda)
     nat.call("anx_conv2_wino", x.data_ptr(), N, 31, 31, C, w.contiguous().data_ptr(), K, groups, b.data_ptr(),
-             y.data_ptr(), 0, cfg, nat.stream_ptr(cuda))
+             y.data_ptr(), 0, cfg, split, nat.stream_ptr(cuda))
     assert torch.isfinite(y).all()
     assert _rel_to_terms(y, x, w.to(cuda), b, 1, 0, groups) < BOUND_CONV2
 
