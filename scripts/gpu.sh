@@ -57,8 +57,8 @@ for s in "$@"; do
       run full_bench 300 python bench.py --model full --steps 20 --warmup 5
       run full_prof 300 rocprofv3 --kernel-trace --stats -d "$O/full_prof" -o run -- python3 bench.py --model full --steps 10 --warmup 3 ;;
     matrix)
-      run matrix_b1 400 bash scripts/run_matrix.sh --no-build --batch 1 --iters 3
-      run matrix_b256 600 bash scripts/run_matrix.sh --no-build --batch 256 --iters 1 ;;
+      run matrix_b1 400 bash scripts/run_matrix.sh --no-build --batch 1 --iters 3 --out "$O/matrix"
+      run matrix_b256 600 bash scripts/run_matrix.sh --no-build --batch 256 --iters 1 --out "$O/matrix" ;;
     peak) run peak 120 bash -c "$B/anx_mfmapeak --waves 1 && $B/anx_mfmapeak --waves 2 && $B/anx_mfmapeak --waves 4" ;;
     workloads)
       run wl_v4 300 python bench.py --workload v4 --steps 10 --warmup 3
