@@ -274,6 +274,199 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   }
 }
 
+// ---- cfg 12: 256x256 ping-pong (8 waves as two staggered groups) ----
+// Group G = wave >> 2 (waves 0-3 / 4-7; wave w runs on SIMD w % 4, so every SIMD holds one wave of
+// each group). Group G owns A rows [128 G, 128 G + 128) (its waves are the wm == G row of the 2 x 4
+// wave grid) and loads them; each group loads half of the B rows. G1 executes one extra barrier
+// first, so one group's fragment reads and DMA issue (L) run while the other group's 64 MFMAs (M)
+// own the SIMD's matrix pipe (cdna_hip_programming.md §5, the 8-phase template's stagger).
+// LDS: A in 2 stages, B in 3 (5 x 32 KiB = 160 KiB). With #0 the prologue barrier:
+//   G0: L_t = (#2t, #2t+1), M_t = (#2t+1, #2t+2);  G1: L_t = (#2t+1, #2t+2), M_t = (#2t+2, #2t+3)
+//   G0 in L_t issues A_{t+1} (own rows) and B_{t+1} (rows 0-127) and retires them (vmcnt 0) at the
+//   end of M_t; G1 in L_t issues A_{t+1} (own rows) and B_{t+2} (rows 128-255, two tiles ahead:
+//   hence 3 B stages), retires B_{t+1} at the end of L_t (vmcnt 8) and A_{t+1} at the end of M_t
+//   (vmcnt 4). Every L section ends with lgkmcnt(0) and every DMA lands in a stage whose last readers
+//   finished at least one barrier earlier (the refills never race a read).
+__global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
+  constexpr int BM = 256, BN = 256, TM = 8, TN = 4, WN = 64;
+  constexpr int SZ = 256 * kBK;      // bf16 per A or B stage
+  constexpr int CH = BN / 8, XM = 7;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = __builtin_amdgcn_readfirstlane(wave >> 2);  // wave-uniform, scalar
+  const int wl = wave & 3, tl = tid & 255, wn = wave & 3, g = blockIdx.z;
+  int tile;
+  {
+    const int nwg = gridDim.x, b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int mt = tile / a.n_ntiles, nt = tile - mt * a.n_ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const bf16* x = a.x + g * a.Cg;
+  const bf16* wg = a.w + static_cast<size_t>(g) * a.kpad_n * a.kpad;
+  // this lane's 4 A rows and 4 B rows: row G*128 + j*32 + tl/8, physical chunk tl&7 holding logical u
+  const int u = (tl & 7) ^ ((tl >> 4) & 7);
+  int aoff[4], boff[4];  // 32-bit element offsets from the (scalar) x / wg bases: fewer VGPRs
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = G * 128 + j * 32 + (tl >> 3);
+    const int m = m0 + row;
+    int o = 0;
+    if (m < a.M) {
+      const int n = m / a.HoWo, rr = m - n * a.HoWo, oy = rr / a.Wo, ox = rr - oy * a.Wo;
+      o = ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
+    }
+    aoff[j] = o;
+    boff[j] = min(n0 + row, a.kpad_n - 1) * a.kpad + u * 8;  // < 2^31: packed weights of one group
+  }
+  const int T = a.ktiles;
+  int uc, ufw, ufh;  // the lane's K unit as (filter row, column, channel), advanced per A issue
+  {
+    const int k = u * 8, tap = k / a.Cg;
+    uc = k - tap * a.Cg;
+    ufh = tap / a.F;
+    ufw = tap - ufh * a.F;
+  }
+  lds_b16* lds3 = (lds_b16*)(lds_b);
+  const int drow = (G * 128 + wl * 8) * kBK;  // this wave's first DMA row (+ j*32 rows)
+  auto issueA = [&](int st) {  // the next K tile of this group's A rows (issued in K order)
+    const int ko = ufh < a.F ? (ufh * a.Wp + ufw) * a.C + uc : 0;
+    uc += kBK;
+    while (uc >= a.Cg) {
+      uc -= a.Cg;
+      if (++ufw == a.F) {
+        ufw = 0;
+        ++ufh;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(x + (aoff[j] + ko), lds3 + st * SZ + drow + j * 32 * kBK);
+  };
+  auto issueB = [&](int kt, int st) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(wg + (boff[j] + kt * kBK), lds3 + 2 * SZ + st * SZ + drow + j * 32 * kBK);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int hq = lane >> 4, sw = (lane >> 1) & 7;
+  const int arow = (G * 128 + (lane & 15)) * kBK, brow = (wn * WN + (lane & 15)) * kBK;
+
+  // prologue: tile 0 (both groups' halves), and G1's B_1
+  issueA(0);
+  issueB(0, 0);
+  if (G == 1 && T > 1) issueB(1, 1);
+  if (G == 1 && T > 1)
+    wait_vm<4>();
+  else
+    wait_vm<0>();
+  __builtin_amdgcn_s_barrier();  // #0
+  if (G == 1) __builtin_amdgcn_s_barrier();  // the stagger
+  asm volatile("" ::: "memory");
+  int sb = 0;  // B stage of tile t (t % 3)
+  for (int t = 0; t < T; ++t) {
+    // ---- L_t: fragments of tile t, then this group's refills ----
+    const bf16* A = lds_b + (t & 1) * SZ;
+    const bf16* B = lds_b + 2 * SZ + sb * SZ;
+    bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(B + brow + j * 16 * kBK + (hq ^ sw) * 8);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a0[i] = *reinterpret_cast<const bf16x8*>(A + arow + i * 16 * kBK + (hq ^ sw) * 8);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b1[j] = *reinterpret_cast<const bf16x8*>(B + brow + j * 16 * kBK + ((4 + hq) ^ sw) * 8);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      a1[i] = *reinterpret_cast<const bf16x8*>(A + arow + i * 16 * kBK + ((4 + hq) ^ sw) * 8);
+    __builtin_amdgcn_sched_barrier(0);
+    const int s1 = sb == 2 ? 0 : sb + 1, s2 = s1 == 2 ? 0 : s1 + 1;
+    if (G == 0) {
+      if (t + 1 < T) {
+        issueA((t + 1) & 1);
+        issueB(t + 1, s1);
+      }
+    } else {
+      if (t + 1 < T) issueA((t + 1) & 1);
+      if (t + 2 < T) issueB(t + 2, s2);
+      if (t + 2 < T)  // retire B_{t+1} (issued one L section earlier) before the barrier
+        wait_vm<8>();
+      else if (t + 1 < T)
+        wait_vm<4>();
+      else
+        wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // ---- M_t ----
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (G == 0) {
+      if (t + 1 < T) wait_vm<0>();  // this group's A_{t+1}, B_{t+1}
+    } else {
+      if (t + 2 < T)  // A_{t+1} (B_{t+2} may fly)
+        wait_vm<4>();
+      else
+        wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    sb = s1;
+  }
+  if (G == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: every wave is past its last read
+  asm volatile("" ::: "memory");
+
+  // epilogue (as conv_bf16_big_kernel): ooff in the third B stage, the tile image in the first 128 KiB
+  int* ooff_s = reinterpret_cast<int*>(lds_b + 4 * SZ);
+  if (tid < BM) {
+    const int m = m0 + tid;
+    int oo = -1;
+    if (m < a.M) {
+      const int n = m / a.HoWo, rr = m - n * a.HoWo, oy = rr / a.Wo, ox = rr - oy * a.Wo;
+      oo = ((n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off;
+    }
+    ooff_s[tid] = oo;
+  }
+  bf16* E = lds_b;
+  using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+  const int mcol = lane & 15;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * WN + j * 16 + hq * 4, f = n0 + nl;
+    const f32x4 bv = (a.bias && f < a.Kg) ? *reinterpret_cast<const f32x4*>(a.bias + g * a.Kg + f) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = G * 128 + i * 16 + mcol;
+      f32x4 v = acc[i][j] + bv;
+      if (a.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+      *reinterpret_cast<bf16x4*>(E + ml * BN + (((nl >> 3) ^ (ml & XM)) << 3) + (nl & 7)) =
+          bf16x4{static_cast<bf16>(v.x), static_cast<bf16>(v.y), static_cast<bf16>(v.z), static_cast<bf16>(v.w)};
+    }
+  }
+  __syncthreads();
+  bf16* out = a.out + g * a.Kg;
+  for (int q = tid; q < BM * CH; q += 512) {
+    const int ml = q / CH, c = q - ml * CH;
+    const int o = ooff_s[ml], f = n0 + c * 8;
+    if (o >= 0 && f < a.Kg)
+      *reinterpret_cast<u32x4*>(out + o + f) = *reinterpret_cast<const u32x4*>(E + ml * BN + ((c ^ (ml & XM)) << 3));
+  }
+}
+
 struct BigCfg {
   int BM, BN, threads, nst;
   int wgs_per_cu;  // co-resident workgroups (LDS / registers)
@@ -287,10 +480,12 @@ struct BigCfg {
 constexpr BigCfg kCfg[] = {{256, 256, 512, 2, 1, 1.0f},  {256, 128, 512, 2, 1, 0.86f}, {256, 96, 512, 2, 1, 0.7f},
                            {128, 128, 256, 2, 2, 0.92f}, {128, 96, 256, 2, 2, 0.74f},  {256, 128, 512, 3, 1, 0.7f},
                            {128, 128, 256, 3, 1, 0.6f},  {128, 96, 256, 3, 1, 0.5f},   {256, 64, 512, 3, 1, 0.6f},
-                           {256, 256, 512, 2, 1, 0.5f},  {128, 128, 256, 2, 2, 0.5f},  {128, 96, 256, 2, 2, 0.5f}};
+                           {256, 256, 512, 2, 1, 0.5f},  {128, 128, 256, 2, 2, 0.5f},  {128, 96, 256, 2, 2, 0.5f},
+                           {256, 256, 512, 0, 1, 1.04f}};  // 12: ping-pong (5 x 32 KiB stages): 2-7 % over 0
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 
 size_t lds_bytes(const BigCfg& c) {
+  if (c.nst == 0) return static_cast<size_t>(5) * 256 * kBK * 2;  // ping-pong: A x 2 + B x 3 stages
   return static_cast<size_t>(c.nst) * (c.BM + c.BN) * kBK * 2 + static_cast<size_t>(c.BM) * 4;
 }
 
@@ -351,6 +546,7 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   if (!conv_bf16_big_ok(p, cfg, out)) return hipErrorInvalidValue;
   const int ksplit = std::max(1, split.ksplit);
   const bool slab = split.ws != nullptr;  // fp32 slabs (also at ksplit 1: an fp32 result via the reduce)
+  if (cfg == 12 && slab) cfg = 0;  // the ping-pong kernel has no split-K slab epilogue (FC layers)
   if ((ksplit > 1 && !slab) || (slab && p.groups != 1)) return hipErrorInvalidValue;
   const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
   if (M == 0) return hipSuccess;
@@ -412,6 +608,13 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
     return hipSuccess;
   }();
   if (attr != hipSuccess) return attr;
+  if (cfg == 12) {
+    static const hipError_t pattr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv_bf16_pp_kernel),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (pattr != hipSuccess) return pattr;
+    conv_bf16_pp_kernel<<<grid, 512, lds, s>>>(a);
+    return hipGetLastError();
+  }
   switch (cfg) {
 #define ANX_CASE(I, BM, BN, WGM, WGN, NST, P)                                                \
   case I:                                                                                    \
