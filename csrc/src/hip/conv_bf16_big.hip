@@ -72,8 +72,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   static_assert(UNITS % 64 == 0, "a DMA instruction never straddles A and B");
   constexpr int STAGE = (BM + BN) * kBK;            // bf16 per stage
   constexpr int CH = BN / 8;                        // 16-B chunks per epilogue row
-  constexpr int XM = (CH % 8 == 0) ? 7 : (CH % 4 == 0) ? 3 : (CH % 2 == 0) ? 1 : 0;
-  static_assert(BM * BN <= NST * STAGE, "the epilogue image fits in the stages");
+  // epilogue image rows: padded by one 16-B chunk where the image still fits the stages (row r at
+  // bank offset 4 * (EW / 8) * r mod 64: 16 consecutive rows on distinct banks), else chunk-XOR
+  // swizzled (a 12-chunk row, BN = 96, only permutes within 4 chunks: 4-way conflicts, 23 % of
+  // the 128x96 conv1 kernel's LDS cycles)
+  constexpr bool EPAD = BM * (BN + 8) <= NST * STAGE;
+  constexpr int EW = EPAD ? BN + 8 : BN;
+  constexpr int XM = EPAD ? 0 : (CH % 8 == 0) ? 7 : (CH % 4 == 0) ? 3 : (CH % 2 == 0) ? 1 : 0;
+  static_assert(BM * EW <= NST * STAGE, "the epilogue image fits in the stages");
   static_assert(NST == 2 || UNITS % NT == 0, "counted vmcnt: every wave issues NJ pieces per stage");
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
   int* ooff_s = reinterpret_cast<int*>(lds_b + NST * STAGE);  // output offset per tile row (-1 past M)
@@ -260,7 +266,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
       const int ml = wm * WM + i * 16 + mcol;
       f32x4 v = acc[i][j] + bv;
       if (a.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
-      *reinterpret_cast<bf16x4*>(E + ml * BN + (((nl >> 3) ^ (ml & XM)) << 3) + (nl & 7)) =
+      *reinterpret_cast<bf16x4*>(E + ml * EW + (((nl >> 3) ^ (ml & XM)) << 3) + (nl & 7)) =
           bf16x4{static_cast<bf16>(v.x), static_cast<bf16>(v.y), static_cast<bf16>(v.z), static_cast<bf16>(v.w)};
     }
   }
@@ -270,7 +276,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
     const int ml = q / CH, c = q - ml * CH;
     const int o = ooff_s[ml], f = n0 + c * 8;
     if (o >= 0 && f < a.Kg)
-      *reinterpret_cast<u32x4*>(out + o + f) = *reinterpret_cast<const u32x4*>(E + ml * BN + ((c ^ (ml & XM)) << 3));
+      *reinterpret_cast<u32x4*>(out + o + f) = *reinterpret_cast<const u32x4*>(E + ml * EW + ((c ^ (ml & XM)) << 3));
   }
 }
 
@@ -290,7 +296,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
 __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
   constexpr int BM = 256, BN = 256, TM = 8, TN = 4, WN = 64;
   constexpr int SZ = 256 * kBK;      // bf16 per A or B stage
-  constexpr int CH = BN / 8, XM = 7;
+  constexpr int CH = BN / 8, EW = BN + 8;  // epilogue image rows padded by 16 B (conflict-free)
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = __builtin_amdgcn_readfirstlane(wave >> 2);  // wave-uniform, scalar
@@ -430,8 +436,9 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
   if (G == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: every wave is past its last read
   asm volatile("" ::: "memory");
 
-  // epilogue (as conv_bf16_big_kernel): ooff in the third B stage, the tile image in the first 128 KiB
-  int* ooff_s = reinterpret_cast<int*>(lds_b + 4 * SZ);
+  // epilogue (as conv_bf16_big_kernel): the padded tile image (132 KiB) from the LDS base, ooff in
+  // the last KiB
+  int* ooff_s = reinterpret_cast<int*>(lds_b + 5 * SZ - 512);
   if (tid < BM) {
     const int m = m0 + tid;
     int oo = -1;
@@ -453,7 +460,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
       const int ml = G * 128 + i * 16 + mcol;
       f32x4 v = acc[i][j] + bv;
       if (a.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
-      *reinterpret_cast<bf16x4*>(E + ml * BN + (((nl >> 3) ^ (ml & XM)) << 3) + (nl & 7)) =
+      *reinterpret_cast<bf16x4*>(E + ml * EW + nl) =
           bf16x4{static_cast<bf16>(v.x), static_cast<bf16>(v.y), static_cast<bf16>(v.z), static_cast<bf16>(v.w)};
     }
   }
@@ -463,7 +470,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
     const int ml = q / CH, c = q - ml * CH;
     const int o = ooff_s[ml], f = n0 + c * 8;
     if (o >= 0 && f < a.Kg)
-      *reinterpret_cast<u32x4*>(out + o + f) = *reinterpret_cast<const u32x4*>(E + ml * BN + ((c ^ (ml & XM)) << 3));
+      *reinterpret_cast<u32x4*>(out + o + f) = *reinterpret_cast<const u32x4*>(E + ml * EW + c * 8);
   }
 }
 
