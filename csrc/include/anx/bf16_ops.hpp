@@ -51,8 +51,8 @@ hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, c
 // only. cfg (BM x BN, waves, LDS stages): 0 = 256x256 8w 2, 1 = 256x128 8w 2, 2 = 256x96 8w 2,
 // 3 = 128x128 4w 2, 4 = 128x96 4w 2, 5 = 256x128 8w 3, 6 = 128x128 4w 3, 7 = 128x96 4w 3,
 // 8 = 256x64 8w 3 (FC); 0, 3, 4 read both k-steps' fragments ahead of their MFMAs (PIPE), 9-11 are
-// those three without it (A/B); 12 = 256x256 ping-pong (two staggered 4-wave groups; A 2 / B 3
-// stages; conv only).
+// those three without it (A/B); 12 / 13 = 256x256 / 256x128 ping-pong (two staggered 4-wave
+// groups; A 2 / B 3 stages; conv only).
 int conv_bf16_big_cfgs();
 bool conv_bf16_big_ok(const ConvPlanB& p, int cfg, const OutViewB& out);
 // The config a cost model of wave quantization picks for this launch (-1: none applies).

@@ -293,9 +293,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
 //   hence 3 B stages), retires B_{t+1} at the end of L_t (vmcnt 8) and A_{t+1} at the end of M_t
 //   (vmcnt 4). Every L section ends with lgkmcnt(0) and every DMA lands in a stage whose last readers
 //   finished at least one barrier earlier (the refills never race a read).
+template <int BN>
 __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
-  constexpr int BM = 256, BN = 256, TM = 8, TN = 4, WN = 64;
-  constexpr int SZ = 256 * kBK;      // bf16 per A or B stage
+  constexpr int BM = 256, TM = 8, WN = BN / 4, TN = WN / 16;
+  constexpr int SZ = 256 * kBK;      // bf16 per A stage
+  constexpr int SB = BN * kBK;       // bf16 per B stage
+  constexpr int NA = 4, NB = BN / 64;  // DMA pieces per lane per K tile: this group's A rows, B half
+  static_assert(TN >= 1 && NB >= 1, "tile split");
   constexpr int CH = BN / 8, EW = BN + 8;  // epilogue image rows padded by 16 B (conflict-free)
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -312,9 +316,9 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
   const bf16* wg = a.w + static_cast<size_t>(g) * a.kpad_n * a.kpad;
   // this lane's 4 A rows and 4 B rows: row G*128 + j*32 + tl/8, physical chunk tl&7 holding logical u
   const int u = (tl & 7) ^ ((tl >> 4) & 7);
-  int aoff[4], boff[4];  // 32-bit element offsets from the (scalar) x / wg bases: fewer VGPRs
+  int aoff[NA], boff[NB];  // 32-bit element offsets from the (scalar) x / wg bases: fewer VGPRs
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NA; ++j) {
     const int row = G * 128 + j * 32 + (tl >> 3);
     const int m = m0 + row;
     int o = 0;
@@ -323,8 +327,10 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
       o = ((n * a.Hp + oy * a.S) * a.Wp + ox * a.S) * a.C;
     }
     aoff[j] = o;
-    boff[j] = min(n0 + row, a.kpad_n - 1) * a.kpad + u * 8;  // < 2^31: packed weights of one group
   }
+#pragma unroll
+  for (int j = 0; j < NB; ++j)  // B row G*BN/2 + j*32 + tl/8 (< 2^31: packed weights of one group)
+    boff[j] = min(n0 + G * (BN / 2) + j * 32 + (tl >> 3), a.kpad_n - 1) * a.kpad + u * 8;
   const int T = a.ktiles;
   int uc, ufw, ufh;  // the lane's K unit as (filter row, column, channel), advanced per A issue
   {
@@ -334,7 +340,8 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
     ufw = tap - ufh * a.F;
   }
   lds_b16* lds3 = (lds_b16*)(lds_b);
-  const int drow = (G * 128 + wl * 8) * kBK;  // this wave's first DMA row (+ j*32 rows)
+  const int drow = (G * 128 + wl * 8) * kBK;  // this wave's first A DMA row (+ j*32 rows)
+  const int dbrow = (G * (BN / 2) + wl * 8) * kBK;  // ... and B row
   auto issueA = [&](int st) {  // the next K tile of this group's A rows (issued in K order)
     const int ko = ufh < a.F ? (ufh * a.Wp + ufw) * a.C + uc : 0;
     uc += kBK;
@@ -346,11 +353,11 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) glds16(x + (aoff[j] + ko), lds3 + st * SZ + drow + j * 32 * kBK);
+    for (int j = 0; j < NA; ++j) glds16(x + (aoff[j] + ko), lds3 + st * SZ + drow + j * 32 * kBK);
   };
   auto issueB = [&](int kt, int st) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) glds16(wg + (boff[j] + kt * kBK), lds3 + 2 * SZ + st * SZ + drow + j * 32 * kBK);
+    for (int j = 0; j < NB; ++j) glds16(wg + (boff[j] + kt * kBK), lds3 + 2 * SZ + st * SB + dbrow + j * 32 * kBK);
   };
 
   f32x4 acc[TM][TN];
@@ -366,7 +373,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
   issueB(0, 0);
   if (G == 1 && T > 1) issueB(1, 1);
   if (G == 1 && T > 1)
-    wait_vm<4>();
+    wait_vm<NB>();
   else
     wait_vm<0>();
   __builtin_amdgcn_s_barrier();  // #0
@@ -376,7 +383,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
   for (int t = 0; t < T; ++t) {
     // ---- L_t: fragments of tile t, then this group's refills ----
     const bf16* A = lds_b + (t & 1) * SZ;
-    const bf16* B = lds_b + 2 * SZ + sb * SZ;
+    const bf16* B = lds_b + 2 * SZ + sb * SB;
     bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(B + brow + j * 16 * kBK + (hq ^ sw) * 8);
@@ -398,9 +405,9 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
       if (t + 1 < T) issueA((t + 1) & 1);
       if (t + 2 < T) issueB(t + 2, s2);
       if (t + 2 < T)  // retire B_{t+1} (issued one L section earlier) before the barrier
-        wait_vm<8>();
+        wait_vm<NA + NB>();
       else if (t + 1 < T)
-        wait_vm<4>();
+        wait_vm<NA>();
       else
         wait_vm<0>();
     }
@@ -425,7 +432,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
       if (t + 1 < T) wait_vm<0>();  // this group's A_{t+1}, B_{t+1}
     } else {
       if (t + 2 < T)  // A_{t+1} (B_{t+2} may fly)
-        wait_vm<4>();
+        wait_vm<NB>();
       else
         wait_vm<0>();
     }
@@ -438,7 +445,8 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
 
   // epilogue (as conv_bf16_big_kernel): the padded tile image (132 KiB) from the LDS base, ooff in
   // the last KiB
-  int* ooff_s = reinterpret_cast<int*>(lds_b + 5 * SZ - 512);
+  int* ooff_s = reinterpret_cast<int*>(lds_b + 2 * SZ + 3 * SB - 512);
+  static_assert(BM * EW + 512 <= 2 * SZ + 3 * SB, "epilogue image + offsets fit the stages");
   if (tid < BM) {
     const int m = m0 + tid;
     int oo = -1;
@@ -488,11 +496,12 @@ constexpr BigCfg kCfg[] = {{256, 256, 512, 2, 1, 1.0f},  {256, 128, 512, 2, 1, 0
                            {128, 128, 256, 2, 2, 0.92f}, {128, 96, 256, 2, 2, 0.74f},  {256, 128, 512, 3, 1, 0.7f},
                            {128, 128, 256, 3, 1, 0.6f},  {128, 96, 256, 3, 1, 0.5f},   {256, 64, 512, 3, 1, 0.6f},
                            {256, 256, 512, 2, 1, 0.5f},  {128, 128, 256, 2, 2, 0.5f},  {128, 96, 256, 2, 2, 0.5f},
-                           {256, 256, 512, 0, 1, 1.04f}};  // 12: ping-pong (5 x 32 KiB stages): 2-7 % over 0
+                           {256, 256, 512, 0, 1, 1.04f},   // 12: ping-pong (A 2 + B 3 stages): 2-7 % over 0
+                           {256, 128, 512, 0, 1, 0.8f}};   // 13: ping-pong 256x128 (conv3/4: 90 / 125 us vs 77 / 109 for cfg 3)
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 
 size_t lds_bytes(const BigCfg& c) {
-  if (c.nst == 0) return static_cast<size_t>(5) * 256 * kBK * 2;  // ping-pong: A x 2 + B x 3 stages
+  if (c.nst == 0) return (static_cast<size_t>(2) * 256 + 3 * c.BN) * kBK * 2;  // ping-pong: A x 2 + B x 3 stages
   return static_cast<size_t>(c.nst) * (c.BM + c.BN) * kBK * 2 + static_cast<size_t>(c.BM) * 4;
 }
 
@@ -553,7 +562,7 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   if (!conv_bf16_big_ok(p, cfg, out)) return hipErrorInvalidValue;
   const int ksplit = std::max(1, split.ksplit);
   const bool slab = split.ws != nullptr;  // fp32 slabs (also at ksplit 1: an fp32 result via the reduce)
-  if (cfg == 12 && slab) cfg = 0;  // the ping-pong kernel has no split-K slab epilogue (FC layers)
+  if ((cfg == 12 || cfg == 13) && slab) cfg = cfg == 12 ? 0 : 1;  // ping-pong: no split-K slab epilogue
   if ((ksplit > 1 && !slab) || (slab && p.groups != 1)) return hipErrorInvalidValue;
   const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
   if (M == 0) return hipSuccess;
@@ -615,11 +624,20 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
     return hipSuccess;
   }();
   if (attr != hipSuccess) return attr;
-  if (cfg == 12) {
-    static const hipError_t pattr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv_bf16_pp_kernel),
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (cfg == 12 || cfg == 13) {
+    static const hipError_t pattr = [] {
+      for (const void* k : {reinterpret_cast<const void*>(conv_bf16_pp_kernel<256>),
+                            reinterpret_cast<const void*>(conv_bf16_pp_kernel<128>)}) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+      }
+      return hipSuccess;
+    }();
     if (pattr != hipSuccess) return pattr;
-    conv_bf16_pp_kernel<<<grid, 512, lds, s>>>(a);
+    if (cfg == 12)
+      conv_bf16_pp_kernel<256><<<grid, 512, lds, s>>>(a);
+    else
+      conv_bf16_pp_kernel<128><<<grid, 512, lds, s>>>(a);
     return hipGetLastError();
   }
   switch (cfg) {

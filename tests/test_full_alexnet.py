@@ -96,7 +96,7 @@ def test_bf16_lds_dma_kernel_matches_register_staged(cuda, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 12])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 12, 13])
 def test_bf16_wide_tile_kernel_matches_register_staged(cuda, cfg):
     """The wide-tile kernel (conv_bf16_big.hip; -1 = the cost model's per-layer pick, else that
     config forced wherever it fits) sums each output's products in the register-staged kernel's
