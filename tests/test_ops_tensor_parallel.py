@@ -152,3 +152,22 @@ def test_filter_shards_bitwise_gpu(cuda, small_case, ws):
     torch.testing.assert_close(tp.simulate(x.to(cuda), w, ws), full, rtol=0, atol=0)
     ref = blocks_forward(x, w, BLOCK1, BLOCK2)
     torch.testing.assert_close(full.cpu().double(), ref, rtol=2e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_conv2d_weight_cache_not_fooled_by_address_reuse(cuda):
+    """Two equal-shape temporary weight shards with different values, back to back (advisor round 1:
+    the packed-weight cache was keyed by the data pointer without keeping the tensor alive, so the
+    second shard could reuse the first's freed address and be served its filters). Each call must
+    match its own fp64 reference; the first temporary is dropped before the second is made."""
+    gen = torch.Generator().manual_seed(3)
+    x = torch.rand(2, 13, 13, 8, generator=gen)
+    full = torch.rand(16, 8, 5, 5, generator=gen) - 0.5
+    b = torch.rand(8, generator=gen)
+    outs = []
+    for lo in (0, 8):
+        shard = full[lo:lo + 8].contiguous()  # a fresh temporary of the same shape each time
+        outs.append(ops.conv2d(x.to(cuda), shard, b, 1, 2, 1, relu=True).cpu())
+        torch.testing.assert_close(outs[-1].double(), _ref_conv(x, shard, b, 1, 2, 1, True), rtol=2e-5, atol=2e-5)
+        del shard
+    assert not torch.equal(outs[0], outs[1])

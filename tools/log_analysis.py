@@ -8,6 +8,7 @@ SURVEY §2.8 A1-A4), on sqlite (duckdb is not available here) + pandas + matplot
     log_analysis.py speedup [--baseline v1]            # S = T(base, np1) / T, E = S / np  (+ self-relative)
     log_analysis.py plot speedup|efficiency|runtime --out FILE.png
     log_analysis.py export --fmt csv|parquet --out FILE
+    log_analysis.py report --out REPORT.md [--ref-root DIR]   # the notebook's synthesis views
 
 Understood record formats (everything becomes one row: source, version, np, batch, time_ms, ...):
   * `ANX_JSON {...}` lines from `anx` / `python -m anx run` (time = warm_ms if present, else cold_ms)
@@ -111,7 +112,8 @@ def parse_file(path: str):
 
 
 @app.command()
-def ingest(root: str = typer.Option(".", help="directory to walk"), db: str = DEFAULT_DB):
+def ingest(root: str = typer.Option(".", help="directory to walk"), db: str = DEFAULT_DB,
+           tag: str = typer.Option("", help="prefix for the source label (e.g. 'reference' for its tree)")):
     """Walk ROOT and load every run record (dedup by SHA1 of path+record)."""
     c = _db(db)
     n = 0
@@ -123,6 +125,8 @@ def ingest(root: str = typer.Option(".", help="directory to walk"), db: str = DE
                 continue
             p = os.path.join(dp, f)
             for row in parse_file(p):
+                if tag and not row["source"].startswith(tag):
+                    row["source"] = f"{tag}-{row['source']}"
                 key = hashlib.sha1((p + json.dumps(row, sort_keys=True)).encode()).hexdigest()
                 row = {**dict(images_per_s=None, extra=""), **row}
                 try:
@@ -218,6 +222,130 @@ def export(fmt: str = "csv", out: str = "runs.csv", db: str = DEFAULT_DB):
     else:
         df.to_csv(out, index=False)
     typer.echo(f"wrote {len(df)} rows to {out}")
+
+
+# Source files that make up each version's own code path (non-blank, non-comment lines counted),
+# ours and the reference's (its notebook's version_loc_map, analysis.md Cell 19).
+OUR_VERSION_SOURCES = {
+    "v1": ["csrc/src/cpu/ref_layers.cpp", "csrc/src/cpu/blocks_cpu.cpp"],
+    "v2.1": ["csrc/src/cpu/ref_layers.cpp", "csrc/src/cpu/blocks_cpu.cpp", "csrc/src/comm/host_comm.cpp"],
+    "v2.2": ["csrc/src/cpu/ref_layers.cpp", "csrc/src/cpu/blocks_cpu.cpp", "csrc/src/comm/host_comm.cpp",
+             "csrc/src/plan.cpp"],
+    "v3": ["csrc/src/engine.cpp", "csrc/src/hip/conv_mfma.hip", "csrc/src/hip/winograd.hip",
+           "csrc/src/hip/conv1_wino.hip", "csrc/src/hip/pool_lrn.hip"],
+    "v4": ["csrc/src/engine.cpp", "csrc/src/hip/conv_mfma.hip", "csrc/src/hip/winograd.hip",
+           "csrc/src/hip/conv1_wino.hip", "csrc/src/hip/pool_lrn.hip", "csrc/src/comm/host_comm.cpp",
+           "csrc/src/plan.cpp"],
+    "v5": ["csrc/src/engine.cpp", "csrc/src/hip/conv_mfma.hip", "csrc/src/hip/winograd.hip",
+           "csrc/src/hip/conv1_wino.hip", "csrc/src/hip/pool_lrn.hip", "csrc/src/plan.cpp",
+           "csrc/src/runtime/schedule.cpp", "csrc/src/comm/device_comm.cpp"],
+}
+REF_VERSION_DIRS = {
+    "v1": ["final_project/v1_serial"], "v2.1": ["final_project/v2_mpi_only/2.1_broadcast_all"],
+    "v2.2": ["final_project/v2_mpi_only/2.2_scatter_halo"], "v3": ["final_project/v3_cuda_only"],
+    "v4": ["final_project/v4_mpi_cuda"], "v5": ["final_project/v5_cuda_aware_mpi"],
+}
+_SRC_EXT = (".cpp", ".cu", ".hip", ".hpp", ".h", ".c", ".inl", ".cuh")
+
+
+def _loc(path: str) -> int:
+    n, block = 0, False
+    try:
+        for line in open(path, errors="replace"):
+            t = line.strip()
+            if block:
+                block = "*/" not in t
+                continue
+            if not t or t.startswith("//"):
+                continue
+            if t.startswith("/*"):
+                block = "*/" not in t
+                continue
+            n += 1
+    except OSError:
+        return 0
+    return n
+
+
+def _loc_tree(root: str, dirs: list[str]) -> int:
+    total = 0
+    for d in dirs:
+        for dp, _, files in os.walk(os.path.join(root, d)):
+            total += sum(_loc(os.path.join(dp, f)) for f in files if f.endswith(_SRC_EXT))
+    return total
+
+
+@app.command()
+def report(out: str = "report.md", plot_out: str = "", ref_root: str = "", repo_root: str = ".",
+           db: str = DEFAULT_DB):
+    """The notebook's synthesis views (analysis.md Cells 17-19) as one markdown report: ours vs the
+    reference per version, scaling with the Karp-Flatt serial fraction, and code size vs speedup."""
+    import pandas as pd
+    sp = _speedup_df(db, "v1")
+    lines = ["# Run-log synthesis", "", f"warehouse: `{db}`, {len(sp)} (source, batch, version, np) groups", ""]
+    # 1. ours vs the reference's logged runs, per version and np (batch 1: the reference's config)
+    ours = sp[(sp.source == "anx-native") & (sp.batch == 1)]
+    ref = sp[sp.source.str.startswith("reference")]  # its logs, and its CSVs ingested with --tag reference
+    rows = []
+    for _, r in ours.iterrows():
+        rr = ref[(ref.version == r.version) & (ref.np == r.np)]
+        if len(rr):
+            t_ref = float(rr.best_ms.min())
+            rows.append(dict(version=r.version, np=int(r.np), ours_ms=r.best_ms, reference_best_ms=t_ref,
+                             speedup_over_reference=t_ref / r.best_ms))
+    lines += ["## Ours vs the reference's own logged runs (batch 1, best of each)", ""]
+    if rows:
+        lines += [pd.DataFrame(rows).to_markdown(index=False, floatfmt=".3f"), ""]
+    else:
+        lines += ["(no overlapping version / np between the two sources)", ""]
+    # 2. scaling: self-relative speedup, efficiency, Karp-Flatt experimentally determined serial fraction
+    lines += ["## Scaling (self-relative) and the Karp-Flatt serial fraction e = (1/S - 1/p) / (1 - 1/p)", ""]
+    sc = sp[sp.np > 1].copy()
+    sc["karp_flatt"] = (1.0 / sc.speedup_self - 1.0 / sc.np) / (1.0 - 1.0 / sc.np)
+    if len(sc):
+        lines += [sc[["source", "batch", "version", "np", "best_ms", "speedup_self", "efficiency_self", "karp_flatt"]]
+                  .sort_values(["source", "batch", "version", "np"]).to_markdown(index=False, floatfmt=".3f"), ""]
+    # 3. code size vs speed (the notebook's LOC x performance synthesis)
+    loc = []
+    for v, files in OUR_VERSION_SOURCES.items():
+        row = dict(version=v, ours_loc=sum(_loc(os.path.join(repo_root, f)) for f in files))
+        if ref_root:
+            row["reference_loc"] = _loc_tree(ref_root, REF_VERSION_DIRS[v])
+        for b in sorted(ours.batch.unique()) if len(ours) else []:
+            g = sp[(sp.source == "anx-native") & (sp.batch == b) & (sp.version == v) & (sp.np == 1)]
+            row[f"speedup_vs_v1_b{b}"] = float(g.speedup_vs_base.iloc[0]) if len(g) else float("nan")
+        loc.append(row)
+    ldf = pd.DataFrame(loc)
+    lines += ["## Code size per version vs speed (np = 1)", "",
+              "Lines of code of each version's own path (non-blank, non-comment; ours: the files each "
+              "version runs, shared kernels counted in every version that uses them).", "",
+              ldf.to_markdown(index=False, floatfmt=".2f"), ""]
+    spcols = [c for c in ldf.columns if c.startswith("speedup_vs_v1_b")]
+    if spcols and ldf[spcols[-1]].notna().sum() >= 3:
+        from scipy.stats import pearsonr
+        ok = ldf[ldf[spcols[-1]].notna()]
+        r, pval = pearsonr(ok.ours_loc, ok[spcols[-1]].map(math.log10))
+        lines += [f"Pearson r(ours LOC, log10 speedup at {spcols[-1][-4:]}) = {r:.2f} (p = {pval:.2g}, "
+                  f"{len(ok)} versions): the larger paths are the device versions (V3-V5, MFMA kernels, "
+                  f"Winograd, runtime), which are also the fast ones.", ""]
+        if plot_out:
+            import matplotlib
+            matplotlib.use("Agg")
+            import matplotlib.pyplot as plt
+            fig, ax = plt.subplots(figsize=(6, 4))
+            ax.scatter(ok.ours_loc, ok[spcols[-1]], label="anx (MI355X)")
+            for _, q in ok.iterrows():
+                ax.annotate(q.version, (q.ours_loc, q[spcols[-1]]), fontsize=8)
+            ax.set_xlabel("lines of code of the version's path")
+            ax.set_ylabel(f"speedup vs V1 ({spcols[-1][-4:]})")
+            ax.set_yscale("log")
+            ax.grid(alpha=0.3)
+            fig.tight_layout()
+            fig.savefig(plot_out, dpi=120)
+            lines += [f"![speedup vs LOC]({os.path.basename(plot_out)})", ""]
+    with open(out, "w") as f:
+        f.write("\n".join(lines))
+    typer.echo(f"wrote {out}")
 
 
 if __name__ == "__main__":
