@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
     ap.add_argument("--lanes", type=int, default=2,
                     help="concurrent HIP streams per GPU the batch is split over (one engine each)")
+    ap.add_argument("--full-lanes", type=int, default=1,
+                    help="--model full: concurrent stream lanes the batch is split over (AlexNetFull lanes)")
     ap.add_argument("--input-source", default="local", choices=["root", "local"],
                     help="dp: local = per-rank synthetic shard; root = rank 0 scatters the batch")
     ap.add_argument("--no-gather", action="store_true", help="dp: leave outputs on their ranks")
@@ -126,7 +128,7 @@ def main():
     if a.model == "full":  # extension config: full AlexNet bf16 (BASELINE.json config 5)
         from anx.models.alexnet_full import FLOPS_PER_IMAGE, AlexNetFull
         B = a.batch_per_gpu or 256
-        model = AlexNetFull(seed=1234, device=dev, max_batch=B)
+        model = AlexNetFull(seed=1234, device=dev, max_batch=B, lanes=a.full_lanes)
         out_shape, flops = (1000,), FLOPS_PER_IMAGE
     elif a.workload == "dp":
         B = a.batch_per_gpu or DEFAULT_BATCH["dp"]

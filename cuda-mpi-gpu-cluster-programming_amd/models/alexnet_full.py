@@ -48,7 +48,8 @@ def init_full_weights(seed: int = 0, classes: int = 1000, groups2: int = 1) -> d
 
 class AlexNetFull:
     def __init__(self, weights: dict | None = None, *, seed: int = 0, classes: int = 1000, device="cuda",
-                 max_batch: int = 1, groups2: int = 1, lrn_mode: str = "div_n", knobs: dict | None = None):
+                 max_batch: int = 1, groups2: int = 1, lrn_mode: str = "div_n", knobs: dict | None = None,
+                 lanes: int = 1):
         self.classes, self.groups2, self.lrn_mode = classes, groups2, lrn_mode
         self.knobs = {k: knob_value(k, v) for k, v in (knobs or {}).items()}  # e.g. {"bf16_glds": 3}
         self.weights = {k: v.detach().to("cpu", torch.float32).contiguous()
@@ -59,6 +60,20 @@ class AlexNetFull:
         self._h = None
         self._cap = 0
         self._ensure(max_batch)
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
+        # lanes > 1: the batch is split over engines on concurrent HIP streams (forked from / joined to
+        # the caller's stream, as AlexNetBlocks does), so one lane's partial last rounds overlap the
+        # other's kernels. Measured slower at 256 images (281k vs 305k img/s: half-size launches of
+        # the 1-workgroup-per-CU kernels quantize worse), 334k at 512 as 2 x 256
+        # (profiles/r02_ab_full_lanes.txt)
+        self._lanes: list[AlexNetFull] = []
+        self._lane_streams: list[torch.cuda.Stream] = []
+        per_lane = -(-max(1, max_batch) // lanes)
+        for _ in range(lanes - 1):
+            self._lanes.append(AlexNetFull(self.weights, classes=classes, device=self.device, max_batch=per_lane,
+                                           groups2=groups2, lrn_mode=lrn_mode, knobs=self.knobs))
+            self._lane_streams.append(torch.cuda.Stream(self.device))
 
     def _ensure(self, n):
         if self._h is not None and n <= self._cap:
@@ -81,8 +96,12 @@ class AlexNetFull:
         v = knob_value(name, value)
         apply_knobs(self._h, {name: v}, full=True)
         self.knobs[name] = v
+        for m in getattr(self, "_lanes", ()):
+            m.set_knob(name, v)
 
     def close(self):
+        for m in getattr(self, "_lanes", ()):
+            m.close()
         if self._h is not None:
             torch.cuda.synchronize(self.device)
             nat.lib().anx_full_destroy(self._h)
@@ -99,9 +118,22 @@ class AlexNetFull:
         if tuple(x.shape[1:]) != (227, 227, 3) or x.dtype != torch.float32 or not x.is_contiguous():
             raise ValueError("expected contiguous fp32 NHWC [N,227,227,3]")
         N = x.shape[0]
-        self._ensure(N)
         y = out if out is not None else torch.empty(N, self.classes, device=self.device)
-        nat.call("anx_full_forward", self._h, x.data_ptr(), N, y.data_ptr(), nat.stream_ptr(self.device))
+        L = 1 + len(self._lanes)
+        if L == 1 or N < L:
+            self._ensure(N)
+            nat.call("anx_full_forward", self._h, x.data_ptr(), N, y.data_ptr(), nat.stream_ptr(self.device))
+            return y
+        bounds = [N * i // L for i in range(L + 1)]
+        cur = torch.cuda.current_stream(self.device)
+        for i, st in enumerate(self._lane_streams, start=1):
+            st.wait_stream(cur)  # fork: inputs produced / outputs free on the current stream
+            with torch.cuda.stream(st):
+                self._lanes[i - 1].forward(x[bounds[i]:bounds[i + 1]], y[bounds[i]:bounds[i + 1]])
+        self._ensure(bounds[1])
+        nat.call("anx_full_forward", self._h, x.data_ptr(), bounds[1], y.data_ptr(), nat.stream_ptr(self.device))
+        for st in self._lane_streams:
+            cur.wait_stream(st)  # join
         return y
 
     __call__ = forward

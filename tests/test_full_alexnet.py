@@ -146,3 +146,17 @@ def test_bf16_pool_lrn_wave_kernel_bitwise(cuda, lrn):
     got = m(x)
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_full_alexnet_lanes_bit_identical(cuda):
+    """lanes=2 splits the batch over two engines on concurrent streams: every image's logits are
+    bit-identical to the one-lane forward of the same images at that lane's batch size."""
+    N = 10
+    x = (init_input(N, "rand", seed=15) * 10).to(cuda)
+    two = AlexNetFull(seed=15, device=cuda, max_batch=N, lanes=2)
+    y = two(x).clone()
+    one = AlexNetFull(two.weights, device=cuda, max_batch=N // 2)
+    ref = torch.cat([one(x[:N // 2].contiguous()).clone(), one(x[N // 2:].contiguous()).clone()])
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
