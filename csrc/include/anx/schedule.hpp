@@ -77,7 +77,8 @@ class Transport {
   // One phase of step k (parity = k & 1) with the full list of that phase's transfers.
   virtual void run_phase(Phase ph, const std::vector<Transfer>& xs, hipStream_t compute, int parity) = 0;
   // End of a step: every buffer this rank received into has been consumed by the work enqueued on
-  // `compute` so far (senders may overwrite them in the next step).
+  // `compute` so far (senders may overwrite them in the next step). On return, work enqueued on
+  // `compute` afterwards may overwrite this rank's send buffers (its pushes so far are complete).
   virtual void end_step(hipStream_t compute) = 0;
   virtual void close() {}
   // Record-only mode (no HIP / RCCL / socket call): every transfer is appended to log() — the

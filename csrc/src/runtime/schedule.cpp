@@ -174,12 +174,15 @@ struct RcclTransport : DeviceBase {
 // event for (phase, parity) and posts a 4-byte "sent" note over the host channel; the receiver's
 // host thread takes the note, and its compute stream waits for the sender's IPC event. Receive
 // buffers alternate by step parity, so a push of step k+1 can never land in a buffer step k is
-// still reading: the sender only gets to step k+1 of a phase after data of the receiver's step k.
+// still reading: the sender only gets to step k+1 of a phase after data of the receiver's step k
+// (the root's scatter of step k+2 follows its gather of step k, which waits for every rank's
+// stage2 of step k).
 struct PeerTransport : DeviceBase {
   HostComm& c_;
   int device_;
   hipStream_t cs_ = nullptr;
   hipEvent_t ready_ = nullptr;
+  hipEvent_t drained_ = nullptr;                 // end_step: all pushes issued so far are done
   hipEvent_t sent_[3][2] = {};                   // own IPC events (phase, parity)
   std::vector<std::array<std::array<hipEvent_t, 2>, 3>> peer_sent_;  // opened IPC events of every rank
   std::vector<std::array<void*, kB * 2>> peer_buf_;                  // mapped buffers of every rank
@@ -226,6 +229,7 @@ struct PeerTransport : DeviceBase {
     if (record_only) return;
     hip_ok(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking), "hipStreamCreate");
     hip_ok(hipEventCreateWithFlags(&ready_, hipEventDisableTiming), "hipEventCreate");
+    hip_ok(hipEventCreateWithFlags(&drained_, hipEventDisableTiming), "hipEventCreate");
     for (auto& ph : sent_)
       for (auto& e : ph)
         hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventInterprocess), "hipEventCreate IPC");
@@ -297,7 +301,13 @@ struct PeerTransport : DeviceBase {
                x.width, x.height, compute);
     }
   }
-  void end_step(hipStream_t) override {}
+  // The stream waits for every push this rank has issued so far (its send buffers may be rewritten
+  // after that; the receivers' buffers are ordered by their own IPC-event waits).
+  void end_step(hipStream_t s) override {
+    if (record_only || !cs_) return;
+    hip_ok(hipEventRecord(drained_, cs_), "hipEventRecord");
+    hip_ok(hipStreamWaitEvent(s, drained_, 0), "hipStreamWaitEvent");
+  }
   void close() override {
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
     opened_.clear();
@@ -309,6 +319,7 @@ struct PeerTransport : DeviceBase {
       for (auto& e : ph)
         if (e) (void)hipEventDestroy(e), e = nullptr;
     if (ready_) (void)hipEventDestroy(ready_), ready_ = nullptr;
+    if (drained_) (void)hipEventDestroy(drained_), drained_ = nullptr;
     if (cs_) (void)hipStreamDestroy(cs_), cs_ = nullptr;
   }
 };

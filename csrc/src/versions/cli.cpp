@@ -55,6 +55,8 @@ struct Options {
   std::string transport = "auto";   // v5 device traffic: auto | rccl | peer (IPC + hipMemcpy2DAsync)
   std::string split = "rows";       // v5 decomposition: rows (reference) | hybrid (batch first) | batch
   bool dry_run = false;             // v5: print the transfer schedule (record-only transports, no GPU)
+  std::string pipeline = "auto";    // v5: scatter / gather on a second stream (auto: on over RCCL)
+  bool poison = false;              // v5: NaN-fill consumed buffers (a mis-ordered step corrupts the output)
   bool check = false;
   bool json = true;
   std::string weights;  // directory with raw fp32 w1/b1/w2/b2 .bin (overrides --init for weights)
@@ -66,7 +68,8 @@ struct Options {
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
                "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd]\n"
                "           [--conv1-algo auto|direct|winograd] [--transport auto|rccl|peer] [--check]\n"
-               "           [--split rows|hybrid|batch] [--dry-run] [--weights DIR] [--no-json]\n",
+               "           [--split rows|hybrid|batch] [--dry-run] [--pipeline auto|on|off] [--poison]\n"
+               "           [--weights DIR] [--no-json]\n",
                msg);
   std::exit(2);
 }
@@ -93,6 +96,10 @@ Options parse(int argc, char** argv) {
     else if (a == "--transport") o.transport = val();
     else if (a == "--split") o.split = val();
     else if (a == "--dry-run") o.dry_run = true;
+    else if (a == "--pipeline") {
+      o.pipeline = val();
+      if (o.pipeline != "on" && o.pipeline != "off" && o.pipeline != "auto") usage("--pipeline must be auto, on or off");
+    } else if (a == "--poison") o.poison = true;
     else if (a == "--check") o.check = true;
     else if (a == "--no-json") o.json = false;
     else if (a == "--weights") o.weights = val();
@@ -631,9 +638,11 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
   };
   float* d_x = rank == 0 ? dalloc(s.x.size()) : nullptr;
   float *d_tile[2], *d_y[2], *d_yfull[2] = {nullptr, nullptr};
+  const size_t tile_bytes = static_cast<size_t>(n) * t.in.size() * s.in_row * 4;
+  const size_t y_bytes = static_cast<size_t>(n) * t.out.size() * s.out_row * 4;
   for (int p = 0; p < 2; ++p) {
-    d_tile[p] = dalloc(static_cast<size_t>(n) * t.in.size() * s.in_row);
-    d_y[p] = dalloc(static_cast<size_t>(n) * t.out.size() * s.out_row);
+    d_tile[p] = dalloc(tile_bytes / 4);
+    d_y[p] = dalloc(y_bytes / 4);
     if (rank == 0) d_yfull[p] = dalloc(static_cast<size_t>(N) * s.d.Hp2 * s.out_row);
   }
   // the conv2 window exists once stage1 has run on this tile geometry: run it once on zeros
@@ -659,15 +668,19 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
   std::vector<float> y_host(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
   const char* names[5] = {"scatter", "compute", "halo_p1", "compute", "gather"};
   constexpr int kEv = 6;
-  auto step = [&](int k, hipEvent_t* ev) {
-    const int par = k & 1;
-    hip_check(hipEventRecord(ev[0], st), "event");
+  // Phases of step k. The transport orders each phase against the stream it is given (the copies /
+  // RCCL group wait for that stream's work so far, and the stream waits for the data to land), so
+  // the scatter and gather can run on `io` while `st` computes another step.
+  auto scatter = [&](int k, hipStream_t on) {
     RoctxRange r0("v5 scatter");
-    x->run_phase(Phase::Scatter, sched.phase[0], st, par);
-    hip_check(hipEventRecord(ev[1], st), "event");
+    x->run_phase(Phase::Scatter, sched.phase[0], on, k & 1);
+  };
+  auto compute = [&](int k, hipEvent_t* ev) {  // ev[1] recorded before, ev[2..4] inside (on st)
+    const int par = k & 1;
     if (n && mode == Decomp::PerLayer) {
       RoctxRange r1("v5 stage1");
       hip_check(eng.stage1(d_tile[par], n, t, st), "stage1");
+      if (s.o.poison) hip_check(hipMemsetAsync(d_tile[par], 0xff, tile_bytes, st), "poison tile");
     }
     hip_check(hipEventRecord(ev[2], st), "event");
     {
@@ -677,18 +690,67 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
     hip_check(hipEventRecord(ev[3], st), "event");
     if (n) {
       RoctxRange r3("v5 stage2");
-      if (mode == Decomp::PerLayer)
+      if (mode == Decomp::PerLayer) {
         hip_check(eng.stage2(n, t, d_y[par], st), "stage2");
-      else
+      } else {
         hip_check(eng.tile_forward(d_tile[par], n, t, d_y[par], st), "tile_forward");
+        if (s.o.poison) hip_check(hipMemsetAsync(d_tile[par], 0xff, tile_bytes, st), "poison tile");
+      }
     }
     hip_check(hipEventRecord(ev[4], st), "event");
+  };
+  auto gather = [&](int k, hipStream_t on) {
     {
       RoctxRange r4("v5 gather");
-      x->run_phase(Phase::Gather, sched.phase[2], st, par);
+      x->run_phase(Phase::Gather, sched.phase[2], on, k & 1);
     }
+    x->end_step(on);  // `on` now also waits for this rank's outgoing pushes of the step
+    if (s.o.poison && n) hip_check(hipMemsetAsync(d_y[k & 1], 0xff, y_bytes, on), "poison y");
+  };
+  // serial step (the cold step, and --pipeline off): every phase on st
+  auto step = [&](int k, hipEvent_t* ev) {
+    hip_check(hipEventRecord(ev[0], st), "event");
+    scatter(k, st);
+    hip_check(hipEventRecord(ev[1], st), "event");
+    compute(k, ev);
+    gather(k, st);
     hip_check(hipEventRecord(ev[5], st), "event");
-    x->end_step(st);
+  };
+  // Pipelined steady state: io runs scatter(k+1) while st computes step k, then gather(k) once
+  // stage2(k) is done; st starts step k+1 as soon as scatter(k+1) has landed. Buffer reuse is
+  // ordered without extra events: Tile[p] is rewritten by scatter(k+2), which io issues after
+  // gather(k), which waited for stage2(k) (so stage1(k) is done everywhere: the root's gather
+  // waits for every sender's push); Y[p] is rewritten by stage2(k+2) on st, which waited for
+  // scatter(k+2) on io, issued after gather(k) and its end_step. Every rank issues the phases in
+  // the same order (halo k, scatter k+1, gather k), as RCCL's in-order matching requires.
+  // Phase times: "scatter" is how long st waited for its input, "gather" the time from the end of
+  // stage2 to the end of the gather on io (off the critical path when the overlap works).
+  hipStream_t io = nullptr;
+  hipEvent_t e_sc[2], e_s2[2];
+  hip_check(hipStreamCreateWithFlags(&io, hipStreamNonBlocking), "stream");
+  for (int p = 0; p < 2; ++p) {
+    hip_check(hipEventCreateWithFlags(&e_sc[p], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&e_s2[p], hipEventDisableTiming), "hipEventCreate");
+  }
+  auto run_pipelined = [&](int k0, int iters, hipEvent_t* evs) {
+    scatter(k0, io);
+    hip_check(hipEventRecord(e_sc[k0 & 1], io), "event");
+    for (int i = 0; i < iters; ++i) {
+      const int k = k0 + i, par = k & 1;
+      hipEvent_t* ev = evs + kEv * i;
+      hip_check(hipEventRecord(ev[0], st), "event");
+      hip_check(hipStreamWaitEvent(st, e_sc[par], 0), "wait scatter");
+      hip_check(hipEventRecord(ev[1], st), "event");
+      compute(k, ev);
+      hip_check(hipEventRecord(e_s2[par], st), "event");
+      if (i + 1 < iters) {
+        scatter(k + 1, io);
+        hip_check(hipEventRecord(e_sc[par ^ 1], io), "event");
+      }
+      hip_check(hipStreamWaitEvent(io, e_s2[par], 0), "wait stage2");
+      gather(k, io);
+      hip_check(hipEventRecord(ev[5], io), "event");
+    }
   };
   auto make_events = [](int count) {
     std::vector<hipEvent_t> v(count);
@@ -714,14 +776,25 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
   if (s.o.iters > 0) {
     c.barrier();
     const double w0 = now_ms();
-    for (int i = 0; i < s.o.iters; ++i) step(1 + i, evw.data() + kEv * i);  // no host sync inside
+    // auto: pipelined over RCCL (one communicator stream per rank serialises all phases, so the
+    // serial schedule puts every transfer on the critical path); serial for the peer transport,
+    // where ranks that share one GPU measured mixed (profiles/r02_ab_v5_pipeline.txt)
+    if (s.o.pipeline == "on" || (s.o.pipeline == "auto" && tr == "rccl"))
+      run_pipelined(1, s.o.iters, evw.data());
+    else
+      for (int i = 0; i < s.o.iters; ++i) step(1 + i, evw.data() + kEv * i);  // no host sync inside
     hip_check(hipStreamSynchronize(st), "sync");
+    hip_check(hipStreamSynchronize(io), "sync");
     c.barrier();
     wall = (now_ms() - w0) / s.o.iters;
     for (int i = 0; i < s.o.iters; ++i) add_phases(warm, evw.data() + kEv * i);
     if (rank == 0) {  // the last warm step's output (parity of step iters)
       hip_check(hipMemcpy(y_host.data(), d_yfull[s.o.iters & 1], y_host.size() * 4, hipMemcpyDeviceToHost), "D2H");
     }
+  }
+  for (int p = 0; p < 2; ++p) {
+    (void)hipEventDestroy(e_sc[p]);
+    (void)hipEventDestroy(e_s2[p]);
   }
   for (auto e : ev0) (void)hipEventDestroy(e);
   for (auto e : evw) (void)hipEventDestroy(e);
@@ -736,6 +809,7 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
   c.barrier();  // every peer has unmapped this rank's buffers before they are freed
   for (float* p : {d_x, d_tile[0], d_tile[1], d_y[0], d_y[1], d_yfull[0], d_yfull[1]})
     if (p) (void)hipFree(p);
+  (void)hipStreamDestroy(io);
   (void)hipStreamDestroy(st);
   c.barrier();
   return 0;

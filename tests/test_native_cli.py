@@ -129,11 +129,16 @@ def test_native_v5_peer_transport(cuda, np_, decomp, split):
     share the box's GPU, and the output is bit-identical to the single-GPU run (direct convs)."""
     d = ["--conv2-algo", "direct", "--conv1-algo", "direct"]
     ref, _ = native(["--version", "v3", "--init", "rand", "--seed", "6", "--batch", "3", *d])
-    rec, out = native(["--version", "v5", "--transport", "peer", "--decomp", decomp, "--split", split, "--init",
-                       "rand", "--seed", "6", "--batch", "3", "--iters", "3", "--lrn-alpha-mode", "raw", *d], np_)
-    assert set(rec["phases_warm"]) >= {"scatter", "halo_p1", "compute", "gather"}
-    assert "Final Output Shape: 13x13x256" in out.stdout or rec["shape"] == [13, 13, 256]
-    assert rec["checksum"] == ref["checksum"]
+    # pipelined steady state (scatter / gather on a second stream) with --poison: every consumed
+    # buffer is NaN-filled after use, so a step that reads or overwrites one out of order changes
+    # the checksum of the last step
+    for pipe in ("on", "off"):
+        rec, out = native(["--version", "v5", "--transport", "peer", "--decomp", decomp, "--split", split, "--init",
+                           "rand", "--seed", "6", "--batch", "3", "--iters", "4", "--lrn-alpha-mode", "raw",
+                           "--pipeline", pipe, "--poison", *d], np_)
+        assert set(rec["phases_warm"]) >= {"scatter", "halo_p1", "compute", "gather"}
+        assert "Final Output Shape: 13x13x256" in out.stdout or rec["shape"] == [13, 13, 256]
+        assert rec["checksum"] == ref["checksum"], pipe
     # default (Winograd) convs: equal to the fp64 oracle within fp32 error
     rec, _ = native(["--version", "v5", "--transport", "peer", "--init", "rand", "--seed", "6", "--batch", "3",
                      "--check"], np_)
