@@ -34,6 +34,8 @@ struct Knobs {
   int bf16_glds = 2;       // bf16 full model: 0 register-staged, 2 / 3 LDS-DMA ring slots
   int bf16_big = -1;       // bf16 conv layers on the wide-tile kernel (conv_bf16_big.hip): -1 cost model
                            // picks the config, -2 off (the 128x128 kernels above), 0.. force that config
+  int bf16_fc = 0;         // bf16 FC layers: 1 = activation-streaming kernel (fc_bf16; measured slower than the
+                           // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
   int conv1_occ = 0;       // cap on Conv1 Winograd GEMM workgroups per CU (0 = natural: 4), by LDS padding,
   int conv2_occ = 0;       // ... and Conv2's (natural 2): leaves room for a concurrent lane's kernels

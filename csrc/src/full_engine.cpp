@@ -114,13 +114,14 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
       if (ks > 1) ws = std::max(ws, static_cast<size_t>(ks) * b * L_[i].K);
       const hip::BigFc f = hip::pick_bf16_big_fc(p, cus_);  // wide-tile FC slabs (at ksplit 1 for fp32 logits)
       if (f.cfg >= 0) ws = std::max(ws, static_cast<size_t>(f.ksplit) * b * L_[i].K);
+      if (hip::fc_bf16_ok(p)) ws = std::max(ws, static_cast<size_t>(std::max(1, hip::pick_fc_split(p, cus_))) * b * L_[i].K);
     }
   if (ws) ws_ = static_cast<float*>(dalloc(ws * 4));
 }
 
 FullEngine::~FullEngine() {
   for (Layer& L : L_)
-    for (void* p : {L.wp, static_cast<void*>(L.koff), static_cast<void*>(L.bias)})
+    for (void* p : {L.wp, L.wfc, static_cast<void*>(L.koff), static_cast<void*>(L.bias)})
       if (p) (void)hipFree(p);
   for (void* p : {xb_, c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_, static_cast<void*>(ws_)})
     if (p) (void)hipFree(p);
@@ -140,9 +141,24 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
     ANX_TRY(hipMalloc(&L.koff, ko.size() * 4));
     ANX_TRY(hipMemcpy(L.wp, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
     ANX_TRY(hipMemcpy(L.koff, ko.data(), ko.size() * 4, hipMemcpyHostToDevice));
+    if (L.wfc) ANX_TRY(hipFree(L.wfc));
+    L.wfc = nullptr;
+    if (hip::fc_bf16_ok(p)) {
+      std::vector<uint16_t> bl;
+      hip::pack_fc_blocked_bf16(p, pk, bl);
+      ANX_TRY(hipMalloc(&L.wfc, bl.size() * 2));
+      ANX_TRY(hipMemcpy(L.wfc, bl.data(), bl.size() * 2, hipMemcpyHostToDevice));
+    }
     L.key = p.variant;
   }
   const bool fc = p.Hp == 1 && p.Wp == 1 && p.F == 1;
+  if (fc && k_.bf16_fc && L.wfc) {  // activation-streaming FC kernel, fp32 slabs + reduce
+    const int ks = hip::pick_fc_split(p, cus_);
+    if (ks > 0) {
+      ANX_TRY(hip::fc_bf16(p, x, L.wfc, ws_, ks, s));
+      return hip::splitk_reduce_bf16(ws_, ks, N, L.K, L.bias, relu, out, out_f32, s);
+    }
+  }
   if (fc && k_.bf16_big != -2) {  // wide-tile FC: one 256-row tile of the batch, K split over the CUs
     hip::BigFc f = hip::pick_bf16_big_fc(p, cus_);
     if (f.cfg >= 0 && k_.bf16_big >= 0 && hip::conv_bf16_big_ok(p, k_.bf16_big, hip::OutViewB{B(ws_), 1, 1, p.Kg, 0, 0, 0}))
@@ -197,10 +213,11 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
 }
 
 size_t FullEngine::tap(int i, int N, void* dst, hipStream_t s) const {
-  static const size_t kElems[10] = {55 * 55 * 96,   31 * 31 * 96,   27 * 27 * 256, 15 * 15 * 256, 15 * 15 * 384,
-                                    15 * 15 * 384, 13 * 13 * 256, 9216,          4096,          4096};
-  void* const bufs[10] = {c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_};
-  if (i < 0 || i >= 10 || N < 1 || N > chunk_) return 0;
+  static const size_t kElems[11] = {55 * 55 * 96,   31 * 31 * 96, 27 * 27 * 256, 15 * 15 * 256,
+                                    15 * 15 * 384,  15 * 15 * 384, 13 * 13 * 256, 9216,
+                                    4096,           4096,          57 * 57 * 48};
+  void* const bufs[11] = {c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_, xb_};
+  if (i < 0 || i >= 11 || (i == 10 && !poly1_) || N < 1 || N > chunk_) return 0;
   if (hipMemcpyAsync(dst, bufs[i], kElems[i] * N * 2, hipMemcpyDeviceToDevice, s) != hipSuccess) return 0;
   return kElems[i];
 }

@@ -347,6 +347,39 @@ __global__ void __launch_bounds__(256) pool_bf16_kernel(const bf16* __restrict__
   }
 }
 
+// Workgroup = (n, output row oy): the F input rows S*oy .. S*oy+F-1 are contiguous; each thread
+// takes the column max over them for (column, 8 channels) pairs (16-B loads), stages it in LDS, then
+// writes the Wo horizontal maxima as 16-B stores. Each input row is fetched by at most
+// ceil(F / S) workgroups instead of each input pixel by ~(F / S)^2 output threads.
+__global__ void __launch_bounds__(256) pool_rows_bf16_kernel(const bf16* __restrict__ x, int H, int W, int C, int F,
+                                                             int S, int Ho, int Wo, OutViewB o) {
+  extern __shared__ __attribute__((aligned(16))) bf16 colmax[];  // [W][C]
+  const int oy = blockIdx.x, n = blockIdx.y, C8 = C / 8;
+  const int y0 = oy * S, fh = min(F, H - y0);
+  const bf16* src = x + (static_cast<size_t>(n) * H + y0) * W * C;
+  for (int q = threadIdx.x; q < W * C8; q += 256) {  // q = column * C8 + chunk
+    bf16x8 m = *reinterpret_cast<const bf16x8*>(src + q * 8);
+    for (int r = 1; r < fh; ++r) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + static_cast<size_t>(r) * W * C + q * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = static_cast<bf16>(fmaxf(static_cast<float>(m[e]), static_cast<float>(v[e])));
+    }
+    *reinterpret_cast<bf16x8*>(colmax + q * 8) = m;
+  }
+  __syncthreads();
+  bf16* dst = o.base + (static_cast<size_t>(n * o.Hb + oy + o.h_off) * o.Wb + o.w_off) * o.Cb + o.c_off;
+  for (int q = threadIdx.x; q < Wo * C8; q += 256) {
+    const int ox = q / C8, c8 = q - ox * C8, x0 = ox * S, fw = min(F, W - x0);
+    bf16x8 m = *reinterpret_cast<const bf16x8*>(colmax + (x0 * C8 + c8) * 8);
+    for (int c = 1; c < fw; ++c) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(colmax + ((x0 + c) * C8 + c8) * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = static_cast<bf16>(fmaxf(static_cast<float>(m[e]), static_cast<float>(v[e])));
+    }
+    *reinterpret_cast<bf16x8*>(dst + static_cast<size_t>(ox) * o.Cb + c8 * 8) = m;
+  }
+}
+
 // One workgroup = PP output pixels x C channels; 8 channels per thread (16-B bf16 loads/stores).
 // Pass 1 pools into LDS as fp32, pass 2 applies LRN from LDS: own 8 channels by two ds_read_b128,
 // the +-2 neighbours by two ds_read_b64 (size-5 window), fp32 math, one bf16x8 store.
@@ -491,34 +524,50 @@ __global__ void __launch_bounds__(256) pool_lrn256_bf16_kernel(const bf16* __res
   }
 }
 
-// Thread = (n, i, j, rh): the 12 floats (rw, c) of polyphase row rh are contiguous in image row
-// 4i+rh, and so are their 12 bf16 outputs (24 B at a 24-B aligned offset: 3 8-byte stores).
-__global__ void __launch_bounds__(256) s2d4_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, int total,
-                                                        int H, int W, int Ho, int Wo) {
-  using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
-  for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
-    const int rh = t & 3;
-    const int pix = t >> 2;  // (n, i, j)
-    const int j = pix % Wo;
-    const int ni = pix / Wo;
-    const int i = ni % Ho;
-    const int n = ni / Ho;
-    const int r = 4 * i + rh;
-    float v[12];
-#pragma unroll
-    for (int e = 0; e < 12; ++e) v[e] = 0.f;
-    if (r < H) {
-      const float* src = x + (static_cast<size_t>(n) * H + r) * W * 3 + 4 * j * 3;
-      const int valid = min(4, W - 4 * j) * 3;
-#pragma unroll
-      for (int e = 0; e < 12; ++e)
-        if (e < valid) v[e] = src[e];
+// Workgroup = (n, i): image rows 4i..4i+3 are one contiguous run of 4 W x 3 floats (one coalesced
+// dword pass into LDS), and output row (n, i) — Wo pixels x 48 bf16 — is contiguous and 16-B
+// aligned (Wo x 96 B): one 16-B store per 8 outputs, each gathered from LDS. (Thread-per-(pixel,
+// polyphase row) with 12 scalar loads moved 238 MB in 54 us at 256 images.)
+__global__ void __launch_bounds__(256) s2d4_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, int H, int W,
+                                                        int Ho, int Wo) {
+  extern __shared__ float rows[];  // [4][W * 3] (+ 4 floats of alignment slack in front)
+  const int i = blockIdx.x, n = blockIdx.y, RW = W * 3;
+  const int nrows = min(4, H - 4 * i);
+  const size_t off = (static_cast<size_t>(n) * H + 4 * i) * RW;  // first float of the row group
+  // 16-B loads from the 16-B aligned float at or below x + off (x may be an interior pointer of a
+  // larger batch: the granule then still lies inside that allocation); LDS float q holds source
+  // float off + q - 4
+  const int mis = static_cast<int>((reinterpret_cast<uintptr_t>(x + off) >> 2) & 3), nval = nrows * RW;
+  const float4* src4 = reinterpret_cast<const float4*>(x + (off - mis));
+  const int n4 = (mis + nval + 3) >> 2;
+  for (int t = threadIdx.x; t < n4; t += 256) {
+    const float4 v = src4[t];  // within [off - mis, off + nval + 3) of a 16-B aligned buffer
+    const int q = 4 * t - mis;  // source float of v.x relative to off
+    float* d = rows + 4 + q;    // q >= -3: the slack in front
+    if (q + 3 < nval) {
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    } else {  // the group's last vector: floats past nval belong to the zero fill below
+      if (q < nval) d[0] = v.x;
+      if (q + 1 < nval) d[1] = v.y;
+      if (q + 2 < nval) d[2] = v.z;
     }
-    bf16x4* dst = reinterpret_cast<bf16x4*>(y + static_cast<size_t>(pix) * 48 + rh * 12);
+  }
+  for (int t = nval + threadIdx.x; t < 4 * RW; t += 256) rows[4 + t] = 0.f;  // rows past the image
+  __syncthreads();
+  const float* rowsv = rows + 4;
+  bf16* dst = y + (static_cast<size_t>(n) * Ho + i) * Wo * 48;
+  for (int c = threadIdx.x; c < Wo * 6; c += 256) {  // 8 outputs per chunk, 6 chunks per pixel
+    bf16x8 v;
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-      dst[q] = bf16x4{static_cast<bf16>(v[4 * q]), static_cast<bf16>(v[4 * q + 1]), static_cast<bf16>(v[4 * q + 2]),
-                      static_cast<bf16>(v[4 * q + 3])};
+    for (int e = 0; e < 8; ++e) {
+      const int q = c * 8 + e, j = q / 48, r = q - j * 48, rh = r / 12, rw = (r - rh * 12) / 3, ch = r - rh * 12 - rw * 3;
+      const int col = 4 * j + rw;
+      v[e] = static_cast<bf16>(col < W ? rowsv[rh * RW + col * 3 + ch] : 0.f);
+    }
+    *reinterpret_cast<bf16x8*>(dst + c * 8) = v;
   }
 }
 
@@ -765,6 +814,11 @@ hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S,
   if (C % 8 || out.Cb % 8 || out.c_off % 8) return hipErrorInvalidValue;
   const long n = static_cast<long>(N) * Ho * Wo * (C / 8);
   if (n == 0) return hipSuccess;
+  const size_t lds = static_cast<size_t>(W) * C * 2;
+  if (lds <= 64 * 1024 && N <= 65535) {  // row kernel (max of bf16 values is exact: same result)
+    pool_rows_bf16_kernel<<<dim3(Ho, N), 256, lds, s>>>(static_cast<const bf16*>(x), H, W, C, F, S, Ho, Wo, out);
+    return hipGetLastError();
+  }
   pool_bf16_kernel<<<grid1d(n), 256, 0, s>>>(static_cast<const bf16*>(x), N, H, W, C, F, S, Ho, Wo, out);
   return hipGetLastError();
 }
@@ -797,10 +851,12 @@ hipError_t f32_to_bf16(const float* x, void* y, size_t n, hipStream_t s) {
 
 hipError_t f32_to_bf16_s2d4(const float* x, void* y, int N, int H, int W, hipStream_t s) {
   const int Ho = (H + 3) / 4, Wo = (W + 3) / 4;
-  const long total = static_cast<long>(N) * Ho * Wo * 4;
-  if (total == 0) return hipSuccess;
-  if (total >= (1L << 31)) return hipErrorInvalidValue;
-  s2d4_bf16_kernel<<<grid1d(total), 256, 0, s>>>(x, static_cast<bf16*>(y), static_cast<int>(total), H, W, Ho, Wo);
+  if (static_cast<long>(N) * Ho * Wo * 4 == 0) return hipSuccess;
+  if (static_cast<long>(N) * H * W * 3 >= (1L << 31) || N > 65535 || W * 3 * 4 * 4 > 64 * 1024)
+    return hipErrorInvalidValue;
+  if (reinterpret_cast<uintptr_t>(x) & 3) return hipErrorInvalidValue;
+  s2d4_bf16_kernel<<<dim3(Ho, N), 256, (static_cast<size_t>(4) * W * 3 + 8) * 4, s>>>(x, static_cast<bf16*>(y), H, W,
+                                                                                      Ho, Wo);
   return hipGetLastError();
 }
 

@@ -139,11 +139,12 @@ class AlexNetFull:
     __call__ = forward
 
     TAPS = ((55, 55, 96), (31, 31, 96), (27, 27, 256), (15, 15, 256), (15, 15, 384), (15, 15, 384), (13, 13, 256),
-            (9216,), (4096,), (4096,))
+            (9216,), (4096,), (4096,), (57, 57, 48))
 
     def tap(self, i: int, N: int) -> torch.Tensor:
         """bf16 activation ``i`` of the last forward (see FullEngine::tap): conv1, pool1 window,
-        conv2, pool2+LRN window, conv3/conv4 windows, conv5, pool5, fc6, fc7."""
+        conv2, pool2+LRN window, conv3/conv4 windows, conv5, pool5, fc6, fc7; 10: the bf16
+        polyphase (space-to-depth by 4) input of conv1."""
         y = torch.empty((N, *self.TAPS[i]), device=self.device, dtype=torch.bfloat16)
         n = C.c_size_t()
         nat.call("anx_full_tap", self._h, i, N, y.data_ptr(), C.byref(n), nat.stream_ptr(self.device))

@@ -40,6 +40,20 @@ def _q(t):  # round to bf16, compute in fp64
 
 
 @pytest.mark.gpu
+def test_s2d4_polyphase_input_exact(cuda):
+    """Conv1's polyphase input (tap 10): bf16(x) space-to-depth by 4, zero past the 227th row and
+    column, [N, 57, 57, (rh*4 + rw)*3 + c] — bit-exact against the same rearrangement in torch (one
+    round-to-nearest-even conversion on both sides)."""
+    N = 5
+    m = AlexNetFull(seed=3, device=cuda, max_batch=N)
+    x = (torch.randn(N, 227, 227, 3, generator=torch.Generator().manual_seed(4)) * 3).to(cuda)
+    m(x)
+    xq = F.pad(x.to(torch.bfloat16), (0, 0, 0, 1, 0, 1))  # 228 x 228
+    ref = xq.reshape(N, 57, 4, 57, 4, 3).permute(0, 1, 3, 2, 4, 5).reshape(N, 57, 57, 48)
+    assert torch.equal(m.tap(10, N), ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("groups2", [1, 2])
 def test_full_alexnet_per_layer_vs_bf16_oracle(cuda, groups2):
     """Each layer of the engine, fed the engine's own (bf16) input of that layer, against the same
