@@ -89,6 +89,7 @@ def test_bench_step_vs_oracle(cuda):
     ref = blocks_forward(x[idx.to(cuda)].cpu(), m.weights, m.b1, m.b2)
     got = y[idx.to(cuda)].cpu().double()
     assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
-    # the second lane's half is bitwise what one engine computes for it alone
-    solo = AlexNetBlocks(init="rand", seed=1234, device=cuda, max_batch=B // 2)
+    # the second lane's half is bitwise what one engine with a lane's knobs (no Winograd tail split,
+    # the multi-lane default) computes for it alone
+    solo = AlexNetBlocks(init="rand", seed=1234, device=cuda, max_batch=B // 2, knobs={"wino_split": 0})
     assert torch.equal(solo(x[B // 2:].contiguous()), y[B // 2:])
