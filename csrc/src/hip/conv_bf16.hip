@@ -530,34 +530,23 @@ __global__ void __launch_bounds__(256) pool_lrn256_bf16_kernel(const bf16* __res
 // polyphase row) with 12 scalar loads moved 238 MB in 54 us at 256 images.)
 __global__ void __launch_bounds__(256) s2d4_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, int H, int W,
                                                         int Ho, int Wo) {
-  extern __shared__ float rows[];  // [4][W * 3] (+ 4 floats of alignment slack in front)
+  extern __shared__ float rows[];  // [4][W * 3] from rows + mis (+ 8 floats of alignment slack)
   const int i = blockIdx.x, n = blockIdx.y, RW = W * 3;
   const int nrows = min(4, H - 4 * i);
   const size_t off = (static_cast<size_t>(n) * H + 4 * i) * RW;  // first float of the row group
   // 16-B loads from the 16-B aligned float at or below x + off (x may be an interior pointer of a
-  // larger batch: the granule then still lies inside that allocation); LDS float q holds source
-  // float off + q - 4
+  // larger batch: the granule then still lies inside that allocation), stored as 16-B LDS writes at
+  // the same alignment: LDS float p holds source float off - mis + p, so the image starts at rows + mis
   const int mis = static_cast<int>((reinterpret_cast<uintptr_t>(x + off) >> 2) & 3), nval = nrows * RW;
   const float4* src4 = reinterpret_cast<const float4*>(x + (off - mis));
   const int n4 = (mis + nval + 3) >> 2;
-  for (int t = threadIdx.x; t < n4; t += 256) {
-    const float4 v = src4[t];  // within [off - mis, off + nval + 3) of a 16-B aligned buffer
-    const int q = 4 * t - mis;  // source float of v.x relative to off
-    float* d = rows + 4 + q;    // q >= -3: the slack in front
-    if (q + 3 < nval) {
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
-    } else {  // the group's last vector: floats past nval belong to the zero fill below
-      if (q < nval) d[0] = v.x;
-      if (q + 1 < nval) d[1] = v.y;
-      if (q + 2 < nval) d[2] = v.z;
-    }
+  for (int t = threadIdx.x; t < n4; t += 256) reinterpret_cast<float4*>(rows)[t] = src4[t];
+  if (nval < 4 * RW) {  // the last row group: rows past the image are zero (block-uniform branch)
+    __syncthreads();    // after the vector writes, whose last vector may reach past nval
+    for (int t = nval + threadIdx.x; t < 4 * RW; t += 256) rows[mis + t] = 0.f;
   }
-  for (int t = nval + threadIdx.x; t < 4 * RW; t += 256) rows[4 + t] = 0.f;  // rows past the image
   __syncthreads();
-  const float* rowsv = rows + 4;
+  const float* rowsv = rows + mis;
   bf16* dst = y + (static_cast<size_t>(n) * Ho + i) * Wo * 48;
   for (int c = threadIdx.x; c < Wo * 6; c += 256) {  // 8 outputs per chunk, 6 chunks per pixel
     bf16x8 v;

@@ -498,7 +498,9 @@ constexpr BigCfg kCfg[] = {{256, 256, 512, 2, 1, 1.0f},  {256, 128, 512, 2, 1, 0
                            {128, 128, 256, 3, 1, 0.6f},  {128, 96, 256, 3, 1, 0.5f},   {256, 64, 512, 3, 1, 0.6f},
                            {256, 256, 512, 2, 1, 0.5f},  {128, 128, 256, 2, 2, 0.5f},  {128, 96, 256, 2, 2, 0.5f},
                            {256, 256, 512, 0, 1, 1.04f},   // 12: ping-pong (A 2 + B 3 stages): 2-7 % over 0
-                           {256, 128, 512, 0, 1, 0.8f}};   // 13: ping-pong 256x128 (conv3/4: 90 / 125 us vs 77 / 109 for cfg 3)
+                           {256, 128, 512, 0, 1, 0.8f},    // 13: ping-pong 256x128 (conv3/4: 90 / 125 us vs 77 / 109 for cfg 3)
+                           {96, 96, 256, 2, 3, 0.8f},      // 14: 96x96, 3 workgroups/CU (short-K conv1p: 101 vs 109 us for cfg 4)
+                           {64, 96, 256, 2, 3, 0.6f}};     // 15: 64x96, 3 workgroups/CU
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 // ---- FC layers (M = batch rows of K contiguous bf16, 1x1): activations straight to VGPRs ----
 // The 256x64 LDS-DMA config (cfg 8) ran FC7 at 23 us for 164 MB of operand traffic: one workgroup
@@ -730,7 +732,9 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   X(8, 256, 64, 8, 1, 3, false)     \
   X(9, 256, 256, 2, 4, 2, false)    \
   X(10, 128, 128, 2, 2, 2, false)   \
-  X(11, 128, 96, 2, 2, 2, false)
+  X(11, 128, 96, 2, 2, 2, false)   \
+  X(14, 96, 96, 2, 2, 2, true)      \
+  X(15, 64, 96, 2, 2, 2, true)
   static const hipError_t attr = [] {
 #define ANX_ATTR(I, BM, BN, WGM, WGN, NST, P)                                                                     \
   for (const void* k : {reinterpret_cast<const void*>(conv_bf16_big_kernel<BM, BN, WGM, WGN, NST, false, P>),    \

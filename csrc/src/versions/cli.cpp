@@ -449,6 +449,57 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
   std::vector<float> y_full(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
   std::vector<std::vector<float>> stage(np);
   std::vector<std::vector<float>> hbufs;
+  // Per-layer decomposition (the reference's second exchange: V2.2 halo2 on pool1 rows, M11, and
+  // V4's device-staged variant, M13): after stage1 every rank holds its own pool1 rows t.p1 in the
+  // conv2 window; the rows of t.q owned by neighbours arrive over the host channel (GPU: D2H of
+  // the sent rows, H2D of the received ones; a window's rows of one image are contiguous).
+  std::vector<std::vector<float>> p1bufs;
+  const size_t wrow = gpu ? geng->q2_row_floats() : ceng->window_row_floats();
+  auto win_rows = [&](int n, int r) { return gpu ? geng->q2_row_ptr(t, n, r) : ceng->window_row(t, n, r); };
+  auto p1_exchange = [&]() {
+    p1bufs.clear();
+    for (const HaloXfer& h : plan.p1_halos)
+      if (h.src == rank || h.dst == rank) p1bufs.emplace_back(static_cast<size_t>(N) * h.rows.size() * wrow);
+    size_t bi = 0;
+    for (const HaloXfer& h : plan.p1_halos) {  // pack the rows this rank sends
+      if (h.src != rank && h.dst != rank) continue;
+      if (h.src == rank) {
+        const size_t blk = h.rows.size() * wrow;
+        for (int n = 0; n < N; ++n) {
+          if (gpu)
+            hip_check(hipMemcpyAsync(p1bufs[bi].data() + n * blk, win_rows(n, h.rows.lo), blk * 4, hipMemcpyDeviceToHost,
+                                     st), "D2H halo");
+          else
+            std::memcpy(p1bufs[bi].data() + n * blk, win_rows(n, h.rows.lo), blk * 4);
+        }
+      }
+      ++bi;
+    }
+    if (gpu) hip_check(hipStreamSynchronize(st), "sync");
+    bi = 0;
+    for (const HaloXfer& h : plan.p1_halos) {
+      if (h.src != rank && h.dst != rank) continue;
+      if (h.src == rank) c.isend(p1bufs[bi].data(), p1bufs[bi].size() * 4, h.dst);
+      else c.irecv(p1bufs[bi].data(), p1bufs[bi].size() * 4, h.src);
+      ++bi;
+    }
+    c.wait_all();
+    bi = 0;
+    for (const HaloXfer& h : plan.p1_halos) {  // unpack the received rows into the window
+      if (h.src != rank && h.dst != rank) continue;
+      if (h.dst == rank) {
+        const size_t blk = h.rows.size() * wrow;
+        for (int n = 0; n < N; ++n) {
+          if (gpu)
+            hip_check(hipMemcpyAsync(win_rows(n, h.rows.lo), p1bufs[bi].data() + n * blk, blk * 4, hipMemcpyHostToDevice,
+                                     st), "H2D halo");
+          else
+            std::memcpy(win_rows(n, h.rows.lo), p1bufs[bi].data() + n * blk, blk * 4);
+        }
+      }
+      ++bi;
+    }
+  };
 
   auto step = [&](Phases& ph) {
     // scatter owned input rows (Scatterv, M9)
@@ -515,7 +566,17 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
         if (mode == Decomp::Overlap) {
           hip_check(geng->tile_forward(d_in, N, t, d_y, st), "tile_forward");
         } else {
-          throw std::runtime_error("v4 supports --decomp overlap (per-layer halos are the v5 path)");
+          hip_check(geng->stage1(d_in, N, t, st), "stage1");
+          hip_check(hipStreamSynchronize(st), "sync");
+          ph.add("compute", now_ms() - q);
+          q = now_ms();
+          {
+            RoctxRange rh("v4 halo_p1");
+            p1_exchange();
+          }
+          ph.add("halo_p1", now_ms() - q);
+          q = now_ms();
+          hip_check(geng->stage2(N, t, d_y, st), "stage2");
         }
         hip_check(hipStreamSynchronize(st), "sync");
         ph.add("compute", now_ms() - q);
@@ -529,7 +590,16 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
         if (mode == Decomp::Overlap) {
           ceng->tile_forward(tile_in.data(), N, t, y_loc.data());
         } else {
-          throw std::runtime_error("v2.2 supports --decomp overlap");
+          ceng->stage1(tile_in.data(), N, t);
+          ph.add("compute", now_ms() - q);
+          q = now_ms();
+          {
+            RoctxRange rh("v2.2 halo_p1");
+            p1_exchange();
+          }
+          ph.add("halo_p1", now_ms() - q);
+          q = now_ms();
+          ceng->stage2(N, t, y_loc.data());
         }
         ph.add("compute", now_ms() - q);
       }

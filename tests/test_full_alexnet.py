@@ -110,7 +110,7 @@ def test_bf16_lds_dma_kernel_matches_register_staged(cuda, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 12, 13])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 12, 13, 14, 15])
 def test_bf16_wide_tile_kernel_matches_register_staged(cuda, cfg):
     """The wide-tile kernel (conv_bf16_big.hip; -1 = the cost model's per-layer pick, else that
     config forced wherever it fits) sums each output's products in the register-staged kernel's
@@ -128,6 +128,28 @@ def test_bf16_wide_tile_kernel_matches_register_staged(cuda, cfg):
     for i in (8, 9):
         t, r = m.tap(i, N).double(), ref_taps[i].double()
         assert ((t - r).norm() / r.norm()).item() < 1e-2, i
+    assert ((got - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [37, 256])
+def test_fc_streaming_kernel_matches_wide_tile(cuda, N):
+    """FC6-8 on the activation-streaming kernel (knob bf16_fc=1: activations global -> VGPR four K
+    tiles ahead, tile-blocked weights through an LDS-DMA ring, split-K slabs + reduce) against the
+    default wide-tile split: conv1..pool5 untouched (bit-identical), FC outputs equal to summation
+    order (rows past the batch clamp to the last image and are never stored)."""
+    x = (init_input(N, "rand", seed=21) * 10).to(cuda)
+    ref_m = AlexNetFull(seed=21, device=cuda, max_batch=N)
+    ref = ref_m(x).double()
+    ref_taps = [ref_m.tap(i, N) for i in range(10)]
+    m = AlexNetFull(seed=21, device=cuda, max_batch=N, knobs={"bf16_fc": 1})
+    got = m(x).double()
+    for i in range(8):
+        assert torch.equal(m.tap(i, N), ref_taps[i]), i
+    for i in (8, 9):
+        t, r = m.tap(i, N).double(), ref_taps[i].double()
+        assert ((t - r).norm() / r.norm()).item() < 1e-2, i
+        assert (t - r).abs().max().item() <= 2e-2 * r.abs().max().item(), i
     assert ((got - ref).norm() / ref.norm()).item() < 1e-2
 
 

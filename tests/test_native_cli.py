@@ -53,10 +53,15 @@ def test_v21(py_serial, np_):
 
 
 @pytest.mark.parametrize("np_", [2, 4, 7])
-def test_v22(py_serial, np_):
-    rec, out = native(["--version", "v2.2", "--init", "rand", "--seed", "3", "--batch", "2", "--iters", "1"], np_)
+@pytest.mark.parametrize("decomp", ["overlap", "per_layer"])
+def test_v22(py_serial, np_, decomp):
+    """overlap: one exact input halo per rank; per_layer: the reference's two exchanges (input rows,
+    then pool1 rows after stage 1, M10 + M11). Both bit-identical to V1."""
+    rec, out = native(["--version", "v2.2", "--init", "rand", "--seed", "3", "--batch", "2", "--iters", "1",
+                       "--decomp", decomp], np_)
     assert rec["checksum"] == py_serial and "shape: 13x13x256" in out.stdout
     assert set(rec["phases_warm"]) >= {"scatter", "halo", "compute", "gather"}
+    assert ("halo_p1" in rec["phases_warm"]) == (decomp == "per_layer")
 
 
 def test_fail_stop_exit():
@@ -96,6 +101,10 @@ def test_native_v4_shared_gpu(cuda, np_):
     rec, out = native(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", "--iters", "2", *d], np_)
     assert "Final Output Shape: 13x13x256" in out.stdout
     assert rec["checksum"] == ref["checksum"]
+    # per-layer: pool1 halo rows device-staged (D2H -> host channel -> H2D) between stage 1 and 2
+    rec, _ = native(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", "--iters", "2",
+                     "--decomp", "per_layer", *d], np_)
+    assert rec["checksum"] == ref["checksum"] and "halo_p1" in rec["phases_warm"]
     # Winograd conv2 (default): tile origins move with the row split -> equal to ~1e-7, not bitwise
     rec, _ = native(["--version", "v4", "--init", "rand", "--seed", "5", "--batch", "3", "--check"], np_)
     assert rec["max_abs_err"] < 1e-3
