@@ -50,11 +50,11 @@ def test_asan_v1(asan_bin):
     assert "44.4152 42.4612 40.6967" in out
 
 
-@pytest.mark.parametrize("np_", [2, 4])
-def test_asan_v22_multirank(asan_bin, np_):
+@pytest.mark.parametrize("np_,decomp", [(2, "overlap"), (4, "overlap"), (3, "per_layer")])
+def test_asan_v22_multirank(asan_bin, np_, decomp):
     b = asan_bin
     out = run([os.path.join(b, "anxrun"), "-np", str(np_), "--timeout", "200", os.path.join(b, "anx"), "--version",
-               "v2.2", "--init", "rand", "--batch", "2", "--iters", "1", "--check"])
+               "v2.2", "--init", "rand", "--batch", "2", "--iters", "1", "--check", "--decomp", decomp])
     assert '"max_abs_err": 0.000000' in out or '"max_abs_err": 0.0' in out
 
 
