@@ -76,6 +76,9 @@ def parse():
                     help="dp, 1 GPU: the step as one captured HIP graph replayed each step (1), eager (0, default; "
                          "measured equal: the step is GPU-bound), -1 auto")
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency measurement")
+    ap.add_argument("--prewarm-s", type=float, default=1.0,
+                    help="GPU: seconds of untimed steps before the warmup steps, so the timed steps run at the "
+                         "loaded clock (0 = off)")
     ap.add_argument("--model", default="blocks", choices=["blocks", "full"],
                     help="blocks = the headline AlexNet Blocks1-2 fp32; full = full AlexNet bf16 extension")
     return ap.parse_args()
@@ -177,6 +180,27 @@ def main():
             step = graph.replay
     sync = torch.cuda.synchronize if cuda else (lambda: None)
 
+    # Clock settle before the W warmup steps: the chip needs ~0.5 s of sustained load to reach its
+    # loaded clock (20 steps after 5 warmups measured 0.676 ms/step, 300 steps 0.628, same box:
+    # profiles/r02_bench_warmup.txt). Untimed, bounded by --prewarm-s, reported in the JSON.
+    # Every rank runs the same number of steps (step() holds collectives): 8 probe steps, then as
+    # many more as the slowest rank's probe says fill the budget.
+    t_pw, n_pw = time.perf_counter(), 0
+    if cuda and a.prewarm_s > 0:
+        for _ in range(8):
+            step()
+        sync()
+        dt = time.perf_counter() - t_pw
+        if world > 1:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        n_pw = 8 + min(20000, int(max(0.0, a.prewarm_s - dt) / max(dt, 1e-6) * 8))
+        for _ in range(n_pw - 8):
+            step()
+        sync()
+    prewarm_ms = round((time.perf_counter() - t_pw) * 1e3, 1)
+
     for _ in range(a.warmup):
         step()
     sync()
@@ -213,7 +237,8 @@ def main():
                 "dtype": "bf16", "data": "synthetic (random images 227x227x3, He-uniform random weights)",
                 "config": {"model": "AlexNet full (reference Blocks1-2 + Conv3-5 + FC6-8, 1000 classes)",
                            "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
-                           "gflop_per_image": round(flops / 1e9, 4), "tflops": round(imgs * flops / 1e12, 2)},
+                           "gflop_per_image": round(flops / 1e9, 4), "tflops": round(imgs * flops / 1e12, 2),
+                           "prewarm_steps": n_pw, "prewarm_ms": prewarm_ms},
             }
             print(json.dumps(rec), flush=True)
         if world > 1:
@@ -265,6 +290,8 @@ def main():
                 "impl": a.impl,
                 **extra,
                 "ms_per_batch": round(ms, 4),
+                "prewarm_steps": n_pw,
+                "prewarm_ms": prewarm_ms,
                 "gflop_per_image_direct": round(anx.flops_per_image() / 1e9, 4),
                 "gflop_per_image_mfma": round(mf / 1e9, 4),
                 "direct_equiv_tflops": round(imgs * anx.flops_per_image() / 1e12, 2),

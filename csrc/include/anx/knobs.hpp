@@ -25,6 +25,8 @@ struct Knobs {
   int wino_cfg = 7;        // Conv2 fused GEMM: bit0 BK 48, bit1 XCD order, bit2 LDS-DMA ring, bit3 16x16 MFMA
   int wino_prio = 257;     // Conv2 fused GEMM bits: 0 s_setprio, 1 NT V stores, 8 interleaved fold; 4-7 probes
   int wino_split = 1;      // Conv2 fused GEMM tail split: 0 off, 1 auto (fill the last round's idle CUs), 2-7 force
+  int wino_sk = 0;         // Conv2 fused GEMM stream-K: 0 off, 1-2 = that many workgroups per CU over equal
+                           // ranges of (point tile, transform point) work (supersedes the tail split)
   int fold_scalar = 0;     // Winograd output folds as scalar v_fma_f32 instead of packed v_pk_fma_f32: bit0 Conv1, bit1 Conv2
   int chunk1 = 0;          // images per stage-1 launch (0 = whole batch up to the 32-bit index chunk)
   int chunk2 = 0;          // images per stage-2 launch

@@ -14,6 +14,7 @@
 //   3. output transform : M -> Y = A^T M A + bias, ReLU, NHWC conv output (VALU, float4 over filters)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -246,6 +247,7 @@ struct FusedArgs {
   // wino_split_reduce_kernel.
   int pt_base, nsplit;
   float* slab;
+  int sk_groups;  // stream-K (wino_fused_sk_kernel): number of point ranges J
 };
 
 // A^T indexed by the runtime transform point: a copy of wino::kAT in constant memory (scalar loads).
@@ -441,35 +443,22 @@ __device__ __forceinline__ void fma2(f32x2& y, float c, float a0, float a1) {
   }
 }
 
-template <int BK, bool XCD, bool IL, bool SF>
-__global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) {  // 2 waves/SIMD
+// One unit of the LDS-DMA kernel: point tile pt (64 tiles), filter tile nt (64 filters), conv group
+// g, over transform points [pb, pe). slab == nullptr: the unit covers all 49 points and ends in the
+// bias + ReLU + NHWC epilogue; otherwise the raw fold Y of the range goes to `slab` as [q][tile]
+// [filter] (9 x 64 x 64 floats) for a reduce kernel. IL: full units run the interleaved-fold schedule.
+template <int BK, bool IL, bool SF>
+__device__ __forceinline__ void fused_glds_unit(const FusedArgs& a, float* lds, int pt, int nt, int g, int pb, int pe,
+                                                float* slab) {
   using f32x16 = __attribute__((ext_vector_type(16))) float;
   constexpr int U4 = BK / 4;              // 16-B units per row
   constexpr int NI = kFB * U4 / 256;      // DMA instructions per thread per operand
   static_assert(NI * 256 == kFB * U4 && U4 % 4 == 0, "BK must be a multiple of 16");
   constexpr int TILE = kFB * BK;          // floats per operand tile
   constexpr int STAGE = 2 * TILE;         // A tile | B tile
-  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int g = blockIdx.z;
-  int pt, nt;
-  if constexpr (XCD) {
-    // the n_ntiles workgroups that read one V slab get equal blockIdx.x % 8 (one XCD, one L2)
-    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-    nt = j % a.n_ntiles;
-    pt = (j / a.n_ntiles) * 8 + xcd;
-    if (pt >= a.n_ptiles) return;  // whole workgroup, before any DMA or barrier
-  } else {
-    pt = blockIdx.x / a.n_ntiles;
-    nt = blockIdx.x - pt * a.n_ntiles;
-  }
-  const int ptl = pt;  // point tile within this launch (slab index)
-  pt += a.pt_base;
   const int p0 = pt * kFB, n0 = nt * kFB;
-  // transform points of this workgroup: all 49, or slice blockIdx.y of a tail split
-  const int nsplit = a.nsplit > 1 ? a.nsplit : 1, sidx = nsplit > 1 ? blockIdx.y : 0;
-  const int pb = kN * kN * sidx / nsplit, pe = kN * kN * (sidx + 1) / nsplit;
 
   // per-lane source offsets of this thread's NI A units and NI B units (swizzled unit order)
   int aoff[NI], boff[NI];
@@ -629,7 +618,7 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
 
   issue(it0);
   if (it0 + 1 < total) issue(it0 + 1);
-  if constexpr (IL) {
+  if (IL && pb == 0 && pe == kN * kN) {
     // acc1 is zero before point 1: the first fold adds +0 (ab = 0's coefficients) and changes nothing
     for (int ab = 0; ab + 1 < kN * kN; ab += 2) {
       const int it = 2 * ab;
@@ -673,9 +662,8 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
   // the last point is still unfolded, in acc0
   fold(pe - 1, acc0);
 
-  if (a.slab) {  // tail split: raw Y of this point range, [q][tile][filter] per (s, tile block)
-    float* sl = a.slab + ((((static_cast<size_t>(g) * nsplit + sidx) * a.n_ptiles + ptl) * a.n_ntiles + nt) * kM * kM) *
-                             (kFB * kFB);
+  if (slab) {  // partial point range: raw Y, [q][tile][filter]
+    float* sl = slab;
 #pragma unroll
     for (int q = 0; q < kM * kM; ++q)
 #pragma unroll
@@ -722,6 +710,63 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
         *reinterpret_cast<f32x4*>(a.y + ((static_cast<size_t>(img[k]) * a.Ho + oy) * a.Wo + ox) * a.K + g * a.Kg + fb +
                                   grp) = v4;
     }
+  }
+}
+
+template <int BK, bool XCD, bool IL, bool SF>
+__global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) {  // 2 waves/SIMD
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int g = blockIdx.z;
+  int pt, nt;
+  if constexpr (XCD) {
+    // the n_ntiles workgroups that read one V slab get equal blockIdx.x % 8 (one XCD, one L2)
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    nt = j % a.n_ntiles;
+    pt = (j / a.n_ntiles) * 8 + xcd;
+    if (pt >= a.n_ptiles) return;  // whole workgroup, before any DMA or barrier
+  } else {
+    pt = blockIdx.x / a.n_ntiles;
+    nt = blockIdx.x - pt * a.n_ntiles;
+  }
+  const int ptl = pt;  // point tile within this launch (slab index)
+  // transform points of this workgroup: all 49, or slice blockIdx.y of a tail split
+  const int nsplit = a.nsplit > 1 ? a.nsplit : 1, sidx = nsplit > 1 ? blockIdx.y : 0;
+  const int pb = kN * kN * sidx / nsplit, pe = kN * kN * (sidx + 1) / nsplit;
+  float* sl = a.slab ? a.slab + ((((static_cast<size_t>(g) * nsplit + sidx) * a.n_ptiles + ptl) * a.n_ntiles + nt) *
+                                 kM * kM) * (kFB * kFB)
+                     : nullptr;
+  fused_glds_unit<BK, IL, SF>(a, lds, pt + a.pt_base, nt, g, pb, pe, sl);
+}
+
+// Stream-K schedule of the same units (Knobs::wino_sk; conv groups == 1). The 49 * n_ptiles
+// (point tile, transform point) pairs are cut into J equal contiguous ranges, one per group of
+// n_ntiles workgroups (one per filter tile, all on one XCD, so a V slab is read by one L2), with J
+// a whole number of workgroups per CU: every CU gets the same MFMA work, whatever the batch (the
+// data-parallel grid leaves CUs with one workgroup next to CUs with two: 324 workgroups on 256 CUs
+// at 64 images). A range covers whole point tiles (the fused epilogue) and at most two partial ones
+// (its first and last), whose raw Y go to the group's two slab slots; wino_sk_reduce_kernel sums
+// the slots of every split point tile in group order (deterministic) and stores act(sum + bias).
+__device__ __forceinline__ long sk_start(long j, long T, int J) { return j * T / J; }
+
+template <bool SF, bool IL>
+__global__ void __launch_bounds__(256, 2) wino_fused_sk_kernel(FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int nt = jb % a.n_ntiles;
+  const int j = (jb / a.n_ntiles) * 8 + xcd;  // range index
+  if (j >= a.sk_groups) return;               // whole workgroup, before any DMA or barrier
+  const long T = static_cast<long>(a.n_ptiles) * (kN * kN);
+  const long end = sk_start(j + 1, T, a.sk_groups);
+  float* slots = a.slab + static_cast<size_t>(j * a.n_ntiles + nt) * 2 * (kM * kM * kFB * kFB);
+  bool first = true;
+  for (long x = sk_start(j, T, a.sk_groups); x < end;) {
+    const int pt = static_cast<int>(x / (kN * kN)), pb = static_cast<int>(x - static_cast<long>(pt) * (kN * kN));
+    const int pe = static_cast<int>(min(static_cast<long>(kN * kN), end - static_cast<long>(pt) * (kN * kN)));
+    float* sl = (pb == 0 && pe == kN * kN) ? nullptr : slots + (first ? 0 : kM * kM * kFB * kFB);
+    if (!first) __syncthreads();  // the previous unit's epilogue / last slices are done with the LDS
+    fused_glds_unit<48, IL, SF>(a, lds, pt, nt, 0, pb, pe, sl);
+    first = false;
+    x = static_cast<long>(pt) * (kN * kN) + pe;
   }
 }
 
@@ -982,6 +1027,55 @@ __global__ void __launch_bounds__(256) wino_split_reduce_kernel(SplitReduceArgs 
   }
 }
 
+// Stream-K fixup: y = act(sum over the ranges j covering point tile pt of their slab slot + bias)
+// for every split point tile (covered by more than one range); ranges in order (deterministic).
+struct SkReduceArgs {
+  const float* slab;
+  const float* bias;
+  float* y;
+  int J, n_ptiles, n_ntiles;
+  int P, Kg, K, Ho, Wo, ty, tx, relu;
+};
+__device__ __forceinline__ int sk_range_of(long x, long T, int J) {  // j with start(j) <= x < start(j+1)
+  int j = static_cast<int>(x * J / T);
+  if (j + 1 < J && sk_start(j + 1, T, J) <= x) ++j;
+  return j;
+}
+__global__ void __launch_bounds__(256) wino_sk_reduce_kernel(SkReduceArgs r) {
+  constexpr int F4 = kFB / 4, Q = kM * kM;
+  const long T = static_cast<long>(r.n_ptiles) * (kN * kN);
+  const long total = static_cast<long>(r.n_ptiles) * r.n_ntiles * Q * kFB * F4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += static_cast<long>(gridDim.x) * 256) {
+    long t = i;
+    const int f4 = static_cast<int>(t % F4);
+    t /= F4;
+    const int tl = static_cast<int>(t % kFB);
+    t /= kFB;
+    const int q = static_cast<int>(t % Q);
+    t /= Q;
+    const int nt = static_cast<int>(t % r.n_ntiles);
+    const int pt = static_cast<int>(t / r.n_ntiles);
+    const long x0 = static_cast<long>(pt) * (kN * kN);
+    const int jlo = sk_range_of(x0, T, r.J), jhi = sk_range_of(x0 + kN * kN - 1, T, r.J);
+    if (jlo == jhi) continue;  // one range covered the whole point tile: stored by its epilogue
+    const int f = nt * kFB + f4 * 4;
+    const int p = pt * kFB + tl;
+    if (f >= r.Kg || p >= r.P) continue;
+    const int tj = p % r.tx, pq = p / r.tx, ti = pq % r.ty, n = pq / r.ty;
+    const int oy = ti * kM + q / kM, ox = tj * kM + q % kM;
+    if (oy >= r.Ho || ox >= r.Wo) continue;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int j = jlo; j <= jhi; ++j) {
+      const int slot = (sk_start(j, T, r.J) / (kN * kN) == pt) ? 0 : 1;  // its first range piece, else its last
+      v += *reinterpret_cast<const f32x4*>(r.slab + ((static_cast<size_t>(j * r.n_ntiles + nt) * 2 + slot) * Q + q) *
+                                                         (kFB * kFB) + tl * kFB + f4 * 4);
+    }
+    if (r.bias) v += *reinterpret_cast<const f32x4*>(r.bias + f);
+    if (r.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+    *reinterpret_cast<f32x4*>(r.y + ((static_cast<size_t>(n) * r.Ho + oy) * r.Wo + ox) * r.K + f) = v;
+  }
+}
+
 int device_cus() {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1172,6 +1266,41 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
     const int bk = (cfg & 1) ? 48 : 32;
     if (a.Cg % bk == 0 && a.kpad == a.Cg) {
       const dim3 grid((xcd ? (a.n_ptiles + 7) / 8 * 8 : a.n_ptiles) * a.n_ntiles, 1, w.groups);
+      if (bk == 48 && xcd && kn.wino_sk > 0 && split_ws && w.groups == 1 && a.kpad == 96 && (prio & ~257) == 0) {
+        // stream-K: J ranges of equal (point tile, point) work, kn.wino_sk workgroups per CU
+        const int J = std::min(a.n_ptiles, device_cus() * kn.wino_sk / a.n_ntiles);
+        if (J >= 1 && static_cast<size_t>(J) * a.n_ntiles * 2 * kM * kM * kFB * kFB <= wino_split_ws_floats()) {
+          FusedArgs k = a;
+          k.slab = split_ws;
+          k.sk_groups = J;
+          const size_t lds = occupancy_lds(3 * 2 * kFB * 48 * sizeof(float), occ);
+          static const hipError_t attr = [] {
+            for (const void* f : {reinterpret_cast<const void*>(wino_fused_sk_kernel<true, true>),
+                                  reinterpret_cast<const void*>(wino_fused_sk_kernel<false, true>),
+                                  reinterpret_cast<const void*>(wino_fused_sk_kernel<true, false>),
+                                  reinterpret_cast<const void*>(wino_fused_sk_kernel<false, false>)}) {
+              const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+              if (e != hipSuccess) return e;
+            }
+            return hipSuccess;
+          }();
+          if (attr != hipSuccess) return attr;
+          const dim3 gk((J + 7) / 8 * 8 * a.n_ntiles);
+          const bool il = (prio & 256) != 0;  // full point tiles on the interleaved-fold schedule
+          if (sf)
+            il ? wino_fused_sk_kernel<true, true><<<gk, 256, lds, s>>>(k) : wino_fused_sk_kernel<true, false><<<gk, 256, lds, s>>>(k);
+          else
+            il ? wino_fused_sk_kernel<false, true><<<gk, 256, lds, s>>>(k)
+               : wino_fused_sk_kernel<false, false><<<gk, 256, lds, s>>>(k);
+          hipError_t e = hipGetLastError();
+          if (e != hipSuccess) return e;
+          SkReduceArgs r{split_ws, bias, y, J, a.n_ptiles, a.n_ntiles, w.P, a.Kg, w.K, w.Ho, w.Wo, w.ty, w.tx,
+                         relu ? 1 : 0};
+          const long n = static_cast<long>(a.n_ptiles) * a.n_ntiles * kM * kM * kFB * (kFB / 4);
+          wino_sk_reduce_kernel<<<grid_for(n), 256, 0, s>>>(r);
+          return hipGetLastError();
+        }
+      }
       const WinoSplit sp = split_ws ? plan_wino_split(w, kn) : WinoSplit{a.n_ptiles, 0, 1};
       if (bk == 48 && xcd && sp.nsplit > 1 &&
           static_cast<size_t>(sp.nsplit) * ((sp.tail_pt + 7) / 8 * 8) * a.n_ntiles * w.groups * kM * kM * kFB * kFB <=

@@ -28,6 +28,7 @@ const Field kFields[] = {
     {"wino_prio", &Knobs::wino_prio, nullptr, 0, 511, "ANX_WINO_PRIO"},
     {"fold_scalar", &Knobs::fold_scalar, nullptr, 0, 3, "ANX_FOLD_SCALAR"},
     {"wino_split", &Knobs::wino_split, nullptr, 0, 7, "ANX_WINO_SPLIT"},
+    {"wino_sk", &Knobs::wino_sk, nullptr, 0, 2, "ANX_WINO_SK"},
     {"chunk1", &Knobs::chunk1, nullptr, 0, 1 << 30, "ANX_CHUNK1"},
     {"chunk2", &Knobs::chunk2, nullptr, 0, 1 << 30, "ANX_CHUNK2"},
     {"fuse_pool1", &Knobs::fuse_pool1, nullptr, 0, 1, "ANX_FUSE_POOL1"},

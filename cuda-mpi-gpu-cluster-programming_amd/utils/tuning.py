@@ -19,7 +19,7 @@ import ctypes as C
 from .. import _native as nat
 
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd_unfused": 3}
-KNOBS = ("conv1_algo", "conv2_algo", "conv1_cfg", "conv1_probe", "wino_cfg", "wino_prio", "wino_split", "fold_scalar",
+KNOBS = ("conv1_algo", "conv2_algo", "conv1_cfg", "conv1_probe", "wino_cfg", "wino_prio", "wino_split", "wino_sk", "fold_scalar",
          "chunk1", "chunk2", "fuse_pool1", "force_vec4", "force_scalar", "bf16_glds", "bf16_big", "bf16_lrn_tile", "bf16_fc",
          "conv1_occ", "conv2_occ")
 

@@ -415,3 +415,22 @@ def test_winograd_tail_split_close_to_unsplit(cuda, N):
     idx = torch.tensor([0, N // 2, N - 1])
     ref = blocks_forward(x[idx.to(cuda)].cpu(), m.weights, m.b1, m.b2)
     assert (y[idx.to(cuda)].cpu().double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("N,sk,lanes", [(64, 1, 1), (64, 2, 1), (128, 1, 2), (300, 1, 1), (7, 1, 1)])
+def test_winograd_stream_k_close_to_unsplit(cuda, N, sk, lanes):
+    """Conv2 stream-K (knob wino_sk: equal ranges of (point tile, transform point) work, sk
+    workgroups per CU; split point tiles summed by wino_sk_reduce_kernel) against the data-parallel
+    launch and the fp64 oracle. Only the split tiles' summation order differs, and the schedule is
+    deterministic (a second forward is bitwise equal). N = 7 stays on the direct conv (no Winograd)."""
+    x = init_input(N, "rand", seed=23).to(cuda)
+    m = AlexNetBlocks(device=cuda, init="rand", seed=23, max_batch=N, lanes=lanes, knobs={"wino_sk": sk, "wino_split": 0})
+    y = m(x).clone()
+    assert torch.equal(m(x), y)
+    m.set_knob("wino_sk", 0)
+    y0 = m(x)
+    torch.cuda.synchronize()
+    assert (y - y0).abs().max().item() <= 1e-6 * y0.abs().max().item()
+    idx = torch.tensor([0, N // 2, N - 1])
+    ref = blocks_forward(x[idx.to(cuda)].cpu(), m.weights, m.b1, m.b2)
+    assert (y[idx.to(cuda)].cpu().double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
