@@ -238,7 +238,8 @@ struct FusedArgs {
   float* y;            // [N][Ho][Wo][K]
   int P, C, Cg, Kg, K, groups, kpad, kpad_n;
   int N, Ho, Wo, ty, tx, relu, n_ptiles, n_ntiles;
-  int prio;  // bit0: s_setprio(1) around each slice's MFMAs (guide technique T5). Cost probes of the
+  int prio;  // bit0: s_setprio(1) around each slice's MFMAs (guide technique T5); bit8: interleaved fold.
+             // Cost probes of the
              // LDS-DMA kernel (wrong results; never set in production): bit4 no fold, bit5 no DMA
              // refills, bit6 no per-slice barrier (only with bit5), bit7 no epilogue stores
   // Tail split (LDS-DMA kernel, non-IL): this launch covers point tiles [pt_base, pt_base +
@@ -447,7 +448,9 @@ __device__ __forceinline__ void fma2(f32x2& y, float c, float a0, float a1) {
 // g, over transform points [pb, pe). slab == nullptr: the unit covers all 49 points and ends in the
 // bias + ReLU + NHWC epilogue; otherwise the raw fold Y of the range goes to `slab` as [q][tile]
 // [filter] (9 x 64 x 64 floats) for a reduce kernel. IL: full units run the interleaved-fold schedule.
-template <int BK, bool IL, bool SF>
+// IL_MODE: 0 = generic point-range schedule only, 1 = interleaved-fold schedule only (whole units),
+// 2 = interleaved for whole units, generic for partial ranges (chosen at run time).
+template <int BK, int IL_MODE, bool SF>
 __device__ __forceinline__ void fused_glds_unit(const FusedArgs& a, float* lds, int pt, int nt, int g, int pb, int pe,
                                                 float* slab) {
   using f32x16 = __attribute__((ext_vector_type(16))) float;
@@ -577,7 +580,7 @@ __device__ __forceinline__ void fused_glds_unit(const FusedArgs& a, float* lds, 
 #pragma unroll
     for (int q = 0; q < kM * kM; ++q) cq[q] = c_coef.v[fab][q];
     const float* base = lds + (it % 3) * STAGE;
-    static_assert(!IL || (BK / 8) * 4 * 3 >= kM * kM * 8, "fold FMAs must fit behind the slice's MFMAs");
+    static_assert(IL_MODE == 0 || (BK / 8) * 4 * 3 >= kM * kM * 8, "fold FMAs must fit behind the slice's MFMAs");
     // fragments of group s4+1 are read while group s4's MFMAs run (two register sets)
     f32x4 af[2], bf[2];
     af[0] = *reinterpret_cast<const f32x4*>(base + a_row + rd[0]);
@@ -618,7 +621,14 @@ __device__ __forceinline__ void fused_glds_unit(const FusedArgs& a, float* lds, 
 
   issue(it0);
   if (it0 + 1 < total) issue(it0 + 1);
-  if (IL && pb == 0 && pe == kN * kN) {
+  bool il_sched;
+  if constexpr (IL_MODE == 1)
+    il_sched = true;  // the caller only passes whole units
+  else if constexpr (IL_MODE == 2)
+    il_sched = pb == 0 && pe == kN * kN;
+  else
+    il_sched = false;
+  if (IL_MODE != 0 && il_sched) {
     // acc1 is zero before point 1: the first fold adds +0 (ab = 0's coefficients) and changes nothing
     for (int ab = 0; ab + 1 < kN * kN; ab += 2) {
       const int it = 2 * ab;
@@ -735,7 +745,7 @@ __global__ void __launch_bounds__(256, 2) wino_fused_glds_kernel(FusedArgs a) { 
   float* sl = a.slab ? a.slab + ((((static_cast<size_t>(g) * nsplit + sidx) * a.n_ptiles + ptl) * a.n_ntiles + nt) *
                                  kM * kM) * (kFB * kFB)
                      : nullptr;
-  fused_glds_unit<BK, IL, SF>(a, lds, pt + a.pt_base, nt, g, pb, pe, sl);
+  fused_glds_unit<BK, IL ? 1 : 0, SF>(a, lds, pt + a.pt_base, nt, g, pb, pe, sl);
 }
 
 // Stream-K schedule of the same units (Knobs::wino_sk; conv groups == 1). The 49 * n_ptiles
@@ -764,7 +774,7 @@ __global__ void __launch_bounds__(256, 2) wino_fused_sk_kernel(FusedArgs a) {
     const int pe = static_cast<int>(min(static_cast<long>(kN * kN), end - static_cast<long>(pt) * (kN * kN)));
     float* sl = (pb == 0 && pe == kN * kN) ? nullptr : slots + (first ? 0 : kM * kM * kFB * kFB);
     if (!first) __syncthreads();  // the previous unit's epilogue / last slices are done with the LDS
-    fused_glds_unit<48, IL, SF>(a, lds, pt, nt, 0, pb, pe, sl);
+    fused_glds_unit<48, IL ? 2 : 0, SF>(a, lds, pt, nt, 0, pb, pe, sl);
     first = false;
     x = static_cast<long>(pt) * (kN * kN) + pe;
   }

@@ -44,7 +44,7 @@ class AlexNetBlocks:
     def __init__(self, weights: dict | None = None, *, init: str = "const", seed: int = 0, lrn_mode: str = "div_n",
                  groups2: int = 1, H: int = IN_H, W: int = IN_W, device="cuda", impl: str = "mfma",
                  max_batch: int = 1, specs: tuple[BlockSpec, BlockSpec] | None = None, lanes: int = 1,
-                 knobs: dict | None = None):
+                 knobs: dict | None = None, lane_priority: int = 0):
         self.b1, self.b2 = specs if specs is not None else blocks(lrn_mode, groups2)
         if self.b1.has_lrn:
             raise ValueError("the native engine implements LRN after block 2 only (the reference's topology)")
@@ -80,7 +80,8 @@ class AlexNetBlocks:
             for _ in range(lanes - 1):
                 self._lanes.append(AlexNetBlocks(self.weights, specs=(self.b1, self.b2), H=H, W=W, device=self.device,
                                                  impl=impl, max_batch=per_lane, knobs=self.knobs))
-                self._lane_streams.append(torch.cuda.Stream(self.device))
+                # lane_priority < 0: side lanes on high-priority streams (their waves dispatch first)
+                self._lane_streams.append(torch.cuda.Stream(self.device, priority=lane_priority))
 
     @property
     def is_cuda(self) -> bool:

@@ -43,7 +43,9 @@ def main():
     x = torch.rand(a.batch, 227, 227, 3, device=dev) * 0.1
     models, ref = [], None
     for knobs in arms:
-        m = AlexNetBlocks(init="rand", device=dev, max_batch=a.batch, lanes=a.lanes, knobs=knobs)
+        kn = dict(knobs)
+        prio = kn.pop("lane_prio", 0)  # not a kernel knob: stream priority of the side lanes
+        m = AlexNetBlocks(init="rand", device=dev, max_batch=a.batch, lanes=a.lanes, knobs=kn, lane_priority=prio)
         y = m(x)
         torch.cuda.synchronize()
         if ref is None:
