@@ -76,6 +76,9 @@ def parse():
                     help="dp, 1 GPU: the step as one captured HIP graph replayed each step (1), eager (0, default; "
                          "measured equal: the step is GPU-bound), -1 auto")
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency measurement")
+    ap.add_argument("--joined-lanes", action="store_true",
+                    help="dp: join the stream lanes every step (AlexNetBlocks.forward) instead of free-running lanes "
+                         "half a step apart (forward_async; the default with local input)")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="GPU: seconds of untimed steps before the warmup steps, so the timed steps run at the "
                          "loaded clock (0 = off)")
@@ -156,7 +159,8 @@ def main():
     use_graph = False
     if wl is None:
         cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather,
-                             prefetch=not a.no_prefetch)
+                             prefetch=not a.no_prefetch,
+                             async_lanes=not a.joined_lanes and a.graph == 0 and a.lanes > 1)
         pipe = ScatterComputeGather(model, cfg, (d.H, d.W, d.C0), out_shape, dev)
         if pipe.x_global is not None:
             pipe.x_global.copy_(torch.rand(pipe.x_global.shape, device=dev, generator=g) * 0.1)
@@ -183,20 +187,25 @@ def main():
     # Clock settle before the W warmup steps: the chip needs ~0.5 s of sustained load to reach its
     # loaded clock (20 steps after 5 warmups measured 0.676 ms/step, 300 steps 0.628, same box:
     # profiles/r02_bench_warmup.txt). Untimed, bounded by --prewarm-s, reported in the JSON.
-    # Every rank runs the same number of steps (step() holds collectives): 8 probe steps, then as
-    # many more as the slowest rank's probe says fill the budget.
+    # Every rank runs the same number of steps (step() holds collectives): 8 steps (first-call setup),
+    # 8 timed probe steps, then as many more as the slowest rank's probe says fill the budget.
     t_pw, n_pw = time.perf_counter(), 0
     if cuda and a.prewarm_s > 0:
         for _ in range(8):
             step()
         sync()
-        dt = time.perf_counter() - t_pw
+        t1 = time.perf_counter()
+        for _ in range(8):
+            step()
+        sync()
+        dt = time.perf_counter() - t1
+        left = a.prewarm_s - (time.perf_counter() - t_pw)
         if world > 1:
-            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            t = torch.tensor([dt, left], device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        n_pw = 8 + min(20000, int(max(0.0, a.prewarm_s - dt) / max(dt, 1e-6) * 8))
-        for _ in range(n_pw - 8):
+            dt, left = float(t[0].item()), float(t[1].item())
+        n_pw = 16 + min(50000, int(max(0.0, left) / max(dt, 1e-6) * 8))
+        for _ in range(n_pw - 16):
             step()
         sync()
     prewarm_ms = round((time.perf_counter() - t_pw) * 1e3, 1)
@@ -256,7 +265,9 @@ def main():
                         if a.input_source == "root" else
                         "per-rank data -> compute -> gather to rank 0 (RCCL, overlapped with the next step)") \
                 if world > 1 else "single GPU"
-            extra = {"input_source": a.input_source, "lanes": a.lanes, "hip_graph": use_graph}
+            extra = {"input_source": a.input_source, "lanes": a.lanes, "hip_graph": use_graph,
+                     "lane_sync": ("free-running lanes half a step apart, per-lane gathers (forward_async)"
+                                   if pipe.async_lanes else "lanes forked/joined every step")}
         else:
             par, scaling = f"{a.workload}-{a.decomp}{world}", "strong"
             pipeline = ("root pinned host -> H2D -> RCCL scatter -> overlap tiles -> RCCL gather -> D2H"

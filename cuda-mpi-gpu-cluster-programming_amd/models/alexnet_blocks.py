@@ -16,7 +16,10 @@ into L contiguous slices, each run by its own engine (own workspace, same weight
 stream forked from and joined back to the current stream: the HBM-bound transforms and pools of one
 lane fill the CUs the MFMA GEMMs of the other leave idle in their tail waves
 (``profiles/r01_streams_probe.jsonl``: 2 x 150 images 1.362 ms vs 1 x 300 1.408 ms). Per-image
-results are bit-identical to one lane. On the CPU it runs libanx's C++ host engine (CpuBlocks). There is no eager-PyTorch
+results are bit-identical to one lane. :meth:`forward_async` is the throughput form for repeated
+forwards: the lanes are not joined per call but run free on their own streams, started half a
+forward apart, so one lane's HBM-bound kernels overlap the other's GEMMs in steady state
+(``profiles/r02_lanes_async.txt``: 128 images 0.629 -> 0.561 ms per forward). On the CPU it runs libanx's C++ host engine (CpuBlocks). There is no eager-PyTorch
 fallback: the PyTorch oracle lives in :mod:`anx.models.reference` and is only used by tests.
 """
 from __future__ import annotations
@@ -82,6 +85,7 @@ class AlexNetBlocks:
                                                  impl=impl, max_batch=per_lane, knobs=self.knobs))
                 # lane_priority < 0: side lanes on high-priority streams (their waves dispatch first)
                 self._lane_streams.append(torch.cuda.Stream(self.device, priority=lane_priority))
+        self._own_stream = None  # lane 0's stream in forward_async (the joined forward uses the current one)
 
     @property
     def is_cuda(self) -> bool:
@@ -180,6 +184,69 @@ class AlexNetBlocks:
         return y
 
     __call__ = forward
+
+    def forward_async(self, x: torch.Tensor, out: torch.Tensor, on_lane=None, pre_lane=None) -> torch.Tensor:
+        """Throughput form of :meth:`forward` for a loop of forwards on the same buffers.
+
+        Each lane enqueues its slice on its own stream and is NOT joined back: consecutive calls
+        pipeline, and the lanes stay half a forward apart (one lane's transforms and pools under the
+        other's GEMMs) instead of being realigned by a join every call. When every lane is idle (the
+        first call, or after any device synchronisation) the lanes fork from the current stream and
+        lane i >= 1 starts when lane i-1's stage 1 (Conv1 + Pool1) is done, which sets that phase.
+
+        Contract: ``out`` holds a call's results once :meth:`join` has made the current stream wait
+        for the lanes (or after a device synchronisation); ``x`` and ``out`` must not be written by
+        other work until then. ``pre_lane(i, lo, hi)`` / ``on_lane(i, lo, hi)``, if given, run with
+        lane i's stream current right before / after it enqueues images [lo, hi) (e.g. waiting for a
+        collective still reading that output slice / a per-lane collective on it)."""
+        L = 1 + len(self._lanes)
+        N = self._check_in(x, self.H)
+        if L == 1 or N < L * LANE_MIN or not self.is_cuda:
+            if pre_lane is not None:
+                pre_lane(0, 0, N)
+            y = self.forward(x, out)
+            if on_lane is not None:
+                on_lane(0, 0, N)
+            return y
+        if self._own_stream is None:
+            self._own_stream = torch.cuda.Stream(self.device)
+        streams = [self._own_stream, *self._lane_streams]
+        engines = [self, *self._lanes]
+        plan = full_plan(self.H, self.W, self.b1, self.b2)
+        bounds = [N * i // L for i in range(L + 1)]
+        fresh = all(st.query() for st in streams)
+        cur = torch.cuda.current_stream(self.device)
+        ev = None
+        for i, (eng, st) in enumerate(zip(engines, streams)):
+            lo, hi = bounds[i], bounds[i + 1]
+            with torch.cuda.stream(st):
+                if fresh:
+                    st.wait_stream(cur)  # inputs produced / outputs free on the current stream
+                    if ev is not None:
+                        st.wait_event(ev)
+                if pre_lane is not None:
+                    pre_lane(i, lo, hi)
+                if fresh and i + 1 < L:
+                    eng.stage1(x[lo:hi], plan)  # = tile_forward as stage1 + stage2, with the phase event between
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    eng.stage2(hi - lo, plan, out[lo:hi])
+                else:
+                    eng.tile_forward(x[lo:hi], plan, out[lo:hi])
+                if on_lane is not None:
+                    on_lane(i, lo, hi)
+        return out
+
+    def join(self) -> None:
+        """Make the current stream wait for every lane of :meth:`forward_async`."""
+        if not self.is_cuda:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for st in ([self._own_stream] if self._own_stream is not None else []) + self._lane_streams:
+            cur.wait_stream(st)
+
+    def lane_count(self) -> int:
+        return 1 + len(self._lanes)
 
     def tile_forward(self, x: torch.Tensor, tile: TilePlan, out: torch.Tensor | None = None) -> torch.Tensor:
         """Row tile: ``x`` holds input rows ``tile.inp`` of N images; returns output rows ``tile.out``."""

@@ -16,6 +16,11 @@ batch scale and MI355X-first:
   one peer's shard) overlaps the compute instead of preceding it. Every step still scatters,
   computes and gathers its full batch; only the order changes.
 
+* ``async_lanes=True`` (local input only): a model with stream lanes runs them free (its
+  ``forward_async``: no per-step join, lanes half a forward apart) and each lane gathers its own
+  slice from its own stream; a lane waits, on its stream, for the gather that read the same output
+  buffer two steps earlier. ``drain()`` joins the lanes.
+
 Input semantics with prefetch: ``step()`` snapshots ``x_global`` as it is at the call (the scatter
 for the NEXT step is issued from it) and computes the batch snapshotted by the previous call (the
 first call computes its own snapshot). Writes to ``x_global`` after ``step()`` returns are safe when
@@ -48,6 +53,7 @@ class PipelineConfig:
     scatter: bool = True   # rank 0 owns the global batch and scatters it
     gather: bool = True    # outputs are gathered to rank 0
     prefetch: bool = False  # scatter step k+1 while step k computes (double-buffered x and y)
+    async_lanes: bool = False  # free-running model lanes (forward_async) with per-lane gathers; local input only
 
 
 class ScatterComputeGather:
@@ -74,6 +80,11 @@ class ScatterComputeGather:
         root = self.rank == 0 and self.world > 1
         self.x_global = torch.empty((self.world, B, *in_shape), device=self.device) if root and cfg.scatter else None
         self.y_global = torch.empty((self.world, B, *out_shape), device=self.device) if root and cfg.gather else None
+        self.async_lanes = cfg.async_lanes and not cfg.scatter and hasattr(model, "forward_async")
+        if self.async_lanes and self.world > 1 and cfg.gather and nbuf < 2:  # a gather may still read y[k-1]
+            self._yb.append(torch.empty_like(self._yb[0]))
+            self._gather_pending.append(None)
+        self._lane_gathers = [dict() for _ in self._yb]  # per output buffer: lane -> gather work reading it
 
     def _scatter(self, x):
         root = self.rank == 0
@@ -112,14 +123,41 @@ class ScatterComputeGather:
         self.x, self.y = x, y
         self._k += 1
 
+    def _step_async(self) -> None:
+        cur = self._k % len(self._yb)
+        y, pend = self._yb[cur], self._lane_gathers[cur]
+        gather = self.cfg.gather and self.world > 1
+
+        def pre_lane(i, lo, hi):  # on lane i's stream: the gather of this slice two steps ago is done
+            w = pend.pop(i, None)
+            if w is not None:
+                w.wait()
+
+        def on_lane(i, lo, hi):  # on lane i's stream: gather its slice as soon as it is computed
+            if gather:
+                dst = [self.y_global[r, lo:hi] for r in range(self.world)] if self.rank == 0 else None
+                pend[i] = dist.gather(y[lo:hi], dst, dst=0, group=self.group, async_op=True)
+
+        self.model.forward_async(self.x, y, on_lane=on_lane, pre_lane=pre_lane)
+        self.y = y
+        self._k += 1
+
     def drain(self) -> None:
         """Wait for every outstanding prefetch/gather (the last step's outputs are then in y_global)."""
+        if self.async_lanes:
+            self.model.join()
+            for pend in self._lane_gathers:
+                for w in pend.values():
+                    w.wait()
+                pend.clear()
         for ws in [self._scatter_pending or []] + [g or [] for g in self._gather_pending]:
             for w in ws:
                 w.wait()
         self._gather_pending = [None] * len(self._gather_pending)
 
     def step(self) -> None:
+        if self.async_lanes:
+            return self._step_async()
         if self.prefetch:
             return self._step_prefetch()
         if self.world == 1:

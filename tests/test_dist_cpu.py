@@ -68,6 +68,52 @@ def test_scatter_compute_gather_gloo(prefetch):
     torch.testing.assert_close(y.view_as(ref), ref, rtol=0, atol=0)
 
 
+def _async_lanes_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import anx  # noqa: F401
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.parallel.pipeline import PipelineConfig, ScatterComputeGather
+    from anx.utils.init import init_input
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    d = anx.blocks_dims()
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    pipe = ScatterComputeGather(m, PipelineConfig(2, scatter=False, prefetch=True, async_lanes=True),
+                                (d.H, d.W, d.C0), (d.Hp2, d.Wp2, d.C2), "cpu")
+    assert pipe.async_lanes and len(pipe._yb) == 2
+    pipe._xb[0].copy_(init_input(2 * world, "rand", seed=2)[2 * rank:2 * rank + 2])
+    for _ in range(3):  # per-lane gathers; a step waits for the gather that read its buffer 2 steps ago
+        pipe.step()
+    pipe.drain()
+    if rank == 0:
+        q.put(pipe.y_global.clone())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_async_lanes_pipeline_gloo():
+    """The bench's default dp step (local input, free-running lanes with per-lane gathers: the
+    model's forward_async; on CPU ranks one lane) gathers exactly the single-process outputs."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_async_lanes_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    y = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, ROOT)
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.utils.init import init_input
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    ref = m(init_input(2 * world, "rand", seed=2))
+    torch.testing.assert_close(y.view_as(ref), ref, rtol=0, atol=0)
+
+
 def _prefetch_changing_worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     import anx  # noqa: F401

@@ -434,3 +434,28 @@ def test_winograd_stream_k_close_to_unsplit(cuda, N, sk, lanes):
     idx = torch.tensor([0, N // 2, N - 1])
     ref = blocks_forward(x[idx.to(cuda)].cpu(), m.weights, m.b1, m.b2)
     assert (y[idx.to(cuda)].cpu().double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("N", [128, 300])
+def test_forward_async_lanes_bit_identical(cuda, N):
+    """forward_async (the bench's dp step: free-running lanes, no per-call join, lanes started half a
+    forward apart when idle) computes exactly the one-lane forward, over repeated calls on the same
+    buffers, after a device synchronisation (fresh start again), with per-lane hooks in order."""
+    x = init_input(N, "rand", seed=31).to(cuda)
+    one = AlexNetBlocks(device=cuda, init="rand", seed=31, max_batch=N, knobs={"wino_split": 0})
+    many = AlexNetBlocks(one.weights, device=cuda, max_batch=N, lanes=2, knobs={"wino_split": 0})
+    ref = one(x).clone()
+    y = torch.full_like(ref, float("nan"))
+    seen = []
+    for _ in range(5):
+        many.forward_async(x, y, on_lane=lambda i, lo, hi: seen.append((i, lo, hi)),
+                           pre_lane=lambda i, lo, hi: seen.append(("pre", i)))
+    many.join()
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert seen[:4] == [("pre", 0), (0, 0, N // 2), ("pre", 1), (1, N // 2, N)] and len(seen) == 20
+    y.fill_(float("nan"))
+    many.forward_async(x, y)
+    many.join()
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
