@@ -160,7 +160,8 @@ def main():
     if wl is None:
         cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather,
                              prefetch=not a.no_prefetch,
-                             async_lanes=not a.joined_lanes and a.graph == 0 and a.lanes > 1)
+                             async_lanes=not a.joined_lanes and a.graph == 0
+                             and (a.full_lanes if a.model == "full" else a.lanes) > 1)
         pipe = ScatterComputeGather(model, cfg, (d.H, d.W, d.C0), out_shape, dev)
         if pipe.x_global is not None:
             pipe.x_global.copy_(torch.rand(pipe.x_global.shape, device=dev, generator=g) * 0.1)
@@ -247,7 +248,9 @@ def main():
                 "config": {"model": "AlexNet full (reference Blocks1-2 + Conv3-5 + FC6-8, 1000 classes)",
                            "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
                            "gflop_per_image": round(flops / 1e9, 4), "tflops": round(imgs * flops / 1e12, 2),
-                           "prewarm_steps": n_pw, "prewarm_ms": prewarm_ms},
+                           "prewarm_steps": n_pw, "prewarm_ms": prewarm_ms, "lanes": a.full_lanes,
+                           "lane_sync": ("free-running lanes half a forward apart (forward_async)" if pipe.async_lanes
+                                         else "lanes forked/joined every step" if a.full_lanes > 1 else "one lane")},
             }
             print(json.dumps(rec), flush=True)
         if world > 1:

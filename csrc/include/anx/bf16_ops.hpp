@@ -105,7 +105,11 @@ class FullEngine {
   FullEngine(const FullEngine&) = delete;
   FullEngine& operator=(const FullEngine&) = delete;
   // x: [N,227,227,3] fp32 device; logits: [N,classes] fp32 device.
-  hipError_t forward(const float* x, int N, float* logits, hipStream_t s);
+  hipError_t forward(const float* x, int N, float* logits, hipStream_t s, bool mark = false);
+  // forward(..., mark = true) records this engine's mark event on `s` once Conv2 + Pool2/LRN of the
+  // first chunk are enqueued (about half of the forward): wait_mark makes another stream wait for it,
+  // which staggers free-running lanes (AlexNetFull.forward_async) by half a forward.
+  hipError_t wait_mark(hipStream_t s) const { return mark_ ? hipStreamWaitEvent(s, mark_, 0) : hipErrorInvalidValue; }
   int classes() const { return classes_; }
   int max_batch() const { return max_batch_; }
   Knobs& knobs() { return k_; }  // read at every launch (bf16_glds, bf16_big)
@@ -117,6 +121,7 @@ class FullEngine {
   size_t tap(int i, int N, void* dst, hipStream_t s) const;
 
  private:
+  hipEvent_t mark_ = nullptr;
   struct Layer {
     int C, K, F, S, groups;
     void* wp = nullptr;

@@ -65,6 +65,10 @@ int anx_full_create(void** out, const float* const* weights, const float* const*
                     int max_batch, int groups2, int lrn_mode);
 int anx_full_destroy(void* e);
 int anx_full_forward(void* e, const float* x, int N, float* logits, void* stream);
+/* forward that records the engine's mark event half-way (after Conv2 + Pool2/LRN of the first chunk);
+   anx_full_wait_mark makes `stream` wait for the last recorded mark of engine e. */
+int anx_full_forward_mark(void* e, const float* x, int N, float* logits, void* stream);
+int anx_full_wait_mark(void* e, void* stream);
 
 /* ---- host engine (same contract as the device engine; V1 / V2 CPU ranks) ---- */
 int anx_cpu_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,

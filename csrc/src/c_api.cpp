@@ -264,6 +264,18 @@ int anx_full_forward(void* e, const float* x, int N, float* logits, void* stream
   });
 }
 
+int anx_full_forward_mark(void* e, const float* x, int N, float* logits, void* stream) {
+  return guarded("anx_full_forward_mark", [&] {
+    return hip_status(static_cast<anx::FullEngine*>(e)->forward(x, N, logits, S(stream), true), "full forward");
+  });
+}
+
+int anx_full_wait_mark(void* e, void* stream) {
+  return guarded("anx_full_wait_mark", [&] {
+    return hip_status(static_cast<anx::FullEngine*>(e)->wait_mark(S(stream)), "full wait mark");
+  });
+}
+
 int anx_cpu_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,
                           const float* bias1, const float* w2, const float* bias2) {
   return guarded("anx_cpu_engine_create", [&] {

@@ -120,6 +120,7 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
 }
 
 FullEngine::~FullEngine() {
+  if (mark_) (void)hipEventDestroy(mark_);
   for (Layer& L : L_)
     for (void* p : {L.wp, L.wfc, static_cast<void*>(L.koff), static_cast<void*>(L.bias)})
       if (p) (void)hipFree(p);
@@ -183,7 +184,8 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
   return hip::conv2d_bf16(p, x, L.wp, L.koff, L.bias, out, out_f32, relu, s, {}, k_.bf16_glds);
 }
 
-hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t s) {
+hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t s, bool mark) {
+  if (mark && !mark_) ANX_TRY(hipEventCreateWithFlags(&mark_, hipEventDisableTiming));
   using hip::OutViewB;
   auto B = [](void* p) { return static_cast<__bf16*>(p); };
   for (int n0 = 0; n0 < N; n0 += chunk_) {
@@ -200,6 +202,7 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
     ANX_TRY(conv(L_[1], n, 31, 31, q2_, OutViewB{B(c2_), 27, 27, 256, 0, 0, 0}, nullptr, true, s));
     ANX_TRY(hip::maxpool_lrn_bf16(c2_, n, 27, 27, 256, 3, 2, 5, 1e-4f, 0.75f, 2.0f, lrn_,
                                   OutViewB{B(q3_), 15, 15, 256, 1, 1, 0}, s, k_.bf16_lrn_tile));
+    if (mark && n0 == 0) ANX_TRY(hipEventRecord(mark_, s));
     ANX_TRY(conv(L_[2], n, 15, 15, q3_, OutViewB{B(q4_), 15, 15, 384, 1, 1, 0}, nullptr, true, s));
     ANX_TRY(conv(L_[3], n, 15, 15, q4_, OutViewB{B(q5_), 15, 15, 384, 1, 1, 0}, nullptr, true, s));
     ANX_TRY(conv(L_[4], n, 15, 15, q5_, OutViewB{B(c5_), 13, 13, 256, 0, 0, 0}, nullptr, true, s));

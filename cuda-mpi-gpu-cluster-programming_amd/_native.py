@@ -77,6 +77,8 @@ _SIGS = {
     "anx_full_create": (_I, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), _I, _I, _I, _I]),
     "anx_full_destroy": (_I, [_P]),
     "anx_full_forward": (_I, [_P, _P, _I, _P, _P]),
+    "anx_full_forward_mark": (_I, [_P, _P, _I, _P, _P]),
+    "anx_full_wait_mark": (_I, [_P, _P]),
     "anx_memcpy2d_async": (_I, [_P, _SZ, _P, _SZ, _SZ, _SZ, _P]),
     "anx_conv2d_direct": (_I, [_P, _P, _P, _P] + [_I] * 10 + [_P]),
     "anx_relu": (_I, [_P, _SZ, _P]),

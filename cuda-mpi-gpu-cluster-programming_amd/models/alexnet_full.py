@@ -138,6 +138,50 @@ class AlexNetFull:
 
     __call__ = forward
 
+    def forward_async(self, x: torch.Tensor, out: torch.Tensor, on_lane=None, pre_lane=None) -> torch.Tensor:
+        """Throughput form for repeated forwards on the same buffers (contract of
+        AlexNetBlocks.forward_async): lanes on their own streams, never joined per call; when all are
+        idle they fork from the current stream and lane i starts at lane i-1's mid-forward mark
+        (after Conv2 + Pool2/LRN), so they run half a forward apart. :meth:`join` before reading out."""
+        N = x.shape[0]
+        L = 1 + len(self._lanes)
+        if L == 1 or N < L or self.device.type != "cuda":
+            if pre_lane is not None:
+                pre_lane(0, 0, N)
+            self.forward(x, out)
+            if on_lane is not None:
+                on_lane(0, 0, N)
+            return out
+        if getattr(self, "_own_stream", None) is None:
+            self._own_stream = torch.cuda.Stream(self.device)
+        streams = [self._own_stream, *self._lane_streams]
+        engines = [self, *self._lanes]
+        bounds = [N * i // L for i in range(L + 1)]
+        fresh = all(st.query() for st in streams)
+        cur = torch.cuda.current_stream(self.device)
+        for i, (eng, st) in enumerate(zip(engines, streams)):
+            lo, hi = bounds[i], bounds[i + 1]
+            eng._ensure(hi - lo)
+            if fresh:
+                st.wait_stream(cur)
+                if i > 0:
+                    nat.call("anx_full_wait_mark", engines[i - 1]._h, st.cuda_stream)
+            fn = "anx_full_forward_mark" if fresh and i + 1 < L else "anx_full_forward"
+            with torch.cuda.stream(st):
+                if pre_lane is not None:
+                    pre_lane(i, lo, hi)
+                nat.call(fn, eng._h, x[lo:hi].data_ptr(), hi - lo, out[lo:hi].data_ptr(), st.cuda_stream)
+                if on_lane is not None:
+                    on_lane(i, lo, hi)
+        return out
+
+    def join(self) -> None:
+        if self.device.type != "cuda":
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for st in [s for s in [getattr(self, "_own_stream", None)] if s is not None] + self._lane_streams:
+            cur.wait_stream(st)
+
     TAPS = ((55, 55, 96), (31, 31, 96), (27, 27, 256), (15, 15, 256), (15, 15, 384), (15, 15, 384), (13, 13, 256),
             (9216,), (4096,), (4096,), (57, 57, 48))
 

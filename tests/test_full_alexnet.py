@@ -196,3 +196,24 @@ def test_full_alexnet_lanes_bit_identical(cuda):
     ref = torch.cat([one(x[:N // 2].contiguous()).clone(), one(x[N // 2:].contiguous()).clone()])
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.gpu
+def test_full_alexnet_forward_async_bit_identical(cuda):
+    """forward_async (free-running lanes, lane 1 started at lane 0's mid-forward mark when idle)
+    equals the joined lane forward over repeated calls on the same buffers and after a device sync."""
+    N = 10
+    x = (init_input(N, "rand", seed=16) * 10).to(cuda)
+    two = AlexNetFull(seed=16, device=cuda, max_batch=N, lanes=2)
+    ref = two(x).clone()
+    y = torch.full_like(ref, float("nan"))
+    for _ in range(4):
+        two.forward_async(x, y)
+    two.join()
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    y.fill_(float("nan"))
+    two.forward_async(x, y)
+    two.join()
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
