@@ -60,6 +60,83 @@ __global__ void __launch_bounds__(256) peak16(float* out, int iters, float seed)
   if (s == 1234.5f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// Random operands: 8 random floats per lane held in registers, cycled through the unrolled loop
+// (different bits every MFMA, no memory traffic), one accumulator chain per wave (the dependent
+// chain of the Winograd GEMMs) or four. The guide's DVFS note: random data lowers the loaded clock.
+template <int NACC>
+__global__ void __launch_bounds__(256) peak32_rand(float* out, int iters, float seed) {
+  f32x16 c[NACC] = {};
+  float r[8];
+  unsigned h = (blockIdx.x * 256 + threadIdx.x) * 2654435761u ^ __float_as_uint(seed);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h = h * 1664525u + 1013904223u;
+    r[j] = __uint_as_float(0x3f800000u | (h >> 9)) - 1.5f;  // uniform [-0.5, 0.5)
+  }
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      c[k % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(r[k & 7], r[(k * 3 + 1) & 7], c[k % NACC], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < NACC; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += c[a][e];
+  if (s == 1234.5f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// The Conv2 fused GEMM's operand feed without its memory pipeline: a 64x64 workgroup tile of 4 waves
+// (32x32 each), BK = 48 slices of A and B rows in LDS (the kernel's swizzled layout), per group of
+// 4 MFMAs two ds_read_b128 fragments; PF = the next group's fragments read before this group's MFMAs.
+template <bool PF>
+__global__ void __launch_bounds__(256, 2) peak32_lds(float* out, int iters, float seed) {
+  constexpr int BK = 48, TILE = 64 * BK;
+  __shared__ __attribute__((aligned(16))) float lds[2 * TILE];
+  unsigned h0 = threadIdx.x * 2654435761u ^ __float_as_uint(seed);
+  for (int i = threadIdx.x; i < 2 * TILE; i += 256) {
+    h0 = h0 * 1664525u + 1013904223u;
+    lds[i] = __uint_as_float(0x3f800000u | (h0 >> 9)) - 1.5f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 31, h = lane >> 5, swz = (r >> 2) & 3;
+  int rd[BK / 8];
+#pragma unroll
+  for (int s4 = 0; s4 < BK / 8; ++s4) rd[s4] = 4 * ((h * (BK / 8) + s4) ^ swz);
+  const int a_row = (wm * 32 + r) * BK, b_row = TILE + (wn * 32 + r) * BK;
+  f32x16 acc = {};
+  for (int i = 0; i < iters; ++i) {
+    if constexpr (PF) {
+      f32x4 af[2], bf[2];
+      af[0] = *reinterpret_cast<const f32x4*>(lds + a_row + rd[0]);
+      bf[0] = *reinterpret_cast<const f32x4*>(lds + b_row + rd[0]);
+#pragma unroll
+      for (int s4 = 0; s4 < BK / 8; ++s4) {
+        if (s4 + 1 < BK / 8) {
+          af[(s4 + 1) & 1] = *reinterpret_cast<const f32x4*>(lds + a_row + rd[s4 + 1]);
+          bf[(s4 + 1) & 1] = *reinterpret_cast<const f32x4*>(lds + b_row + rd[s4 + 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s4 & 1][q], bf[s4 & 1][q], acc, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int s4 = 0; s4 < BK / 8; ++s4) {
+        const f32x4 af = *reinterpret_cast<const f32x4*>(lds + a_row + rd[s4]);
+        const f32x4 bf = *reinterpret_cast<const f32x4*>(lds + b_row + rd[s4]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q], bf[q], acc, 0, 0, 0);
+      }
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) s += acc[e];
+  if (s == 1234.5f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <class K>
 double run(K kernel, int grid, int iters, double flop_per_wave_iter, float* out) {
   hipEvent_t e0, e1;
@@ -104,6 +181,18 @@ int main(int argc, char** argv) {
               p.multiProcessorCount, waves, t32);
   std::printf("{\"form\": \"v_mfma_f32_16x16x4_f32\", \"cus\": %d, \"waves_per_simd\": %d, \"tflops\": %.1f}\n",
               p.multiProcessorCount, waves, t16);
+  const double l0 = run(peak32_lds<false>, grid, iters / 4, 24.0 * 2 * 32 * 32 * 2, out);
+  const double l1 = run(peak32_lds<true>, grid, iters / 4, 24.0 * 2 * 32 * 32 * 2, out);
+  std::printf("{\"form\": \"v_mfma_f32_32x32x2_f32 fed by ds_read_b128 (Conv2 GEMM layout), scheduler order\", "
+              "\"cus\": %d, \"waves_per_simd\": %d, \"tflops\": %.1f}\n", p.multiProcessorCount, waves, l0);
+  std::printf("{\"form\": \"v_mfma_f32_32x32x2_f32 fed by ds_read_b128 (Conv2 GEMM layout), prefetch pinned\", "
+              "\"cus\": %d, \"waves_per_simd\": %d, \"tflops\": %.1f}\n", p.multiProcessorCount, waves, l1);
+  const double r1 = run(peak32_rand<1>, grid, iters, 16.0 * 2 * 32 * 32 * 2, out);
+  const double r4 = run(peak32_rand<4>, grid, iters, 16.0 * 2 * 32 * 32 * 2, out);
+  std::printf("{\"form\": \"v_mfma_f32_32x32x2_f32 random operands, 1 accumulator chain\", \"cus\": %d, "
+              "\"waves_per_simd\": %d, \"tflops\": %.1f}\n", p.multiProcessorCount, waves, r1);
+  std::printf("{\"form\": \"v_mfma_f32_32x32x2_f32 random operands, 4 accumulators\", \"cus\": %d, "
+              "\"waves_per_simd\": %d, \"tflops\": %.1f}\n", p.multiProcessorCount, waves, r4);
   CHECK(hipFree(out));
   return 0;
 }
