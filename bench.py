@@ -29,6 +29,7 @@ kernels execute (0.278 GFLOP/image); ``direct_equiv_tflops`` counts direct-convo
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -36,6 +37,11 @@ import time
 from datetime import timedelta
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues round-robin (4 on the MI355X boxes). Two
+# lanes' streams on one queue serialise (0.80 vs 0.57 ms per 128-image step when other streams were
+# created first: profiles/r02_lanes_async.txt); 8 gives every stream here (current, 2 lanes, RCCL) its
+# own. Read by the HIP runtime at its first call, so set before torch touches the GPU.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -217,6 +223,10 @@ def main():
     if world > 1:
         dist.barrier()
     sync()
+    # no collector pause inside the timed steps: a pause of a few ms starves the GPU queue the host
+    # is only just ahead of (measured with free-running lanes: tools/sweep_batch.py)
+    gc.collect()
+    gc.disable()
     t0 = time.perf_counter()
     if wl is not None:
         for _ in range(a.steps):
@@ -229,6 +239,7 @@ def main():
         dist.barrier()
     sync()
     el = time.perf_counter() - t0
+    gc.enable()
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -306,6 +317,7 @@ def main():
                 "ms_per_batch": round(ms, 4),
                 "prewarm_steps": n_pw,
                 "prewarm_ms": prewarm_ms,
+                "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "gflop_per_image_direct": round(anx.flops_per_image() / 1e9, 4),
                 "gflop_per_image_mfma": round(mf / 1e9, 4),
                 "direct_equiv_tflops": round(imgs * anx.flops_per_image() / 1e12, 2),
