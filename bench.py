@@ -29,7 +29,6 @@ kernels execute (0.278 GFLOP/image); ``direct_equiv_tflops`` counts direct-convo
 from __future__ import annotations
 
 import argparse
-import gc
 import json
 import os
 import sys
@@ -40,8 +39,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues round-robin (4 on the MI355X boxes). Two
 # lanes' streams on one queue serialise (0.80 vs 0.57 ms per 128-image step when other streams were
 # created first: profiles/r02_lanes_async.txt); 8 gives every stream here (current, 2 lanes, RCCL) its
-# own. Read by the HIP runtime at its first call, so set before torch touches the GPU.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# own. Read by the HIP runtime at its first call, so set before torch touches the GPU (the boxes
+# export 4 explicitly; ANX_HW_QUEUES overrides the 8).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ANX_HW_QUEUES", "8")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -223,10 +223,6 @@ def main():
     if world > 1:
         dist.barrier()
     sync()
-    # no collector pause inside the timed steps: a pause of a few ms starves the GPU queue the host
-    # is only just ahead of (measured with free-running lanes: tools/sweep_batch.py)
-    gc.collect()
-    gc.disable()
     t0 = time.perf_counter()
     if wl is not None:
         for _ in range(a.steps):
@@ -239,7 +235,6 @@ def main():
         dist.barrier()
     sync()
     el = time.perf_counter() - t0
-    gc.enable()
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -36,9 +36,6 @@ def main():
     for b in bs:
         models[b](xs[b], out=ys[b])
     torch.cuda.synchronize()
-    import gc
-    gc.collect()
-    gc.disable()  # a collector pause inside a timed round would starve the GPU queue
     for _ in range(a.rounds):
         for b in bs:
             m = models[b]
