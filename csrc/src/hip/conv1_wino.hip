@@ -465,6 +465,11 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
     }
   };
   auto fold = [&](int ab, f32x4 (&acc)[2]) {
+    if (a.probe & 1) {  // cost probe: keep the accumulators live, skip the output-transform FMAs
+      Y[0][0][0] += f32x2{acc[0][0] + acc[1][0], acc[0][1] + acc[1][1]};
+      acc[0] = acc[1] = f32x4{};
+      return;
+    }
     const int aa = ab / kN5, bb = ab - aa * kN5;
 #pragma unroll
     for (int i3 = 0; i3 < 3; ++i3)
@@ -483,9 +488,9 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
   };
   auto step = [&](int ab, f32x4 (&acc)[2]) {
     wait_vmcnt<0>();  // this wave's DMA of point ab landed (it was issued one point ago)
-    __builtin_amdgcn_s_barrier();  // ... and every other wave's; every wave is done with slot ab-1
+    if ((a.probe & 6) != 6) __builtin_amdgcn_s_barrier();  // ... and every other wave's (probe 6: skipped)
     asm volatile("" ::: "memory");
-    if (ab + 1 < kPts) issue(ab + 1);
+    if (ab + 1 < kPts && !(a.probe & 2)) issue(ab + 1);  // probe 2: no refills (operands stale)
     if (a.probe & 16) __builtin_amdgcn_s_setprio(1);
     mfma_point(ab, acc);
     if (a.probe & 16) __builtin_amdgcn_s_setprio(0);
