@@ -210,7 +210,7 @@ __global__ void __launch_bounds__(256, 2) conv1_wino_gemm_kernel(GemmArgs a) {
   constexpr int KS = kCh / BK;        // slices per transform point
   constexpr int TOTAL = kPts * KS;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   // XCD-aware order: the n_ntiles workgroups that read one V slab get equal blockIdx.x % 8, i.e.
   // one XCD under round-robin dispatch, so the slab comes from HBM/MALL once (speed only).
   const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
@@ -399,7 +399,7 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
   constexpr int STAGE = A_FL + B_FL;
   constexpr int NS_LO = A_PW + B_INS / 4, NS_HI = NS_LO + 1;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
   const int nt = jb % a.n_ntiles;
   const int pt = (jb / a.n_ntiles) * 8 + xcd;

@@ -459,7 +459,7 @@ __device__ __forceinline__ void fused_glds_unit(const FusedArgs& a, float* lds, 
   static_assert(NI * 256 == kFB * U4 && U4 % 4 == 0, "BK must be a multiple of 16");
   constexpr int TILE = kFB * BK;          // floats per operand tile
   constexpr int STAGE = 2 * TILE;         // A tile | B tile
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   const int wm = wave >> 1, wn = wave & 1;
   const int p0 = pt * kFB, n0 = nt * kFB;
 
@@ -802,7 +802,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, 4) wino_fused_glds16_kernel(Fu
   constexpr int A_FL = BMT * BK, B_FL = BNT * BK;
   constexpr int STAGE = A_FL + B_FL;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   const int wm = wave % WMW, wn = wave / WMW;
   const int g = blockIdx.z;
   int pt, nt;
