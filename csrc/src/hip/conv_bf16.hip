@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(kThreads, VEC8 ? 3 : 2) conv_bf16_kernel(ArgsB
   int* koff_s = reinterpret_cast<int*>(lds_b + (BM + BN) * kLDA);
   int* ooff_s = koff_s + a.kpad;  // output offset per tile row (-1 past M), from the prologue
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   const int wm = wave / WAVES_N, wn = wave % WAVES_N, g = blockIdx.z;
   const int mt = blockIdx.x / a.n_ntiles, nt = blockIdx.x - mt * a.n_ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(128 * WMW) conv_bf16_glds_kernel(ArgsB a) {
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
   int* koff_s = reinterpret_cast<int*>(lds_b + NST * STAGE);
   int* ooff_s = koff_s + a.kpad;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   const int wm = wave >> 1, wn = wave & 1, g = blockIdx.z;
   const int mt = blockIdx.x / a.n_ntiles, nt = blockIdx.x - mt * a.n_ntiles;
   const int m0 = mt * BM, n0 = nt * BN;

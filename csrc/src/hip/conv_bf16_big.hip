@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
   int* ooff_s = reinterpret_cast<int*>(lds_b + NST * STAGE);  // output offset per tile row (-1 past M)
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   const int wm = wave / WGN, wn = wave % WGN, g = blockIdx.z;
   // XCD-aware bijective remap: dispatch round-robins blocks over the 8 XCDs; give each XCD a
   // contiguous run of tiles (m-major, n inner) so neighbouring tiles share its L2.
@@ -303,7 +303,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
   static_assert(TN >= 1 && NB >= 1, "tile split");
   constexpr int CH = BN / 8, EW = BN + 8;  // epilogue image rows padded by 16 B (conflict-free)
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   const int G = __builtin_amdgcn_readfirstlane(wave >> 2);  // wave-uniform, scalar
   const int wl = wave & 3, tl = tid & 255, wn = wave & 3, g = blockIdx.z;
   int tile;
@@ -523,7 +523,7 @@ __global__ void __launch_bounds__(512) fc_bf16_kernel(ArgsFc a) {
   constexpr int VM = 5;                               // vm ops per lane per K tile: 4 A loads + 1 DMA
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
   lds_b16* lds3 = (lds_b16*)(lds_b);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
   // XCD-aware bijective remap over (K slice, tile), K-slice-major: each XCD walks a contiguous run,
   // so it streams one or two K slices of the activations (L2-resident) instead of all of them.
   int w;
