@@ -23,7 +23,8 @@ struct Knobs {
   int conv1_cfg = 4;       // Conv1 Winograd GEMM variant 0..4 (conv1_wino.hip; 4 = 16x16 MFMA, 4 WG/CU)
   int conv1_probe = 16;    // Conv1 GEMM bits: 4 s_setprio, 5 NT V stores, 6 interleaved fold; 0-3 cost probes
   int wino_cfg = 7;        // Conv2 fused GEMM: bit0 BK 48, bit1 XCD order, bit2 LDS-DMA ring, bit3 16x16 MFMA
-  int wino_prio = 257;     // Conv2 fused GEMM bits: 0 s_setprio, 1 NT V stores, 8 interleaved fold; 4-7 probes
+  int wino_prio = 257;     // Conv2 fused GEMM bits: 0 s_setprio, 1 NT V stores, 2 scalar (1-channel) input
+                           // transform, 8 interleaved fold; 4-7 probes
   int wino_split = 1;      // Conv2 fused GEMM tail split: 0 off, 1 auto (fill the last round's idle CUs), 2-7 force
   int wino_sk = 0;         // Conv2 fused GEMM stream-K: 0 off, 1-2 = that many workgroups per CU over equal
                            // ranges of (point tile, transform point) work (supersedes the tail split)

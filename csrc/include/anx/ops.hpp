@@ -100,7 +100,8 @@ size_t wino_m_floats(const WinoPlan& w);
 // U = G g G^T in fp64, laid out as KCFF weights of the grouped 1x1 GEMM ([49*K][C/g]).
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
 // nt: non-temporal V stores (Knobs::wino_prio bit1, A/B).
-hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s, bool nt = false);
+// nt: non-temporal V stores (A/B); scalar: one channel per thread instead of two (A/B)
+hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s, bool nt = false, bool scalar = false);
 // Pool1 (3x3 / 2, post-ReLU conv1 input) fused into the input transform: V of the zero-bordered
 // pool1 window without materialising it. Window row r = pool1 row r + q_lo; pool1 rows outside
 // [p1_lo, p1_hi) and columns outside [0, Wp) are the border; conv1 rows [c1_lo, c1_lo + H1) are in

@@ -202,7 +202,7 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
       wino_key_ = w.gemm.variant;
     }
     if (qc) {
-      ANX_TRY(hip::wino_input(w, qc, wv_, s, (k_.wino_prio & 2) != 0));
+      ANX_TRY(hip::wino_input(w, qc, wv_, s, (k_.wino_prio & 2) != 0, (k_.wino_prio & 4) != 0));
     } else {
       const hip::WinoPoolGeom pg{t.c1.size(), d_.W1, d_.Wp1, k2.P, t.q.lo, t.p1.lo, t.p1.hi, t.c1.lo};
       ANX_TRY(hip::wino_input_pool(w, c1_, pg, wv_, s));
