@@ -82,6 +82,7 @@ def parse():
                     help="dp, 1 GPU: the step as one captured HIP graph replayed each step (1), eager (0, default; "
                          "measured equal: the step is GPU-bound), -1 auto")
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency measurement")
+    ap.add_argument("--lane-priority", type=int, default=0, help="dp: HIP stream priority of the side lanes (-1 = high)")
     ap.add_argument("--joined-lanes", action="store_true",
                     help="dp: join the stream lanes every step (AlexNetBlocks.forward) instead of free-running lanes "
                          "half a step apart (forward_async; the default with local input)")
@@ -144,7 +145,8 @@ def main():
         out_shape, flops = (1000,), FLOPS_PER_IMAGE
     elif a.workload == "dp":
         B = a.batch_per_gpu or DEFAULT_BATCH["dp"]
-        model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B, lanes=a.lanes)
+        model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B, lanes=a.lanes,
+                              lane_priority=a.lane_priority)
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
     else:
         from anx.parallel.workloads import RowsWorkload
