@@ -83,6 +83,8 @@ def parse():
                          "measured equal: the step is GPU-bound), -1 auto")
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency measurement")
     ap.add_argument("--lane-priority", type=int, default=0, help="dp: HIP stream priority of the side lanes (-1 = high)")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="blocks model: engine knob override (anx.utils.tuning.KNOBS), repeatable; A/B only")
     ap.add_argument("--joined-lanes", action="store_true",
                     help="dp: join the stream lanes every step (AlexNetBlocks.forward) instead of free-running lanes "
                          "half a step apart (forward_async; the default with local input)")
@@ -145,8 +147,9 @@ def main():
         out_shape, flops = (1000,), FLOPS_PER_IMAGE
     elif a.workload == "dp":
         B = a.batch_per_gpu or DEFAULT_BATCH["dp"]
+        knobs = {k: int(v) if v.lstrip("-").isdigit() else v for k, v in (kv.split("=", 1) for kv in a.knob)}
         model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B, lanes=a.lanes,
-                              lane_priority=a.lane_priority)
+                              lane_priority=a.lane_priority, knobs=knobs)
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
     else:
         from anx.parallel.workloads import RowsWorkload
@@ -276,7 +279,7 @@ def main():
                         if a.input_source == "root" else
                         "per-rank data -> compute -> gather to rank 0 (RCCL, overlapped with the next step)") \
                 if world > 1 else "single GPU"
-            extra = {"input_source": a.input_source, "lanes": a.lanes, "hip_graph": use_graph,
+            extra = {"input_source": a.input_source, "lanes": a.lanes, "hip_graph": use_graph, "knobs": a.knob,
                      "lane_sync": ("free-running lanes half a step apart, per-lane gathers (forward_async)"
                                    if pipe.async_lanes else "lanes forked/joined every step")}
         else:
