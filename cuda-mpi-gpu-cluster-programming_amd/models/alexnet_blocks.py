@@ -158,6 +158,17 @@ class AlexNetBlocks:
             raise ValueError(f"input on {x.device}, model on {self.device}")
         return x.shape[0]
 
+    def _out(self, out: torch.Tensor | None, N: int, rows: int | None = None) -> torch.Tensor:
+        """``out`` checked against the output the kernels will write (shape, dtype, layout, device), or a
+        new tensor: the native engines write through the raw pointer."""
+        shape = self.out_shape(N, rows)
+        if out is None:
+            return torch.empty(shape, device=self.device)
+        if tuple(out.shape) != shape or out.dtype != torch.float32 or not out.is_contiguous() or out.device != self.device:
+            raise ValueError(f"out must be a contiguous float32 {shape} tensor on {self.device}, got "
+                             f"{tuple(out.shape)} {out.dtype} on {out.device}")
+        return out
+
     def _stream(self) -> int:
         return nat.stream_ptr(self.device)
 
@@ -170,7 +181,7 @@ class AlexNetBlocks:
         if L == 1 or N < L * LANE_MIN:
             return self.tile_forward(x, plan, out)
         self._check_in(x, self.H)
-        y = out if out is not None else torch.empty(self.out_shape(N), device=self.device)
+        y = self._out(out, N)
         bounds = [N * i // L for i in range(L + 1)]
         cur = torch.cuda.current_stream(self.device)
         for i, st in enumerate(self._lane_streams, start=1):
@@ -201,6 +212,7 @@ class AlexNetBlocks:
         collective still reading that output slice / a per-lane collective on it)."""
         L = 1 + len(self._lanes)
         N = self._check_in(x, self.H)
+        out = self._out(out, N)
         if L == 1 or N < L * LANE_MIN or not self.is_cuda:
             if pre_lane is not None:
                 pre_lane(0, 0, N)
@@ -251,7 +263,7 @@ class AlexNetBlocks:
     def tile_forward(self, x: torch.Tensor, tile: TilePlan, out: torch.Tensor | None = None) -> torch.Tensor:
         """Row tile: ``x`` holds input rows ``tile.inp`` of N images; returns output rows ``tile.out``."""
         N = self._check_in(x, tile.inp.size)
-        y = out if out is not None else torch.empty(self.out_shape(N, tile.out.size), device=self.device)
+        y = self._out(out, N, tile.out.size)
         if tile.out.size == 0 or N == 0:
             return y
         self._ensure(N)
@@ -274,7 +286,7 @@ class AlexNetBlocks:
 
     def stage2(self, N: int, tile: TilePlan, out: torch.Tensor | None = None) -> torch.Tensor:
         """conv2+ReLU+pool2+LRN of the (halo-completed) window -> output rows ``tile.out``."""
-        y = out if out is not None else torch.empty(self.out_shape(N, tile.out.size), device=self.device)
+        y = self._out(out, N, tile.out.size)
         if tile.out.size == 0 or N == 0:
             return y
         if self.is_cuda:

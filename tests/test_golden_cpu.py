@@ -35,3 +35,30 @@ def test_grouped_conv2_matches_oracle():
     m = AlexNetBlocks(device="cpu", init="rand", seed=5, groups2=2)
     x = init_input(1, "rand", seed=5)
     torch.testing.assert_close(m(x).double(), blocks_forward(x, m.weights, m.b1, m.b2), rtol=1e-5, atol=1e-6)
+
+
+def test_out_tensor_is_checked():
+    """The engines write through the raw output pointer: a caller-supplied ``out`` of the wrong shape,
+    dtype or layout is rejected before any native call (forward, forward_async, tile_forward, stage2)."""
+    import pytest
+    import torch
+
+    from anx.models.alexnet_blocks import AlexNetBlocks, full_plan
+    from anx.utils.init import init_input
+
+    m = AlexNetBlocks(init="rand", seed=5, device="cpu")
+    x = init_input(1, "rand", seed=5)
+    good = m(x).clone()
+    plan = full_plan(m.H, m.W, m.b1, m.b2)
+    for bad in (torch.empty(1, 13, 13, 255), torch.empty(2, 13, 13, 256), torch.empty(1, 13, 13, 256, dtype=torch.float64),
+                torch.empty(1, 13, 256, 13).transpose(2, 3)):
+        with pytest.raises(ValueError):
+            m(x, out=bad)
+        with pytest.raises(ValueError):
+            m.forward_async(x, bad)
+        with pytest.raises(ValueError):
+            m.tile_forward(x, plan, out=bad)
+    y = torch.empty(1, 13, 13, 256)
+    m.forward_async(x, y)
+    m.join()
+    assert torch.equal(y, good)
