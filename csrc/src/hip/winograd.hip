@@ -534,7 +534,8 @@ __device__ __forceinline__ void fused_glds_unit(const FusedArgs& a, float* lds, 
     boff[j] = (n0 + row) * a.kpad + 4 * u;
   }
   const float* Vg = a.V + g * a.Cg;
-  const int ksteps = a.kpad / BK;
+  // the interleaved schedule only runs at kpad == 2 * BK (launch condition): a compile-time slice count
+  const int ksteps = IL_MODE == 1 ? 2 : a.kpad / BK;
   const int it0 = pb * ksteps, total = pe * ksteps;  // K slices [it0, total) (all 49 points unless split)
   lds_f32* lds3 = (lds_f32*)(lds);  // generic -> LDS address space (C-style cast required)
 
