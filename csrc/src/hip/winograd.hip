@@ -309,6 +309,7 @@ struct FusedArgs {
   int pt_base, nsplit;
   float* slab;
   int sk_groups;  // stream-K (wino_fused_sk_kernel): number of point ranges J
+  int vbytes, ubytes;  // > 0: V / U sizes in bytes (< 2^31): operands by buffer_load ... lds; 0: global_load_lds
 };
 
 // A^T indexed by the runtime transform point: a copy of wino::kAT in constant memory (scalar loads).
@@ -485,6 +486,7 @@ __global__ void __launch_bounds__(256) wino_fused_kernel(FusedArgs a) {
 // of the 32x32 fragment reads hit 16 distinct bank quads. The swizzle is applied on the global
 // source address of each lane.
 using lds_f32 = __attribute__((address_space(3))) float;
+using lds_void = __attribute__((address_space(3))) void;
 // 16 B per lane, global -> LDS (lane i lands at lds + 16*i; lds must be wave-uniform)
 __device__ __forceinline__ void glds16(const float* g, lds_f32* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
 template <int N>
@@ -539,11 +541,30 @@ __device__ __forceinline__ void fused_glds_unit(const FusedArgs& a, float* lds, 
   const int it0 = pb * ksteps, total = pe * ksteps;  // K slices [it0, total) (all 49 points unless split)
   lds_f32* lds3 = (lds_f32*)(lds);  // generic -> LDS address space (C-style cast required)
 
+  // buffer_load ... lds when V and U fit 32-bit byte offsets (a.vbytes > 0): the per-lane offsets
+  // stay in VGPRs once, the per-slice offset is scalar (no 64-bit VALU address per DMA)
+#if __HIP_DEVICE_COMPILE__  // the buffer-resource type exists in the device pass only
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.V), 0, a.vbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
+#endif
   auto issue = [&](int it) {
     const int ab = it / ksteps, kk = (it - ab * ksteps) * BK;
+    lds_f32* st = lds3 + (it % 3) * STAGE;
+#if __HIP_DEVICE_COMPILE__
+    if (a.vbytes > 0) {
+      const int vso = (g * a.Cg + ab * a.C + kk) * 4;
+      const int uso = ((ab * a.groups + g) * a.kpad_n * a.kpad + kk) * 4;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (lds_void*)(st + (j * 4 + wave) * 256), 16, aoff[j] * 4, vso, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + TILE + (j * 4 + wave) * 256), 16, boff[j] * 4,
+                                                 uso, 0, 0);
+      }
+      return;
+    }
+#endif
     const float* va = Vg + ab * a.C + kk;
     const float* ub = a.U + static_cast<size_t>(ab * a.groups + g) * a.kpad_n * a.kpad + kk;
-    lds_f32* st = lds3 + (it % 3) * STAGE;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       glds16(va + aoff[j], st + (j * 4 + wave) * 256);
@@ -1277,7 +1298,7 @@ WinoSplit plan_wino_split(const WinoPlan& w, const Knobs& kn) {
   WinoSplit sp{0, 0, 1};
   const int n_ptiles = (w.P + kFB - 1) / kFB, per_pt = (w.K / w.groups + kFB - 1) / kFB * w.groups;  // WGs per point tile
   sp.pt_full = n_ptiles;
-  if (kn.wino_split == 0 || (kn.wino_cfg & 15) != 7 || (kn.wino_prio & ~257) != 0) return sp;
+  if (kn.wino_split == 0 || (kn.wino_cfg & 15) != 7 || (kn.wino_prio & ~(257 | 512)) != 0) return sp;
   const long slots = device_cus();  // throughput rounds (see above)
   const long wgs = static_cast<long>(n_ptiles) * per_pt;
   const long full_rounds = wgs / slots;
@@ -1333,6 +1354,12 @@ hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const f
   a.n_ptiles = (w.P + kFB - 1) / kFB;
   a.n_ntiles = (a.Kg + kFB - 1) / kFB;
   if (a.n_ntiles * kFB > a.kpad_n || a.Cg % 4) return hipErrorInvalidValue;
+  {
+    const long vb = static_cast<long>(w.P) * kN * kN * w.C * 4, ub = static_cast<long>(kN * kN) * w.groups * a.kpad_n * a.kpad * 4;
+    const bool buf = !(prio & 512) && vb < (1L << 31) && ub < (1L << 31);  // prio bit 9: global_load_lds (A/B)
+    a.vbytes = buf ? static_cast<int>(vb) : 0;
+    a.ubytes = buf ? static_cast<int>(ub) : 0;
+  }
   const bool xcd = (cfg & 2) != 0;
   if ((cfg & 8) && a.Cg % 48 == 0 && a.kpad == a.Cg && a.Kg % 32 == 0) {
     // 16x16 MFMA: bit0 set -> 64 tiles x 64 filters, 8 waves, 2 workgroups/CU; bit0 clear -> 64 tiles

@@ -25,7 +25,7 @@ const Field kFields[] = {
     {"conv1_cfg", &Knobs::conv1_cfg, nullptr, 0, 4, "ANX_CONV1_WINO_CFG"},
     {"conv1_probe", &Knobs::conv1_probe, nullptr, 0, 255, "ANX_CONV1_WINO_PROBE"},
     {"wino_cfg", &Knobs::wino_cfg, nullptr, 0, 15, "ANX_WINO_FUSED_CFG"},
-    {"wino_prio", &Knobs::wino_prio, nullptr, 0, 511, "ANX_WINO_PRIO"},
+    {"wino_prio", &Knobs::wino_prio, nullptr, 0, 1023, "ANX_WINO_PRIO"},
     {"fold_scalar", &Knobs::fold_scalar, nullptr, 0, 3, "ANX_FOLD_SCALAR"},
     {"wino_split", &Knobs::wino_split, nullptr, 0, 7, "ANX_WINO_SPLIT"},
     {"wino_sk", &Knobs::wino_sk, nullptr, 0, 2, "ANX_WINO_SK"},
