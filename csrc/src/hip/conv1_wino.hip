@@ -146,9 +146,11 @@ struct GemmArgs {
   int probe;  // cost probes (wrong results; never set in production): bit0 no fold, bit1 no DMA
               // refill, bit2 no per-slice barrier (only with bit1), bit3 no epilogue stores;
               // bit4: s_setprio(1) around each slice's MFMAs (guide technique T5; on by default)
+  int vbytes, ubytes;  // gemm16: > 0 = V / U byte sizes (< 2^31), operands by buffer_load ... lds
 };
 
 using lds_f32 = __attribute__((address_space(3))) float;
+using lds_void = __attribute__((address_space(3))) void;
 // 16 B per lane, global -> LDS (lane i lands at lds + 16*i; lds must be wave-uniform)
 __device__ __forceinline__ void glds16(const float* g, lds_f32* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
 template <int N>
@@ -424,10 +426,30 @@ __global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
     boff[s] = (n0 + row) * kCh + 4 * ((su + U4 - rot16(row)) % U4);
   }
   lds_f32* lds3 = (lds_f32*)(lds);
+  // buffer_load ... lds when V fits 31-bit byte offsets (a.vbytes > 0): per-lane offsets in VGPRs once,
+  // the per-point offset scalar (no 64-bit VALU address per DMA)
+#if __HIP_DEVICE_COMPILE__  // the buffer-resource type exists in the device pass only
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.V), 0, a.vbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
+#endif
   auto issue = [&](int ab) {
+    lds_f32* st = lds3 + (ab & 1) * STAGE;
+#if __HIP_DEVICE_COMPILE__
+    if (a.vbytes > 0) {
+#pragma unroll
+      for (int j = 0; j < A_PW; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (lds_void*)(st + (j * 4 + wave) * 256), 16, aoff[j] * 4,
+                                                 ab * kCh * 4, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        if (wave + 4 * s < B_INS)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + A_FL + (wave + 4 * s) * 256), 16, boff[s] * 4,
+                                                   ab * a.K * kCh * 4, 0, 0);
+      return;
+    }
+#endif
     const float* va = a.V + ab * kCh;
     const float* ub = a.U + static_cast<size_t>(ab) * a.K * kCh;
-    lds_f32* st = lds3 + (ab & 1) * STAGE;
 #pragma unroll
     for (int j = 0; j < A_PW; ++j) glds16(va + aoff[j], st + (j * 4 + wave) * 256);
 #pragma unroll
@@ -720,6 +742,12 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
       if (attr != hipSuccess) return attr;
       GemmArgs b = a;
       b.n_ptiles = (a.P + kBM16 - 1) / kBM16;
+      {  // probe bit 7: global_load_lds operands (A/B)
+        const long vb = static_cast<long>(w.P) * kPts * kCh * 4, ub = static_cast<long>(conv1_wino_u_floats(w.K)) * 4;
+        const bool buf = !(probe & 128) && vb < (1L << 31) && ub < (1L << 31);
+        b.vbytes = buf ? static_cast<int>(vb) : 0;
+        b.ubytes = buf ? static_cast<int>(ub) : 0;
+      }
       const dim3 grid((b.n_ptiles + 7) / 8 * 8 * b.n_ntiles);
       if (probe & 64) {
         if (sf)
