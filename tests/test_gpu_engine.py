@@ -459,3 +459,17 @@ def test_forward_async_lanes_bit_identical(cuda, N):
     many.join()
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("knobs", [{"wino_prio": 257 | 512}, {"conv1_probe": 16 | 128}])
+def test_winograd_global_dma_path_bitwise(cuda, knobs):
+    """The Winograd GEMMs load their operands by buffer_load ... lds while V/U fit 31-bit offsets and
+    by global_load_lds above that (or with these A/B bits): both paths give bit-identical outputs."""
+    N = 64
+    x = init_input(N, "rand", seed=41).to(cuda)
+    a = AlexNetBlocks(device=cuda, init="rand", seed=41, max_batch=N, knobs={"wino_split": 0})
+    b = AlexNetBlocks(a.weights, device=cuda, max_batch=N, knobs={"wino_split": 0, **knobs})
+    ya = a(x).clone()
+    yb = b(x)
+    torch.cuda.synchronize()
+    assert torch.equal(ya, yb)
