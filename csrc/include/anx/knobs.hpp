@@ -40,8 +40,9 @@ struct Knobs {
   int bf16_fc = 0;         // bf16 FC layers: 1 = activation-streaming kernel (fc_bf16; measured slower than the
                            // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
-  int conv1_occ = 3;       // cap on Conv1 Winograd GEMM workgroups per CU (0 = natural: 4), by LDS padding;
-                           // 3 leaves room for the other lane's kernels (+1.5 % with free-running lanes),
+  int conv1_occ = 3;       // cap on Conv1 Winograd GEMM workgroups per CU by LDS padding (the 16x16 kernel's
+                           // launch bounds allow 3: 168 VGPRs, no spills); 3 leaves room for the other
+                           // lane's kernels (+1.5 % with free-running lanes),
   int conv2_occ = 0;       // ... and Conv2's (natural 2): leaves room for a concurrent lane's kernels
 };
 

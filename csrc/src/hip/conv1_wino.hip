@@ -393,7 +393,7 @@ constexpr int kBM16 = 64;
 __device__ __forceinline__ int rot16(int row) { return 3 * ((row >> 1) & 3); }
 
 template <bool IL, bool SF>
-__global__ void __launch_bounds__(256, 4) conv1_wino_gemm16_kernel(GemmArgs a) {
+__global__ void __launch_bounds__(256, 3) conv1_wino_gemm16_kernel(GemmArgs a) {  // 3 per CU (Knobs::conv1_occ default): 168 VGPRs, no spills
   constexpr int BK = kCh, U4 = BK / 4;            // 48 channels, 12 units per row
   constexpr int A_PW = kBM16 * U4 / 64 / 4;       // 3 DMA instructions per wave
   constexpr int B_INS = kBN * U4 / 64;            // 6
