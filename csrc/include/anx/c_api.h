@@ -103,8 +103,8 @@ int anx_maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int F,
 int anx_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups, int* plan_out,
                   size_t* packed_floats, size_t* koff_ints);
 int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff);
-/* Per-engine kernel knobs (anx/knobs.hpp): names conv1_algo, conv2_algo, conv1_cfg, conv1_probe,
-   wino_cfg, wino_prio, fold_scalar, chunk1, chunk2, fuse_pool1, force_vec4, force_scalar, bf16_glds.
+/* Per-engine kernel knobs (anx/knobs.hpp): names conv1_algo, conv2_algo, chunk1, chunk2, force_vec4,
+   force_scalar, bf16_glds, bf16_big, bf16_lrn_tile, bf16_fc, conv1_occ, conv2_occ.
    set returns non-zero for an unknown name or an out-of-range value. */
 int anx_engine_set_knob(void* engine, const char* name, int value);
 int anx_engine_get_knob(void* engine, const char* name, int* value);
@@ -117,12 +117,11 @@ int anx_default_knob(const char* name, int* value);
 /* Conv1 by polyphase Winograd on device buffers (test entry; allocates and frees its workspaces,
    synchronises `stream`): x [N,Hin,W,3], KCFF weights on the HOST, y [N,H1,W1,K]. */
 int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, int K, int F, const float* bias,
-                   float* y, int relu, int fold_scalar, void* stream);
+                   float* y, int relu, void* stream);
 /* Conv2-shaped 5x5/1 conv by Winograd F(3x3,5x5) on device buffers (test entry; allocates, syncs):
-   x [N,Hq,Wq,C] (padding already in the window), KCFF weights on the HOST, y [N,Hq-4,Wq-4,K].
-   wino_cfg -1 = the default fused kernel; wino_split -1 = the default (auto tail split), 0 off. */
+   x [N,Hq,Wq,C] (padding already in the window), KCFF weights on the HOST, y [N,Hq-4,Wq-4,K]. */
 int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
-                   const float* bias, float* y, int relu, int wino_cfg, int wino_split, void* stream);
+                   const float* bias, float* y, int relu, void* stream);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

@@ -24,6 +24,8 @@ namespace anx {
 
 struct RankInfo {
   int rank = 0, world = 1, local_rank = 0;
+  int local_world = 1;  // ranks on this node (ANX_LOCAL_WORLD_SIZE / LOCAL_WORLD_SIZE; default: world)
+  int nnodes = 1;       // nodes in the job (ANX_NNODES / world / local_world)
   std::string master_addr = "127.0.0.1";
   int master_port = 29555;
 };

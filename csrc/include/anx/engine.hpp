@@ -90,15 +90,12 @@ class BlocksEngine {
   // zero-state cache for the conv2 window
   int win_lo_ = 1 << 30, win_hi_ = -(1 << 30), win_n_ = -1;
   int plan_key1_ = -1, plan_key2_ = -1;
-  // Winograd conv2: transformed weights packed for the batched GEMM + V / M workspaces
-  float *u2p_ = nullptr, *wv_ = nullptr, *wm_ = nullptr;
-  float* wsplit_ = nullptr;  // Conv2 fused GEMM tail-split slabs (hip::wino_split_ws_floats)
-  int* ukoff_ = nullptr;
-  int wino_key_ = -1;
+  // Winograd conv2: transformed weights [49][K][C/groups] + V workspace
+  float *u2w_ = nullptr, *wv_ = nullptr;
+  size_t wv_cap_ = 0;
   // Winograd conv1: transformed polyphase weights + V workspace (full-height tiles of chunk_ images)
   float *u1w_ = nullptr, *wv1_ = nullptr;
   size_t wv1_cap_ = 0;
-  size_t wv_cap_ = 0, wm_cap_ = 0;
   std::vector<float> w1h_, w2h_;  // KCFF host copies for re-packing on geometry change
 };
 

@@ -14,24 +14,13 @@ namespace anx {
 
 // Algorithm for a convolution on the Mfma path. Auto = Winograd when eligible and the launch is
 // larger than 8 images' worth of output rows (use_winograd), the direct implicit GEMM below that.
-// WinogradUnfused = input transform + separate batched GEMM (M in HBM) + output transform (A/B only).
-enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2, WinogradUnfused = 3 };
+enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2 };
 
 struct Knobs {
   ConvAlgo conv1_algo = ConvAlgo::Auto;  // Conv1: polyphase Winograd F(3x3,3x3) / direct implicit GEMM
   ConvAlgo conv2_algo = ConvAlgo::Auto;  // Conv2: Winograd F(3x3,5x5) / direct implicit GEMM
-  int conv1_cfg = 4;       // Conv1 Winograd GEMM variant 0..4 (conv1_wino.hip; 4 = 16x16 MFMA, 4 WG/CU)
-  int conv1_probe = 16;    // Conv1 GEMM bits: 4 s_setprio, 5 NT V stores, 6 interleaved fold; 0-3 cost probes
-  int wino_cfg = 7;        // Conv2 fused GEMM: bit0 BK 48, bit1 XCD order, bit2 LDS-DMA ring, bit3 16x16 MFMA
-  int wino_prio = 257;     // Conv2 fused GEMM bits: 0 s_setprio, 1 NT V stores, 2 scalar (1-channel) input
-                           // transform, 8 interleaved fold; 4-7 probes
-  int wino_split = 1;      // Conv2 fused GEMM tail split: 0 off, 1 auto (fill the last round's idle CUs), 2-7 force
-  int wino_sk = 0;         // Conv2 fused GEMM stream-K: 0 off, 1-2 = that many workgroups per CU over equal
-                           // ranges of (point tile, transform point) work (supersedes the tail split)
-  int fold_scalar = 0;     // Winograd output folds as scalar v_fma_f32 instead of packed v_pk_fma_f32: bit0 Conv1, bit1 Conv2
   int chunk1 = 0;          // images per stage-1 launch (0 = whole batch up to the 32-bit index chunk)
   int chunk2 = 0;          // images per stage-2 launch
-  int fuse_pool1 = 0;      // pool1 fused into Conv2's Winograd input transform (measured slower: off)
   int force_vec4 = -1;     // conv_mfma tile variant override for Cg % 4 == 0 convs (-1 = heuristic)
   int force_scalar = -1;   // conv_mfma tile variant override for scalar-gather convs
   int bf16_glds = 2;       // bf16 full model: 0 register-staged, 2 / 3 LDS-DMA ring slots
@@ -40,15 +29,12 @@ struct Knobs {
   int bf16_fc = 0;         // bf16 FC layers: 1 = activation-streaming kernel (fc_bf16; measured slower than the
                            // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
-  int conv1_occ = 3;       // cap on Conv1 Winograd GEMM workgroups per CU by LDS padding (the 16x16 kernel's
-                           // launch bounds allow 3: 168 VGPRs, no spills); 3 leaves room for the other
-                           // lane's kernels (+1.5 % with free-running lanes),
-  int conv2_occ = 0;       // ... and Conv2's (natural 2): leaves room for a concurrent lane's kernels
+  int conv1_occ = 0;       // cap on the Conv1 Winograd GEMM's workgroups per CU (LDS padding; 0 = none: 4)
+  int conv2_occ = 0;       // ... and Conv2's (0 = none: 2); a cap leaves room for a concurrent lane's kernels
 };
 
-// Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CONV1_WINO_CFG,
-// ANX_CONV1_WINO_PROBE, ANX_WINO_FUSED_CFG, ANX_WINO_PRIO, ANX_FOLD_SCALAR, ANX_CHUNK1, ANX_CHUNK2,
-// ANX_FUSE_POOL1, ANX_BF16_GLDS, ANX_BF16_BIG when set.
+// Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
+// ANX_BF16_GLDS, ANX_BF16_BIG, ANX_BF16_FC, ANX_CONV1_OCC, ANX_CONV2_OCC when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

@@ -91,46 +91,19 @@ hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, 
 struct WinoPlan {
   int N, Hq, Wq, C, K, groups;
   int Ho, Wo, ty, tx, P;  // output dims, 3x3 tiles per column/row, total tiles
-  ConvPlan gemm;          // the 49*groups batched GEMMs as one grouped 1x1 conv
 };
+// 96 or 48 channels per group and a multiple of 64 filters per group (the fused GEMM's shapes)
 bool wino_eligible(int F, int S, int C, int K, int groups);
 WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups);
-size_t wino_v_floats(const WinoPlan& w);
-size_t wino_m_floats(const WinoPlan& w);
-// U = G g G^T in fp64, laid out as KCFF weights of the grouped 1x1 GEMM ([49*K][C/g]).
+size_t wino_v_floats(const WinoPlan& w);  // V workspace [P][49][C]
+size_t wino_u_floats(const WinoPlan& w);  // transformed weights [49][K][C/groups]
+// U[(ab*groups + g)*Kg + k][c] = (G g G^T)[a][b] in fp64, rounded once.
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
-// nt: non-temporal V stores (Knobs::wino_prio bit1, A/B).
-// nt: non-temporal V stores (A/B); scalar: one channel per thread instead of two (A/B)
-hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s, bool nt = false, bool scalar = false);
-// Pool1 (3x3 / 2, post-ReLU conv1 input) fused into the input transform: V of the zero-bordered
-// pool1 window without materialising it. Window row r = pool1 row r + q_lo; pool1 rows outside
-// [p1_lo, p1_hi) and columns outside [0, Wp) are the border; conv1 rows [c1_lo, c1_lo + H1) are in
-// `c1` ([N][H1][W1][C]). Bit-identical to maxpool + wino_input.
-struct WinoPoolGeom {
-  int H1, W1, Wp, pad, q_lo, p1_lo, p1_hi, c1_lo;
-};
-hipError_t wino_input_pool(const WinoPlan& w, const float* c1, const WinoPoolGeom& pg, float* V, hipStream_t s);
-hipError_t wino_output(const WinoPlan& w, const float* Mt, const float* bias, float* y, bool relu, hipStream_t s);
-// Batched GEMM + output transform in one kernel (M stays in registers); U packed as for w.gemm.
-// Kernel choice from the engine's knobs: wino_cfg bit0 = K-slice 48 instead of 32, bit1 = XCD-aware
-// block order, bit2 = LDS-DMA ring, bit3 = 16x16 MFMA (default 7; measured at 300 images: ring
-// +17 %, BK 48 +3 %, XCD order +1 %); wino_prio bit0 s_setprio around the MFMA slices, bit8
-// interleaved output fold (default 257), bits 4-7 cost probes (wrong results): no fold / no refills
-// / no barrier / no stores; fold_scalar: v_fma_f32 instead of v_pk_fma_f32 folds.
-// split_ws (wino_split_ws_floats() floats, or nullptr = never split): when the launch's last round of
-// workgroups would leave CUs idle (wave quantization: 648 workgroups on 512 slots at 128 images),
-// the whole rounds run as usual and the tail point tiles run their 49 transform points split
-// nsplit ways (Knobs::wino_split: 0 off, 1 auto by a cost model, 2-7 forced where the workspace
-// allows), writing raw folds to split_ws, then a reduce adds them in slice order with bias / ReLU.
-// Deterministic for a given launch size; the summation order (hence the last bits) depends on
-// whether a tile was split.
-hipError_t wino_fused(const WinoPlan& w, const float* V, const float* U, const float* bias, float* y, bool relu,
-                      hipStream_t s, const Knobs& k, float* split_ws = nullptr);
-struct WinoSplit {
-  int pt_full, tail_pt, nsplit;  // whole point tiles, split tail tiles, slices (1: no split)
-};
-WinoSplit plan_wino_split(const WinoPlan& w, const Knobs& k);
-size_t wino_split_ws_floats();  // workspace: two rounds of workgroups (2 per CU) x 9 x 64 x 64 fold floats
+hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s);
+// Fused batched GEMM + output transform + bias + optional ReLU into `out` (wino_gemm.hpp); Knobs:
+// conv2_occ (workgroups per CU cap).
+hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,
+                      hipStream_t s, const Knobs& k);
 
 // Conv1 (stride 4, C = 3, 8 < F <= 12, no padding) as Winograd F(3x3,3x3) on the polyphase image
 // (conv1_wino.hip): 48 polyphase channels, 3x3 output tiles, 25 transform points.
@@ -143,14 +116,20 @@ Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F);
 size_t conv1_wino_v_floats(const Conv1WinoPlan& w);  // V workspace [P][25][48]
 size_t conv1_wino_u_floats(int K);                   // transformed weights [25][K][48]
 void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u);
-// GEMM configuration ids 0..4 (Knobs::conv1_cfg; 4 = default).
-bool conv1_wino_cfg_valid(int cfg);
-// x: [N, Hin, W, 3] image rows; writes conv1 (+bias, optional ReLU) through `out`. Knobs: conv1_cfg;
-// conv1_probe bit4 s_setprio around the MFMA slices (default 16), bit5 NT V stores, bit6 interleaved
-// fold, bits 0-3 cost probes (wrong results): no fold / no refills / no barrier / no stores;
-// fold_scalar.
+// x: [N, Hin, W, 3] image rows; writes conv1 (+bias, optional ReLU) through `out`. Knobs: conv1_occ.
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
                       bool relu, hipStream_t s, const Knobs& k);
+
+// The fused Winograd GEMM + output transform (wino_gemm.hip). V [P][points][C], U [points][K][C/groups]
+// (row = filter), bias + optional ReLU, NHWC store through `out` (Cb, c_off multiples of 4). P tiles of
+// 3x3 outputs on a ty x tx grid per image, Ho x Wo outputs. occ: workgroups-per-CU cap (0 = none).
+// abl / cfg: 0 / -1 = the production kernel; other ablations and configurations exist only in the
+// anx_wgemm A/B build.
+hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
+                           int Wo, int C, int K, int groups, bool relu, hipStream_t s, int occ = 0, int abl = 0,
+                           int cfg = -1);
+hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
+                           int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
 
 // Dynamic LDS bytes that cap a kernel at `wgs` workgroups per CU (160 KiB LDS per CU): the larger of
 // `natural` and just over 160 KiB / (wgs + 1). wgs <= 0: `natural`.

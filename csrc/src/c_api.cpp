@@ -427,7 +427,7 @@ int anx_default_knob(const char* name, int* value) {
 }
 
 int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, int K, int F, const float* bias,
-                   float* y, int relu, int fold_scalar, void* stream) {
+                   float* y, int relu, void* stream) {
   return guarded("anx_conv1_wino", [&] {
     if (!anx::hip::conv1_wino_eligible(3, K, F, 4, 0, 1)) return fail("anx_conv1_wino: shape not eligible");
     const auto w = anx::hip::make_conv1_wino_plan(N, Hin, W, K, F);
@@ -441,12 +441,9 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
       return fail("anx_conv1_wino: hipMalloc");
     }
     hipError_t e = hipMemcpy(du, u.data(), u.size() * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) {
-      anx::Knobs kn = anx::default_knobs();
-      kn.fold_scalar = fold_scalar != 0;
+    if (e == hipSuccess)
       e = anx::hip::conv1_wino(w, x, dv, du, bias, anx::hip::OutView{y, w.H1, w.W1, K, 0, 0, 0}, relu != 0, S(stream),
-                               kn);
-    }
+                               anx::default_knobs());
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));  // the workspaces are freed below
     (void)hipFree(dv);
     (void)hipFree(du);
@@ -455,33 +452,27 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
 }
 
 int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
-                   const float* bias, float* y, int relu, int wino_cfg, int wino_split, void* stream) {
+                   const float* bias, float* y, int relu, void* stream) {
   return guarded("anx_conv2_wino", [&] {
     if (!anx::hip::wino_eligible(5, 1, C, K, groups)) return fail("anx_conv2_wino: shape not eligible");
     const auto w = anx::hip::make_wino_plan(N, Hq, Wq, C, K, groups);
-    std::vector<float> u, packed;
-    std::vector<int> koff;
+    std::vector<float> u;
     anx::hip::wino_transform_weights_host(w, w_kcff, u);
-    anx::hip::pack_conv_weights_host(w.gemm, u.data(), packed, koff);
-    float *dv = nullptr, *du = nullptr, *ws = nullptr;
+    float *dv = nullptr, *du = nullptr;
     if (hipMalloc(reinterpret_cast<void**>(&dv), std::max<size_t>(anx::hip::wino_v_floats(w), 1) * 4) != hipSuccess)
       return fail("anx_conv2_wino: hipMalloc");
-    if (hipMalloc(reinterpret_cast<void**>(&du), packed.size() * 4) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&ws), anx::hip::wino_split_ws_floats() * 4) != hipSuccess) {
+    if (hipMalloc(reinterpret_cast<void**>(&du), u.size() * 4) != hipSuccess) {
       (void)hipFree(dv);
-      (void)hipFree(du);
       return fail("anx_conv2_wino: hipMalloc");
     }
-    hipError_t e = hipMemcpy(du, packed.data(), packed.size() * 4, hipMemcpyHostToDevice);
-    anx::Knobs kn = anx::default_knobs();
-    if (wino_cfg >= 0) kn.wino_cfg = wino_cfg;
-    if (wino_split >= 0) kn.wino_split = wino_split;
+    hipError_t e = hipMemcpy(du, u.data(), u.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = anx::hip::wino_input(w, x, dv, S(stream));
-    if (e == hipSuccess) e = anx::hip::wino_fused(w, dv, du, bias, y, relu != 0, S(stream), kn, ws);
+    if (e == hipSuccess)
+      e = anx::hip::wino_conv2(w, dv, du, bias, anx::hip::OutView{y, w.Ho, w.Wo, K, 0, 0, 0}, relu != 0, S(stream),
+                               anx::default_knobs());
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));  // the workspaces are freed below
     (void)hipFree(dv);
     (void)hipFree(du);
-    (void)hipFree(ws);
     return hip_status(e, "conv2_wino");
   });
 }

@@ -144,6 +144,10 @@ RankInfo rank_info_from_env() {
   r.rank = env_int("ANX_RANK", "RANK", 0);
   r.world = env_int("ANX_WORLD_SIZE", "WORLD_SIZE", 1);
   r.local_rank = env_int("ANX_LOCAL_RANK", "LOCAL_RANK", r.rank);
+  r.local_world = env_int("ANX_LOCAL_WORLD_SIZE", "LOCAL_WORLD_SIZE", r.world);
+  if (r.local_world < 1 || r.local_world > r.world) r.local_world = r.world;
+  r.nnodes = env_int("ANX_NNODES", "GROUP_WORLD_SIZE", (r.world + r.local_world - 1) / r.local_world);
+  if (r.nnodes < 1) r.nnodes = 1;
   r.master_addr = env_str("ANX_MASTER_ADDR", "MASTER_ADDR", "127.0.0.1");
   r.master_port = env_int("ANX_MASTER_PORT", "MASTER_PORT", 29555);
   return r;

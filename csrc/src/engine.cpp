@@ -68,11 +68,13 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
   const size_t per_img = std::max<size_t>(
       {static_cast<size_t>(H) * W * d_.C0, static_cast<size_t>(d_.H1) * d_.W1 * d_.C1,
        static_cast<size_t>(d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1, static_cast<size_t>(d_.H2) * d_.W2 * d_.C2,
-       // Winograd M buffer: 49 transform points x K per 3x3 output tile
-       static_cast<size_t>((d_.H2 + 2) / 3) * ((d_.W2 + 2) / 3) * 49 * d_.C2,
+       // Winograd conv2 V buffer: 49 transform points x C per 3x3 output tile
+       static_cast<size_t>((d_.H2 + 2) / 3) * ((d_.W2 + 2) / 3) * 49 * d_.C1,
        // Winograd conv1 V buffer: 25 points x 48 polyphase channels per 3x3 output tile
        static_cast<size_t>((d_.H1 + 2) / 3) * ((d_.W1 + 2) / 3) * 25 * 48});
-  chunk_ = static_cast<int>(std::min<size_t>(max_batch, ((1UL << 31) - 1) / per_img));
+  // images per launch: every buffer a kernel addresses stays below 2^31 bytes (the Winograd GEMMs
+  // reach their operands through 32-bit buffer offsets)
+  chunk_ = static_cast<int>(std::min<size_t>(max_batch, ((1UL << 31) - 1) / (per_img * sizeof(float))));
   if (chunk_ < 1) throw std::invalid_argument("image too large for 32-bit kernel indexing");
   w1h_ = w.w1;
   w2h_ = w.w2;
@@ -94,15 +96,14 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
     wv1_ = dev_alloc<float>(wv1_cap_);
   }
   if (impl == Impl::Mfma && hip::wino_eligible(b2.conv.F, b2.conv.S, d_.C1, d_.C2, b2.conv.groups)) {
-    // Winograd workspaces for a full-height window of chunk_ images (row tiles need less).
-    // The M buffer (49 x K per tile: 520 MB at 128 images) only exists for the unfused A/B path and
-    // is allocated on its first use; the default fused kernel never materialises M.
+    // Winograd workspace for a full-height window of chunk_ images (row tiles need less)
     const hip::WinoPlan wp = hip::make_wino_plan(chunk_, d_.Hp1 + 2 * b2.conv.P, wq_, d_.C1, d_.C2, b2.conv.groups);
-    if (hip::wino_m_floats(wp) < (1UL << 31)) {
+    if (hip::wino_v_floats(wp) < (1UL << 31)) {
+      std::vector<float> u;
+      hip::wino_transform_weights_host(wp, w.w2.data(), u);
+      u2w_ = dev_upload(u);
       wv_cap_ = hip::wino_v_floats(wp);
-      wm_cap_ = hip::wino_m_floats(wp);
       wv_ = dev_alloc<float>(wv_cap_);
-      wsplit_ = dev_alloc<float>(hip::wino_split_ws_floats());
     }
   }
 }
@@ -111,9 +112,8 @@ BlocksEngine::~BlocksEngine() {
   for (void* p : {static_cast<void*>(w1_), static_cast<void*>(b1d_), static_cast<void*>(w2_),
                   static_cast<void*>(b2d_), static_cast<void*>(w1p_), static_cast<void*>(w2p_),
                   static_cast<void*>(koff1_), static_cast<void*>(koff2_), static_cast<void*>(c1_),
-                  static_cast<void*>(q2_), static_cast<void*>(c2_), static_cast<void*>(u2p_),
-                  static_cast<void*>(ukoff_), static_cast<void*>(wv_), static_cast<void*>(wm_),
-                  static_cast<void*>(u1w_), static_cast<void*>(wv1_), static_cast<void*>(wsplit_)})
+                  static_cast<void*>(q2_), static_cast<void*>(c2_), static_cast<void*>(u2w_),
+                  static_cast<void*>(wv_), static_cast<void*>(u1w_), static_cast<void*>(wv1_)})
     if (p) (void)hipFree(p);
 }
 
@@ -180,41 +180,16 @@ hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStr
   return hipSuccess;
 }
 
-// Conv2 (+ReLU) and Pool2(+LRN) of n images. qc: their conv2 input window; nullptr = pool1 fused
-// into the Winograd input transform, reading the conv1 rows in c1_ (conv1_chunk just wrote them).
+// Conv2 (+ReLU) and Pool2(+LRN) of n images; qc: their conv2 input window.
 hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, float* yc, hipStream_t s) {
   RoctxRange rx("anx conv2+pool2+lrn");
   const ConvSpec& k2 = b2_.conv;
-  const bool wino = impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(k_.conv2_algo, n, t.c2.size(), d_.H2);
-  if (!qc && !wino) return hipErrorInvalidValue;
-  if (wino) {
+  const hip::OutView c2v{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
+  if (impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(k_.conv2_algo, n, t.c2.size(), d_.H2)) {
     const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
-    if (hip::wino_v_floats(w) > wv_cap_ || hip::wino_m_floats(w) > wm_cap_) return hipErrorInvalidValue;
-    if (w.gemm.variant != wino_key_) {
-      std::vector<float> u, packed;
-      std::vector<int> koff;
-      hip::wino_transform_weights_host(w, w2h_.data(), u);
-      hip::pack_conv_weights_host(w.gemm, u.data(), packed, koff);
-      if (u2p_) ANX_TRY(hipFree(u2p_));
-      if (ukoff_) ANX_TRY(hipFree(ukoff_));
-      u2p_ = dev_upload(packed);
-      ukoff_ = dev_upload(koff);
-      wino_key_ = w.gemm.variant;
-    }
-    if (qc) {
-      ANX_TRY(hip::wino_input(w, qc, wv_, s, (k_.wino_prio & 2) != 0, (k_.wino_prio & 4) != 0));
-    } else {
-      const hip::WinoPoolGeom pg{t.c1.size(), d_.W1, d_.Wp1, k2.P, t.q.lo, t.p1.lo, t.p1.hi, t.c1.lo};
-      ANX_TRY(hip::wino_input_pool(w, c1_, pg, wv_, s));
-    }
-    if (k_.conv2_algo == ConvAlgo::WinogradUnfused) {
-      if (!wm_) ANX_TRY(hipMalloc(reinterpret_cast<void**>(&wm_), wm_cap_ * sizeof(float)));
-      ANX_TRY(hip::conv2d_mfma(w.gemm, wv_, u2p_, ukoff_, nullptr, hip::OutView{wm_, 1, 1, w.gemm.K, 0, 0, 0}, false,
-                               s));
-      ANX_TRY(hip::wino_output(w, wm_, b2d_, c2_, true, s));
-    } else {
-      ANX_TRY(hip::wino_fused(w, wv_, u2p_, b2d_, c2_, true, s, k_, wsplit_));
-    }
+    if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
+    ANX_TRY(hip::wino_input(w, qc, wv_, s));
+    ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
   } else if (impl_ == Impl::Mfma) {
     const hip::ConvPlan p =
         hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups, k_.force_vec4, k_.force_scalar);
@@ -229,8 +204,7 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
       koff2_ = dev_upload(koff);
       plan_key2_ = key;
     }
-    ANX_TRY(hip::conv2d_mfma(p, qc, w2p_, koff2_, b2d_, hip::OutView{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0}, true,
-                             s));
+    ANX_TRY(hip::conv2d_mfma(p, qc, w2p_, koff2_, b2d_, c2v, true, s));
   } else {
     ANX_TRY(hip::conv2d_direct(qc, w2_, b2d_, c2_, n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, 0, k2.groups, true,
                                s));
@@ -264,26 +238,8 @@ hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t 
 hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, float* y, hipStream_t s) {
   if (N > max_batch_) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
-  // Pool1 fused into Conv2's Winograd input transform when every chunk runs Winograd Conv2 (the
-  // conv2 window is then never written: no memset, no pool1 pass).
-  const int c1c = k_.chunk1 > 0 ? std::min(chunk_, k_.chunk1) : chunk_;
-  const int c2c = k_.chunk2 > 0 ? std::min(chunk_, k_.chunk2) : chunk_;
-  const int chunk = std::min(c1c, c2c);
-  const int n_min = N % chunk ? std::min(N % chunk, chunk) : std::min(N, chunk);
-  const bool fuse = k_.fuse_pool1 && impl_ == Impl::Mfma && wv_ != nullptr && b1_.pool.F == 3 && b1_.pool.S == 2 &&
-                    k_.conv2_algo != ConvAlgo::WinogradUnfused && use_winograd(k_.conv2_algo, n_min, t.c2.size(), d_.H2);
-  if (!fuse) {
-    ANX_TRY(stage1(x, N, t, s));
-    return stage2(N, t, y, s);
-  }
-  const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
-  const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
-  for (int n0 = 0; n0 < N; n0 += chunk) {
-    const int n = std::min(chunk, N - n0);
-    ANX_TRY(conv1_chunk(x + n0 * in_img, n, t, s));
-    ANX_TRY(conv2_chunk(n, t, nullptr, y + n0 * y_img, s));
-  }
-  return hipSuccess;
+  ANX_TRY(stage1(x, N, t, s));
+  return stage2(N, t, y, s);
 }
 
 hipError_t BlocksEngine::forward(const float* x, int N, float* y, hipStream_t s) {

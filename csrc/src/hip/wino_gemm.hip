@@ -1,0 +1,128 @@
+// Launchers of the fused Winograd GEMM (wino_gemm.hpp) for Conv2 (F(3x3,5x5)) and Conv1 (polyphase
+// F(3x3,3x3)). The production build instantiates one configuration per channel count; the anx_wgemm
+// A/B tool (ANX_WGEMM_ABLATIONS) also instantiates the alternative ring / tile shapes and ablations.
+//
+// Measured at 300 images, each kernel alone (profiles/r03_wgemm_ab.md): 64x64 tiles, BK 48 and a 2-slot
+// ring beat BK 32 x 4 slots and BK 16 x 6 slots (the deeper rings raised MFMA-busy but the chip then
+// held a lower clock); Conv2 623 us (old fused kernel 649, bit-identical output), Conv1 380 us.
+#include "wino_gemm.hpp"
+
+namespace anx::hip {
+namespace {
+
+template <class G, int ABL>
+hipError_t launch(const wg::Args& a0, hipStream_t s, int occ) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wg::gemm_kernel<G, ABL>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  wg::Args a = a0;
+  a.n_ptiles = (a.P + G::BM - 1) / G::BM;
+  if (a.n_ntiles < 1 || a.u_rows < a.n_ntiles * G::BN) return hipErrorInvalidValue;
+  const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
+  wg::gemm_kernel<G, ABL><<<grid, G::NT, occupancy_lds(G::kLdsBytes, occ), s>>>(a);
+  return hipGetLastError();
+}
+
+// Configurations: <points, channels, waves along tiles, waves along filters, K slice, ring slots>
+using C2 = wg::Cfg<49, 96, 2, 2, 48, 2>;    // Conv2: 64 tiles x 64 filters, 48 KiB ring, 2 workgroups per CU
+using C2g = wg::Cfg<49, 48, 2, 2, 48, 2>;   // Conv2 with 2 groups (48 channels per group)
+using C1 = wg::Cfg<25, 48, 2, 1, 48, 2>;    // Conv1: 64 tiles x 32 filters, 2 waves, 4 workgroups per CU
+#ifdef ANX_WGEMM_ABLATIONS
+using C2_32x4 = wg::Cfg<49, 96, 2, 2, 32, 4>;    // 64 KiB ring: 2 slices in flight behind the current one
+using C2_16x6 = wg::Cfg<49, 96, 2, 2, 16, 6>;    // 48 KiB ring
+using C1_16x6w4 = wg::Cfg<25, 48, 4, 1, 16, 6>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
+using C1_16x6w2 = wg::Cfg<25, 48, 2, 1, 16, 6>;  // 64 x 32, 2 waves, 36 KiB ring, 4 per CU
+using C1_48x2w4 = wg::Cfg<25, 48, 4, 1, 48, 2>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
+#endif
+
+template <class G>
+hipError_t launch_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
+  switch (abl) {
+    case 0: return launch<G, 0>(a, s, occ);
+#ifdef ANX_WGEMM_ABLATIONS
+    case 1: return launch<G, 1>(a, s, occ);
+    case 2: return launch<G, 2>(a, s, occ);
+    case 3: return launch<G, 3>(a, s, occ);
+#endif
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
+                           int Wo, int C, int K, int groups, bool relu, hipStream_t s, int occ, int abl, int cfg) {
+  if (groups < 1 || C % groups || K % groups) return hipErrorInvalidValue;
+  const int Cg = C / groups, Kg = K / groups;
+  const long vb = static_cast<long>(P) * 49 * C * 4, ub = static_cast<long>(49) * K * Cg * 4;
+  if ((Cg != 96 && Cg != 48) || Kg % 64 || vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4)
+    return hipErrorInvalidValue;
+  if (P == 0) return hipSuccess;
+  for (int g = 0; g < groups; ++g) {
+    wg::Args a{};
+    a.V = V + g * Cg;
+    a.U = U + static_cast<size_t>(g) * Kg * Cg;
+    a.bias = bias ? bias + g * Kg : nullptr;
+    a.out = out;
+    a.out.c_off += g * Kg;
+    a.P = P;
+    a.ty = ty;
+    a.tx = tx;
+    a.Ho = Ho;
+    a.Wo = Wo;
+    a.n_ntiles = Kg / 64;
+    a.u_rows = K;  // rows (ab*groups + g)*Kg + k: a point's rows of every group
+    a.vct = C;
+    a.vbytes = static_cast<int>(vb - g * Cg * 4);
+    a.ubytes = static_cast<int>(ub - static_cast<long>(g) * Kg * Cg * 4);
+    a.relu = relu ? 1 : 0;
+    hipError_t e = hipErrorInvalidValue;
+    if (Cg == 48)
+      e = cfg < 0 ? launch_abl<C2g>(a, s, occ, abl) : hipErrorInvalidValue;
+    else
+      switch (cfg < 0 ? 0 : cfg) {
+        case 0: e = launch_abl<C2>(a, s, occ, abl); break;
+#ifdef ANX_WGEMM_ABLATIONS
+        case 1: e = launch_abl<C2_32x4>(a, s, occ, abl); break;
+        case 3: e = launch_abl<C2_16x6>(a, s, occ, abl); break;
+#endif
+        default: break;
+      }
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
+                           int Wo, int K, bool relu, hipStream_t s, int occ, int abl, int cfg) {
+  const long vb = static_cast<long>(P) * 25 * 48 * 4, ub = static_cast<long>(25) * K * 48 * 4;
+  if (vb >= (1L << 31) || ub >= (1L << 31) || K % 32 || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
+  if (P == 0) return hipSuccess;
+  wg::Args a{};
+  a.V = V;
+  a.U = U;
+  a.bias = bias;
+  a.out = out;
+  a.P = P;
+  a.ty = ty;
+  a.tx = tx;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.n_ntiles = K / 32;
+  a.u_rows = K;
+  a.vct = 48;
+  a.vbytes = static_cast<int>(vb);
+  a.ubytes = static_cast<int>(ub);
+  a.relu = relu ? 1 : 0;
+  switch (cfg < 0 ? 0 : cfg) {
+    case 0: return launch_abl<C1>(a, s, occ, abl);
+#ifdef ANX_WGEMM_ABLATIONS
+    case 1: return launch_abl<C1_16x6w4>(a, s, occ, abl);
+    case 2: return launch_abl<C1_16x6w2>(a, s, occ, abl);
+    case 3: return launch_abl<C1_48x2w4>(a, s, occ, abl);
+#endif
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace anx::hip

@@ -21,17 +21,9 @@ struct Field {
 
 const Field kFields[] = {
     {"conv1_algo", nullptr, &Knobs::conv1_algo, 0, 2, "ANX_CONV1_ALGO"},
-    {"conv2_algo", nullptr, &Knobs::conv2_algo, 0, 3, "ANX_CONV2_ALGO"},
-    {"conv1_cfg", &Knobs::conv1_cfg, nullptr, 0, 4, "ANX_CONV1_WINO_CFG"},
-    {"conv1_probe", &Knobs::conv1_probe, nullptr, 0, 255, "ANX_CONV1_WINO_PROBE"},
-    {"wino_cfg", &Knobs::wino_cfg, nullptr, 0, 15, "ANX_WINO_FUSED_CFG"},
-    {"wino_prio", &Knobs::wino_prio, nullptr, 0, 1023, "ANX_WINO_PRIO"},
-    {"fold_scalar", &Knobs::fold_scalar, nullptr, 0, 3, "ANX_FOLD_SCALAR"},
-    {"wino_split", &Knobs::wino_split, nullptr, 0, 7, "ANX_WINO_SPLIT"},
-    {"wino_sk", &Knobs::wino_sk, nullptr, 0, 2, "ANX_WINO_SK"},
+    {"conv2_algo", nullptr, &Knobs::conv2_algo, 0, 2, "ANX_CONV2_ALGO"},
     {"chunk1", &Knobs::chunk1, nullptr, 0, 1 << 30, "ANX_CHUNK1"},
     {"chunk2", &Knobs::chunk2, nullptr, 0, 1 << 30, "ANX_CHUNK2"},
-    {"fuse_pool1", &Knobs::fuse_pool1, nullptr, 0, 1, "ANX_FUSE_POOL1"},
     {"force_vec4", &Knobs::force_vec4, nullptr, -1, 255, nullptr},
     {"force_scalar", &Knobs::force_scalar, nullptr, -1, 255, nullptr},
     {"bf16_glds", &Knobs::bf16_glds, nullptr, 0, 3, "ANX_BF16_GLDS"},

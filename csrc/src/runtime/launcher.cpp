@@ -3,7 +3,8 @@
 //
 //   anxrun -np N [--timeout SEC] [--port P] [--] program [args...]
 //
-// Each rank gets ANX_RANK / ANX_LOCAL_RANK / ANX_WORLD_SIZE / ANX_MASTER_ADDR / ANX_MASTER_PORT
+// Each rank gets ANX_RANK / ANX_LOCAL_RANK / ANX_WORLD_SIZE / ANX_LOCAL_WORLD_SIZE / ANX_NNODES /
+// ANX_MASTER_ADDR / ANX_MASTER_PORT
 // (rendezvous on 127.0.0.1). Ranks bind GPU `local_rank % device_count` themselves — the binding
 // the reference documents but never calls. Fail-stop like MPI_Abort: the first rank
 // that exits nonzero (or dies on a signal) takes the job down; a watchdog timeout exits 124.
@@ -89,6 +90,8 @@ int main(int argc, char** argv) {
       setenv("ANX_RANK", std::to_string(node_rank * np + r).c_str(), 1);
       setenv("ANX_LOCAL_RANK", std::to_string(r).c_str(), 1);
       setenv("ANX_WORLD_SIZE", std::to_string(np * nnodes).c_str(), 1);
+      setenv("ANX_LOCAL_WORLD_SIZE", std::to_string(np).c_str(), 1);  // ranks on this node
+      setenv("ANX_NNODES", std::to_string(nnodes).c_str(), 1);
       setenv("ANX_MASTER_ADDR", master.c_str(), 1);
       setenv("ANX_MASTER_PORT", std::to_string(port).c_str(), 1);
       execvp(argv[i], argv + i);

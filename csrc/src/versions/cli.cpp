@@ -643,6 +643,20 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
   return 0;
 }
 
+// V5 transport for this rank (see run_v5): "auto" = RCCL when every rank of this node has its own GPU
+// or the job spans nodes, else peer. Throws for a combination that cannot run.
+std::string pick_v5_transport(const std::string& want, const RankInfo& ri, int ndev, bool dry) {
+  const bool shared = !dry && ri.local_world > ndev;  // ranks of this node outnumber its GPUs
+  const std::string tr = want == "auto" ? (shared && ri.nnodes == 1 ? "peer" : "rccl") : want;
+  if (tr != "rccl" && tr != "peer") throw std::runtime_error("--transport must be auto, rccl or peer");
+  if (tr == "peer" && ri.nnodes > 1)
+    throw std::runtime_error("the peer transport (IPC) is single-node: use --transport rccl across nodes");
+  if (tr == "rccl" && shared)
+    throw std::runtime_error("v5 over RCCL needs one GPU per rank on each node (" + std::to_string(ri.local_world) +
+                             " ranks, " + std::to_string(ndev) + " GPUs here; --transport peer shares a GPU)");
+  return tr;
+}
+
 // ------------------------------------------------------------------------------ V5 (device-resident)
 // One transfer schedule per step (anx/schedule.hpp: scatter of images x input rows, pool1 halos
 // inside each row group, gather of output rows), executed by a pluggable transport:
@@ -671,10 +685,9 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
     hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
     if (ndev < 1) throw std::runtime_error("v5 needs a GPU");
   }
-  const std::string tr = s.o.transport == "auto" ? (!dry && np > ndev ? "peer" : "rccl") : s.o.transport;
-  if (tr != "rccl" && tr != "peer") throw std::runtime_error("--transport must be auto, rccl or peer");
-  if (tr == "rccl" && !dry && np > ndev)
-    throw std::runtime_error("v5 over RCCL needs one GPU per rank (use --transport peer to share)");
+  // The transport is chosen per NODE: peer (IPC-mapped buffers, ranks may share a GPU) works only
+  // inside one host; RCCL needs one GPU per rank of this node. Multi-node jobs are RCCL only.
+  const std::string tr = pick_v5_transport(s.o.transport, s.ri, ndev, dry);
   const int dev = dry ? 0 : s.ri.local_rank % ndev;
   std::unique_ptr<Transport> x = tr == "rccl" ? make_rccl_transport(c, dev, rank) : make_peer_transport(c, dev, rank);
   constexpr int kB = static_cast<int>(BufId::kCount);

@@ -94,8 +94,8 @@ int main(int argc, char** argv) {
     if (wino) {
       wp = hip::make_wino_plan(N, Hp, Wp, L.C, L.K, L.groups);
       std::vector<float> u;
-      hip::wino_transform_weights_host(wp, hw.data(), u);
-      hip::pack_conv_weights_host(wp.gemm, u.data(), pk, ko);
+      hip::wino_transform_weights_host(wp, hw.data(), pk);  // U [49][K][C/groups]
+      ko.assign(1, 0);
       ck(hipMalloc(&dv, hip::wino_v_floats(wp) * 4), "malloc");
     } else {
       hip::pack_conv_weights_host(p, hw.data(), pk, ko);
@@ -107,7 +107,8 @@ int main(int argc, char** argv) {
     auto run = [&]() {
       if (wino) {
         ck(hip::wino_input(wp, dxp, dv, s), "wino_input");
-        ck(hip::wino_fused(wp, dv, dpk, db, dy, false, s, default_knobs()), "wino_fused");
+        ck(hip::wino_conv2(wp, dv, dpk, db, hip::OutView{dy, Ho, Wo, L.K, 0, 0, 0}, false, s, default_knobs()),
+           "wino_conv2");
       } else {
         ck(hip::conv2d_mfma(p, dxp, dpk, dko, db, hip::OutView{dy, Ho, Wo, L.K, 0, 0, 0}, false, s), "mfma");
       }

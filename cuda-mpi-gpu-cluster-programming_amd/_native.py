@@ -88,8 +88,8 @@ _SIGS = {
     "anx_maxpool_lrn": (_I, [_P, _P] + [_I] * 6 + [_I, _F, _F, _F, _I, _P]),
     "anx_conv_plan": (_I, [_I] * 8 + [C.POINTER(_I), C.POINTER(_SZ), C.POINTER(_SZ)]),
     "anx_conv_pack": (_I, [C.POINTER(_I), _P, _P, _P]),
-    "anx_conv1_wino": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P, _I, _I, _P]),
-    "anx_conv2_wino": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _I, _I, _P]),
+    "anx_conv1_wino": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P]),
+    "anx_conv2_wino": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P]),
     "anx_engine_set_knob": (_I, [_P, C.c_char_p, _I]),
     "anx_engine_get_knob": (_I, [_P, C.c_char_p, C.POINTER(_I)]),
     "anx_full_set_knob": (_I, [_P, C.c_char_p, _I]),

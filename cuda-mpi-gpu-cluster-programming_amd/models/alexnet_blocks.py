@@ -65,11 +65,6 @@ class AlexNetBlocks:
         self.impl = impl
         # kernel knobs of this model's engines (anx.utils.tuning): applied at every engine creation
         self.knobs = {k: knob_value(k, v) for k, v in (knobs or {}).items()}
-        if lanes > 1:
-            # concurrent lanes already fill the CUs a lane's last round leaves idle; the Conv2 tail
-            # split (planned per launch as if the GPU were free) measured slower there: 183k vs 192k
-            # img/s at 2 x 64 images, against +3 % for one lane of 256 (profiles/r02_ab_wino_split.txt)
-            self.knobs.setdefault("wino_split", 0)
         self._engine = None
         self._cap = 0
         self._ensure(max_batch)

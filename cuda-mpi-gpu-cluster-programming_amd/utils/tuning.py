@@ -6,11 +6,12 @@ Names and values:
 
 * ``conv2_algo``: Conv2 (5x5, stride 1) on the MFMA path — ``auto`` (Winograd F(3x3,5x5) when
   eligible and the launch exceeds 8 images), ``direct`` (implicit GEMM; bit-identical across any row
-  decomposition), ``winograd``, ``winograd_unfused`` (separate batched GEMM + output transform; A/B).
+  decomposition), ``winograd``.
 * ``conv1_algo``: Conv1 (11x11, stride 4) — ``auto``/``winograd`` (polyphase Winograd F(3x3,3x3)) or
   ``direct``.
-* integer knobs: ``conv1_cfg``, ``conv1_probe``, ``wino_cfg``, ``wino_prio``, ``fold_scalar``,
-  ``chunk1``, ``chunk2``, ``fuse_pool1``, ``force_vec4``, ``force_scalar``, ``bf16_glds``.
+* integer knobs: ``chunk1``, ``chunk2`` (images per launch), ``conv1_occ``, ``conv2_occ`` (Winograd
+  GEMM workgroups-per-CU caps), ``force_vec4``, ``force_scalar`` (direct GEMM tiles), and the bf16
+  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``.
 """
 from __future__ import annotations
 
@@ -18,10 +19,9 @@ import ctypes as C
 
 from .. import _native as nat
 
-ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd_unfused": 3}
-KNOBS = ("conv1_algo", "conv2_algo", "conv1_cfg", "conv1_probe", "wino_cfg", "wino_prio", "wino_split", "wino_sk", "fold_scalar",
-         "chunk1", "chunk2", "fuse_pool1", "force_vec4", "force_scalar", "bf16_glds", "bf16_big", "bf16_lrn_tile", "bf16_fc",
-         "conv1_occ", "conv2_occ")
+ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
+KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
+         "bf16_lrn_tile", "bf16_fc", "conv1_occ", "conv2_occ")
 
 
 def knob_value(name: str, value) -> int:
@@ -29,7 +29,7 @@ def knob_value(name: str, value) -> int:
     if name not in KNOBS:
         raise ValueError(f"unknown knob {name!r}; known: {', '.join(KNOBS)}")
     if name.endswith("_algo") and isinstance(value, str):
-        if value not in ALGOS or (name == "conv1_algo" and value == "winograd_unfused"):
+        if value not in ALGOS:
             raise ValueError(f"{name} must be one of {sorted(ALGOS)}")
         return ALGOS[value]
     return int(value)

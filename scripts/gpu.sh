@@ -44,7 +44,7 @@ for s in "$@"; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 $BARGS ;;
     sweep) run sweep 600 python tools/sweep_batch.py --batches ${SWEEP:-64,128,256,300,600} --rounds 3 --iters 10 ;;
-    ab) run ab 900 python tools/ab_variants.py --arms "${AB_ARMS:-|fold_scalar=1}" --batch "${AB_BATCH:-300}" \
+    ab) run ab 900 python tools/ab_variants.py --arms "${AB_ARMS:-|conv1_occ=3}" --batch "${AB_BATCH:-300}" \
           --lanes "${AB_LANES:-1}" --rounds "${AB_ROUNDS:-5}" ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 10 --warmup 3 $BARGS ;;
     pmc)

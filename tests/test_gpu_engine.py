@@ -231,22 +231,21 @@ def test_conv1_wino_kernel_vs_torch(cuda, shape):
     H1, W1 = (H - F) // 4 + 1, (W - F) // 4 + 1
     y = torch.full((N, H1, W1, K), float("nan"), device=cuda)
     nat.call("anx_conv1_wino", x.data_ptr(), N, H, W, w.contiguous().data_ptr(), K, F, b.data_ptr(), y.data_ptr(), 0,
-             0, nat.stream_ptr(cuda))
+             nat.stream_ptr(cuda))
     ref = conv2d_nhwc(x.double(), w.to(cuda).double(), b.double(), 4, 0)
     torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("fold_scalar", [0, 1])
-def test_conv1_wino_ring_configs(cuda, cfg, fold_scalar):
-    """Every Conv1 GEMM configuration (32x32 MFMA: BK 48 x 2 slots, BK 16 x 4/6/8; 16x16 MFMA) and
-    both fold forms (packed / scalar FMAs) give the same Blocks 1-2 output, bitwise across the folds."""
+@pytest.mark.parametrize("occ1,occ2", [(0, 0), (2, 1), (3, 1)])
+def test_winograd_gemm_occupancy_caps_bitwise(cuda, occ1, occ2):
+    """The Winograd GEMMs' workgroups-per-CU caps (conv1_occ / conv2_occ: LDS padding) change only
+    where workgroups run, never what they compute: outputs are bit-identical to the uncapped run."""
     x = init_input(9, "rand", seed=5).to(cuda)
-    knobs = {**WINO1, "conv1_cfg": cfg, "fold_scalar": fold_scalar}
-    m = AlexNetBlocks(device=cuda, init="rand", seed=5, max_batch=9, knobs=knobs)
-    y = m(x)
-    assert m.get_knob("conv1_cfg") == cfg and m.get_knob("fold_scalar") == fold_scalar
-    m.set_knob("fold_scalar", 1 - fold_scalar)
+    m = AlexNetBlocks(device=cuda, init="rand", seed=5, max_batch=9, knobs={**WINO1, **WINO2})
+    y = m(x).clone()
+    m.set_knob("conv1_occ", occ1)
+    m.set_knob("conv2_occ", occ2)
+    assert m.get_knob("conv1_occ") == occ1 and m.get_knob("conv2_occ") == occ2
     assert torch.equal(m(x), y)
     ref = blocks_forward(x.cpu(), m.weights, m.b1, m.b2)
     torch.testing.assert_close(y.cpu().double(), ref, rtol=2e-5, atol=2e-6)
@@ -265,8 +264,8 @@ def test_knobs_are_per_engine(cuda):
     with pytest.raises(ValueError):
         a.set_knob("no_such_knob", 1)
     with pytest.raises(nat.NativeError):
-        a.set_knob("wino_cfg", 99)
-    assert a.get_knob("wino_cfg") == 7
+        a.set_knob("conv1_occ", 99)
+    assert a.get_knob("conv1_occ") == 0
 
 
 @pytest.mark.parametrize("N", [1, 7, 128])
@@ -310,68 +309,38 @@ def test_conv1_winograd_golden(cuda, mode, gold):
     assert y.flatten()[:5].tolist() == pytest.approx(gold, abs=2e-4)
 
 
-@pytest.mark.parametrize("cfg", [1, 5, 7, 12, 13, 14, 15])  # register ring / LDS-DMA 32x32 / 16x16 64x128, 64x64; +-XCD
-@pytest.mark.parametrize("groups2", [1, 2])
-def test_winograd_fused_configs(cuda, cfg, groups2):
-    m = AlexNetBlocks(device=cuda, init="rand", seed=80 + cfg, max_batch=9, groups2=groups2,
-                      knobs={**WINO2, "wino_cfg": cfg})
-    x = init_input(9, "rand", seed=80 + cfg)
+@pytest.mark.parametrize("N,groups2", [(9, 1), (9, 2), (300, 1), (130, 2)])
+def test_winograd_conv2_gemm_sizes(cuda, N, groups2):
+    """The fused Conv2 GEMM (64-tile x 64-filter workgroups, XCD-ordered grid with empty slots) at
+    ragged tile counts, both group counts (96 / 48 channels per group), against the fp64 oracle."""
+    m = AlexNetBlocks(device=cuda, init="rand", seed=80 + N, max_batch=N, groups2=groups2, knobs=WINO2)
+    x = init_input(N, "rand", seed=80 + N)
     y = m(x.to(cuda)).cpu().double()
-    torch.testing.assert_close(y, blocks_forward(x, m.weights, m.b1, m.b2), rtol=2e-5, atol=2e-6)
+    idx = torch.arange(N) if N <= 9 else torch.tensor([0, 1, 63, 64, N // 2, N - 1])
+    torch.testing.assert_close(y[idx], blocks_forward(x[idx], m.weights, m.b1, m.b2), rtol=2e-5, atol=2e-6)
 
 
-@pytest.mark.parametrize("prio", [1, 257])  # the plain and the interleaved-fold LDS-DMA kernel
-def test_winograd_scalar_fold_bitwise(cuda, prio):
-    """Scalar (v_fma_f32) and packed (v_pk_fma_f32) Conv2 output folds compute the same FMAs."""
-    x = init_input(20, "rand", seed=81).to(cuda)
-    m = AlexNetBlocks(device=cuda, init="rand", seed=81, max_batch=20, knobs={**WINO2, "wino_prio": prio})
-    y = m(x).clone()
-    m.set_knob("fold_scalar", 2)
-    assert torch.equal(m(x), y)
-
-
-
-
-@pytest.mark.parametrize("N", [9, 20])
-def test_fused_pool1_winograd_input_bitwise(cuda, N):
-    """Pool1 fused into Conv2's Winograd input transform == maxpool + window + transform, bit for bit
-    (whole images and overlap row tiles), and both match the fp64 oracle."""
-    m = AlexNetBlocks(device=cuda, init="rand", seed=90 + N, max_batch=N)
-    x = init_input(N, "rand", seed=N).to(cuda)
-    fuse_pool1 = lambda on: m.set_knob("fuse_pool1", on)  # noqa: E731
-    fuse_pool1(0)
-    ref = m(x).clone()
-    fuse_pool1(1)
-    got = m(x)
-    torch.cuda.synchronize()
-    assert torch.equal(got, ref)
-    oracle = blocks_forward(x.cpu(), m.weights, m.b1, m.b2).float()
-    assert (got.cpu() - oracle).abs().max().item() <= 1e-4 * oracle.abs().max().item()
-    for np_ in (2, 3):
-        plan = make_plan(227, 227, np_, OVERLAP)
-        for t in plan.tiles:
-            if t.out.empty:
-                continue
-            xs = x[:, t.inp.lo:t.inp.hi].contiguous()
-            fuse_pool1(0)
-            a = m.tile_forward(xs, t).clone()
-            fuse_pool1(1)
-            b = m.tile_forward(xs, t)
-            torch.cuda.synchronize()
-            assert torch.equal(a, b)
+def test_engine_batch_above_launch_chunk(cuda):
+    """Above ~1239 images the engine splits a forward into launches whose buffers stay below 2^31
+    bytes (the Winograd GEMMs address their operands through 32-bit buffer offsets)."""
+    N = 1300
+    m = AlexNetBlocks(device=cuda, init="rand", seed=44, max_batch=N)
+    x = init_input(N, "rand", seed=44)
+    y = m(x.to(cuda))
+    idx = torch.tensor([0, 1238, 1239, N - 1])
+    ref = blocks_forward(x[idx], m.weights, m.b1, m.b2)
+    torch.testing.assert_close(y[idx.to(cuda)].cpu().double(), ref, rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.parametrize("lanes,N", [(2, 150), (3, 200), (2, 100)])
 def test_stream_lanes_bit_identical(cuda, lanes, N):
     """lanes > 1 splits the batch over concurrent HIP streams (one engine each): every image's output
     is bit-identical to the one-lane forward (same kernels per image), eager and under graph capture;
-    below lanes * LANE_MIN images the forward stays on one stream. The Conv2 tail split is off: it
-    depends on the launch size (which tiles are split changes their summation order), see
-    test_winograd_tail_split_close_to_unsplit."""
+    below lanes * LANE_MIN images the forward stays on one stream."""
     from anx.models.alexnet_blocks import LANE_MIN
     x = (init_input(N, "rand", seed=13)).to(cuda)
-    one = AlexNetBlocks(device=cuda, init="rand", seed=13, max_batch=N, knobs={"wino_split": 0})
-    many = AlexNetBlocks(one.weights, device=cuda, max_batch=N, lanes=lanes, knobs={"wino_split": 0})
+    one = AlexNetBlocks(device=cuda, init="rand", seed=13, max_batch=N)
+    many = AlexNetBlocks(one.weights, device=cuda, max_batch=N, lanes=lanes)
     assert len(many._lanes) == lanes - 1
     ref = one(x).clone()
     y = torch.full_like(ref, float("nan"))
@@ -396,54 +365,14 @@ def test_stream_lanes_bit_identical(cuda, lanes, N):
     assert N >= lanes * LANE_MIN or torch.equal(many(x), ref2)
 
 
-@pytest.mark.parametrize("N", [64, 128, 256])
-def test_winograd_tail_split_close_to_unsplit(cuda, N):
-    """The Conv2 tail split (plan_wino_split: the point tiles of the last, partial round of
-    workgroups run their 49 transform points split S ways; S = 2 / 3 / 7 at 64 / 128 / 256 images)
-    against the unsplit launch and the fp64 oracle: only the split tiles' summation order differs.
-    The split is deterministic: a second forward is bitwise equal."""
-    x = init_input(N, "rand", seed=21).to(cuda)
-    m = AlexNetBlocks(device=cuda, init="rand", seed=21, max_batch=N)
-    assert m.get_knob("wino_split") == 1
-    y = m(x).clone()
-    assert torch.equal(m(x), y)
-    m.set_knob("wino_split", 0)
-    y0 = m(x)
-    torch.cuda.synchronize()
-    assert not torch.equal(y, y0)  # the split did run
-    assert (y - y0).abs().max().item() <= 1e-6 * y0.abs().max().item()
-    idx = torch.tensor([0, N // 2, N - 1])
-    ref = blocks_forward(x[idx.to(cuda)].cpu(), m.weights, m.b1, m.b2)
-    assert (y[idx.to(cuda)].cpu().double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
-
-
-@pytest.mark.parametrize("N,sk,lanes", [(64, 1, 1), (64, 2, 1), (128, 1, 2), (300, 1, 1), (7, 1, 1)])
-def test_winograd_stream_k_close_to_unsplit(cuda, N, sk, lanes):
-    """Conv2 stream-K (knob wino_sk: equal ranges of (point tile, transform point) work, sk
-    workgroups per CU; split point tiles summed by wino_sk_reduce_kernel) against the data-parallel
-    launch and the fp64 oracle. Only the split tiles' summation order differs, and the schedule is
-    deterministic (a second forward is bitwise equal). N = 7 stays on the direct conv (no Winograd)."""
-    x = init_input(N, "rand", seed=23).to(cuda)
-    m = AlexNetBlocks(device=cuda, init="rand", seed=23, max_batch=N, lanes=lanes, knobs={"wino_sk": sk, "wino_split": 0})
-    y = m(x).clone()
-    assert torch.equal(m(x), y)
-    m.set_knob("wino_sk", 0)
-    y0 = m(x)
-    torch.cuda.synchronize()
-    assert (y - y0).abs().max().item() <= 1e-6 * y0.abs().max().item()
-    idx = torch.tensor([0, N // 2, N - 1])
-    ref = blocks_forward(x[idx.to(cuda)].cpu(), m.weights, m.b1, m.b2)
-    assert (y[idx.to(cuda)].cpu().double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
-
-
 @pytest.mark.parametrize("N", [128, 300])
 def test_forward_async_lanes_bit_identical(cuda, N):
     """forward_async (the bench's dp step: free-running lanes, no per-call join, lanes started half a
     forward apart when idle) computes exactly the one-lane forward, over repeated calls on the same
     buffers, after a device synchronisation (fresh start again), with per-lane hooks in order."""
     x = init_input(N, "rand", seed=31).to(cuda)
-    one = AlexNetBlocks(device=cuda, init="rand", seed=31, max_batch=N, knobs={"wino_split": 0})
-    many = AlexNetBlocks(one.weights, device=cuda, max_batch=N, lanes=2, knobs={"wino_split": 0})
+    one = AlexNetBlocks(device=cuda, init="rand", seed=31, max_batch=N)
+    many = AlexNetBlocks(one.weights, device=cuda, max_batch=N, lanes=2)
     ref = one(x).clone()
     y = torch.full_like(ref, float("nan"))
     seen = []
@@ -459,17 +388,3 @@ def test_forward_async_lanes_bit_identical(cuda, N):
     many.join()
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
-
-
-@pytest.mark.parametrize("knobs", [{"wino_prio": 257 | 512}, {"conv1_probe": 16 | 128}])
-def test_winograd_global_dma_path_bitwise(cuda, knobs):
-    """The Winograd GEMMs load their operands by buffer_load ... lds while V/U fit 31-bit offsets and
-    by global_load_lds above that (or with these A/B bits): both paths give bit-identical outputs."""
-    N = 64
-    x = init_input(N, "rand", seed=41).to(cuda)
-    a = AlexNetBlocks(device=cuda, init="rand", seed=41, max_batch=N, knobs={"wino_split": 0})
-    b = AlexNetBlocks(a.weights, device=cuda, max_batch=N, knobs={"wino_split": 0, **knobs})
-    ya = a(x).clone()
-    yb = b(x)
-    torch.cuda.synchronize()
-    assert torch.equal(ya, yb)

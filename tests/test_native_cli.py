@@ -178,3 +178,34 @@ def test_multinode_emulation(py_serial):
     assert n0.returncode == 0 and n1.returncode == 0, err0
     rec = json.loads(next(l for l in out0.splitlines() if l.startswith("ANX_JSON "))[9:])
     assert rec["np"] == 4 and rec["checksum"] == py_serial
+
+
+def _two_nodes(args, timeout=120):
+    """One 4-rank job as two 2-rank `anxrun` "nodes" on this host (--nnodes 2)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    node = lambda r: subprocess.Popen(  # noqa: E731
+        [ANXRUN, "-np", "2", "--nnodes", "2", "--node-rank", str(r), "--master-addr", "127.0.0.1", "--port",
+         str(port), "--timeout", str(timeout), ANX, *args], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+        env=env)
+    n1, n0 = node(1), node(0)
+    out0, err0 = n0.communicate(timeout=timeout + 60)
+    out1, err1 = n1.communicate(timeout=60)
+    return (n0.returncode, out0, err0), (n1.returncode, out1, err1)
+
+
+def test_v5_multinode_transport_choice():
+    """The V5 transport is chosen per node: across nodes `auto` is RCCL (the peer transport maps IPC
+    buffers and works inside one host only) and an explicit `--transport peer` fails fast with a
+    clear error instead of failing inside hipIpcOpenMemHandle."""
+    base = ["--version", "v5", "--dry-run", "--batch", "4", "--split", "rows", "--decomp", "per_layer"]
+    (rc0, out0, err0), (rc1, out1, _) = _two_nodes(base + ["--transport", "auto"])
+    assert rc0 == 0 and rc1 == 0, err0
+    lines = [l for l in out0.splitlines() + out1.splitlines() if l.startswith("ANX_SCHEDULE ")]
+    assert lines and all(l.split(" ")[1] == "rccl" for l in lines)
+    (rc0, _, err0), (rc1, _, err1) = _two_nodes(base + ["--transport", "peer"], timeout=60)
+    assert rc0 != 0 and rc1 != 0
+    assert "single-node" in err0 + err1

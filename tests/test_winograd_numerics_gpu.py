@@ -28,11 +28,9 @@ def _rel_to_terms(y, x, w, b, S, P, groups=1):
     return rel.max().item()
 
 
-@pytest.mark.parametrize("N,groups,cfg,split", [(12, 1, -1, -1), (12, 2, -1, -1), (9, 1, 15, -1), (9, 1, 1, -1),
-                                               (128, 1, -1, -1), (140, 2, -1, -1), (128, 1, -1, 0)])
-def test_conv2_winograd_randn_he(cuda, N, groups, cfg, split):
-    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights. At 128 / 140
-    images the default launch splits its tail point tiles' 49 points 3 / 2 ways (plan_wino_split)."""
+@pytest.mark.parametrize("N,groups", [(12, 1), (12, 2), (9, 1), (128, 1), (140, 2)])
+def test_conv2_winograd_randn_he(cuda, N, groups):
+    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights."""
     torch.manual_seed(21 + N)
     C, K = 96, 256
     x = torch.randn(N, 31, 31, C, device=cuda)
@@ -44,7 +42,7 @@ def test_conv2_winograd_randn_he(cuda, N, groups, cfg, split):
     b = torch.randn(K, device=cuda) * 0.1
     y = torch.full((N, 27, 27, K), float("nan"), device=cuda)
     nat.call("anx_conv2_wino", x.data_ptr(), N, 31, 31, C, w.contiguous().data_ptr(), K, groups, b.data_ptr(),
-             y.data_ptr(), 0, cfg, split, nat.stream_ptr(cuda))
+             y.data_ptr(), 0, nat.stream_ptr(cuda))
     assert torch.isfinite(y).all()
     assert _rel_to_terms(y, x, w.to(cuda), b, 1, 0, groups) < BOUND_CONV2
 
@@ -58,7 +56,7 @@ def test_conv1_polyphase_winograd_randn_he(cuda, N):
     b = torch.randn(96, device=cuda) * 0.1
     y = torch.full((N, 55, 55, 96), float("nan"), device=cuda)
     nat.call("anx_conv1_wino", x.data_ptr(), N, 227, 227, w.contiguous().data_ptr(), 96, 11, b.data_ptr(),
-             y.data_ptr(), 0, 0, nat.stream_ptr(cuda))
+             y.data_ptr(), 0, nat.stream_ptr(cuda))
     assert torch.isfinite(y).all()
     assert _rel_to_terms(y, x, w.to(cuda), b, 4, 0) < BOUND_CONV1
 
@@ -89,7 +87,6 @@ def test_bench_step_vs_oracle(cuda):
     ref = blocks_forward(x[idx.to(cuda)].cpu(), m.weights, m.b1, m.b2)
     got = y[idx.to(cuda)].cpu().double()
     assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
-    # the second lane's half is bitwise what one engine with a lane's knobs (no Winograd tail split,
-    # the multi-lane default) computes for it alone
-    solo = AlexNetBlocks(init="rand", seed=1234, device=cuda, max_batch=B // 2, knobs={"wino_split": 0})
+    # the second lane's half is bitwise what one engine computes for it alone
+    solo = AlexNetBlocks(init="rand", seed=1234, device=cuda, max_batch=B // 2)
     assert torch.equal(solo(x[B // 2:].contiguous()), y[B // 2:])

@@ -4,12 +4,10 @@ interleaved rounds in ONE process, report median and min).
 
 Every arm is its own model (own engine, own knobs: anx/knobs.hpp), so arms never touch shared state.
 
-usage: tools/ab_variants.py --arms "fold_scalar=0|fold_scalar=1" --batch 300
-       tools/ab_variants.py --arms "|wino_prio=17|wino_prio=33" --batch 300   # cost probes (wrong results)
+usage: tools/ab_variants.py --arms "|conv1_occ=3|conv2_occ=1" --batch 128 --lanes 2
 An arm is ';'-separated name=value pairs over the defaults (empty arm = defaults); '|' separates
 arms. Names: anx.utils.tuning.KNOBS (algorithm knobs take auto/direct/winograd). --lanes L runs
-every arm as L stream lanes. Probe arms (bits 0-3 of conv1_probe, 4-7 of wino_prio) give wrong
-outputs by design: only their times matter; max_abs_diff_vs_arm0 says which arms are exact."""
+every arm as L stream lanes; max_abs_diff_vs_arm0 says which arms are bit-identical to arm 0."""
 import argparse
 import json
 import os
@@ -32,7 +30,7 @@ def parse_arm(spec: str) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--arms", default="|fold_scalar=1")
+    ap.add_argument("--arms", default="|conv1_occ=3")
     ap.add_argument("--batch", type=int, default=300)
     ap.add_argument("--lanes", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=7)
