@@ -35,7 +35,7 @@ from ..utils.init import init_weights
 from ..utils.tuning import apply_knobs, knob_value, read_knob
 
 IMPLS = {"mfma": 0, "direct": 1}
-LANE_MIN = 64  # images per lane below which a forward stays on one stream
+LANE_MIN = 16  # images per lane below which a forward stays on one stream (Winograd needs > 8)
 
 
 def _tile_c(t: TilePlan) -> nat.TileC:
