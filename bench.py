@@ -14,9 +14,12 @@ MI355X". Workloads (--workload):
   halo rows, overlap tiles, RCCL gather, D2H) — the reference's program shape
   (final_project/v4_mpi_cuda/src/main_mpi_cuda.cpp:52-130).
 * ``v5``: BASELINE config "V5 GPU-aware, batch 1024": the same, device-resident, with per-layer
-  tiles and a pool1-halo exchange between the GPUs of a row group (README.md:157-166).
-  --decomp rows (default: the reference's row split over every rank) | hybrid (batch first, rows
-  only below one image per rank) | batch.
+  tiles and a pool1-halo exchange between the GPUs of a row group (README.md:157-166), run by the
+  native V5 runtime (anx/v5.hpp through libanx_dist: halo chunks pipelined against stage1, scatter
+  of the next step and gather of this one on a second stream, weights broadcast device to device).
+  --transport auto | rccl (one GPU per rank) | peer (IPC, ranks may share a GPU); --decomp auto
+  (default for v5: balanced batch groups x 2-way row split) | rows (the reference's row split over
+  every rank) | hybrid (batch first, rows only below one image per rank) | batch.
 
 Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
 bench.py --gpus N``. Rank 0 prints ONE JSON line. After the timed loop it also measures the
@@ -66,7 +69,12 @@ def parse():
     ap.add_argument("--batch-per-gpu", type=int, default=None,
                     help="dp: images per GPU (default 128 for blocks; 256 for full = BASELINE's 2048 over 8 GPUs)")
     ap.add_argument("--batch", type=int, default=None, help="v4/v5: global batch (default 256 / 1024)")
-    ap.add_argument("--decomp", default="rows", choices=["rows", "hybrid", "batch"], help="v4/v5 decomposition")
+    ap.add_argument("--decomp", default=None, choices=["auto", "rows", "hybrid", "batch"],
+                    help="v4/v5 decomposition (default: rows for v4, auto = balanced for v5)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer"], help="v5 device transport")
+    ap.add_argument("--chunks", type=int, default=0, help="v5: halo pipeline chunks per step (0 = auto)")
+    ap.add_argument("--pipeline", type=int, default=-1, choices=[-1, 0, 1],
+                    help="v5: next-step scatter / this-step gather on a second stream (-1 auto)")
     ap.add_argument("--micro", type=int, default=1, help="dp: micro-batches per step for scatter/compute/gather overlap")
     ap.add_argument("--no-prefetch", action="store_true", help="dp: scatter each step's input inside that step only")
     ap.add_argument("--impl", default="mfma", choices=["mfma", "direct"])
@@ -152,17 +160,29 @@ def main():
                               lane_priority=a.lane_priority, knobs=knobs)
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
     else:
-        from anx.parallel.workloads import RowsWorkload
         GB = a.batch or DEFAULT_BATCH[a.workload]
-        # every rank holds an engine sized for the largest share any rank gets
-        from anx.parallel.plan import make_hybrid_plan
-        rw = {"rows": world, "hybrid": 0, "batch": 1}[a.decomp]
-        hp = make_hybrid_plan(227, 227, world, GB, rw)
-        cap = max(1, max(hp.images_of(q).size for q in range(world)))
-        model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=cap, lanes=a.lanes)
-        wl = RowsWorkload(model, GB, a.workload, a.decomp, device=dev)
-        if rank == 0:
-            wl.fill(torch.rand((GB, d.H, d.W, d.C0), device=dev, generator=g) * 0.1)
+        a.decomp = a.decomp or ("auto" if a.workload == "v5" else "rows")
+        if a.workload == "v5" and cuda:
+            # the native V5 runtime: plan, buffers, streams and transport live in C++ (anx/v5.hpp)
+            from anx.parallel.workloads import NativeV5
+            from anx.utils.init import init_weights
+            b1, b2 = anx.config.blocks()
+            wl = NativeV5(GB, init_weights("rand", 1234, b1, b2) if rank == 0 else None, specs=(b1, b2),
+                          decomp=a.decomp, transport=a.transport, chunks=a.chunks, pipeline=a.pipeline, impl=a.impl)
+            wl.fill((torch.rand((GB, d.H, d.W, d.C0), device=dev, generator=g) * 0.1) if rank == 0 else None)
+        else:
+            from anx.parallel.plan import balanced_row_ways, make_hybrid_plan
+            from anx.parallel.workloads import RowsWorkload
+            if a.decomp == "auto":
+                a.decomp = {world: "rows", 1: "batch"}.get(balanced_row_ways(world, GB), "rows")
+            # every rank holds an engine sized for the largest share any rank gets
+            rw = {"rows": world, "hybrid": 0, "batch": 1}[a.decomp]
+            hp = make_hybrid_plan(227, 227, world, GB, rw)
+            cap = max(1, max(hp.images_of(q).size for q in range(world)))
+            model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=cap, lanes=a.lanes)
+            wl = RowsWorkload(model, GB, a.workload, a.decomp, device=dev)
+            if rank == 0:
+                wl.fill(torch.rand((GB, d.H, d.W, d.C0), device=dev, generator=g) * 0.1)
         step = wl.step
         B = GB  # images per step (whole job)
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
@@ -225,6 +245,8 @@ def main():
     for _ in range(a.warmup):
         step()
     sync()
+    if hasattr(wl, "reset_phases"):
+        wl.reset_phases()  # the native runtime times every step: keep only the timed ones
     if world > 1:
         dist.barrier()
     sync()
@@ -286,8 +308,11 @@ def main():
             par, scaling = f"{a.workload}-{a.decomp}{world}", "strong"
             pipeline = ("root pinned host -> H2D -> RCCL scatter -> overlap tiles -> RCCL gather -> D2H"
                         if a.workload == "v4" else
-                        "root device -> RCCL scatter -> stage1 -> RCCL pool1 halos -> stage2 -> RCCL gather")
-            extra = {**wl.describe(), "decomp": a.decomp, "lanes": a.lanes, "phases_ms": phases}
+                        "root device -> scatter -> stage1 (chunks) -> pool1 halo chunks -> stage2 -> gather "
+                        "(native V5 runtime; next scatter / this gather on a second stream)")
+            extra = {**wl.describe(), "decomp": a.decomp, "phases_ms": phases}
+            if a.workload == "v4":
+                extra["lanes"] = a.lanes
         rec = {
             "metric": METRIC,
             "value": round(imgs, 2),

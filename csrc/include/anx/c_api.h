@@ -28,6 +28,7 @@ typedef struct anx_xfer_c {
 } anx_xfer_c;
 
 const char* anx_last_error(void);
+void anx_set_last_error(const char* msg); /* for the companion libraries (libanx_dist) */
 int anx_abi_version(void);
 int anx_device_count(void);
 void anx_default_blocks(anx_block_c* b1, anx_block_c* b2);
@@ -124,6 +125,30 @@ int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_
                    const float* bias, float* y, int relu, void* stream);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
+
+/* ---- V5 multi-GPU runtime (libanx_dist.so: anx/v5.hpp) ----
+ * anx_v5_create is collective over the `world` ranks (TCP bootstrap at master_addr:master_port, then
+ * the transport: RCCL or peer IPC). Weights are read on rank 0 only (others may pass NULL).
+ * mode: 0 overlap, 1 per_layer; row_ways: -1 balanced, 0 batch first, r > 0 groups of r ranks;
+ * transport: "auto" | "rccl" | "peer"; chunks: 0 auto; pipeline: -1 auto, 0 off, 1 on;
+ * peer_sync: "" | "flags" | "notes". */
+int anx_v5_create(void** out, int rank, int world, int local_rank, int local_world, int nnodes,
+                  const char* master_addr, int master_port, double timeout_s, const anx_block_c* b1,
+                  const anx_block_c* b2, int H, int W, const float* w1, const float* bias1, const float* w2,
+                  const float* bias2, int batch, int row_ways, int mode, const char* transport, int chunks,
+                  int pipeline, int poison, int impl, const char* peer_sync);
+int anx_v5_destroy(void* h);
+int anx_v5_set_input(void* h, const float* host_x); /* collective; rank 0's batch, others NULL */
+int anx_v5_step(void* h, int steps);                /* enqueue `steps` steps, no host sync */
+int anx_v5_sync(void* h);
+int anx_v5_output(void* h, float* host_y);          /* rank 0: last step's output */
+/* JSON objects into buf (truncated to cap): per-phase mean ms since the last reset / the layout */
+int anx_v5_phases(void* h, char* buf, size_t cap, int reset);
+int anx_v5_describe(void* h, char* buf, size_t cap);
+/* Record-only schedule, no GPU: rank < 0 -> every transfer of one step (scatter, halo chunks,
+ * gather), else the transfers rank `rank`'s transport issues, in order; one per line. */
+int anx_v5_schedule(int np, const anx_block_c* b1, const anx_block_c* b2, int H, int W, int batch, int row_ways,
+                    int mode, int chunks, int rank, const char* transport, char* buf, size_t cap);
 
 /* ---- CPU reference ---- */
 int anx_cpu_conv2d(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C, int K, int F,

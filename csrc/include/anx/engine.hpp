@@ -61,8 +61,10 @@ class BlocksEngine {
   // Split stages for per-layer halo exchange (V5). stage1 runs conv1+ReLU+pool1 on input rows
   // t.in and writes pool1 rows t.p1 into the conv2 input window (q2_buffer(), window t.q,
   // zero elsewhere). The caller then fills halo rows of the window (q2_row_ptr) and runs stage2.
-  hipError_t stage1(const float* x, int N, const TilePlan& t, hipStream_t s);
-  hipError_t stage2(int N, const TilePlan& t, float* y, hipStream_t s);
+  // [n_lo, n_hi) restricts either stage to those images of the N-image buffers (x / y / window
+  // still address image 0): the V5 runtime pipelines the halo exchange over such image chunks.
+  hipError_t stage1(const float* x, int N, const TilePlan& t, hipStream_t s, int n_lo = 0, int n_hi = -1);
+  hipError_t stage2(int N, const TilePlan& t, float* y, hipStream_t s, int n_lo = 0, int n_hi = -1);
   // Pointer to row `r` (pool1 index space, inside t.q) of image n in the conv2 input window; rows
   // are (Wp1 + 2*P2) * C1 floats with the first P2 pixels of padding, i.e. a full padded row.
   float* q2_row_ptr(const TilePlan& t, int n, int r);

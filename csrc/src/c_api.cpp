@@ -78,6 +78,11 @@ anx_tile_c tile_to_c(const anx::TilePlan& p) {
   return {p.in.lo, p.in.hi, p.c1.lo, p.c1.hi, p.p1.lo, p.p1.hi, p.q.lo, p.q.hi, p.c2.lo, p.c2.hi, p.out.lo, p.out.hi};
 }
 hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+}  // namespace
+
+extern "C" void anx_set_last_error(const char* msg) { g_err = msg ? msg : ""; }
+
+namespace {
 
 // ConvPlan <-> 16 ints
 void plan_to_ints(const anx::hip::ConvPlan& p, int* o) {

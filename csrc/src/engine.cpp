@@ -161,8 +161,9 @@ hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, 
                             s);
 }
 
-hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStream_t s) {
-  if (N > max_batch_) return hipErrorInvalidValue;
+hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStream_t s, int n_lo, int n_hi) {
+  if (n_hi < 0) n_hi = N;
+  if (N > max_batch_ || n_lo < 0 || n_hi > N) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
   // pool1 rows t.p1 are written into the window t.q at p1.lo - q.lo: they must lie inside it
   if (t.p1.lo < t.q.lo || t.p1.hi > t.q.hi) return hipErrorInvalidValue;
@@ -170,8 +171,8 @@ hipError_t BlocksEngine::stage1(const float* x, int N, const TilePlan& t, hipStr
   const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
   const size_t q_img = q2_image_stride_floats(t);
   const int chunk = k_.chunk1 > 0 ? std::min(chunk_, k_.chunk1) : chunk_;
-  for (int n0 = 0; n0 < N; n0 += chunk) {
-    const int n = std::min(chunk, N - n0);
+  for (int n0 = n_lo; n0 < n_hi; n0 += chunk) {
+    const int n = std::min(chunk, n_hi - n0);
     ANX_TRY(conv1_chunk(x + n0 * in_img, n, t, s));
     RoctxRange rx("anx pool1");
     ANX_TRY(hip::maxpool(c1_, n, t.c1.size(), d_.W1, d_.C1, b1_.pool.F, b1_.pool.S,
@@ -222,14 +223,15 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
                       hip::OutView{yc, t.out.size(), d_.Wp2, d_.C2, 0, 0, 0}, s);
 }
 
-hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t s) {
-  if (N > max_batch_) return hipErrorInvalidValue;
+hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t s, int n_lo, int n_hi) {
+  if (n_hi < 0) n_hi = N;
+  if (N > max_batch_ || n_lo < 0 || n_hi > N) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
   const size_t q_img = q2_image_stride_floats(t);
   const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
   const int chunk = k_.chunk2 > 0 ? std::min(chunk_, k_.chunk2) : chunk_;
-  for (int n0 = 0; n0 < N; n0 += chunk) {
-    const int n = std::min(chunk, N - n0);
+  for (int n0 = n_lo; n0 < n_hi; n0 += chunk) {
+    const int n = std::min(chunk, n_hi - n0);
     ANX_TRY(conv2_chunk(n, t, q2_ + n0 * q_img, y + n0 * y_img, s));
   }
   return hipSuccess;

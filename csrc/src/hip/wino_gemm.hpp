@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(G::NT, 2) gemm_kernel(Args a) {
   const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.V), 0, a.vbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
 #endif
-  lds_f32* lds3 = (lds_f32*)(lds);
+  [[maybe_unused]] lds_f32* lds3 = (lds_f32*)(lds);
   // DMA of slice (ab, ks) into ring slot `slot`
   auto issue = [&](int ab, int ks, int slot) {
     if constexpr (kDma) {

@@ -3,10 +3,13 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <array>
+#include <cstdint>
 #include <cstdio>
-#include <tuple>
+#include <cstdlib>
 #include <cstring>
+#include <tuple>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -33,11 +36,31 @@ const char* phase_name(Phase p) {
 }
 
 std::string Transfer::str() const {
-  char b[200];
-  std::snprintf(b, sizeof b, "%s %d->%d w=%zu h=%zu from=%s+%zu/%zu to=%s+%zu/%zu", phase_name(phase), src, dst, width,
-                height, kBufName[static_cast<int>(from.buf)], from.off, from.pitch, kBufName[static_cast<int>(to.buf)],
-                to.off, to.pitch);
+  char b[220], ph[24];
+  if (chunk >= 0) std::snprintf(ph, sizeof ph, "%s#%d", phase_name(phase), chunk);
+  else std::snprintf(ph, sizeof ph, "%s", phase_name(phase));
+  std::snprintf(b, sizeof b, "%s %d->%d w=%zu h=%zu from=%s+%zu/%zu to=%s+%zu/%zu", ph, src, dst, width, height,
+                kBufName[static_cast<int>(from.buf)], from.off, from.pitch, kBufName[static_cast<int>(to.buf)], to.off,
+                to.pitch);
   return b;
+}
+
+std::vector<Transfer> chunk_of(const std::vector<Transfer>& xs, int c, int chunks) {
+  std::vector<Transfer> out;
+  for (size_t i = 0; i < xs.size(); ++i) {
+    const Transfer& x = xs[i];
+    const size_t lo = x.height * c / chunks, hi = x.height * (c + 1) / chunks;
+    if (hi <= lo) continue;
+    Transfer y = x;
+    y.chunk = c;
+    y.seq = static_cast<int>(i);
+    y.img0 = lo;
+    y.from.off += lo * x.from.pitch;
+    y.to.off += lo * x.to.pitch;
+    y.height = hi - lo;
+    out.push_back(y);
+  }
+  return out;
 }
 
 Schedule make_step_schedule(const HybridPlan& p, const StepGeometry& g) {
@@ -88,123 +111,159 @@ struct DeviceBase : Transport {
   void copy2d(char* dst, size_t dpitch, const char* src, size_t spitch, size_t w, size_t h, hipStream_t s) {
     hip_ok(hipMemcpy2DAsync(dst, dpitch, src, spitch, w, h, hipMemcpyDeviceToDevice, s), "hipMemcpy2DAsync");
   }
-  // src == dst transfers (the root's own scatter / gather share) on the compute stream
+  // src == dst transfers (the root's own scatter / gather share) on the given stream; none when the
+  // runtime aliased the two buffers (the root's whole-image tiles live inside X / YFull)
   void local(const std::vector<Transfer>& xs, hipStream_t compute, int par) {
     for (const Transfer& x : xs)
       if (x.src == rank_ && x.dst == rank_) {
         note(x);
-        if (!record_only) copy2d(at(par, x.to), x.to.pitch, at(par, x.from), x.from.pitch, x.width, x.height, compute);
+        if (!record_only && at(par, x.to) != at(par, x.from))
+          copy2d(at(par, x.to), x.to.pitch, at(par, x.from), x.from.pitch, x.width, x.height, compute);
       }
   }
+  static bool remote(const Transfer& x, int r) { return x.src != x.dst && (x.src == r || x.dst == r); }
 };
 
 // ---------------------------------------------------------------------------------------- RCCL
-// Grouped ncclSend/ncclRecv on the communicator's stream, ordered after the compute stream by an
-// event and before it by another: non-contiguous blocks are packed into / unpacked from staging
-// buffers with one 2-D copy each (allocated once per transfer).
+// Grouped ncclSend/ncclRecv on a communicator stream, ordered after the given stream by an event and
+// before it by another: non-contiguous blocks are packed into / unpacked from staging buffers with one
+// 2-D copy each (allocated once per transfer and chunk). Two communicators: scatter / gather / weight
+// broadcast on one, the pool1 halos on the other, so a halo chunk never queues behind the previous
+// step's gather on one communicator stream.
 struct RcclTransport : DeviceBase {
-  HostComm& hc_;
+  HostComm* hc_;
   int device_;
-  std::unique_ptr<DeviceComm> dc_;
-  std::map<std::pair<int, int>, void*> stage_;  // (phase, transfer index) -> contiguous staging
-  RcclTransport(HostComm& c, int device, int rank) : hc_(c), device_(device) { rank_ = rank; }
+  std::unique_ptr<DeviceComm> dc_[2];
+  std::map<std::tuple<int, int, int>, void*> stage_;  // (phase, chunk, transfer) -> contiguous staging
+  RcclTransport(HostComm* c, int device, int rank) : hc_(c), device_(device) { rank_ = rank; }
   ~RcclTransport() override { close(); }
   const char* name() const override { return "rccl"; }
-  void bind(const Schedule&, void* const bufs[2][kB], hipStream_t) override {
-    bind_bufs(bufs);
-    if (!record_only) dc_ = std::make_unique<DeviceComm>(hc_, device_);
+  const char* ordering() const override { return "events"; }
+  bool live() const { return !record_only && hc_ && hc_->size() > 1; }
+  void connect() {
+    if (live() && !dc_[0]) dc_[0] = std::make_unique<DeviceComm>(*hc_, device_);
   }
-  void* staging(int ph, int i, size_t bytes) {
-    void*& p = stage_[{ph, i}];
-    if (!p) hip_ok(hipMalloc(&p, bytes), "hipMalloc staging");
+  void bcast(void* buf, size_t bytes, int root) override {
+    if (!live()) return;
+    connect();
+    dc_[0]->bcast(buf, bytes, root);
+    hip_ok(hipStreamSynchronize(dc_[0]->stream()), "hipStreamSynchronize");
+  }
+  void bind(const Schedule& s, void* const bufs[2][kB], hipStream_t) override {
+    bind_bufs(bufs);
+    if (!live()) return;
+    connect();
+    if (!s.phase[static_cast<int>(Phase::P1Halo)].empty()) dc_[1] = std::make_unique<DeviceComm>(*hc_, device_);
+  }
+  void* staging(Phase ph, const Transfer& x, size_t i) {
+    void*& p = stage_[{static_cast<int>(ph), x.chunk, x.seq >= 0 ? x.seq : static_cast<int>(i)}];
+    if (!p) hip_ok(hipMalloc(&p, x.bytes()), "hipMalloc staging");
     return p;
   }
   void run_phase(Phase ph, const std::vector<Transfer>& xs, hipStream_t compute, int par) override {
     local(xs, compute, par);
     bool any = false;
-    for (const Transfer& x : xs) any |= (x.src != x.dst) && (x.src == rank_ || x.dst == rank_);
+    for (const Transfer& x : xs) any |= remote(x, rank_);
     if (!any) return;
-    hipStream_t cs = record_only ? nullptr : dc_->stream();
-    if (!record_only) dc_->after(compute);
+    DeviceComm* dc = record_only ? nullptr : dc_[ph == Phase::P1Halo && dc_[1] ? 1 : 0].get();
+    hipStream_t cs = dc ? dc->stream() : nullptr;
+    if (dc) dc->after(compute);
     std::vector<std::pair<const Transfer*, void*>> unpack;
-    // pack
-    for (size_t i = 0; i < xs.size(); ++i) {
+    for (size_t i = 0; i < xs.size(); ++i) {  // pack
       const Transfer& x = xs[i];
-      if (x.src != rank_ || x.dst == rank_ || record_only || x.from.pitch == x.width) continue;
-      copy2d(static_cast<char*>(staging(static_cast<int>(ph), static_cast<int>(i), x.bytes())), x.width,
-             at(par, x.from), x.from.pitch, x.width, x.height, cs);
+      if (x.src != rank_ || x.dst == rank_ || !dc || x.from.pitch == x.width) continue;
+      copy2d(static_cast<char*>(staging(ph, x, i)), x.width, at(par, x.from), x.from.pitch, x.width, x.height, cs);
     }
-    if (!record_only) dc_->group_start();
+    if (dc) dc->group_start();
     for (size_t i = 0; i < xs.size(); ++i) {
       const Transfer& x = xs[i];
-      if (x.src == x.dst || (x.src != rank_ && x.dst != rank_)) continue;
+      if (!remote(x, rank_)) continue;
       note(x);
-      if (record_only) continue;
+      if (!dc) continue;
       if (x.src == rank_) {
-        const void* src = x.from.pitch == x.width ? at(par, x.from)
-                                                  : staging(static_cast<int>(ph), static_cast<int>(i), x.bytes());
-        dc_->send(src, x.bytes(), x.dst);
+        dc->send(x.from.pitch == x.width ? at(par, x.from) : staging(ph, x, i), x.bytes(), x.dst);
       } else {
-        void* dst = x.to.pitch == x.width ? static_cast<void*>(at(par, x.to))
-                                          : staging(static_cast<int>(ph), static_cast<int>(i), x.bytes());
+        void* dst = x.to.pitch == x.width ? static_cast<void*>(at(par, x.to)) : staging(ph, x, i);
         if (x.to.pitch != x.width) unpack.push_back({&x, dst});
-        dc_->recv(dst, x.bytes(), x.src);
+        dc->recv(dst, x.bytes(), x.src);
       }
     }
-    if (record_only) return;
-    dc_->group_end();
+    if (!dc) return;
+    dc->group_end();
     for (auto& u : unpack)
       copy2d(at(par, u.first->to), u.first->to.pitch, static_cast<char*>(u.second), u.first->width, u.first->width,
              u.first->height, cs);
-    dc_->before(compute);
+    dc->before(compute);
   }
-  void end_step(hipStream_t) override {}  // receive buffers are reused in comm-stream order
   void close() override {
     for (auto& kv : stage_) (void)hipFree(kv.second);
     stage_.clear();
-    dc_.reset();
+    dc_[1].reset();
+    dc_[0].reset();
   }
 };
 
 // ---------------------------------------------------------------------------------------- peer
 // Every byte moves by ONE hipMemcpy2DAsync from the sender's buffer straight into the receiver's
-// IPC-mapped buffer (Tile / YFull of the step's parity; a per-transfer parity staging slot for the
-// conv2-window halos, unpacked by the receiver on its compute stream). Ordering without host stream
-// syncs: the sender's copy stream waits for its compute stream (event), pushes, records its IPC
-// event for (phase, parity) and posts a 4-byte "sent" note over the host channel; the receiver's
-// host thread takes the note, and its compute stream waits for the sender's IPC event. Receive
-// buffers alternate by step parity, so a push of step k+1 can never land in a buffer step k is
-// still reading: the sender only gets to step k+1 of a phase after data of the receiver's step k
-// (the root's scatter of step k+2 follows its gather of step k, which waits for every rank's
-// stage2 of step k).
+// IPC-mapped buffer (Tile / YFull of the step's parity; for the conv2-window halos a per-transfer,
+// per-parity slot the receiver unpacks into its window on its own stream), issued on the stream the
+// phase is given. Ordering, "flags" mode: every rank owns a word per (sender, channel) in device
+// memory, IPC-mapped by the senders; after its pushes the sender's stream writes the next sequence
+// number of that channel into the receiver's word (hipStreamWriteValue32: after every earlier command
+// of the stream) and the receiver's stream waits for it (hipStreamWaitValue32 >=). Both sides count
+// the same calls, so no host message is exchanged per phase. "notes" mode (fallback): IPC events per
+// (channel, parity) plus a 4-byte host note over the TCP channel.
+// Receive buffers alternate by step parity, so a push of step k+2 can only land after the receiver's
+// step k consumed that parity: the root's scatter of step k+2 follows its gather of step k, which
+// waits for every rank's stage2 of step k (anx/v5.hpp).
 struct PeerTransport : DeviceBase {
-  HostComm& c_;
+  static constexpr int kMaxChunks = 16;
+  static constexpr int kCh = 2 + kMaxChunks;  // scatter, gather, halo chunks
+  HostComm* c_;
   int device_;
-  hipStream_t cs_ = nullptr;
-  hipEvent_t ready_ = nullptr;
-  hipEvent_t drained_ = nullptr;                 // end_step: all pushes issued so far are done
-  hipEvent_t sent_[3][2] = {};                   // own IPC events (phase, parity)
-  std::vector<std::array<std::array<hipEvent_t, 2>, 3>> peer_sent_;  // opened IPC events of every rank
-  std::vector<std::array<void*, kB * 2>> peer_buf_;                  // mapped buffers of every rank
-  std::map<std::tuple<int, int, int>, void*> halo_stage_;            // (src, transfer idx, parity) -> own slot
-  std::vector<std::map<std::tuple<int, int, int>, void*>> peer_halo_; // mapped halo slots of every rank
+  bool flags_ = true;
+  int np_ = 1;
+  std::vector<std::array<void*, kB * 2>> peer_buf_;  // mapped Tile / YFull of every rank
+  std::map<std::pair<int, int>, void*> slot_;        // own halo slots: (transfer, parity)
+  std::map<std::pair<int, int>, void*> peer_slot_;   // receivers' slots this rank pushes into
+  // flags mode
+  uint32_t* flags_mine_ = nullptr;  // [np][kCh], written by the senders
+  std::vector<uint32_t*> flags_of_;  // every rank's flag array, mapped
+  std::vector<std::array<uint32_t, kCh>> sent_seq_, recv_seq_;
+  // notes mode
+  hipEvent_t sent_[kCh][2] = {};
+  std::vector<std::array<std::array<hipEvent_t, 2>, kCh>> peer_sent_;
   std::vector<void*> opened_;
   std::vector<hipEvent_t> opened_ev_;
-  int np_ = 1;
-  const Schedule* sched_ = nullptr;
+  bool connected_ = false;
 
-  PeerTransport(HostComm& c, int device, int rank) : c_(c), device_(device) { rank_ = rank; }
-  ~PeerTransport() override { close(); }
+  PeerTransport(HostComm* c, int device, int rank, const std::string& sync) : c_(c), device_(device) {
+    rank_ = rank;
+    std::string mode = sync;
+    if (mode.empty()) {
+      const char* e = std::getenv("ANX_PEER_SYNC");
+      mode = e ? e : "flags";
+    }
+    if (mode != "flags" && mode != "notes") throw std::runtime_error("peer sync must be flags or notes");
+    flags_ = mode == "flags";
+  }
+  ~PeerTransport() override { release(); }
   const char* name() const override { return "peer"; }
+  const char* ordering() const override { return flags_ ? "flags" : "notes"; }
+  static int channel(Phase ph, int chunk) {
+    if (ph == Phase::Scatter) return 0;
+    if (ph == Phase::Gather) return 1;
+    if (chunk >= kMaxChunks) throw std::runtime_error("peer transport: too many halo chunks");
+    return 2 + (chunk < 0 ? 0 : chunk);
+  }
 
   void* share(void* mine, int r) {  // collective: rank r's allocation mapped here
     hipIpcMemHandle_t h{};
-    const int has = mine ? 1 : 0;
-    int flag = has;
+    int flag = mine ? 1 : 0;
     if (r == rank_ && mine) hip_ok(hipIpcGetMemHandle(&h, mine), "hipIpcGetMemHandle");
-    c_.bcast(&flag, sizeof flag, r);
+    c_->bcast(&flag, sizeof flag, r);
     if (!flag) return nullptr;
-    c_.bcast(&h, sizeof h, r);
+    c_->bcast(&h, sizeof h, r);
     if (r == rank_) return mine;
     void* p = nullptr;
     hip_ok(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
@@ -214,7 +273,7 @@ struct PeerTransport : DeviceBase {
   hipEvent_t share_ev(hipEvent_t mine, int r) {
     hipIpcEventHandle_t h{};
     if (r == rank_) hip_ok(hipIpcGetEventHandle(&h, mine), "hipIpcGetEventHandle");
-    c_.bcast(&h, sizeof h, r);
+    c_->bcast(&h, sizeof h, r);
     if (r == rank_) return mine;
     hipEvent_t e = nullptr;
     hip_ok(hipIpcOpenEventHandle(&e, h), "hipIpcOpenEventHandle");
@@ -222,115 +281,157 @@ struct PeerTransport : DeviceBase {
     return e;
   }
 
-  void bind(const Schedule& sch, void* const bufs[2][kB], hipStream_t) override {
-    sched_ = &sch;
-    bind_bufs(bufs);
-    np_ = c_.size();
-    if (record_only) return;
-    hip_ok(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking), "hipStreamCreate");
-    hip_ok(hipEventCreateWithFlags(&ready_, hipEventDisableTiming), "hipEventCreate");
-    hip_ok(hipEventCreateWithFlags(&drained_, hipEventDisableTiming), "hipEventCreate");
-    for (auto& ph : sent_)
-      for (auto& e : ph)
-        hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventInterprocess), "hipEventCreate IPC");
-    peer_buf_.assign(np_, {});
-    peer_sent_.assign(np_, {});
-    for (int r = 0; r < np_; ++r) {
-      for (int p = 0; p < 2; ++p)
-        for (int b = 0; b < kB; ++b) {
-          // only buffers that are written remotely: Tile (scatter) and YFull (gather)
-          const bool remote = b == static_cast<int>(BufId::Tile) || b == static_cast<int>(BufId::YFull);
-          peer_buf_[r][p * kB + b] = remote ? share(r == rank_ ? buf_[p][b] : nullptr, r) : nullptr;
-        }
-      for (int ph = 0; ph < 3; ++ph)
-        for (int p = 0; p < 2; ++p) peer_sent_[r][ph][p] = share_ev(sent_[ph][p], r);
+  // collective: ordering primitives (flag words or IPC events) of every rank
+  void connect() {
+    if (connected_ || record_only) return;
+    connected_ = true;
+    np_ = c_->size();
+    hip_ok(hipSetDevice(device_), "hipSetDevice");
+    if (flags_) {
+      int can = 0;
+      if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device_) != hipSuccess || !can)
+        throw std::runtime_error("peer transport: device lacks hipStreamWaitValue32 (set ANX_PEER_SYNC=notes)");
+      const size_t bytes = static_cast<size_t>(np_) * kCh * sizeof(uint32_t);
+      hip_ok(hipMalloc(reinterpret_cast<void**>(&flags_mine_), bytes), "hipMalloc flags");
+      hip_ok(hipMemset(flags_mine_, 0, bytes), "hipMemset flags");
+      hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      flags_of_.assign(np_, nullptr);
+      for (int r = 0; r < np_; ++r) flags_of_[r] = static_cast<uint32_t*>(share(r == rank_ ? flags_mine_ : nullptr, r));
+      sent_seq_.assign(np_, {});
+      recv_seq_.assign(np_, {});
+    } else {
+      for (auto& ch : sent_)
+        for (auto& e : ch)
+          hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventInterprocess), "hipEventCreate IPC");
+      peer_sent_.assign(np_, {});
+      for (int r = 0; r < np_; ++r)
+        for (int ch = 0; ch < kCh; ++ch)
+          for (int p = 0; p < 2; ++p) peer_sent_[r][ch][p] = share_ev(sent_[ch][p], r);
     }
-    // halo slots: the receiver owns one per incoming halo transfer and parity
-    peer_halo_.assign(np_, {});
-    const auto& hs = sched_->phase[static_cast<int>(Phase::P1Halo)];
+  }
+
+  void bcast(void* buf, size_t bytes, int root) override {
+    if (record_only || !c_ || c_->size() == 1) return;
+    connect();
+    void* src = share(rank_ == root ? buf : nullptr, root);
+    if (rank_ != root) hip_ok(hipMemcpy(buf, src, bytes, hipMemcpyDeviceToDevice), "hipMemcpy bcast");
+    c_->barrier();  // every rank copied: unmap the root's buffer
+    if (rank_ != root) {
+      hip_ok(hipIpcCloseMemHandle(src), "hipIpcCloseMemHandle");
+      opened_.pop_back();
+    }
+  }
+
+  void bind(const Schedule& sch, void* const bufs[2][kB], hipStream_t) override {
+    bind_bufs(bufs);
+    if (record_only) return;
+    connect();
+    peer_buf_.assign(np_, {});
+    for (int r = 0; r < np_; ++r)
+      for (int p = 0; p < 2; ++p)
+        for (BufId b : {BufId::Tile, BufId::YFull})  // the buffers written remotely
+          peer_buf_[r][p * kB + static_cast<int>(b)] = share(r == rank_ ? buf_[p][static_cast<int>(b)] : nullptr, r);
+    const auto& hs = sch.phase[static_cast<int>(Phase::P1Halo)];
     for (size_t i = 0; i < hs.size(); ++i)
       for (int p = 0; p < 2; ++p) {
         void* mine = nullptr;
         if (hs[i].dst == rank_) {
           hip_ok(hipMalloc(&mine, hs[i].bytes()), "hipMalloc halo slot");
-          halo_stage_[{hs[i].src, static_cast<int>(i), p}] = mine;
+          slot_[{static_cast<int>(i), p}] = mine;
         }
-        peer_halo_[hs[i].src][{hs[i].dst, static_cast<int>(i), p}] = share(mine, hs[i].dst);
+        void* m = share(mine, hs[i].dst);
+        if (hs[i].src == rank_) peer_slot_[{static_cast<int>(i), p}] = m;
       }
   }
 
-  void run_phase(Phase ph, const std::vector<Transfer>& xs, hipStream_t compute, int par) override {
-    local(xs, compute, par);
-    const int phi = static_cast<int>(ph);
+  void run_phase(Phase ph, const std::vector<Transfer>& xs, hipStream_t s, int par) override {
+    local(xs, s, par);
     const bool halo = ph == Phase::P1Halo;
-    bool sends = false;
-    std::vector<int> notify;
+    std::vector<int> to;  // receivers of this rank's pushes, in first-push order
     for (size_t i = 0; i < xs.size(); ++i) {
       const Transfer& x = xs[i];
       if (x.src != rank_ || x.dst == rank_) continue;
       note(x);
       if (record_only) continue;
-      if (!sends) {
-        hip_ok(hipEventRecord(ready_, compute), "hipEventRecord");
-        hip_ok(hipStreamWaitEvent(cs_, ready_, 0), "hipStreamWaitEvent");
-        sends = true;
-      }
-      char* dst = halo ? static_cast<char*>(peer_halo_[rank_][{x.dst, static_cast<int>(i), par}])
+      const int seq = x.seq >= 0 ? x.seq : static_cast<int>(i);
+      char* dst = halo ? static_cast<char*>(peer_slot_.at({seq, par})) + x.img0 * x.width
                        : static_cast<char*>(peer_buf_[x.dst][par * kB + static_cast<int>(x.to.buf)]) + x.to.off;
-      copy2d(dst, halo ? x.width : x.to.pitch, at(par, x.from), x.from.pitch, x.width, x.height, cs_);
-      notify.push_back(x.dst);
+      copy2d(dst, halo ? x.width : x.to.pitch, at(par, x.from), x.from.pitch, x.width, x.height, s);
+      if (std::find(to.begin(), to.end(), x.dst) == to.end()) to.push_back(x.dst);
     }
-    if (sends) {
-      hip_ok(hipEventRecord(sent_[phi][par], cs_), "hipEventRecord IPC");
-      const int msg = phi * 2 + par;
-      for (int d : notify) c_.isend(&msg, sizeof msg, d);
-      c_.wait_all();
+    const int ch = xs.empty() ? 0 : channel(ph, xs.front().chunk);
+    if (!to.empty()) {
+      if (flags_) {
+        for (int d : to)
+          hip_ok(hipStreamWriteValue32(s, flags_of_[d] + rank_ * kCh + ch, ++sent_seq_[d][ch], 0),
+                 "hipStreamWriteValue32");
+      } else {
+        hip_ok(hipEventRecord(sent_[ch][par], s), "hipEventRecord IPC");
+        const int msg = ch * 2 + par;
+        for (int d : to) c_->isend(&msg, sizeof msg, d);
+        c_->wait_all();
+      }
     }
-    // receive: take each sender's note, then make the compute stream wait for its IPC event
+    std::vector<int> from;
     for (size_t i = 0; i < xs.size(); ++i) {
       const Transfer& x = xs[i];
       if (x.dst != rank_ || x.src == rank_) continue;
       note(x);
       if (record_only) continue;
-      int msg = -1;
-      c_.recv(&msg, sizeof msg, x.src);
-      if (msg != phi * 2 + par) throw std::runtime_error("peer transport: out-of-order note");
-      hip_ok(hipStreamWaitEvent(compute, peer_sent_[x.src][phi][par], 0), "hipStreamWaitEvent IPC");
-      if (halo)
-        copy2d(at(par, x.to), x.to.pitch, static_cast<char*>(halo_stage_[{x.src, static_cast<int>(i), par}]), x.width,
-               x.width, x.height, compute);
+      if (std::find(from.begin(), from.end(), x.src) == from.end()) {
+        from.push_back(x.src);
+        if (flags_) {
+          hip_ok(hipStreamWaitValue32(s, flags_mine_ + x.src * kCh + ch, ++recv_seq_[x.src][ch],
+                                      hipStreamWaitValueGte, 0xffffffffu),
+                 "hipStreamWaitValue32");
+        } else {
+          int msg = -1;
+          c_->recv(&msg, sizeof msg, x.src);
+          if (msg != ch * 2 + par) throw std::runtime_error("peer transport: out-of-order note");
+          hip_ok(hipStreamWaitEvent(s, peer_sent_[x.src][ch][par], 0), "hipStreamWaitEvent IPC");
+        }
+      }
+      if (halo) {
+        const int seq = x.seq >= 0 ? x.seq : static_cast<int>(i);
+        copy2d(at(par, x.to), x.to.pitch, static_cast<char*>(slot_.at({seq, par})) + x.img0 * x.width, x.width,
+               x.width, x.height, s);
+      }
     }
   }
-  // The stream waits for every push this rank has issued so far (its send buffers may be rewritten
-  // after that; the receivers' buffers are ordered by their own IPC-event waits).
-  void end_step(hipStream_t s) override {
-    if (record_only || !cs_) return;
-    hip_ok(hipEventRecord(drained_, cs_), "hipEventRecord");
-    hip_ok(hipStreamWaitEvent(s, drained_, 0), "hipStreamWaitEvent");
-  }
+
+  // Collective: unmap every peer's buffers, wait for every rank to have done so, then free this
+  // rank's own (a mapped peer buffer must not be freed under its importer).
   void close() override {
+    const bool collective = connected_ && c_ && c_->size() > 1;
+    for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+    opened_.clear();
+    if (collective) c_->barrier();
+    release();
+  }
+  void release() {
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
     opened_.clear();
     for (hipEvent_t e : opened_ev_) (void)hipEventDestroy(e);
     opened_ev_.clear();
-    for (auto& kv : halo_stage_) (void)hipFree(kv.second);
-    halo_stage_.clear();
-    for (auto& ph : sent_)
-      for (auto& e : ph)
+    for (auto& kv : slot_) (void)hipFree(kv.second);
+    slot_.clear();
+    peer_slot_.clear();
+    for (auto& ch : sent_)
+      for (auto& e : ch)
         if (e) (void)hipEventDestroy(e), e = nullptr;
-    if (ready_) (void)hipEventDestroy(ready_), ready_ = nullptr;
-    if (drained_) (void)hipEventDestroy(drained_), drained_ = nullptr;
-    if (cs_) (void)hipStreamDestroy(cs_), cs_ = nullptr;
+    if (flags_mine_) (void)hipFree(flags_mine_), flags_mine_ = nullptr;
+    flags_of_.clear();
+    connected_ = false;
   }
 };
 
 }  // namespace
 
-std::unique_ptr<Transport> make_rccl_transport(HostComm& c, int device, int rank) {
+std::unique_ptr<Transport> make_rccl_transport(HostComm* c, int device, int rank) {
   return std::make_unique<RcclTransport>(c, device, rank);
 }
-std::unique_ptr<Transport> make_peer_transport(HostComm& c, int device, int rank) {
-  return std::make_unique<PeerTransport>(c, device, rank);
+std::unique_ptr<Transport> make_peer_transport(HostComm* c, int device, int rank, const std::string& sync) {
+  return std::make_unique<PeerTransport>(c, device, rank, sync);
 }
 
 }  // namespace anx

@@ -35,6 +35,7 @@
 #include "anx/rng.hpp"
 #include "anx/schedule.hpp"
 #include "anx/trace.hpp"
+#include "anx/v5.hpp"
 
 using namespace anx;
 
@@ -53,7 +54,9 @@ struct Options {
   std::string conv2_algo = "auto";  // auto | direct | winograd
   std::string conv1_algo = "auto";  // auto | direct | winograd
   std::string transport = "auto";   // v5 device traffic: auto | rccl | peer (IPC + hipMemcpy2DAsync)
-  std::string split = "rows";       // v5 decomposition: rows (reference) | hybrid (batch first) | batch
+  std::string split = "auto";       // v5 decomposition: auto (balanced) | rows (reference) | hybrid | batch
+  int chunks = 0;                   // v5: halo pipeline chunks per step (0 = auto)
+  std::string peer_sync;            // v5 peer transport ordering: flags | notes ("" = default)
   bool dry_run = false;             // v5: print the transfer schedule (record-only transports, no GPU)
   std::string pipeline = "auto";    // v5: scatter / gather on a second stream (auto: on over RCCL)
   bool poison = false;              // v5: NaN-fill consumed buffers (a mis-ordered step corrupts the output)
@@ -68,7 +71,8 @@ struct Options {
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
                "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd]\n"
                "           [--conv1-algo auto|direct|winograd] [--transport auto|rccl|peer] [--check]\n"
-               "           [--split rows|hybrid|batch] [--dry-run] [--pipeline auto|on|off] [--poison]\n"
+               "           [--split auto|rows|hybrid|batch] [--chunks K] [--peer-sync flags|notes]\n"
+               "           [--dry-run] [--pipeline auto|on|off] [--poison]\n"
                "           [--weights DIR] [--no-json]\n",
                msg);
   std::exit(2);
@@ -95,6 +99,8 @@ Options parse(int argc, char** argv) {
     else if (a == "--conv1-algo") o.conv1_algo = val();
     else if (a == "--transport") o.transport = val();
     else if (a == "--split") o.split = val();
+    else if (a == "--chunks") o.chunks = std::atoi(val().c_str());
+    else if (a == "--peer-sync") o.peer_sync = val();
     else if (a == "--dry-run") o.dry_run = true;
     else if (a == "--pipeline") {
       o.pipeline = val();
@@ -111,7 +117,9 @@ Options parse(int argc, char** argv) {
   if (o.lrn.empty()) o.lrn = (o.version == "v1" || o.version == "v2.1" || o.version == "v2.2") ? "div_n" : "raw";
   if (o.decomp.empty()) o.decomp = o.version == "v5" ? "per_layer" : "overlap";
   if (o.batch < 1) usage("--batch must be >= 1");
-  if (o.split != "rows" && o.split != "hybrid" && o.split != "batch") usage("bad --split");
+  if (o.split != "auto" && o.split != "rows" && o.split != "hybrid" && o.split != "batch") usage("bad --split");
+  if (o.chunks < 0) usage("--chunks must be >= 0");
+  if (!o.peer_sync.empty() && o.peer_sync != "flags" && o.peer_sync != "notes") usage("--peer-sync must be flags or notes");
   return o;
 }
 
@@ -255,7 +263,7 @@ void bcast_weights(HostComm& c, HostWeights& w) {
 }
 
 void report(const Setup& s, int np, const std::vector<float>& y, double cold_ms, double warm_ms,
-            const Phases& cold, const Phases& warm, int warm_iters, double err) {
+            const Phases& cold, const Phases& warm, int warm_iters, double err, const std::string& v5 = "") {
   const Options& o = s.o;
   char vals[512] = {0};
   for (int i = 0; i < 10 && i < static_cast<int>(y.size()); ++i) {
@@ -293,12 +301,12 @@ void report(const Setup& s, int np, const std::vector<float>& y, double cold_ms,
     std::printf(
         "ANX_JSON {\"version\": \"%s\", \"np\": %d, \"batch\": %d, \"shape\": [%d, %d, %d], \"checksum\": %u, "
         "\"cold_ms\": %.4f, \"warm_ms\": %s, \"images_per_s\": %s, \"phases_cold\": %s, \"phases_warm\": %s, "
-        "\"max_abs_err\": %s, \"lrn_mode\": \"%s\", \"decomp\": \"%s\", \"impl\": \"%s\", \"native\": true}\n",
+        "\"max_abs_err\": %s, \"lrn_mode\": \"%s\", \"decomp\": \"%s\", \"impl\": \"%s\", \"native\": true%s%s}\n",
         o.version.c_str(), np, o.batch, s.d.Hp2, s.d.Wp2, s.d.C2, crc32(y.data(), y.size() * 4), cold_ms,
         warm_iters ? std::to_string(warm_ms).c_str() : "null",
         warm_iters ? std::to_string(o.batch / (warm_ms / 1e3)).c_str() : "null", cold.json().c_str(),
         warm.json(warm_iters ? 1.0 / warm_iters : 1.0).c_str(), err >= 0 ? std::to_string(err).c_str() : "null",
-        o.lrn.c_str(), o.decomp.c_str(), o.impl.c_str());
+        o.lrn.c_str(), o.decomp.c_str(), o.impl.c_str(), v5.empty() ? "" : ", \"v5\": ", v5.c_str());
   }
   std::fflush(stdout);
 }
@@ -643,259 +651,74 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
   return 0;
 }
 
-// V5 transport for this rank (see run_v5): "auto" = RCCL when every rank of this node has its own GPU
-// or the job spans nodes, else peer. Throws for a combination that cannot run.
-std::string pick_v5_transport(const std::string& want, const RankInfo& ri, int ndev, bool dry) {
-  const bool shared = !dry && ri.local_world > ndev;  // ranks of this node outnumber its GPUs
-  const std::string tr = want == "auto" ? (shared && ri.nnodes == 1 ? "peer" : "rccl") : want;
-  if (tr != "rccl" && tr != "peer") throw std::runtime_error("--transport must be auto, rccl or peer");
-  if (tr == "peer" && ri.nnodes > 1)
-    throw std::runtime_error("the peer transport (IPC) is single-node: use --transport rccl across nodes");
-  if (tr == "rccl" && shared)
-    throw std::runtime_error("v5 over RCCL needs one GPU per rank on each node (" + std::to_string(ri.local_world) +
-                             " ranks, " + std::to_string(ndev) + " GPUs here; --transport peer shares a GPU)");
-  return tr;
-}
-
 // ------------------------------------------------------------------------------ V5 (device-resident)
-// One transfer schedule per step (anx/schedule.hpp: scatter of images x input rows, pool1 halos
-// inside each row group, gather of output rows), executed by a pluggable transport:
+// The V5 runtime (anx/v5.hpp): one transfer schedule per step (scatter of images x input rows, pool1
+// halos inside each row group cut into image chunks that move while stage1 computes the next chunk,
+// gather of output rows), executed by a pluggable transport:
 //   rccl  grouped ncclSend/ncclRecv over xGMI (one GPU per rank),
-//   peer  one hipMemcpy2DAsync per transfer into the receiver's IPC-mapped buffer, IPC events for
-//         ordering (ranks may share a GPU: the configuration the one-GPU test box can run).
-// Steady-state steps never synchronise a stream with the host: compute, copies and RCCL are
-// ordered by events; Tile / Y / YFull alternate by step parity so a step's pushes never land in a
-// buffer the previous step still reads. Phase times come from events on the compute stream (the
-// time that stream spent in or waiting for each phase). --dry-run prints the schedule each rank's
-// transport would execute (record-only, no GPU) as ANX_SCHEDULE lines.
+//   peer  one hipMemcpy2DAsync per transfer into the receiver's IPC-mapped buffer, ordered by
+//         device-side flags (ranks may share a GPU: the configuration the one-GPU test box can run).
+// Steady-state steps never synchronise a stream with the host. Phase times are the compute stream's
+// critical path (scatter / halo_p1 = time spent waiting for data). --dry-run prints the schedule each
+// rank's transport would execute (record-only, no GPU) as ANX_SCHEDULE lines.
 int run_v5(Setup& s, HostComm& c, bool dry) {
   const int N = s.o.batch, rank = c.rank(), np = c.size();
-  const Decomp mode = s.o.decomp == "overlap" ? Decomp::Overlap : Decomp::PerLayer;
-  const int row_ways = s.o.split == "rows" ? np : s.o.split == "batch" ? 1 : 0;
-  HybridPlan hp;
-  if (!make_hybrid_plan(s.d.H, s.d.W, np, N, row_ways, mode, hp, s.b1, s.b2))
-    throw std::runtime_error("invalid plan for --split " + s.o.split);
-  const TilePlan& t = hp.tile(rank);
-  const RowRange im = hp.images[hp.group_of[rank]];
-  const int n = t.out.empty() ? 0 : im.size();
-  const size_t win_row = static_cast<size_t>(s.d.Wp1 + 2 * s.b2.conv.P) * s.d.C1 * 4;
-  const Schedule sched = make_step_schedule(hp, {s.in_row * 4, s.out_row * 4, win_row, s.d.H, s.d.Hp2});
-  int ndev = 0;
-  if (!dry) {
-    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
-    if (ndev < 1) throw std::runtime_error("v5 needs a GPU");
-  }
-  // The transport is chosen per NODE: peer (IPC-mapped buffers, ranks may share a GPU) works only
-  // inside one host; RCCL needs one GPU per rank of this node. Multi-node jobs are RCCL only.
-  const std::string tr = pick_v5_transport(s.o.transport, s.ri, ndev, dry);
-  const int dev = dry ? 0 : s.ri.local_rank % ndev;
-  std::unique_ptr<Transport> x = tr == "rccl" ? make_rccl_transport(c, dev, rank) : make_peer_transport(c, dev, rank);
-  constexpr int kB = static_cast<int>(BufId::kCount);
+  V5Options o;
+  o.batch = N;
+  o.row_ways = s.o.split == "rows" ? np : s.o.split == "hybrid" ? 0 : s.o.split == "batch" ? 1 : -1;
+  o.mode = s.o.decomp == "overlap" ? Decomp::Overlap : Decomp::PerLayer;
+  o.transport = s.o.transport;
+  o.chunks = s.o.chunks;
+  o.pipeline = s.o.pipeline == "on" ? 1 : s.o.pipeline == "off" ? 0 : -1;
+  o.poison = s.o.poison;
+  o.impl = s.o.impl == "direct" ? Impl::Direct : Impl::Mfma;
+  o.knobs = s.k;
+  o.peer_sync = s.o.peer_sync;
   if (dry) {  // the schedule this rank's transport would execute, one step
-    x->record_only = true;
-    void* none[2][kB] = {};
-    x->bind(sched, none, nullptr);
-    for (int ph = 0; ph < 3; ++ph) x->run_phase(static_cast<Phase>(ph), sched.phase[ph], nullptr, 0);
+    const std::string tr = pick_v5_transport(o.transport, s.ri, 0, true);
+    const std::vector<std::string> log = v5_dry_schedule(rank, np, s.b1, s.b2, s.d.H, s.d.W, o, tr);
     for (int r = 0; r < np; ++r) {
       if (r == rank)
-        for (const std::string& l : x->log()) std::printf("ANX_SCHEDULE %s rank %d: %s\n", x->name(), rank, l.c_str());
+        for (const std::string& l : log) std::printf("ANX_SCHEDULE %s rank %d: %s\n", tr.c_str(), rank, l.c_str());
       std::fflush(stdout);
       c.barrier();
     }
     return 0;
   }
-  hip_check(hipSetDevice(dev), "hipSetDevice");
   Phases cold, warm;
   c.barrier();
   const double t0 = now_ms();
   double a = now_ms();
   if (rank == 0) fill_input(s);
-  bcast_weights(c, s.w);
-  hipStream_t st;
-  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
-  BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, std::max(1, n), s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
-  auto dalloc = [](size_t floats) {
-    float* p = nullptr;
-    hip_check(hipMalloc(&p, std::max<size_t>(1, floats) * 4), "hipMalloc");
-    return p;
-  };
-  float* d_x = rank == 0 ? dalloc(s.x.size()) : nullptr;
-  float *d_tile[2], *d_y[2], *d_yfull[2] = {nullptr, nullptr};
-  const size_t tile_bytes = static_cast<size_t>(n) * t.in.size() * s.in_row * 4;
-  const size_t y_bytes = static_cast<size_t>(n) * t.out.size() * s.out_row * 4;
-  for (int p = 0; p < 2; ++p) {
-    d_tile[p] = dalloc(tile_bytes / 4);
-    d_y[p] = dalloc(y_bytes / 4);
-    if (rank == 0) d_yfull[p] = dalloc(static_cast<size_t>(N) * s.d.Hp2 * s.out_row);
-  }
-  // the conv2 window exists once stage1 has run on this tile geometry: run it once on zeros
-  float* d_win = nullptr;
-  if (n) {
-    hip_check(hipMemsetAsync(d_tile[0], 0, static_cast<size_t>(n) * t.in.size() * s.in_row * 4, st), "memset");
-    hip_check(eng.stage1(d_tile[0], n, t, st), "stage1");
-    d_win = eng.q2_row_ptr(t, 0, t.q.lo);
-  }
-  if (rank == 0) hip_check(hipMemcpy(d_x, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice), "H2D input");
-  hip_check(hipDeviceSynchronize(), "sync");
-  void* bufs[2][kB];
-  for (int p = 0; p < 2; ++p) {
-    bufs[p][static_cast<int>(BufId::X)] = d_x;
-    bufs[p][static_cast<int>(BufId::Tile)] = d_tile[p];
-    bufs[p][static_cast<int>(BufId::Win)] = d_win;
-    bufs[p][static_cast<int>(BufId::Y)] = d_y[p];
-    bufs[p][static_cast<int>(BufId::YFull)] = d_yfull[p];
-  }
-  x->bind(sched, bufs, st);
-  c.barrier();
+  V5Runtime rt(c, s.ri, s.b1, s.b2, s.d.H, s.d.W, s.w, o);
+  rt.set_input(rank == 0 ? s.x.data() : nullptr);
   cold.add("setup", now_ms() - a);
   std::vector<float> y_host(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
-  const char* names[5] = {"scatter", "compute", "halo_p1", "compute", "gather"};
-  constexpr int kEv = 6;
-  // Phases of step k. The transport orders each phase against the stream it is given (the copies /
-  // RCCL group wait for that stream's work so far, and the stream waits for the data to land), so
-  // the scatter and gather can run on `io` while `st` computes another step.
-  auto scatter = [&](int k, hipStream_t on) {
-    RoctxRange r0("v5 scatter");
-    x->run_phase(Phase::Scatter, sched.phase[0], on, k & 1);
-  };
-  auto compute = [&](int k, hipEvent_t* ev) {  // ev[1] recorded before, ev[2..4] inside (on st)
-    const int par = k & 1;
-    if (n && mode == Decomp::PerLayer) {
-      RoctxRange r1("v5 stage1");
-      hip_check(eng.stage1(d_tile[par], n, t, st), "stage1");
-      if (s.o.poison) hip_check(hipMemsetAsync(d_tile[par], 0xff, tile_bytes, st), "poison tile");
-    }
-    hip_check(hipEventRecord(ev[2], st), "event");
-    {
-      RoctxRange r2("v5 halo_p1");
-      x->run_phase(Phase::P1Halo, sched.phase[1], st, par);
-    }
-    hip_check(hipEventRecord(ev[3], st), "event");
-    if (n) {
-      RoctxRange r3("v5 stage2");
-      if (mode == Decomp::PerLayer) {
-        hip_check(eng.stage2(n, t, d_y[par], st), "stage2");
-      } else {
-        hip_check(eng.tile_forward(d_tile[par], n, t, d_y[par], st), "tile_forward");
-        if (s.o.poison) hip_check(hipMemsetAsync(d_tile[par], 0xff, tile_bytes, st), "poison tile");
-      }
-    }
-    hip_check(hipEventRecord(ev[4], st), "event");
-  };
-  auto gather = [&](int k, hipStream_t on) {
-    {
-      RoctxRange r4("v5 gather");
-      x->run_phase(Phase::Gather, sched.phase[2], on, k & 1);
-    }
-    x->end_step(on);  // `on` now also waits for this rank's outgoing pushes of the step
-    if (s.o.poison && n) hip_check(hipMemsetAsync(d_y[k & 1], 0xff, y_bytes, on), "poison y");
-  };
-  // serial step (the cold step, and --pipeline off): every phase on st
-  auto step = [&](int k, hipEvent_t* ev) {
-    hip_check(hipEventRecord(ev[0], st), "event");
-    scatter(k, st);
-    hip_check(hipEventRecord(ev[1], st), "event");
-    compute(k, ev);
-    gather(k, st);
-    hip_check(hipEventRecord(ev[5], st), "event");
-  };
-  // Pipelined steady state: io runs scatter(k+1) while st computes step k, then gather(k) once
-  // stage2(k) is done; st starts step k+1 as soon as scatter(k+1) has landed. Buffer reuse is
-  // ordered without extra events: Tile[p] is rewritten by scatter(k+2), which io issues after
-  // gather(k), which waited for stage2(k) (so stage1(k) is done everywhere: the root's gather
-  // waits for every sender's push); Y[p] is rewritten by stage2(k+2) on st, which waited for
-  // scatter(k+2) on io, issued after gather(k) and its end_step. Every rank issues the phases in
-  // the same order (halo k, scatter k+1, gather k), as RCCL's in-order matching requires.
-  // Phase times: "scatter" is how long st waited for its input, "gather" the time from the end of
-  // stage2 to the end of the gather on io (off the critical path when the overlap works).
-  hipStream_t io = nullptr;
-  hipEvent_t e_sc[2], e_s2[2];
-  hip_check(hipStreamCreateWithFlags(&io, hipStreamNonBlocking), "stream");
-  for (int p = 0; p < 2; ++p) {
-    hip_check(hipEventCreateWithFlags(&e_sc[p], hipEventDisableTiming), "hipEventCreate");
-    hip_check(hipEventCreateWithFlags(&e_s2[p], hipEventDisableTiming), "hipEventCreate");
-  }
-  auto run_pipelined = [&](int k0, int iters, hipEvent_t* evs) {
-    scatter(k0, io);
-    hip_check(hipEventRecord(e_sc[k0 & 1], io), "event");
-    for (int i = 0; i < iters; ++i) {
-      const int k = k0 + i, par = k & 1;
-      hipEvent_t* ev = evs + kEv * i;
-      hip_check(hipEventRecord(ev[0], st), "event");
-      hip_check(hipStreamWaitEvent(st, e_sc[par], 0), "wait scatter");
-      hip_check(hipEventRecord(ev[1], st), "event");
-      compute(k, ev);
-      hip_check(hipEventRecord(e_s2[par], st), "event");
-      if (i + 1 < iters) {
-        scatter(k + 1, io);
-        hip_check(hipEventRecord(e_sc[par ^ 1], io), "event");
-      }
-      hip_check(hipStreamWaitEvent(io, e_s2[par], 0), "wait stage2");
-      gather(k, io);
-      hip_check(hipEventRecord(ev[5], io), "event");
-    }
-  };
-  auto make_events = [](int count) {
-    std::vector<hipEvent_t> v(count);
-    for (auto& e : v) hip_check(hipEventCreate(&e), "hipEventCreate");
-    return v;
-  };
-  auto add_phases = [&](Phases& ph, hipEvent_t* ev) {
-    for (int i = 0; i < kEv - 1; ++i) {
-      float ms = 0;
-      hip_check(hipEventElapsedTime(&ms, ev[i], ev[i + 1]), "elapsed");
-      ph.add(names[i], ms);
-    }
-  };
-  std::vector<hipEvent_t> ev0 = make_events(kEv);
-  step(0, ev0.data());
-  if (rank == 0)
-    hip_check(hipMemcpyAsync(y_host.data(), d_yfull[0], y_host.size() * 4, hipMemcpyDeviceToHost, st), "D2H");
-  hip_check(hipStreamSynchronize(st), "sync");
-  add_phases(cold, ev0.data());
-  double cold_ms = now_ms() - t0;
-  std::vector<hipEvent_t> evw = make_events(kEv * std::max(1, s.o.iters));
+  rt.step();
+  rt.sync();
+  for (const auto& kv : rt.phase_ms()) cold.add(kv.first, kv.second);
+  rt.reset_phases();
+  if (rank == 0) rt.output(y_host.data());
+  const double cold_ms = now_ms() - t0;
   double wall = 0;
   if (s.o.iters > 0) {
     c.barrier();
     const double w0 = now_ms();
-    // auto: pipelined over RCCL (one communicator stream per rank serialises all phases, so the
-    // serial schedule puts every transfer on the critical path); serial for the peer transport,
-    // where ranks that share one GPU measured mixed (profiles/r02_ab_v5_pipeline.txt)
-    if (s.o.pipeline == "on" || (s.o.pipeline == "auto" && tr == "rccl"))
-      run_pipelined(1, s.o.iters, evw.data());
-    else
-      for (int i = 0; i < s.o.iters; ++i) step(1 + i, evw.data() + kEv * i);  // no host sync inside
-    hip_check(hipStreamSynchronize(st), "sync");
-    hip_check(hipStreamSynchronize(io), "sync");
+    for (int i = 0; i < s.o.iters; ++i) rt.step();  // no host sync inside
+    rt.sync();
     c.barrier();
     wall = (now_ms() - w0) / s.o.iters;
-    for (int i = 0; i < s.o.iters; ++i) add_phases(warm, evw.data() + kEv * i);
-    if (rank == 0) {  // the last warm step's output (parity of step iters)
-      hip_check(hipMemcpy(y_host.data(), d_yfull[s.o.iters & 1], y_host.size() * 4, hipMemcpyDeviceToHost), "D2H");
-    }
+    for (const auto& kv : rt.phase_ms()) warm.add(kv.first, kv.second * s.o.iters);
+    if (rank == 0) rt.output(y_host.data());
   }
-  for (int p = 0; p < 2; ++p) {
-    (void)hipEventDestroy(e_sc[p]);
-    (void)hipEventDestroy(e_s2[p]);
-  }
-  for (auto e : ev0) (void)hipEventDestroy(e);
-  for (auto e : evw) (void)hipEventDestroy(e);
   double tm[2] = {cold_ms, wall};
   c.allreduce_max(tm, 2);
   if (rank == 0) {
-    std::printf("ANX_TRANSPORT %s transfers %zu\n", x->name(), x->log().size());
-    report(s, np, y_host, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y_host) : -1);
+    std::printf("ANX_TRANSPORT %s ordering %s\n", rt.transport(), rt.pipelined() ? "pipelined" : "serial");
+    report(s, np, y_host, tm[0], tm[1], cold, warm, s.o.iters, s.o.check ? check_err(s, y_host) : -1,
+           rt.describe_json());
   }
-  c.barrier();  // nobody pushes into a peer's buffers any more: unmap, then free
-  x->close();
-  c.barrier();  // every peer has unmapped this rank's buffers before they are freed
-  for (float* p : {d_x, d_tile[0], d_tile[1], d_y[0], d_y[1], d_yfull[0], d_yfull[1]})
-    if (p) (void)hipFree(p);
-  (void)hipStreamDestroy(io);
-  (void)hipStreamDestroy(st);
-  c.barrier();
-  return 0;
+  return 0;  // ~V5Runtime: collective teardown
 }
 
 }  // namespace

@@ -20,9 +20,11 @@ import torch  # noqa: F401  (load torch's HIP runtime before libanx)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ANX_LIB", os.path.join(_HERE, "lib", "libanx.so"))
+DIST_PATH = os.path.join(os.path.dirname(LIB_PATH), "libanx_dist.so")
 
 _lock = threading.Lock()
 _lib = None
+_dist = None
 
 
 class BlockC(C.Structure):
@@ -105,6 +107,22 @@ _SIGS = {
 }
 
 
+_DIST_SIGS = {
+    "anx_v5_create": (_I, [C.POINTER(_P), _I, _I, _I, _I, _I, C.c_char_p, _I, C.c_double, C.POINTER(BlockC),
+                           C.POINTER(BlockC), _I, _I, _P, _P, _P, _P, _I, _I, _I, C.c_char_p, _I, _I, _I, _I,
+                           C.c_char_p]),
+    "anx_v5_destroy": (_I, [_P]),
+    "anx_v5_set_input": (_I, [_P, _P]),
+    "anx_v5_step": (_I, [_P, _I]),
+    "anx_v5_sync": (_I, [_P]),
+    "anx_v5_output": (_I, [_P, _P]),
+    "anx_v5_phases": (_I, [_P, C.c_char_p, _SZ, _I]),
+    "anx_v5_describe": (_I, [_P, C.c_char_p, _SZ]),
+    "anx_v5_schedule": (_I, [_I, C.POINTER(BlockC), C.POINTER(BlockC), _I, _I, _I, _I, _I, _I, _I, C.c_char_p,
+                             C.c_char_p, _SZ]),
+}
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -137,6 +155,33 @@ def lib():
             fn.argtypes = args
         _lib = h
         return _lib
+
+
+def dist():
+    """libanx_dist (the V5 multi-GPU runtime's C ABI; needs RCCL, so loaded only when used)."""
+    global _dist
+    if _dist is not None:
+        return _dist
+    lib()  # libanx first: libanx_dist links against it and reports errors through anx_last_error
+    with _lock:
+        if _dist is not None:
+            return _dist
+        if not os.path.exists(DIST_PATH):
+            raise NativeError(f"libanx_dist not built: {DIST_PATH} missing (run `python __graft_entry__.py build`)")
+        try:
+            h = C.CDLL(DIST_PATH, mode=C.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - depends on the machine
+            raise NativeError(f"cannot load {DIST_PATH}: {e}") from e
+        for name, (res, args) in _DIST_SIGS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _dist = h
+        return _dist
+
+
+def dist_call(name: str, *args) -> None:
+    check(getattr(dist(), name)(*args), name)
 
 
 def check(status: int, what: str = "") -> None:

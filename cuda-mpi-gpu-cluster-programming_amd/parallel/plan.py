@@ -238,3 +238,83 @@ def check_plan(p: DecompPlan, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) ->
         need(t.c2.lo == t.out.lo * b2.pool.S and pool_out_dim(t.c2.size, b2.pool.F, b2.pool.S) == t.out.size,
              f"rank {r}: pool2 window")
     need(nxt == d.Hp2, "output rows do not cover the image")
+
+
+# ----------------------------------------------------------------------------- V5 step schedule
+# Mirror of anx::plan_stats / balanced_row_ways / make_v5_layout (csrc/src/runtime/v5.cpp) and of
+# anx::make_step_schedule / chunk_of (csrc/src/runtime/schedule.cpp): tests/test_v5_runtime.py checks
+# that the native runtime issues exactly this transfer list.
+
+MAX_CHUNKS = 16
+
+
+def plan_stats(p: HybridPlan) -> dict:
+    """Per-rank work balance: output rows (max / mean) and images x rows (imbalance = max / mean)."""
+    rows = [p.tile(r).out.size for r in range(p.np)]
+    imgs = [p.images_of(r).size if rows[r] else 0 for r in range(p.np)]
+    work = [a * b for a, b in zip(rows, imgs)]
+    mean = sum(work) / p.np
+    return {"groups": p.groups, "row_ways": max(p.group_size), "out_rows_max": max(rows),
+            "out_rows_mean": sum(rows) / p.np, "imbalance": max(work) / mean if mean else 1.0,
+            "conv1_redundancy": hybrid_conv1_redundancy(p), "images_per_rank_max": max(imgs)}
+
+
+def balanced_row_ways(np_: int, batch: int, H: int = 227, W: int = 227) -> int:
+    """Fewest row ways r >= 2 (r | np) whose images x rows work is within 10% of the mean (np = 8,
+    batch 1024: r = 2, four groups of 256 images split 7 / 6 output rows, max / mean 1.077); else the
+    most balanced r."""
+    if np_ <= 1:
+        return 1
+    best, best_imb = np_, float("inf")
+    for r in range(2, np_ + 1):
+        if np_ % r:
+            continue
+        imb = plan_stats(make_hybrid_plan(H, W, np_, batch, r, PER_LAYER))["imbalance"]
+        if imb <= 1.1:
+            return r
+        if imb < best_imb - 1e-9:
+            best, best_imb = r, imb
+    return best
+
+
+def _xfer(phase, src, dst, frm, to, width, height):
+    return (f"{phase} {src}->{dst} w={width} h={height} from={frm[0]}+{frm[1]}/{frm[2]} "
+            f"to={to[0]}+{to[1]}/{to[2]}")
+
+
+def step_schedule(p: HybridPlan, chunks: int = 0, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> list[str]:
+    """Every transfer of one V5 step in issue order (scatter, pool1-halo chunks, gather), in the
+    native Transfer::str() format: a 2-D block of `h` images x `w` bytes between buffer regions
+    (X / Tile / Win / Y / YFull + byte offset / image pitch)."""
+    d = blocks_dims(p.row_plans[0].H, p.row_plans[0].W, b1, b2)
+    in_row, out_row = d.W * d.C0 * 4, d.Wp2 * d.C2 * 4
+    win_row = (d.Wp1 + 2 * b2.conv.P) * d.C1 * 4
+    scatter, gather, halos = [], [], []
+    for q in range(p.np):
+        t, im = p.tile(q), p.images_of(q)
+        if t.out.empty or im.empty:
+            continue
+        scatter.append(("scatter", 0, q, ("X", (im.lo * d.H + t.inp.lo) * in_row, d.H * in_row),
+                        ("Tile", 0, t.inp.size * in_row), t.inp.size * in_row, im.size))
+        gather.append(("gather", q, 0, ("Y", 0, t.out.size * out_row),
+                       ("YFull", (im.lo * d.Hp2 + t.out.lo) * out_row, d.Hp2 * out_row), t.out.size * out_row,
+                       im.size))
+    for g, rp in enumerate(p.row_plans):
+        base, n = sum(p.group_size[:g]), p.images[g].size
+        if n == 0:
+            continue
+        for h in rp.p1_halos:
+            ts, td = rp.tiles[h.src], rp.tiles[h.dst]
+            halos.append(("halo_p1", base + h.src, base + h.dst,
+                          ("Win", (h.rows.lo - ts.q.lo) * win_row, ts.q.size * win_row),
+                          ("Win", (h.rows.lo - td.q.lo) * win_row, td.q.size * win_row), h.rows.size * win_row, n))
+    if halos:
+        chunks = max(1, min(chunks if chunks > 0 else 4, min(x[6] for x in halos), MAX_CHUNKS))
+    out = [_xfer(*x) for x in scatter]
+    for c in range(chunks if halos else 0):
+        for ph, s, t, frm, to, w, hgt in halos:
+            lo, hi = hgt * c // chunks, hgt * (c + 1) // chunks
+            if hi > lo:
+                out.append(_xfer(f"{ph}#{c}", s, t, (frm[0], frm[1] + lo * frm[2], frm[2]),
+                                 (to[0], to[1] + lo * to[2], to[2]), w, hi - lo))
+    return out + [_xfer(*x) for x in gather]

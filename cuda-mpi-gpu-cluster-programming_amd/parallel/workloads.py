@@ -1,32 +1,48 @@
 """The reference's multi-GPU programs as steady-state, strong-scaling benchmark steps
-(``bench.py --workload v4|v5``), over torch.distributed (RCCL over xGMI).
+(``bench.py --workload v4|v5``).
 
 The reference's V4 (final_project/v4_mpi_cuda/src/main_mpi_cuda.cpp:52-130) keeps the batch on rank
 0's host, scatters input rows, runs the tile forward and gathers output rows back to the host; its
 planned V5 (README.md:157-166) keeps every byte on the device and exchanges per-layer halos between
-GPUs. Here both are one class, a fixed global batch split by the hybrid planner
-(:func:`anx.parallel.plan.make_hybrid_plan`: ``rows`` = the reference's pure row split over all ranks,
-``hybrid`` = batch first, rows only below one image per rank, ``batch`` = images only):
+GPUs.
+
+* :class:`NativeV5` — V5 on GPUs: a thin client of the native V5 runtime (``anx/v5.hpp`` through
+  ``libanx_dist``'s C ABI). The runtime owns the plan, the buffers, the streams and the transport
+  (RCCL over xGMI, or the peer IPC transport with device-side flags when ranks share a GPU); Python
+  only passes the job shape and the root's weights / batch and reads back the output, the phase
+  times and the layout. Its transfer list is :func:`anx.parallel.plan.step_schedule` exactly
+  (tests/test_v5_runtime.py).
+* :class:`RowsWorkload` — V4 on GPUs and the CPU (gloo) rehearsal of both versions, over
+  torch.distributed: a fixed global batch split by the hybrid planner
+  (:func:`anx.parallel.plan.make_hybrid_plan`: ``rows`` = the reference's pure row split over all
+  ranks, ``hybrid`` = batch first, rows only below one image per rank, ``batch`` = images only)::
 
     v4  root pinned host --H2D--> root GPU --RCCL scatter (images x input rows incl. halo)--> ranks
         --tile_forward (overlap tiles: no mid-network exchange)--> RCCL gather --D2H--> root pinned host
-    v5  root GPU --RCCL scatter--> ranks --stage1 (conv1+pool1)--> RCCL pool1-halo exchange inside each
-        row group (per_layer tiles) --stage2 (conv2+pool2+LRN)--> RCCL gather --> root GPU
+    v5  root --scatter--> ranks --stage1 (conv1+pool1)--> pool1-halo exchange inside each row group
+        (per_layer tiles) --stage2 (conv2+pool2+LRN)--> gather --> root
 
-Every transfer is a grouped point-to-point op (RCCL has no Scatterv/Gatherv; root-centred grouped
-P2P drives one xGMI link per peer at once). Buffers are allocated once. Each phase ends
-with a CUDA event on the compute stream (no host sync inside a step), so the per-phase times come
-from event pairs after the timed loop.
+  Every transfer is a grouped point-to-point op (RCCL has no Scatterv/Gatherv). Buffers are allocated
+  once. Each phase ends with an event on the compute stream (no host sync inside a step), so the
+  per-phase times come from event pairs after the timed loop.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
+import ctypes as C
+import json
+import os
+import socket
+
+from .. import _native as nat
+from ..config import BLOCK1, BLOCK2, blocks_dims
 from .comm import world
 from .plan import OVERLAP, PER_LAYER, HybridPlan, make_hybrid_plan
 
 DECOMPS = {"rows": None, "hybrid": 0, "batch": 1}  # row_ways (None = all ranks)
+V5_DECOMPS = {"auto": -1, "rows": None, "hybrid": 0, "batch": 1}  # -1: balanced (anx::balanced_row_ways)
 PHASES = ("h2d", "scatter", "stage1", "halo_p1", "compute", "gather", "d2h")
 
 
@@ -47,7 +63,11 @@ class RowsWorkload:
         self.layer = layer or (OVERLAP if version == "v4" else PER_LAYER)
         if version == "v4" and self.layer != OVERLAP:
             raise ValueError("v4 runs overlap tiles (host-staged, no mid-network exchange)")
-        rw = DECOMPS[decomp]
+        if decomp == "auto":  # the balanced default of the native runtime (anx::balanced_row_ways)
+            from .plan import balanced_row_ways
+            rw = balanced_row_ways(self.world, batch, model.H, model.W)
+        else:
+            rw = DECOMPS[decomp]
         self.plan: HybridPlan = make_hybrid_plan(model.H, model.W, self.world, batch,
                                                  self.world if rw is None else rw, self.layer, model.b1, model.b2)
         d = model.dims
@@ -221,3 +241,129 @@ class RowsWorkload:
         return {"workload": self.version, "layer": self.layer, "groups": p.groups,
                 "ranks_per_group": sorted(set(p.group_size)),
                 "images_per_rank_max": max(p.images_of(q).size for q in range(self.world))}
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class NativeV5:
+    """V5 on GPUs through the native runtime (one instance per rank; construction is collective).
+
+    ``weights``: rank 0's dict w1/b1/w2/b2 (fp32 KCFF, any device; other ranks may pass None: the
+    runtime broadcasts rank 0's device copy over the transport). The rendezvous port of the runtime's
+    own bootstrap channel is chosen by rank 0 and shared over torch.distributed when it is
+    initialised (else ``port`` / ANX_V5_PORT).
+    """
+
+    def __init__(self, batch: int, weights: dict | None, *, specs=(BLOCK1, BLOCK2), H: int = 227, W: int = 227,
+                 decomp: str = "auto", layer: str = PER_LAYER, transport: str = "auto", chunks: int = 0,
+                 pipeline: int = -1, poison: bool = False, impl: str = "mfma", peer_sync: str = "",
+                 port: int | None = None, timeout_s: float = 300.0):
+        if decomp not in V5_DECOMPS:
+            raise ValueError(f"decomp must be one of {sorted(V5_DECOMPS)}")
+        if layer not in (OVERLAP, PER_LAYER):
+            raise ValueError("layer must be overlap or per_layer")
+        import torch.distributed as tdist
+        if tdist.is_available() and tdist.is_initialized():
+            self.rank, self.world = world()
+        else:  # a launcher's environment (torchrun / anxrun) without a torch process group
+            self.rank = int(os.environ.get("RANK", "0"))
+            self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.batch, self.b1, self.b2, self.H, self.W = batch, specs[0], specs[1], H, W
+        self.dims = blocks_dims(H, W, *specs)
+        local_rank = int(os.environ.get("LOCAL_RANK", self.rank))
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", self.world))
+        nnodes = max(1, self.world // max(1, local_world))
+        if port is None:
+            port = int(os.environ.get("ANX_V5_PORT", "0")) or (_free_port() if self.rank == 0 else 0)
+            if self.world > 1 and tdist.is_available() and tdist.is_initialized():
+                box = [port]
+                tdist.broadcast_object_list(box, src=0)
+                port = box[0]
+            elif self.world > 1 and not os.environ.get("ANX_V5_PORT"):
+                raise ValueError("NativeV5 at world > 1 needs torch.distributed, `port` or ANX_V5_PORT")
+        rw = V5_DECOMPS[decomp]
+        rw = self.world if rw is None else rw
+        ptrs = [None] * 4
+        if self.rank == 0:
+            if weights is None:
+                raise ValueError("rank 0 needs the weights")
+            self._w = {k: weights[k].detach().to("cpu", torch.float32).contiguous() for k in ("w1", "b1", "w2", "b2")}
+            ptrs = [self._w[k].data_ptr() for k in ("w1", "b1", "w2", "b2")]
+        h = C.c_void_p()
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1").encode()
+        nat.dist_call("anx_v5_create", C.byref(h), self.rank, self.world, local_rank, local_world, nnodes, addr, port,
+                      timeout_s, C.byref(nat.block_c(self.b1)), C.byref(nat.block_c(self.b2)), H, W, *ptrs, batch, rw,
+                      1 if layer == PER_LAYER else 0, transport.encode(), chunks, pipeline, int(poison),
+                      0 if impl == "mfma" else 1, peer_sync.encode())
+        self._h = h
+        self.version, self.layer = "v5", layer
+
+    # ------------------------------------------------------------------ data
+    def fill(self, x: torch.Tensor | None) -> None:
+        """Collective: rank 0's global batch [B,H,W,C0] (any device) becomes the input of the following
+        steps; other ranks pass None (or anything: ignored)."""
+        if self.rank == 0:
+            xs = x.detach().to("cpu", torch.float32).contiguous()
+            if tuple(xs.shape) != (self.batch, self.H, self.W, self.dims.C0):
+                raise ValueError(f"expected [{self.batch},{self.H},{self.W},{self.dims.C0}], got {tuple(xs.shape)}")
+            nat.dist_call("anx_v5_set_input", self._h, xs.data_ptr())
+        else:
+            nat.dist_call("anx_v5_set_input", self._h, None)
+
+    def output(self) -> torch.Tensor | None:
+        """Rank 0: the gathered output of the last step (host fp32 [B, Hp2, Wp2, C2])."""
+        if self.rank != 0:
+            return None
+        d = self.dims
+        y = torch.empty((self.batch, d.Hp2, d.Wp2, d.C2), dtype=torch.float32)
+        nat.dist_call("anx_v5_output", self._h, y.data_ptr())
+        return y
+
+    # ------------------------------------------------------------------ steps
+    def step(self, record: bool = False, steps: int = 1) -> None:
+        nat.dist_call("anx_v5_step", self._h, steps)
+
+    def sync(self) -> None:
+        nat.dist_call("anx_v5_sync", self._h)
+
+    def _json(self, name, *extra) -> dict:
+        buf = C.create_string_buffer(4096)
+        nat.dist_call(name, self._h, buf, len(buf), *extra)
+        return json.loads(buf.value.decode())
+
+    def phase_ms(self, reset: bool = False) -> dict:
+        """Mean ms per step since the last reset on the compute stream's critical path (syncs)."""
+        return {k: round(v, 4) for k, v in self._json("anx_v5_phases", int(reset)).items()}
+
+    def reset_phases(self) -> None:
+        self.phase_ms(reset=True)
+
+    def describe(self) -> dict:
+        return {"workload": "v5", "runtime": "native (anx/v5.hpp via libanx_dist)", **self._json("anx_v5_describe")}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            nat.dist_call("anx_v5_destroy", self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def native_schedule(np_: int, batch: int, row_ways: int = -1, layer: str = PER_LAYER, chunks: int = 0,
+                    rank: int = -1, transport: str = "rccl", specs=(BLOCK1, BLOCK2), H: int = 227,
+                    W: int = 227) -> list[str]:
+    """The native runtime's record-only schedule (no GPU): rank < 0 -> every transfer of one step in
+    issue order; else what rank `rank`'s transport issues."""
+    buf = C.create_string_buffer(1 << 22)
+    nat.check(nat.dist().anx_v5_schedule(np_, C.byref(nat.block_c(specs[0])), C.byref(nat.block_c(specs[1])), H, W,
+                                         batch, row_ways, 1 if layer == PER_LAYER else 0, chunks, rank,
+                                         transport.encode(), buf, len(buf)), "anx_v5_schedule")
+    return [l for l in buf.value.decode().splitlines() if l]

@@ -8,7 +8,7 @@ CXX=/opt/rocm/llvm/bin/clang++
 flags=(-std=c++17 -Icsrc/include -isystem /opt/rocm/include -Wall -Wextra -Wshadow -Werror -Wno-unused-parameter -fsyntax-only)
 fail=0
 for f in $(git ls-files 'csrc/*.cpp' 'csrc/**/*.cpp'); do
-  if grep -q '<<<' "$f"; then  # HIP-language .cpp (CMake LANGUAGE HIP)
+  if grep -q -e '<<<' -e '\.hip"' "$f"; then  # HIP-language .cpp (CMake LANGUAGE HIP)
     $CXX -x hip --offload-arch=gfx950 "${flags[@]}" "$f" || { echo "LINT FAIL: $f"; fail=1; }
   else
     $CXX "${flags[@]}" -D__HIP_PLATFORM_AMD__ "$f" || { echo "LINT FAIL: $f"; fail=1; }

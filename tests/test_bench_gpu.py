@@ -43,7 +43,10 @@ def test_bench_workloads_one_gpu(workload):
     rec = bench(["--workload", workload, "--batch", "16", "--no-b1"])
     c = rec["config"]
     assert rec["scaling"] == "strong" and c["global_batch"] == 16 and c["workload"] == workload
-    assert c["phases_ms"]["compute"] > 0
+    if workload == "v4":
+        assert c["phases_ms"]["compute"] > 0
+    else:  # the native runtime: critical-path phases, balanced layout, transport
+        assert c["phases_ms"]["stage2"] > 0 and c["transport"] == "rccl" and c["imbalance"] == 1.0
 
 
 @pytest.mark.gpu

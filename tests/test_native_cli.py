@@ -123,19 +123,22 @@ def test_v5_transports_issue_identical_transfers(np_, split):
     schedule."""
     rccl, peer = _schedule(np_, "rccl", split), _schedule(np_, "peer", split)
     assert rccl == peer and len(rccl) > 0
-    phases = {l.split(" ")[2] for l in rccl}
+    phases = {l.split(" ")[2].split("#")[0] for l in rccl}
     assert {"scatter", "gather"} <= phases
     assert ("halo_p1" in phases) == (split == "rows" or np_ > 3)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("np_,decomp,split", [(2, "per_layer", "rows"), (3, "per_layer", "rows"),
-                                              (4, "per_layer", "rows"), (2, "overlap", "rows"),
-                                              (4, "per_layer", "hybrid"), (3, "per_layer", "batch")])
-def test_native_v5_peer_transport(cuda, np_, decomp, split):
-    """V5 on the schedule runtime with the peer transport (one hipMemcpy2DAsync per transfer into
-    IPC-mapped receiver buffers, IPC-event ordering, no host stream sync in steady state): ranks
-    share the box's GPU, and the output is bit-identical to the single-GPU run (direct convs)."""
+@pytest.mark.parametrize("np_,decomp,split,extra", [(2, "per_layer", "rows", []), (3, "per_layer", "rows", []),
+                                                    (4, "per_layer", "rows", ["--chunks", "2"]),
+                                                    (2, "overlap", "rows", []),
+                                                    (4, "per_layer", "auto", ["--peer-sync", "notes"]),
+                                                    (4, "per_layer", "hybrid", []), (3, "per_layer", "batch", [])])
+def test_native_v5_peer_transport(cuda, np_, decomp, split, extra):
+    """V5 on the native runtime with the peer transport (one hipMemcpy2DAsync per transfer into
+    IPC-mapped receiver buffers, device-side flag ordering, halo chunks on their own stream, no host
+    stream sync in steady state): ranks share the box's GPU, and the output is bit-identical to the
+    single-GPU run (direct convs)."""
     d = ["--conv2-algo", "direct", "--conv1-algo", "direct"]
     ref, _ = native(["--version", "v3", "--init", "rand", "--seed", "6", "--batch", "3", *d])
     # pipelined steady state (scatter / gather on a second stream) with --poison: every consumed
@@ -144,10 +147,11 @@ def test_native_v5_peer_transport(cuda, np_, decomp, split):
     for pipe in ("on", "off"):
         rec, out = native(["--version", "v5", "--transport", "peer", "--decomp", decomp, "--split", split, "--init",
                            "rand", "--seed", "6", "--batch", "3", "--iters", "4", "--lrn-alpha-mode", "raw",
-                           "--pipeline", pipe, "--poison", *d], np_)
-        assert set(rec["phases_warm"]) >= {"scatter", "halo_p1", "compute", "gather"}
+                           "--pipeline", pipe, "--poison", *extra, *d], np_)
+        assert set(rec["phases_warm"]) == {"scatter", "stage1", "halo_p1", "stage2", "gather"}
         assert "Final Output Shape: 13x13x256" in out.stdout or rec["shape"] == [13, 13, 256]
         assert rec["checksum"] == ref["checksum"], pipe
+        assert rec["v5"]["ordering"] == ("notes" if "notes" in extra else "flags")
     # default (Winograd) convs: equal to the fp64 oracle within fp32 error
     rec, _ = native(["--version", "v5", "--transport", "peer", "--init", "rand", "--seed", "6", "--batch", "3",
                      "--check"], np_)
