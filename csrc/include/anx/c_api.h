@@ -126,7 +126,7 @@ int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 
-/* ---- V5 multi-GPU runtime (libanx_dist.so: anx/v5.hpp) ----
+/* ---- V5 device-resident runtime (libanx_dist.so: anx/v5.hpp) ----
  * anx_v5_create is collective over the `world` ranks (TCP bootstrap at master_addr:master_port, then
  * the transport: RCCL or peer IPC). Weights are read on rank 0 only (others may pass NULL).
  * mode: 0 overlap, 1 per_layer; row_ways: -1 balanced, 0 batch first, r > 0 groups of r ranks;
@@ -149,6 +149,24 @@ int anx_v5_describe(void* h, char* buf, size_t cap);
  * gather), else the transfers rank `rank`'s transport issues, in order; one per line. */
 int anx_v5_schedule(int np, const anx_block_c* b1, const anx_block_c* b2, int H, int W, int batch, int row_ways,
                     int mode, int chunks, int rank, const char* transport, char* buf, size_t cap);
+
+/* ---- V4 host-staged runtime (libanx_dist.so: anx/v4.hpp) ----
+ * Collective create; the batch and the output live in a shared pinned host segment every rank maps
+ * (anx_v4_segment): write the input, call anx_v4_input_ready (collective), step, anx_v4_sync_all
+ * (collective), read the output. row_ways: -1 balanced, 0 batch first, r > 0 groups of r ranks. */
+int anx_v4_create(void** out, int rank, int world, int local_rank, int local_world, int nnodes,
+                  const char* master_addr, int master_port, double timeout_s, const anx_block_c* b1,
+                  const anx_block_c* b2, int H, int W, const float* w1, const float* bias1, const float* w2,
+                  const float* bias2, int batch, int row_ways, int chunks, int impl);
+int anx_v4_destroy(void* h);
+int anx_v4_segment(void* h, float** input, const float** output);
+int anx_v4_input_ready(void* h);
+int anx_v4_step(void* h, int steps);
+int anx_v4_sync_all(void* h);
+int anx_v4_phases(void* h, char* buf, size_t cap, int reset); /* h2d / compute / d2h ms per step */
+int anx_v4_describe(void* h, char* buf, size_t cap);
+/* GB/s of one H2D of this rank's whole share (its link alone, no compute): the H2D bound */
+int anx_v4_probe_h2d(void* h, int reps, double* gbps);
 
 /* ---- CPU reference ---- */
 int anx_cpu_conv2d(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C, int K, int F,

@@ -1,5 +1,5 @@
-// C ABI of the V5 runtime (anx/c_api.h, "V5 multi-GPU runtime"): libanx_dist.so, loaded by
-// anx._native.dist() for bench.py --workload v5 and anx.parallel.workloads.
+// C ABI of the multi-GPU runtimes (anx/c_api.h, "V4 / V5 multi-GPU runtimes"): libanx_dist.so, loaded
+// by anx._native.dist() for bench.py --workload v4|v5 and anx.parallel.workloads.
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -9,6 +9,7 @@
 #include <string>
 
 #include "anx/c_api.h"
+#include "anx/v4.hpp"
 #include "anx/v5.hpp"
 
 namespace {
@@ -61,6 +62,52 @@ anx::V5Options options(int batch, int row_ways, int mode, const char* transport,
   return o;
 }
 
+struct V4Handle {
+  std::unique_ptr<anx::HostComm> comm;
+  std::unique_ptr<anx::V4Runtime> rt;
+};
+V4Handle* H4(void* h) {
+  if (!h) throw std::invalid_argument("null v4 handle");
+  return static_cast<V4Handle*>(h);
+}
+
+anx::RankInfo rank_info(int rank, int world, int local_rank, int local_world, int nnodes, const char* master_addr,
+                        int master_port) {
+  anx::RankInfo ri;
+  ri.rank = rank;
+  ri.world = world;
+  ri.local_rank = local_rank;
+  ri.local_world = local_world;
+  ri.nnodes = nnodes;
+  ri.master_addr = master_addr ? master_addr : "127.0.0.1";
+  ri.master_port = master_port;
+  return ri;
+}
+
+anx::HostWeights root_weights(int rank, const anx::BlockSpec& s1, const anx::BlockSpec& s2, const float* w1,
+                              const float* bias1, const float* w2, const float* bias2) {
+  anx::HostWeights w;
+  if (rank == 0) {
+    if (!w1 || !bias1 || !w2 || !bias2) throw std::invalid_argument("rank 0 needs the weights");
+    anx::init_const(w, s1, s2);
+    std::memcpy(w.w1.data(), w1, w.w1.size() * 4);
+    std::memcpy(w.b1.data(), bias1, w.b1.size() * 4);
+    std::memcpy(w.w2.data(), w2, w.w2.size() * 4);
+    std::memcpy(w.b2.data(), bias2, w.b2.size() * 4);
+  }
+  return w;
+}
+
+std::string phases_json(const std::vector<std::pair<std::string, double>>& v) {
+  std::string s = "{";
+  char b[96];
+  for (size_t i = 0; i < v.size(); ++i) {
+    std::snprintf(b, sizeof b, "%s\"%s\": %.5f", i ? ", " : "", v[i].first.c_str(), v[i].second);
+    s += b;
+  }
+  return s + "}";
+}
+
 V5Handle* H(void* h) {
   if (!h) throw std::invalid_argument("null v5 handle");
   return static_cast<V5Handle*>(h);
@@ -77,29 +124,14 @@ int anx_v5_create(void** out, int rank, int world, int local_rank, int local_wor
                   int pipeline, int poison, int impl, const char* peer_sync) {
   return guarded("anx_v5_create", [&] {
     if (!out || !b1 || !b2) throw std::invalid_argument("null argument");
-    anx::RankInfo ri;
-    ri.rank = rank;
-    ri.world = world;
-    ri.local_rank = local_rank;
-    ri.local_world = local_world;
-    ri.nnodes = nnodes;
-    ri.master_addr = master_addr ? master_addr : "127.0.0.1";
-    ri.master_port = master_port;
+    const anx::RankInfo ri = rank_info(rank, world, local_rank, local_world, nnodes, master_addr, master_port);
     anx::V5Options o = options(batch, row_ways, mode, transport, chunks);
     o.pipeline = pipeline;
     o.poison = poison != 0;
     o.impl = impl ? anx::Impl::Direct : anx::Impl::Mfma;
     o.peer_sync = peer_sync ? peer_sync : "";
     const anx::BlockSpec s1 = spec(*b1), s2 = spec(*b2);
-    anx::HostWeights w;
-    if (rank == 0) {
-      if (!w1 || !bias1 || !w2 || !bias2) throw std::invalid_argument("rank 0 needs the weights");
-      anx::init_const(w, s1, s2);
-      std::memcpy(w.w1.data(), w1, w.w1.size() * 4);
-      std::memcpy(w.b1.data(), bias1, w.b1.size() * 4);
-      std::memcpy(w.w2.data(), w2, w.w2.size() * 4);
-      std::memcpy(w.b2.data(), bias2, w.b2.size() * 4);
-    }
+    const anx::HostWeights w = root_weights(rank, s1, s2, w1, bias1, w2, bias2);
     auto h = std::make_unique<V5Handle>();
     h->comm = std::make_unique<anx::HostComm>(ri, timeout_s > 0 ? timeout_s : 300.0);
     h->rt = std::make_unique<anx::V5Runtime>(*h->comm, ri, s1, s2, H, W, w, o);
@@ -147,15 +179,7 @@ int anx_v5_output(void* h, float* host_y) {
 int anx_v5_phases(void* h, char* buf, size_t cap, int reset) {
   return guarded("anx_v5_phases", [&] {
     anx::V5Runtime& rt = *H(h)->rt;
-    std::string s = "{";
-    char b[96];
-    bool first = true;
-    for (const auto& kv : rt.phase_ms()) {
-      std::snprintf(b, sizeof b, "%s\"%s\": %.5f", first ? "" : ", ", kv.first.c_str(), kv.second);
-      s += b;
-      first = false;
-    }
-    s += "}";
+    const std::string s = phases_json(rt.phase_ms());
     if (reset) rt.reset_phases();
     return put(s, buf, cap);
   });
@@ -180,6 +204,86 @@ int anx_v5_schedule(int np, const anx_block_c* b1, const anx_block_c* b2, int H,
     }
     return put(s, buf, cap);
   });
+}
+
+// ---------------------------------------------------------------------------------------------- V4
+int anx_v4_create(void** out, int rank, int world, int local_rank, int local_world, int nnodes,
+                  const char* master_addr, int master_port, double timeout_s, const anx_block_c* b1,
+                  const anx_block_c* b2, int H, int W, const float* w1, const float* bias1, const float* w2,
+                  const float* bias2, int batch, int row_ways, int chunks, int impl) {
+  return guarded("anx_v4_create", [&] {
+    if (!out || !b1 || !b2) throw std::invalid_argument("null argument");
+    const anx::RankInfo ri = rank_info(rank, world, local_rank, local_world, nnodes, master_addr, master_port);
+    anx::V4Options o;
+    o.batch = batch;
+    o.row_ways = row_ways;
+    o.chunks = chunks;
+    o.impl = impl ? anx::Impl::Direct : anx::Impl::Mfma;
+    const anx::BlockSpec s1 = spec(*b1), s2 = spec(*b2);
+    const anx::HostWeights w = root_weights(rank, s1, s2, w1, bias1, w2, bias2);
+    auto h = std::make_unique<V4Handle>();
+    h->comm = std::make_unique<anx::HostComm>(ri, timeout_s > 0 ? timeout_s : 300.0);
+    h->rt = std::make_unique<anx::V4Runtime>(*h->comm, ri, s1, s2, H, W, w, o);
+    *out = h.release();
+    return 0;
+  });
+}
+
+int anx_v4_destroy(void* h) {
+  return guarded("anx_v4_destroy", [&] {
+    std::unique_ptr<V4Handle> p(static_cast<V4Handle*>(h));
+    if (p) p->rt.reset();
+    return 0;
+  });
+}
+
+int anx_v4_segment(void* h, float** input, const float** output) {
+  return guarded("anx_v4_segment", [&] {
+    if (input) *input = H4(h)->rt->host_input();
+    if (output) *output = H4(h)->rt->host_output();
+    return 0;
+  });
+}
+
+int anx_v4_input_ready(void* h) {
+  return guarded("anx_v4_input_ready", [&] {
+    H4(h)->rt->input_ready();
+    return 0;
+  });
+}
+
+int anx_v4_step(void* h, int steps) {
+  return guarded("anx_v4_step", [&] {
+    for (int i = 0; i < steps; ++i) H4(h)->rt->step();
+    return 0;
+  });
+}
+
+int anx_v4_sync_all(void* h) {
+  return guarded("anx_v4_sync_all", [&] {
+    H4(h)->rt->sync_all();
+    return 0;
+  });
+}
+
+int anx_v4_phases(void* h, char* buf, size_t cap, int reset) {
+  return guarded("anx_v4_phases", [&] {
+    anx::V4Runtime& rt = *H4(h)->rt;
+    const std::string s = phases_json(rt.phase_ms());
+    if (reset) rt.reset_phases();
+    return put(s, buf, cap);
+  });
+}
+
+int anx_v4_probe_h2d(void* h, int reps, double* gbps) {
+  return guarded("anx_v4_probe_h2d", [&] {
+    *gbps = H4(h)->rt->probe_h2d_gbps(reps);
+    return 0;
+  });
+}
+
+int anx_v4_describe(void* h, char* buf, size_t cap) {
+  return guarded("anx_v4_describe", [&] { return put(H4(h)->rt->describe_json(), buf, cap); });
 }
 
 }  // extern "C"

@@ -118,6 +118,16 @@ _DIST_SIGS = {
     "anx_v5_output": (_I, [_P, _P]),
     "anx_v5_phases": (_I, [_P, C.c_char_p, _SZ, _I]),
     "anx_v5_describe": (_I, [_P, C.c_char_p, _SZ]),
+    "anx_v4_create": (_I, [C.POINTER(_P), _I, _I, _I, _I, _I, C.c_char_p, _I, C.c_double, C.POINTER(BlockC),
+                           C.POINTER(BlockC), _I, _I, _P, _P, _P, _P, _I, _I, _I, _I]),
+    "anx_v4_destroy": (_I, [_P]),
+    "anx_v4_segment": (_I, [_P, _P, _P]),
+    "anx_v4_input_ready": (_I, [_P]),
+    "anx_v4_step": (_I, [_P, _I]),
+    "anx_v4_sync_all": (_I, [_P]),
+    "anx_v4_phases": (_I, [_P, C.c_char_p, _SZ, _I]),
+    "anx_v4_describe": (_I, [_P, C.c_char_p, _SZ]),
+    "anx_v4_probe_h2d": (_I, [_P, _I, C.POINTER(C.c_double)]),
     "anx_v5_schedule": (_I, [_I, C.POINTER(BlockC), C.POINTER(BlockC), _I, _I, _I, _I, _I, _I, _I, C.c_char_p,
                              C.c_char_p, _SZ]),
 }

@@ -43,6 +43,19 @@ def _tile_c(t: TilePlan) -> nat.TileC:
                      t.out.lo, t.out.hi)
 
 
+def _check_hw_queues(lanes: int) -> None:
+    """HIP maps a process's streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default on
+    MI355X): two lanes on one queue serialise (0.80 vs 0.57 ms per 128-image step,
+    profiles/r02_lanes_async.txt). A lane model uses lanes + 1 streams (the caller's and its own)."""
+    import os
+    import warnings
+    q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    if q < lanes + 1:
+        warnings.warn(f"AlexNetBlocks(lanes={lanes}) uses {lanes + 1} streams but GPU_MAX_HW_QUEUES={q}: lanes "
+                      "sharing a hardware queue serialise (set GPU_MAX_HW_QUEUES >= 8 before the first GPU call, "
+                      "as bench.py does)", RuntimeWarning, stacklevel=3)
+
+
 class AlexNetBlocks:
     def __init__(self, weights: dict | None = None, *, init: str = "const", seed: int = 0, lrn_mode: str = "div_n",
                  groups2: int = 1, H: int = IN_H, W: int = IN_W, device="cuda", impl: str = "mfma",
@@ -67,14 +80,17 @@ class AlexNetBlocks:
         self.knobs = {k: knob_value(k, v) for k, v in (knobs or {}).items()}
         self._engine = None
         self._cap = 0
-        self._ensure(max_batch)
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
+        multi = lanes > 1 and self.is_cuda
+        per_lane = -(-max(1, max_batch) // lanes)
+        # lane 0's engine runs slice 0, or the whole batch when it is too small to split
+        self._ensure(max(per_lane, min(max_batch, lanes * LANE_MIN - 1)) if multi else max_batch)
         # side lanes (GPU only): engines for slices 1..L-1, each on its own stream; slice 0 runs here
         self._lanes: list[AlexNetBlocks] = []
         self._lane_streams: list[torch.cuda.Stream] = []
-        if lanes > 1 and self.is_cuda:
-            per_lane = -(-max(1, max_batch) // lanes)
+        if multi:
+            _check_hw_queues(lanes)
             for _ in range(lanes - 1):
                 self._lanes.append(AlexNetBlocks(self.weights, specs=(self.b1, self.b2), H=H, W=W, device=self.device,
                                                  impl=impl, max_batch=per_lane, knobs=self.knobs))
@@ -105,7 +121,7 @@ class AlexNetBlocks:
     def _ensure(self, n: int) -> None:
         if self._engine is not None and (n <= self._cap or not self.is_cuda):
             return
-        self.close()
+        self._close_engine()  # this engine only: the side lanes keep theirs
         h = C.c_void_p()
         w = self.weights
         args = (C.byref(nat.block_c(self.b1)), C.byref(nat.block_c(self.b2)), self.H, self.W, w["w1"].data_ptr(),
@@ -125,6 +141,9 @@ class AlexNetBlocks:
     def close(self) -> None:
         for m in getattr(self, "_lanes", ()):
             m.close()
+        self._close_engine()
+
+    def _close_engine(self) -> None:
         if self._engine is not None:
             if self.is_cuda:
                 torch.cuda.synchronize(self.device)

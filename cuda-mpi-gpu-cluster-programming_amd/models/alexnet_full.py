@@ -113,12 +113,26 @@ class AlexNetFull:
         except Exception:
             pass
 
+    def _check(self, x: torch.Tensor, out: torch.Tensor | None) -> torch.Tensor:
+        """The engine reads x and writes out through raw pointers: both must be exactly what the
+        kernels assume (shape, dtype, contiguity, device)."""
+        if (x.dim() != 4 or tuple(x.shape[1:]) != (227, 227, 3) or x.dtype != torch.float32 or not x.is_contiguous()
+                or x.device != self.device):
+            raise ValueError(f"expected contiguous fp32 NHWC [N,227,227,3] on {self.device}, got "
+                             f"{tuple(x.shape)} {x.dtype} on {x.device}")
+        shape = (x.shape[0], self.classes)
+        if out is None:
+            return torch.empty(shape, device=self.device)
+        if (tuple(out.shape) != shape or out.dtype != torch.float32 or not out.is_contiguous()
+                or out.device != self.device):
+            raise ValueError(f"out must be a contiguous fp32 {shape} tensor on {self.device}, got "
+                             f"{tuple(out.shape)} {out.dtype} on {out.device}")
+        return out
+
     def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """x: [N,227,227,3] fp32 NHWC on the device -> logits [N, classes] fp32."""
-        if tuple(x.shape[1:]) != (227, 227, 3) or x.dtype != torch.float32 or not x.is_contiguous():
-            raise ValueError("expected contiguous fp32 NHWC [N,227,227,3]")
+        y = self._check(x, out)
         N = x.shape[0]
-        y = out if out is not None else torch.empty(N, self.classes, device=self.device)
         L = 1 + len(self._lanes)
         if L == 1 or N < L:
             self._ensure(N)
@@ -143,6 +157,7 @@ class AlexNetFull:
         AlexNetBlocks.forward_async): lanes on their own streams, never joined per call; when all are
         idle they fork from the current stream and lane i starts at lane i-1's mid-forward mark
         (after Conv2 + Pool2/LRN), so they run half a forward apart. :meth:`join` before reading out."""
+        out = self._check(x, out)
         N = x.shape[0]
         L = 1 + len(self._lanes)
         if L == 1 or N < L or self.device.type != "cuda":

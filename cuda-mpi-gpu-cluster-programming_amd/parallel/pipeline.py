@@ -21,6 +21,10 @@ batch scale and MI355X-first:
   slice from its own stream; a lane waits, on its stream, for the gather that read the same output
   buffer two steps earlier. ``drain()`` joins the lanes.
 
+``inputs`` (local input only): a list of input batches used round-robin, step k computing
+``inputs[k % len(inputs)]`` — a benchmark streams distinct data through the engine instead of one
+cache-resident batch.
+
 Input semantics with prefetch: ``step()`` snapshots ``x_global`` as it is at the call (the scatter
 for the NEXT step is issued from it) and computes the batch snapshotted by the previous call (the
 first call computes its own snapshot). Writes to ``x_global`` after ``step()`` returns are safe when
@@ -85,6 +89,12 @@ class ScatterComputeGather:
             self._yb.append(torch.empty_like(self._yb[0]))
             self._gather_pending.append(None)
         self._lane_gathers = [dict() for _ in self._yb]  # per output buffer: lane -> gather work reading it
+        self.inputs: list | None = None  # local input only: batches used round-robin (see module doc)
+
+    def _local_input(self, default):
+        if self.inputs and not self.cfg.scatter:
+            return self.inputs[self._k % len(self.inputs)]
+        return default
 
     def _scatter(self, x):
         root = self.rank == 0
@@ -96,7 +106,7 @@ class ScatterComputeGather:
 
     def _step_prefetch(self) -> None:
         cur = self._k % 2
-        x, y = self._xb[cur], self._yb[cur]
+        x, y = self._local_input(self._xb[cur]), self._yb[cur]
         if self.cfg.scatter and self._scatter_pending is None:  # pipeline fill (first step only)
             self._scatter_pending = self._scatter(x)
         mine = self._scatter_pending or []
@@ -138,7 +148,7 @@ class ScatterComputeGather:
                 dst = [self.y_global[r, lo:hi] for r in range(self.world)] if self.rank == 0 else None
                 pend[i] = dist.gather(y[lo:hi], dst, dst=0, group=self.group, async_op=True)
 
-        self.model.forward_async(self.x, y, on_lane=on_lane, pre_lane=pre_lane)
+        self.model.forward_async(self._local_input(self.x), y, on_lane=on_lane, pre_lane=pre_lane)
         self.y = y
         self._k += 1
 
@@ -163,19 +173,22 @@ class ScatterComputeGather:
         if self.world == 1:
             if self.x_global is not None:
                 self.x.copy_(self.x_global[0])
-            self.model(self.x, out=self.y)
+            self.model(self._local_input(self.x), out=self.y)
             if self.y_global is not None:
                 self.y_global[0].copy_(self.y)
+            self._k += 1
             return
         root = self.rank == 0
         sw = self._scatter(self.x) if self.cfg.scatter else []
         gw = []
+        x = self._local_input(self.x)
         for i, (lo, hi) in enumerate(self.splits):
             if sw:
                 sw[i].wait()
-            self.model(self.x[lo:hi], out=self.y[lo:hi])
+            self.model(x[lo:hi], out=self.y[lo:hi])
             if self.cfg.gather:
                 dst = [self.y_global[r, lo:hi] for r in range(self.world)] if root else None
                 gw.append(dist.gather(self.y[lo:hi], dst, dst=0, group=self.group, async_op=True))
         for w in gw:
             w.wait()
+        self._k += 1

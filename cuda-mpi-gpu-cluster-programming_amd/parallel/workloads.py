@@ -249,6 +249,38 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def _launch(port):
+    """rank, world, local rank / world, nodes and the runtime's rendezvous port (chosen by rank 0 and
+    shared over torch.distributed when it is initialised, else `port` / ANX_V5_PORT)."""
+    import torch.distributed as tdist
+    up = tdist.is_available() and tdist.is_initialized()
+    if up:
+        rank, size = world()
+    else:  # a launcher's environment (torchrun / anxrun) without a torch process group
+        rank, size = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", size))
+    nnodes = max(1, size // max(1, local_world))
+    if port is None:
+        port = int(os.environ.get("ANX_V5_PORT", "0")) or (_free_port() if rank == 0 else 0)
+        if size > 1 and up:
+            box = [port]
+            tdist.broadcast_object_list(box, src=0)
+            port = box[0]
+        elif size > 1 and not os.environ.get("ANX_V5_PORT"):
+            raise ValueError("a native runtime at world > 1 needs torch.distributed, `port` or ANX_V5_PORT")
+    return rank, size, local_rank, local_world, nnodes, port
+
+
+def _root_weights(rank, weights):
+    if rank != 0:
+        return [None] * 4, None
+    if weights is None:
+        raise ValueError("rank 0 needs the weights")
+    w = {k: weights[k].detach().to("cpu", torch.float32).contiguous() for k in ("w1", "b1", "w2", "b2")}
+    return [w[k].data_ptr() for k in ("w1", "b1", "w2", "b2")], w
+
+
 class NativeV5:
     """V5 on GPUs through the native runtime (one instance per rank; construction is collective).
 
@@ -266,33 +298,12 @@ class NativeV5:
             raise ValueError(f"decomp must be one of {sorted(V5_DECOMPS)}")
         if layer not in (OVERLAP, PER_LAYER):
             raise ValueError("layer must be overlap or per_layer")
-        import torch.distributed as tdist
-        if tdist.is_available() and tdist.is_initialized():
-            self.rank, self.world = world()
-        else:  # a launcher's environment (torchrun / anxrun) without a torch process group
-            self.rank = int(os.environ.get("RANK", "0"))
-            self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank, self.world, local_rank, local_world, nnodes, port = _launch(port)
         self.batch, self.b1, self.b2, self.H, self.W = batch, specs[0], specs[1], H, W
         self.dims = blocks_dims(H, W, *specs)
-        local_rank = int(os.environ.get("LOCAL_RANK", self.rank))
-        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", self.world))
-        nnodes = max(1, self.world // max(1, local_world))
-        if port is None:
-            port = int(os.environ.get("ANX_V5_PORT", "0")) or (_free_port() if self.rank == 0 else 0)
-            if self.world > 1 and tdist.is_available() and tdist.is_initialized():
-                box = [port]
-                tdist.broadcast_object_list(box, src=0)
-                port = box[0]
-            elif self.world > 1 and not os.environ.get("ANX_V5_PORT"):
-                raise ValueError("NativeV5 at world > 1 needs torch.distributed, `port` or ANX_V5_PORT")
         rw = V5_DECOMPS[decomp]
         rw = self.world if rw is None else rw
-        ptrs = [None] * 4
-        if self.rank == 0:
-            if weights is None:
-                raise ValueError("rank 0 needs the weights")
-            self._w = {k: weights[k].detach().to("cpu", torch.float32).contiguous() for k in ("w1", "b1", "w2", "b2")}
-            ptrs = [self._w[k].data_ptr() for k in ("w1", "b1", "w2", "b2")]
+        ptrs, self._w = _root_weights(self.rank, weights)
         h = C.c_void_p()
         addr = os.environ.get("MASTER_ADDR", "127.0.0.1").encode()
         nat.dist_call("anx_v5_create", C.byref(h), self.rank, self.world, local_rank, local_world, nnodes, addr, port,
@@ -367,3 +378,84 @@ def native_schedule(np_: int, batch: int, row_ways: int = -1, layer: str = PER_L
                                          batch, row_ways, 1 if layer == PER_LAYER else 0, chunks, rank,
                                          transport.encode(), buf, len(buf)), "anx_v5_schedule")
     return [l for l in buf.value.decode().splitlines() if l]
+
+
+class NativeV4:
+    """V4 on GPUs through the native host-staged runtime (anx/v4.hpp; construction is collective):
+    the batch and the output live in one shared pinned host segment, every rank DMAs its own images x
+    input rows (halo included) from it and its output rows back, chunked so H2D / compute / D2H
+    overlap. ``x_host`` / ``y_host`` are zero-copy views of the segment."""
+
+    def __init__(self, batch: int, weights: dict | None, *, specs=(BLOCK1, BLOCK2), H: int = 227, W: int = 227,
+                 decomp: str = "auto", chunks: int = 0, impl: str = "mfma", port: int | None = None,
+                 timeout_s: float = 300.0):
+        import numpy as np
+        if decomp not in V5_DECOMPS:
+            raise ValueError(f"decomp must be one of {sorted(V5_DECOMPS)}")
+        self.rank, self.world, local_rank, local_world, nnodes, port = _launch(port)
+        self.batch, self.b1, self.b2, self.H, self.W = batch, specs[0], specs[1], H, W
+        d = self.dims = blocks_dims(H, W, *specs)
+        rw = V5_DECOMPS[decomp]
+        rw = self.world if rw is None else rw
+        ptrs, self._w = _root_weights(self.rank, weights)
+        h = C.c_void_p()
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1").encode()
+        nat.dist_call("anx_v4_create", C.byref(h), self.rank, self.world, local_rank, local_world, nnodes, addr, port,
+                      timeout_s, C.byref(nat.block_c(self.b1)), C.byref(nat.block_c(self.b2)), H, W, *ptrs, batch, rw,
+                      chunks, 0 if impl == "mfma" else 1)
+        self._h = h
+        pin, pout = C.POINTER(C.c_float)(), C.POINTER(C.c_float)()
+        nat.dist_call("anx_v4_segment", h, C.byref(pin), C.byref(pout))
+        self.x_host = torch.from_numpy(np.ctypeslib.as_array(pin, shape=(batch, H, W, d.C0)))
+        self.y_host = torch.from_numpy(np.ctypeslib.as_array(pout, shape=(batch, d.Hp2, d.Wp2, d.C2)))
+        self.version, self.layer = "v4", OVERLAP
+
+    def fill(self, x: torch.Tensor | None) -> None:
+        """Collective: rank 0 writes the global batch into the shared segment."""
+        if self.rank == 0:
+            if tuple(x.shape) != tuple(self.x_host.shape):
+                raise ValueError(f"expected {tuple(self.x_host.shape)}, got {tuple(x.shape)}")
+            self.x_host.copy_(x.detach().to("cpu", torch.float32))
+        nat.dist_call("anx_v4_input_ready", self._h)
+
+    def step(self, record: bool = False, steps: int = 1) -> None:
+        nat.dist_call("anx_v4_step", self._h, steps)
+
+    def sync(self) -> None:
+        """Collective: every rank's copies are done (the output segment is complete)."""
+        nat.dist_call("anx_v4_sync_all", self._h)
+
+    def output(self) -> torch.Tensor | None:
+        return self.y_host.clone() if self.rank == 0 else None
+
+    def _json(self, name, *extra) -> dict:
+        buf = C.create_string_buffer(4096)
+        nat.dist_call(name, self._h, buf, len(buf), *extra)
+        return json.loads(buf.value.decode())
+
+    def phase_ms(self, reset: bool = False) -> dict:
+        return {k: round(v, 4) for k, v in self._json("anx_v4_phases", int(reset)).items()}
+
+    def reset_phases(self) -> None:
+        self.phase_ms(reset=True)
+
+    def describe(self) -> dict:
+        return {"workload": "v4", "runtime": "native (anx/v4.hpp via libanx_dist)", **self._json("anx_v4_describe")}
+
+    def probe_h2d_gbps(self, reps: int = 5) -> float:
+        """This rank's host link alone: GB/s of one H2D of its whole share (syncs its streams)."""
+        v = C.c_double()
+        nat.dist_call("anx_v4_probe_h2d", self._h, reps, C.byref(v))
+        return v.value
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.x_host = self.y_host = None
+            nat.dist_call("anx_v4_destroy", self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass

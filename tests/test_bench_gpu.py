@@ -31,6 +31,12 @@ def test_bench_blocks_contract():
     c = rec["config"]
     assert rec["metric"] == metric and rec["dtype"] == "fp32" and c["global_batch"] == 64
     assert c["lanes"] == 2 and rec["vs_baseline"] > 1 and c["b1_warm_ms"] > 0
+    # unambiguous semantics: distinct input batches beyond the Infinity Cache, an engine-cold and a
+    # process-cold (fresh `anx --version v3` process) batch-1 latency next to the reference's 610.661 ms
+    assert c["input_batches_rotated"] >= 4 and c["input_bytes_rotated"] > (256 << 20)
+    assert c["b1_engine_cold_ms"] > c["b1_warm_ms"] and "b1_cold_ms" not in c
+    assert c["b1_process_cold_ms"] > c["b1_engine_cold_ms"] * 0.5 and c["b1_process_cold_vs_reference"] > 0
+    assert c["gpu_max_hw_queues"] == "8"
     # the matrix-core work actually executed stays below the fp32 MFMA peak; the direct-convolution
     # equivalent may not (Winograd does 4x fewer multiplies)
     assert 0 < c["mfma_tflops"] < 160
@@ -43,10 +49,19 @@ def test_bench_workloads_one_gpu(workload):
     rec = bench(["--workload", workload, "--batch", "16", "--no-b1"])
     c = rec["config"]
     assert rec["scaling"] == "strong" and c["global_batch"] == 16 and c["workload"] == workload
-    if workload == "v4":
-        assert c["phases_ms"]["compute"] > 0
+    if workload == "v4":  # the native host-staged runtime: chunked per-rank DMA, link rate reported
+        assert c["phases_ms"]["compute"] > 0 and c["h2d_gbps_link"] > 1 and 0 < c["h2d_bound_fraction"] < 1.5
+        assert c["chunks"] >= 1 and c["runtime"].startswith("native")
     else:  # the native runtime: critical-path phases, balanced layout, transport
         assert c["phases_ms"]["stage2"] > 0 and c["transport"] == "rccl" and c["imbalance"] == 1.0
+
+
+@pytest.mark.gpu
+def test_bench_v5_peer_transport_one_gpu():
+    """bench.py --workload v5 --transport peer (the IPC transport with device-side flags) at N=1."""
+    rec = bench(["--workload", "v5", "--transport", "peer", "--batch", "32", "--no-b1"])
+    c = rec["config"]
+    assert c["transport"] == "peer" and c["ordering"] == "flags" and c["phases_ms"]["stage2"] > 0
 
 
 @pytest.mark.gpu

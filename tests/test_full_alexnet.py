@@ -35,6 +35,27 @@ def test_full_alexnet_vs_torch(cuda, N, groups2):
     assert rel < 3e-2, rel
 
 
+@pytest.mark.gpu
+def test_full_alexnet_rejects_bad_buffers(cuda):
+    """forward / forward_async write through raw pointers: a wrong x or out is refused, never written."""
+    m = AlexNetFull(seed=5, device=cuda, max_batch=4, classes=10, lanes=2)
+    x = init_input(4, "rand", seed=5).to(cuda)
+    good = torch.empty(4, 10, device=cuda)
+    bad = [torch.empty(4, 11, device=cuda), torch.empty(3, 10, device=cuda), torch.empty(4, 10),
+           torch.empty(4, 10, device=cuda, dtype=torch.float16), torch.empty(10, 4, device=cuda).t()]
+    for out in bad:
+        for fn in (m.forward, m.forward_async):
+            with pytest.raises(ValueError):
+                fn(x, out)
+    for xb in (x.cpu(), x[:, :, :200], x.half(), x.permute(0, 2, 1, 3)):
+        with pytest.raises(ValueError):
+            m.forward(xb, good)
+    m.forward_async(x, good)
+    m.join()
+    torch.testing.assert_close(good, m(x), rtol=0, atol=0)
+    m.close()
+
+
 def _q(t):  # round to bf16, compute in fp64
     return t.to(torch.bfloat16).double()
 

@@ -7,7 +7,7 @@ balanced default decomposition stays within 10% of the mean work per rank.
 
 GPU: ranks sharing the box's one GPU (peer transport, device-side flags or host notes) run the
 pipelined, chunked schedule with every consumed buffer NaN-poisoned after use; the gathered output
-must equal the single-GPU engine's.
+must equal the single-GPU engine's. The native V4 runtime (anx/v4.hpp) likewise.
 """
 import os
 import socket
@@ -103,19 +103,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _v5_rank(rank, world, port, q, kw, batch, steps):
+def _v5_rank(rank, world, port, q, kw, batch, steps, kind="v5"):
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
     sys.path.insert(0, ROOT)
     import torch as T
     from anx.models.alexnet_blocks import AlexNetBlocks
-    from anx.parallel.workloads import NativeV5
+    from anx.parallel.workloads import NativeV4, NativeV5
     from anx.utils.init import init_input
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
     try:
         T.cuda.set_device(0)
         w = AlexNetBlocks(init="rand", seed=9, device="cpu", lrn_mode="raw").weights if rank == 0 else None
         from anx.config import blocks
-        wl = NativeV5(batch, w, specs=blocks("raw", 1), port=port, timeout_s=60, **kw)
+        wl = (NativeV5 if kind == "v5" else NativeV4)(batch, w, specs=blocks("raw", 1), port=port, timeout_s=60, **kw)
         wl.fill(init_input(batch, "rand", seed=9) if rank == 0 else None)
         wl.step(steps=steps)
         wl.sync()
@@ -128,12 +128,12 @@ def _v5_rank(rank, world, port, q, kw, batch, steps):
         q.put((rank, repr(e)))
 
 
-def _run_v5(world, kw, batch=6, steps=4):
+def _run_v5(world, kw, batch=6, steps=4, kind="v5"):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_v5_rank, args=(r, world, port, q, kw, batch, steps)) for r in range(world)]
+    procs = [ctx.Process(target=_v5_rank, args=(r, world, port, q, kw, batch, steps, kind)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(world))
@@ -174,3 +174,16 @@ def test_native_v5_shared_gpu(v5_reference, world, kw):
     assert set(phases) == {"scatter", "stage1", "halo_p1", "stage2", "gather"}
     if kw.get("transport") == "peer":
         assert desc["ordering"] == kw.get("peer_sync", "flags")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,kw", [(1, {}), (2, {}), (3, {"decomp": "rows", "chunks": 2}), (4, {"decomp": "hybrid"})])
+def test_native_v4_shared_gpu(v5_reference, world, kw):
+    """V4 through the native host-staged runtime (shared pinned segment, per-rank chunked H2D / tile /
+    D2H on three streams, parity buffers across steps) on ranks sharing the GPU."""
+    y, desc, phases = _run_v5(world, kw, kind="v4")
+    y = torch.from_numpy(y)
+    err = (y - v5_reference).abs().max().item() / v5_reference.abs().max().item()
+    assert err < 1e-5, (err, desc)
+    assert set(phases) == {"h2d", "compute", "d2h"} and phases["h2d"] > 0
+    assert desc["runtime"].startswith("native") and desc["h2d_bytes_per_step_rank"] > 0
