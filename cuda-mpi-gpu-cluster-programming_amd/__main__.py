@@ -80,11 +80,15 @@ def cmd_launch(a, rest):
 
 
 def cmd_plan(a):
-    from .parallel.plan import conv1_redundancy, hybrid_conv1_redundancy, make_hybrid_plan, make_plan
+    from .parallel.plan import balanced_row_ways, conv1_redundancy, make_hybrid_plan, make_plan, plan_stats
     if a.batch is not None:  # hybrid batch x rows plan
-        hp = make_hybrid_plan(227, 227, a.np, a.batch, a.row_ways, a.decomp)
-        print(f"np {a.np} batch {a.batch}: {hp.groups} group(s); redundant conv1 rows "
-              f"{100 * hybrid_conv1_redundancy(hp):.1f}% of one device's")
+        rw = balanced_row_ways(a.np, a.batch) if a.row_ways < 0 else a.row_ways
+        hp = make_hybrid_plan(227, 227, a.np, a.batch, rw, a.decomp)
+        st = plan_stats(hp)
+        print(f"np {a.np} batch {a.batch}: {hp.groups} group(s) of {st['row_ways']} rank(s) (row_ways {rw}"
+              f"{' = balanced default' if a.row_ways < 0 else ''}); output rows per rank max {st['out_rows_max']} / "
+              f"mean {st['out_rows_mean']:.3f}; work max/mean {st['imbalance']:.3f}; redundant conv1 rows "
+              f"{100 * st['conv1_redundancy']:.1f}% of one device's")
         for r in range(a.np):
             t, im = hp.tile(r), hp.images_of(r)
             print(f"rank {r}: group {hp.group_of[r]} ({hp.group_size[hp.group_of[r]]} ranks) images "
@@ -113,7 +117,8 @@ def main(argv=None):
     pp.add_argument("--np", "-n", type=int, default=4)
     pp.add_argument("--decomp", default="overlap", choices=["overlap", "per_layer"])
     pp.add_argument("--batch", "-b", type=int, default=None, help="hybrid batch x rows plan for this many images")
-    pp.add_argument("--row-ways", type=int, default=0, help="ranks per image group (0 = auto: batch first)")
+    pp.add_argument("--row-ways", type=int, default=-1,
+                    help="ranks per image group (-1 = the V4/V5 runtimes' balanced default, 0 = batch first)")
     sub.add_parser("bench")
     if argv and argv[0] == "launch":
         a, rest = ap.parse_known_args(argv)
