@@ -17,7 +17,8 @@ hipError_t launch(const wg::Args& a0, hipStream_t s, int occ) {
   if (attr != hipSuccess) return attr;
   wg::Args a = a0;
   a.n_ptiles = (a.P + G::BM - 1) / G::BM;
-  if (a.n_ntiles < 1 || a.u_rows < a.n_ntiles * G::BN) return hipErrorInvalidValue;
+  a.n_ntiles = a.kg / G::BN;
+  if (a.kg % G::BN || a.n_ntiles < 1 || a.u_rows < a.n_ntiles * G::BN) return hipErrorInvalidValue;
   const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
   wg::gemm_kernel<G, ABL><<<grid, G::NT, occupancy_lds(G::kLdsBytes, occ), s>>>(a);
   return hipGetLastError();
@@ -29,9 +30,9 @@ using C2g = wg::Cfg<49, 48, 2, 2, 48, 2>;   // Conv2 with 2 groups (48 channels 
 using C1 = wg::Cfg<25, 48, 2, 1, 48, 2>;    // Conv1: 64 tiles x 32 filters, 2 waves, 4 workgroups per CU
 #ifdef ANX_WGEMM_ABLATIONS
 using C2_32x4 = wg::Cfg<49, 96, 2, 2, 32, 4>;    // 64 KiB ring: 2 slices in flight behind the current one
-using C2_16x6 = wg::Cfg<49, 96, 2, 2, 16, 6>;    // 48 KiB ring
-using C1_16x6w4 = wg::Cfg<25, 48, 4, 1, 16, 6>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
-using C1_16x6w2 = wg::Cfg<25, 48, 2, 1, 16, 6>;  // 64 x 32, 2 waves, 36 KiB ring, 4 per CU
+using C2_64x128 = wg::Cfg<49, 96, 2, 4, 48, 2>;  // 64 tiles x 128 filters, 8 waves, 72 KiB ring
+using C1_64x96 = wg::Cfg<25, 48, 2, 3, 48, 2>;   // 64 x 96 (every filter: V read once), 6 waves, 60 KiB ring
+using C1_32x96 = wg::Cfg<25, 48, 1, 3, 48, 2>;   // 32 x 96, 3 waves, 48 KiB ring
 using C1_48x2w4 = wg::Cfg<25, 48, 4, 1, 48, 2>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
 #endif
 
@@ -40,9 +41,8 @@ hipError_t launch_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
   switch (abl) {
     case 0: return launch<G, 0>(a, s, occ);
 #ifdef ANX_WGEMM_ABLATIONS
-    case 1: return launch<G, 1>(a, s, occ);
-    case 2: return launch<G, 2>(a, s, occ);
     case 3: return launch<G, 3>(a, s, occ);
+    case 32: return launch<G, 32>(a, s, occ);
 #endif
     default: return hipErrorInvalidValue;
   }
@@ -70,7 +70,7 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
     a.tx = tx;
     a.Ho = Ho;
     a.Wo = Wo;
-    a.n_ntiles = Kg / 64;
+    a.kg = Kg;
     a.u_rows = K;  // rows (ab*groups + g)*Kg + k: a point's rows of every group
     a.vct = C;
     a.vbytes = static_cast<int>(vb - g * Cg * 4);
@@ -84,7 +84,7 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
         case 0: e = launch_abl<C2>(a, s, occ, abl); break;
 #ifdef ANX_WGEMM_ABLATIONS
         case 1: e = launch_abl<C2_32x4>(a, s, occ, abl); break;
-        case 3: e = launch_abl<C2_16x6>(a, s, occ, abl); break;
+        case 2: e = launch_abl<C2_64x128>(a, s, occ, abl); break;
 #endif
         default: break;
       }
@@ -96,7 +96,7 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
                            int Wo, int K, bool relu, hipStream_t s, int occ, int abl, int cfg) {
   const long vb = static_cast<long>(P) * 25 * 48 * 4, ub = static_cast<long>(25) * K * 48 * 4;
-  if (vb >= (1L << 31) || ub >= (1L << 31) || K % 32 || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
+  if (vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
   if (P == 0) return hipSuccess;
   wg::Args a{};
   a.V = V;
@@ -108,7 +108,7 @@ hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, Ou
   a.tx = tx;
   a.Ho = Ho;
   a.Wo = Wo;
-  a.n_ntiles = K / 32;
+  a.kg = K;
   a.u_rows = K;
   a.vct = 48;
   a.vbytes = static_cast<int>(vb);
@@ -117,8 +117,8 @@ hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, Ou
   switch (cfg < 0 ? 0 : cfg) {
     case 0: return launch_abl<C1>(a, s, occ, abl);
 #ifdef ANX_WGEMM_ABLATIONS
-    case 1: return launch_abl<C1_16x6w4>(a, s, occ, abl);
-    case 2: return launch_abl<C1_16x6w2>(a, s, occ, abl);
+    case 1: return launch_abl<C1_64x96>(a, s, occ, abl);
+    case 2: return launch_abl<C1_32x96>(a, s, occ, abl);
     case 3: return launch_abl<C1_48x2w4>(a, s, occ, abl);
 #endif
     default: return hipErrorInvalidValue;

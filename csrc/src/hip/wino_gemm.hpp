@@ -55,7 +55,8 @@ struct Args {
   const float* bias;  // [K]
   OutView out;        // conv output (NHWC through a view)
   int P, ty, tx, Ho, Wo;
-  int n_ptiles, n_ntiles;
+  int n_ptiles, n_ntiles;  // set by the launcher from P and kg
+  int kg;                  // filters of this launch (one conv group): n_ntiles = kg / BN
   int u_rows;          // filter rows per point in U (>= n_ntiles * BN)
   int vct;             // V floats per (tile, point): C, or groups * C
   int vbytes, ubytes;  // buffer sizes (< 2^31)
@@ -136,11 +137,13 @@ __device__ __forceinline__ void wait_vm_lgkm() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
 }
 // ABL (A/B tool only; production instantiates 0): bit0 no fold, bit1 no DMA refills, bit2 no barrier,
-// bit3 packed v_pk_fma_f32 fold instead of scalar, bit4 no sched_group_barrier pinning.
+// bit3 packed v_pk_fma_f32 fold instead of scalar, bit4 no sched_group_barrier pinning, bit5 no epilogue
+// stores (the outputs are computed, never written).
 template <class G, int ABL>
 __global__ void __launch_bounds__(G::NT, 2) gemm_kernel(Args a) {
   constexpr int NPT = G::NPT, KS = G::KS, BK = G::BK, NW = G::NW, NST = G::NST, U4 = G::U4, MF = G::MF;
   constexpr bool kFold = !(ABL & 1), kDma = !(ABL & 2), kBar = !(ABL & 4), kPk = (ABL & 8) != 0, kPin = !(ABL & 16);
+  constexpr bool kStore = !(ABL & 32);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: the DMA M0 values stay scalar
@@ -345,7 +348,7 @@ __global__ void __launch_bounds__(G::NT, 2) gemm_kernel(Args a) {
     for (int k = 0; k < 4; ++k) {
       const f32x4 v4 = *reinterpret_cast<const f32x4*>(tr + ((k * 64 + lane) >> 3) * kTS + grp);
       const int oy = oy0[k] + q / 3, ox = ox0[k] + q % 3;
-      if (oy < a.Ho && ox < a.Wo)
+      if (oy < a.Ho && ox < a.Wo && (kStore || v4.x == -1.f))  // ABL 32: ReLU outputs are never -1
         *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(img[k] * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) *
                                                o.Cb + o.c_off + fb + grp) = v4;
     }

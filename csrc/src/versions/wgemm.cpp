@@ -19,8 +19,8 @@
 #include <vector>
 
 namespace {
-// ablations (wino_gemm.hpp): 0 full kernel, 1 no fold, 3 no fold + no DMA
-constexpr int kAbl[] = {0, 1, 3};
+// ablations (wino_gemm.hpp): 0 full kernel, 3 no fold + no DMA, 32 no epilogue stores
+constexpr int kAbl[] = {0, 3, 32};
 #define CHECK(x)                                                                     \
   do {                                                                               \
     hipError_t e_ = (x);                                                             \
