@@ -98,8 +98,6 @@ class BlocksEngine {
   // Winograd conv1: transformed polyphase weights + V workspace (full-height tiles of chunk_ images)
   float *u1w_ = nullptr, *wv1_ = nullptr;
   size_t wv1_cap_ = 0;
-  // 4x4-tile variants' transformed weights (knobs conv1_tile / conv2_tile = 4), built on first use
-  float *u1w4_ = nullptr, *u2w4_ = nullptr;
   std::vector<float> w1h_, w2h_;  // KCFF host copies for re-packing on geometry change
 };
 

@@ -31,13 +31,10 @@ struct Knobs {
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
   int conv1_occ = 0;       // cap on the Conv1 Winograd GEMM's workgroups per CU (LDS padding; 0 = none: 4)
   int conv2_occ = 0;       // ... and Conv2's (0 = none: 2); a cap leaves room for a concurrent lane's kernels
-  int conv1_tile = 3;      // Winograd output tile edge: 3 (F(3x3,3x3), wino_gemm.hpp) or 4 (F(4x4,3x3), wino_gemm16.hpp)
-  int conv2_tile = 3;      // 3 (F(3x3,5x5)) or 4 (F(4x4,5x5); one group only, else 3)
 };
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
-// ANX_BF16_GLDS, ANX_BF16_BIG, ANX_BF16_FC, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_TILE,
-// ANX_CONV2_TILE when set.
+// ANX_BF16_GLDS, ANX_BF16_BIG, ANX_BF16_FC, ANX_CONV1_OCC, ANX_CONV2_OCC when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

@@ -87,23 +87,16 @@ void pack_conv_weights_host(const ConvPlan& p, const float* w_kcff, std::vector<
 hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, const int* koff,
                        const float* bias, OutView out, bool relu, hipStream_t s);
 
-// Winograd F(mxm,5x5) for stride-1 5x5 convolutions over a pre-padded input window (winograd.hip):
-// m = 3 (7x7 transform tiles, 49 points; any group count) or m = 4 (8x8 tiles, 64 points, one group:
-// wino_gemm16.hpp).
+// Winograd F(3x3,5x5) for stride-1 5x5 convolutions over a pre-padded input window (winograd.hip).
 struct WinoPlan {
   int N, Hq, Wq, C, K, groups;
-  int Ho, Wo, ty, tx, P;  // output dims, mxm tiles per column/row, total tiles
-  int m = 3;              // output tile edge
-  int n() const { return m + 4; }
-  int pts() const { return n() * n(); }
+  int Ho, Wo, ty, tx, P;  // output dims, 3x3 tiles per column/row, total tiles
 };
 // 96 or 48 channels per group and a multiple of 64 filters per group (the fused GEMM's shapes)
 bool wino_eligible(int F, int S, int C, int K, int groups);
-// m = 4 is eligible for 96 channels, one group, a multiple of 32 filters
-bool wino4_eligible(int C, int K, int groups);
-WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups, int m = 3);
-size_t wino_v_floats(const WinoPlan& w);  // V workspace [P][points][C]
-size_t wino_u_floats(const WinoPlan& w);  // transformed weights [points][K][C/groups]
+WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups);
+size_t wino_v_floats(const WinoPlan& w);  // V workspace [P][49][C]
+size_t wino_u_floats(const WinoPlan& w);  // transformed weights [49][K][C/groups]
 // U[(ab*groups + g)*Kg + k][c] = (G g G^T)[a][b] in fp64, rounded once.
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s);
@@ -112,21 +105,17 @@ hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,
                       hipStream_t s, const Knobs& k);
 
-// Conv1 (stride 4, C = 3, 8 < F <= 12, no padding) as Winograd F(mxm,3x3) on the polyphase image
-// (conv1_wino.hip): 48 polyphase channels; m = 3 (5x5 transform tiles, 25 points) or m = 4 (6x6, 36
-// points: wino_gemm16.hpp).
+// Conv1 (stride 4, C = 3, 8 < F <= 12, no padding) as Winograd F(3x3,3x3) on the polyphase image
+// (conv1_wino.hip): 48 polyphase channels, 3x3 output tiles, 25 transform points.
 struct Conv1WinoPlan {
   int N, Hin, W, K, F;
-  int H1, W1, ty, tx, P;  // output dims, mxm tiles per column/row, total tiles
-  int m = 3;              // output tile edge
-  int n() const { return m + 2; }
-  int pts() const { return n() * n(); }
+  int H1, W1, ty, tx, P;  // output dims, 3x3 tiles per column/row, total tiles
 };
 bool conv1_wino_eligible(int C, int K, int F, int S, int P, int groups);
-Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F, int m = 3);
-size_t conv1_wino_v_floats(const Conv1WinoPlan& w);  // V workspace [P][points][48]
-size_t conv1_wino_u_floats(int K, int m = 3);        // transformed weights [points][K][48]
-void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u, int m = 3);
+Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F);
+size_t conv1_wino_v_floats(const Conv1WinoPlan& w);  // V workspace [P][25][48]
+size_t conv1_wino_u_floats(int K);                   // transformed weights [25][K][48]
+void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u);
 // x: [N, Hin, W, 3] image rows; writes conv1 (+bias, optional ReLU) through `out`. Knobs: conv1_occ.
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
                       bool relu, hipStream_t s, const Knobs& k);
@@ -141,13 +130,6 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
                            int cfg = -1);
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
                            int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
-// The 4x4-tile GEMMs (wino_gemm16.hpp): Conv2 F(4x4,5x5) (64 points, C = 96, one group) and Conv1
-// polyphase F(4x4,3x3) (36 points, 48 channels); K a multiple of 32.
-hipError_t wino4_gemm_conv2(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
-                            int Ho, int Wo, int C, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0,
-                            int cfg = -1);
-hipError_t wino4_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
-                            int Ho, int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
 
 // Dynamic LDS bytes that cap a kernel at `wgs` workgroups per CU (160 KiB LDS per CU): the larger of
 // `natural` and just over 160 KiB / (wgs + 1). wgs <= 0: `natural`.

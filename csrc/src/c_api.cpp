@@ -435,10 +435,9 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
                    float* y, int relu, void* stream) {
   return guarded("anx_conv1_wino", [&] {
     if (!anx::hip::conv1_wino_eligible(3, K, F, 4, 0, 1)) return fail("anx_conv1_wino: shape not eligible");
-    const anx::Knobs kn = anx::default_knobs();  // ANX_CONV1_TILE picks the 3x3 or 4x4 tile
-    const auto w = anx::hip::make_conv1_wino_plan(N, Hin, W, K, F, kn.conv1_tile);
+    const auto w = anx::hip::make_conv1_wino_plan(N, Hin, W, K, F);
     std::vector<float> u;
-    anx::hip::conv1_wino_weights_host(K, F, w_kcff, u, w.m);
+    anx::hip::conv1_wino_weights_host(K, F, w_kcff, u);
     float *dv = nullptr, *du = nullptr;
     if (hipMalloc(reinterpret_cast<void**>(&dv), std::max<size_t>(anx::hip::conv1_wino_v_floats(w), 1) * 4) != hipSuccess)
       return fail("anx_conv1_wino: hipMalloc");
@@ -449,7 +448,7 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
     hipError_t e = hipMemcpy(du, u.data(), u.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess)
       e = anx::hip::conv1_wino(w, x, dv, du, bias, anx::hip::OutView{y, w.H1, w.W1, K, 0, 0, 0}, relu != 0, S(stream),
-                               kn);
+                               anx::default_knobs());
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));  // the workspaces are freed below
     (void)hipFree(dv);
     (void)hipFree(du);
@@ -461,9 +460,7 @@ int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_
                    const float* bias, float* y, int relu, void* stream) {
   return guarded("anx_conv2_wino", [&] {
     if (!anx::hip::wino_eligible(5, 1, C, K, groups)) return fail("anx_conv2_wino: shape not eligible");
-    const anx::Knobs kn = anx::default_knobs();  // ANX_CONV2_TILE picks the 3x3 or 4x4 tile
-    const int m = kn.conv2_tile == 4 && anx::hip::wino4_eligible(C, K, groups) ? 4 : 3;
-    const auto w = anx::hip::make_wino_plan(N, Hq, Wq, C, K, groups, m);
+    const auto w = anx::hip::make_wino_plan(N, Hq, Wq, C, K, groups);
     std::vector<float> u;
     anx::hip::wino_transform_weights_host(w, w_kcff, u);
     float *dv = nullptr, *du = nullptr;
@@ -476,7 +473,8 @@ int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_
     hipError_t e = hipMemcpy(du, u.data(), u.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = anx::hip::wino_input(w, x, dv, S(stream));
     if (e == hipSuccess)
-      e = anx::hip::wino_conv2(w, dv, du, bias, anx::hip::OutView{y, w.Ho, w.Wo, K, 0, 0, 0}, relu != 0, S(stream), kn);
+      e = anx::hip::wino_conv2(w, dv, du, bias, anx::hip::OutView{y, w.Ho, w.Wo, K, 0, 0, 0}, relu != 0, S(stream),
+                               anx::default_knobs());
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));  // the workspaces are freed below
     (void)hipFree(dv);
     (void)hipFree(du);

@@ -113,8 +113,7 @@ BlocksEngine::~BlocksEngine() {
                   static_cast<void*>(b2d_), static_cast<void*>(w1p_), static_cast<void*>(w2p_),
                   static_cast<void*>(koff1_), static_cast<void*>(koff2_), static_cast<void*>(c1_),
                   static_cast<void*>(q2_), static_cast<void*>(c2_), static_cast<void*>(u2w_),
-                  static_cast<void*>(wv_), static_cast<void*>(u1w_), static_cast<void*>(wv1_),
-                  static_cast<void*>(u1w4_), static_cast<void*>(u2w4_)})
+                  static_cast<void*>(wv_), static_cast<void*>(u1w_), static_cast<void*>(wv1_)})
     if (p) (void)hipFree(p);
 }
 
@@ -138,15 +137,9 @@ hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, 
   const ConvSpec& k1 = b1_.conv;
   const hip::OutView c1v{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0};
   if (impl_ == Impl::Mfma && wv1_ != nullptr && use_winograd(k_.conv1_algo, n, t.c1.size(), d_.H1)) {
-    const int m = k_.conv1_tile == 4 ? 4 : 3;
-    const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F, m);
+    const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
     if (hip::conv1_wino_v_floats(w) > wv1_cap_) return hipErrorInvalidValue;
-    if (m == 4 && !u1w4_) {  // first use of the 4x4-tile variant: transform its weights once
-      std::vector<float> u;
-      hip::conv1_wino_weights_host(k1.K, k1.F, w1h_.data(), u, 4);
-      u1w4_ = dev_upload(u);
-    }
-    return hip::conv1_wino(w, xc, wv1_, m == 4 ? u1w4_ : u1w_, b1d_, c1v, true, s, k_);
+    return hip::conv1_wino(w, xc, wv1_, u1w_, b1d_, c1v, true, s, k_);
   }
   if (impl_ == Impl::Mfma) {
     const hip::ConvPlan p =
@@ -194,16 +187,10 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
   const ConvSpec& k2 = b2_.conv;
   const hip::OutView c2v{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
   if (impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(k_.conv2_algo, n, t.c2.size(), d_.H2)) {
-    const int m = k_.conv2_tile == 4 && hip::wino4_eligible(d_.C1, k2.K, k2.groups) ? 4 : 3;
-    const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups, m);
+    const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
     if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
-    if (m == 4 && !u2w4_) {  // first use of the 4x4-tile variant: transform its weights once
-      std::vector<float> u;
-      hip::wino_transform_weights_host(w, w2h_.data(), u);
-      u2w4_ = dev_upload(u);
-    }
     ANX_TRY(hip::wino_input(w, qc, wv_, s));
-    ANX_TRY(hip::wino_conv2(w, wv_, m == 4 ? u2w4_ : u2w_, b2d_, c2v, true, s, k_));
+    ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
   } else if (impl_ == Impl::Mfma) {
     const hip::ConvPlan p =
         hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups, k_.force_vec4, k_.force_scalar);

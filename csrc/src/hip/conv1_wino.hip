@@ -25,7 +25,6 @@
 
 #include "anx/ops.hpp"
 #include "anx/winograd_f33.hpp"
-#include "anx/winograd_f43.hpp"
 
 namespace anx::hip {
 namespace {
@@ -104,71 +103,6 @@ __global__ void __launch_bounds__(kT) conv1_wino_in_kernel(const float* __restri
   }
 }
 
-// Polyphase F(4x4,3x3) input transform: thread = (tile p, phase row rh, 8-B unit j of the 12 (rw, c)
-// floats): at each of the 6x6 X' positions of the tile, unit j of phase row rh is 2 floats of one
-// image row. 72 transform registers; X' positions past the image (the 56th output row / column of
-// the 14x14 tile grid over 55x55, and the missing phase columns of X' column 56) read zeros.
-__global__ void __launch_bounds__(kT) conv1_wino4_in_kernel(const float* __restrict__ x, float* __restrict__ V,
-                                                            int total, int Hin, int rowf, int ty, int tx) {
-  namespace w43 = anx::wino43;
-  using f32x2 = __attribute__((ext_vector_type(2))) float;
-  constexpr int n6 = w43::kN, pitch = w43::kM * kPh;  // 6x6 transform tile, 16 image rows/cols between tiles
-  for (int i = blockIdx.x * kT + threadIdx.x; i < total; i += gridDim.x * kT) {
-    const int q = i % 24;
-    const int p = i / 24;
-    const int rh = q / 6, j = q - rh * 6;
-    const int tj = p % tx;
-    const int pq = p / tx;
-    const int ti = pq % ty;
-    const int n = pq / ty;
-    const float* img = x + static_cast<size_t>(n) * Hin * rowf;
-    f32x2 t[n6][n6];
-#pragma unroll
-    for (int a = 0; a < n6; ++a)
-#pragma unroll
-      for (int v = 0; v < n6; ++v) t[a][v] = f32x2{0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < n6; ++u) {
-      const int row = ti * pitch + kPh * u + rh;
-      f32x2 d[n6];
-#pragma unroll
-      for (int v = 0; v < n6; ++v) {
-        const int o = (tj * pitch + kPh * v) * 3 + 2 * j;  // even float offset: 8-B aligned
-        d[v] = f32x2{0.f, 0.f};
-        if (row < Hin) {
-          const float* src = img + static_cast<size_t>(row) * rowf + o;
-          if (o + 2 <= rowf)
-            d[v] = *reinterpret_cast<const f32x2*>(src);
-          else if (o < rowf)
-            d[v].x = src[0];
-        }
-      }
-#pragma unroll
-      for (int a = 0; a < n6; ++a)
-        if (w43::kBT[a][u] != 0.f)
-#pragma unroll
-          for (int v = 0; v < n6; ++v) {
-            t[a][v].x = fmaf(w43::kBT[a][u], d[v].x, t[a][v].x);
-            t[a][v].y = fmaf(w43::kBT[a][u], d[v].y, t[a][v].y);
-          }
-    }
-    float* out = V + static_cast<size_t>(p) * (n6 * n6) * kCh + rh * 12 + 2 * j;
-#pragma unroll
-    for (int a = 0; a < n6; ++a)
-#pragma unroll
-      for (int b = 0; b < n6; ++b) {
-        f32x2 s2 = f32x2{0.f, 0.f};
-#pragma unroll
-        for (int v = 0; v < n6; ++v)
-          if (w43::kBT[b][v] != 0.f) {
-            s2.x = fmaf(w43::kBT[b][v], t[a][v].x, s2.x);
-            s2.y = fmaf(w43::kBT[b][v], t[a][v].y, s2.y);
-          }
-        *reinterpret_cast<f32x2*>(out + (a * n6 + b) * kCh) = s2;
-      }
-  }
-}
-
 }  // namespace
 
 bool conv1_wino_eligible(int C, int K, int F, int S, int P, int groups) {
@@ -176,9 +110,8 @@ bool conv1_wino_eligible(int C, int K, int F, int S, int P, int groups) {
   return C == 3 && S == kPh && P == 0 && groups == 1 && F > 2 * kPh && F <= 3 * kPh && K > 0 && K % kBN == 0;
 }
 
-Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F, int m) {
+Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F) {
   Conv1WinoPlan w{};
-  w.m = m == 4 ? 4 : 3;
   w.N = N;
   w.Hin = Hin;
   w.W = W;
@@ -186,20 +119,18 @@ Conv1WinoPlan make_conv1_wino_plan(int N, int Hin, int W, int K, int F, int m) {
   w.F = F;
   w.H1 = conv_out_dim(Hin, F, kPh, 0);
   w.W1 = conv_out_dim(W, F, kPh, 0);
-  w.ty = (w.H1 + w.m - 1) / w.m;
-  w.tx = (w.W1 + w.m - 1) / w.m;
+  w.ty = (w.H1 + 2) / 3;
+  w.tx = (w.W1 + 2) / 3;
   w.P = N * w.ty * w.tx;
   return w;
 }
 
-size_t conv1_wino_v_floats(const Conv1WinoPlan& w) { return static_cast<size_t>(w.P) * w.pts() * kCh; }
-size_t conv1_wino_u_floats(int K, int m) { return static_cast<size_t>((m + 2) * (m + 2)) * K * kCh; }
+size_t conv1_wino_v_floats(const Conv1WinoPlan& w) { return static_cast<size_t>(w.P) * kPts * kCh; }
+size_t conv1_wino_u_floats(int K) { return static_cast<size_t>(kPts) * K * kCh; }
 
-void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u, int m) {
+void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u) {
   // U[ab][k][ch] = (G W'_{k,ch} G^T)[a][b], fp64 then rounded once
-  const int nt = m == 4 ? 6 : kN5;
-  auto G = [&](int a, int q) { return m == 4 ? anx::wino43::kG[a][q] : w33::kG[a][q]; };
-  u.assign(conv1_wino_u_floats(K, m), 0.f);
+  u.assign(conv1_wino_u_floats(K), 0.f);
   for (int k = 0; k < K; ++k)
     for (int ch = 0; ch < kCh; ++ch) {
       const int rh = ch / 12, rw = (ch % 12) / 3, c = ch % 3;
@@ -209,18 +140,18 @@ void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<floa
           const int fh = kPh * qh + rh, fw = kPh * qw + rw;
           g[qh][qw] = (fh < F && fw < F) ? w_kcff[((static_cast<size_t>(k) * 3 + c) * F + fh) * F + fw] : 0.0;
         }
-      double tmp[6][3];
-      for (int a = 0; a < nt; ++a)
+      double tmp[kN5][3];
+      for (int a = 0; a < kN5; ++a)
         for (int qw = 0; qw < 3; ++qw) {
           double s = 0;
-          for (int qh = 0; qh < 3; ++qh) s += G(a, qh) * g[qh][qw];
+          for (int qh = 0; qh < 3; ++qh) s += w33::kG[a][qh] * g[qh][qw];
           tmp[a][qw] = s;
         }
-      for (int a = 0; a < nt; ++a)
-        for (int b = 0; b < nt; ++b) {
+      for (int a = 0; a < kN5; ++a)
+        for (int b = 0; b < kN5; ++b) {
           double s = 0;
-          for (int qw = 0; qw < 3; ++qw) s += tmp[a][qw] * G(b, qw);
-          u[(static_cast<size_t>(a * nt + b) * K + k) * kCh + ch] = static_cast<float>(s);
+          for (int qw = 0; qw < 3; ++qw) s += tmp[a][qw] * w33::kG[b][qw];
+          u[(static_cast<size_t>(a * kN5 + b) * K + k) * kCh + ch] = static_cast<float>(s);
         }
     }
 }
@@ -228,18 +159,9 @@ void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<floa
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
                       bool relu, hipStream_t s, const Knobs& kn) {
   if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
-  if (w.K % kBN || static_cast<long>(w.P) * w.pts() * kCh >= (1L << 31) || static_cast<long>(w.P) * 24 >= (1L << 31) ||
+  if (w.K % kBN || static_cast<long>(w.P) * kPts * kCh >= (1L << 31) || static_cast<long>(w.P) * 12 >= (1L << 31) ||
       out.Cb % 4 || out.c_off % 4)  // 16-B epilogue stores
     return hipErrorInvalidValue;
-  if (w.m == 4) {
-    const int total4 = w.P * 24;
-    long g4 = (total4 + kT - 1) / kT;
-    if (g4 > (1 << 20)) g4 = 1 << 20;
-    conv1_wino4_in_kernel<<<static_cast<unsigned>(g4), kT, 0, s>>>(x, V, total4, w.Hin, w.W * 3, w.ty, w.tx);
-    const hipError_t e4 = hipGetLastError();
-    if (e4 != hipSuccess) return e4;
-    return wino4_gemm_conv1(V, U, bias, out, w.P, w.ty, w.tx, w.H1, w.W1, w.K, relu, s, kn.conv1_occ);
-  }
   const int total = w.P * 12;
   long g = (total + kT - 1) / kT;
   if (g > (1 << 20)) g = 1 << 20;

@@ -6,7 +6,6 @@
 // ring beat BK 32 x 4 slots and BK 16 x 6 slots (the deeper rings raised MFMA-busy but the chip then
 // held a lower clock); Conv2 623 us (old fused kernel 649, bit-identical output), Conv1 380 us.
 #include "wino_gemm.hpp"
-#include "wino_gemm16.hpp"
 
 namespace anx::hip {
 namespace {
@@ -25,31 +24,6 @@ hipError_t launch(const wg::Args& a0, hipStream_t s, int occ) {
   return hipGetLastError();
 }
 
-template <class G, int ABL>
-hipError_t launch16(const wg::Args& a0, hipStream_t s, int occ) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wg16::gemm16_kernel<G, ABL>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (attr != hipSuccess) return attr;
-  wg::Args a = a0;
-  a.n_ptiles = (a.P + G::BM - 1) / G::BM;
-  a.n_ntiles = a.kg / G::BN;
-  if (a.kg % G::BN || a.n_ntiles < 1 || a.u_rows < a.n_ntiles * G::BN) return hipErrorInvalidValue;
-  const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
-  wg16::gemm16_kernel<G, ABL><<<grid, G::NT, occupancy_lds(G::kLdsBytes, occ), s>>>(a);
-  return hipGetLastError();
-}
-
-// 4x4-tile configurations: <tile edge, channels, waves along tiles (16 tiles each), waves along
-// filters, K slice, ring slots, 16-filter blocks per wave, workgroups per CU the registers allow>
-using F4C2 = wg16::Cfg<8, 96, 4, 2, 48, 2, 1, 2>;  // Conv2 F(4x4,5x5): 64 tiles x 32 filters, 8 waves
-using F4C1 = wg16::Cfg<6, 48, 4, 2, 48, 2, 1, 2>;  // Conv1 polyphase F(4x4,3x3): 64 tiles x 32 filters, 8 waves
-#ifdef ANX_WGEMM_ABLATIONS
-using F4C2w = wg16::Cfg<8, 96, 4, 1, 48, 2, 2, 2>;  // 4 waves of 16 x 32 (2 blocks each), 2 per CU
-using F4C1w = wg16::Cfg<6, 48, 4, 1, 48, 2, 2, 2>;
-using F4C2n = wg16::Cfg<8, 96, 4, 1, 48, 2, 1, 3>;  // 4 waves of 16 x 16: 64 tiles x 16 filters, 3 per CU
-using F4C1n = wg16::Cfg<6, 48, 4, 1, 48, 2, 1, 3>;
-#endif
-
 // Configurations: <points, channels, waves along tiles, waves along filters, K slice, ring slots>
 using C2 = wg::Cfg<49, 96, 2, 2, 48, 2>;    // Conv2: 64 tiles x 64 filters, 48 KiB ring, 2 workgroups per CU
 using C2g = wg::Cfg<49, 48, 2, 2, 48, 2>;   // Conv2 with 2 groups (48 channels per group)
@@ -57,8 +31,6 @@ using C1 = wg::Cfg<25, 48, 2, 1, 48, 2>;    // Conv1: 64 tiles x 32 filters, 2 w
 #ifdef ANX_WGEMM_ABLATIONS
 using C2_32x4 = wg::Cfg<49, 96, 2, 2, 32, 4>;    // 64 KiB ring: 2 slices in flight behind the current one
 using C2_64x128 = wg::Cfg<49, 96, 2, 4, 48, 2>;  // 64 tiles x 128 filters, 8 waves, 72 KiB ring
-using C2_128x64 = wg::Cfg<49, 96, 4, 2, 48, 2>;  // 128 tiles x 64 filters, 8 waves, 72 KiB ring
-using C2_128x128 = wg::Cfg<49, 96, 4, 4, 48, 2, 1>;  // 16 waves, 96 KiB ring, 1 per CU
 using C1_64x96 = wg::Cfg<25, 48, 2, 3, 48, 2>;   // 64 x 96 (every filter: V read once), 6 waves, 60 KiB ring
 using C1_32x96 = wg::Cfg<25, 48, 1, 3, 48, 2>;   // 32 x 96, 3 waves, 48 KiB ring
 using C1_48x2w4 = wg::Cfg<25, 48, 4, 1, 48, 2>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
@@ -113,8 +85,6 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
 #ifdef ANX_WGEMM_ABLATIONS
         case 1: e = launch_abl<C2_32x4>(a, s, occ, abl); break;
         case 2: e = launch_abl<C2_64x128>(a, s, occ, abl); break;
-        case 3: e = launch_abl<C2_128x64>(a, s, occ, abl); break;
-        case 4: e = launch_abl<C2_128x128>(a, s, occ, abl); break;
 #endif
         default: break;
       }
@@ -150,85 +120,6 @@ hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, Ou
     case 1: return launch_abl<C1_64x96>(a, s, occ, abl);
     case 2: return launch_abl<C1_32x96>(a, s, occ, abl);
     case 3: return launch_abl<C1_48x2w4>(a, s, occ, abl);
-#endif
-    default: return hipErrorInvalidValue;
-  }
-}
-
-}  // namespace anx::hip
-
-namespace anx::hip {
-
-template <class G>
-hipError_t launch16_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
-  switch (abl) {
-    case 0: return launch16<G, 0>(a, s, occ);
-#ifdef ANX_WGEMM_ABLATIONS
-    case 3: return launch16<G, 3>(a, s, occ);
-    case 32: return launch16<G, 32>(a, s, occ);
-#endif
-    default: return hipErrorInvalidValue;
-  }
-}
-
-hipError_t wino4_gemm_conv2(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
-                            int Ho, int Wo, int C, int K, bool relu, hipStream_t s, int occ, int abl, int cfg) {
-  const long vb = static_cast<long>(P) * 64 * C * 4, ub = static_cast<long>(64) * K * C * 4;
-  if (C != 96 || K % 32 || vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4)
-    return hipErrorInvalidValue;
-  if (P == 0) return hipSuccess;
-  wg::Args a{};
-  a.V = V;
-  a.U = U;
-  a.bias = bias;
-  a.out = out;
-  a.P = P;
-  a.ty = ty;
-  a.tx = tx;
-  a.Ho = Ho;
-  a.Wo = Wo;
-  a.kg = K;
-  a.u_rows = K;
-  a.vct = C;
-  a.vbytes = static_cast<int>(vb);
-  a.ubytes = static_cast<int>(ub);
-  a.relu = relu ? 1 : 0;
-  switch (cfg < 0 ? 0 : cfg) {
-    case 0: return launch16_abl<F4C2>(a, s, occ, abl);
-#ifdef ANX_WGEMM_ABLATIONS
-    case 1: return launch16_abl<F4C2w>(a, s, occ, abl);
-    case 2: return launch16_abl<F4C2n>(a, s, occ, abl);
-#endif
-    default: return hipErrorInvalidValue;
-  }
-}
-
-hipError_t wino4_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
-                            int Ho, int Wo, int K, bool relu, hipStream_t s, int occ, int abl, int cfg) {
-  const long vb = static_cast<long>(P) * 36 * 48 * 4, ub = static_cast<long>(36) * K * 48 * 4;
-  if (K % 32 || vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
-  if (P == 0) return hipSuccess;
-  wg::Args a{};
-  a.V = V;
-  a.U = U;
-  a.bias = bias;
-  a.out = out;
-  a.P = P;
-  a.ty = ty;
-  a.tx = tx;
-  a.Ho = Ho;
-  a.Wo = Wo;
-  a.kg = K;
-  a.u_rows = K;
-  a.vct = 48;
-  a.vbytes = static_cast<int>(vb);
-  a.ubytes = static_cast<int>(ub);
-  a.relu = relu ? 1 : 0;
-  switch (cfg < 0 ? 0 : cfg) {
-    case 0: return launch16_abl<F4C1>(a, s, occ, abl);
-#ifdef ANX_WGEMM_ABLATIONS
-    case 1: return launch16_abl<F4C1w>(a, s, occ, abl);
-    case 2: return launch16_abl<F4C1n>(a, s, occ, abl);
 #endif
     default: return hipErrorInvalidValue;
   }

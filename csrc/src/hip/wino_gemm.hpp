@@ -94,10 +94,9 @@ constexpr int even_up(int ks, int nst) {  // smallest even UP with UP*ks % nst =
 }
 
 // Compile-time shape of one configuration.
-template <int NPT_, int C_, int WM_, int WN_, int BK_, int NST_, int MINB_ = 2>
+template <int NPT_, int C_, int WM_, int WN_, int BK_, int NST_>
 struct Cfg {
   static constexpr int NPT = NPT_, C = C_, WM = WM_, WN = WN_, BK = BK_, NST = NST_;
-  static constexpr int MINB = MINB_;  // launch bound: waves per SIMD (EU) the register budget must allow
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int BM = 32 * WM, BN = 32 * WN, U4 = BK / 4;
   static constexpr int KS = C / BK, TOTAL = NPT * KS;              // K slices per point / in all
@@ -141,7 +140,7 @@ __device__ __forceinline__ void wait_vm_lgkm() {
 // bit3 packed v_pk_fma_f32 fold instead of scalar, bit4 no sched_group_barrier pinning, bit5 no epilogue
 // stores (the outputs are computed, never written).
 template <class G, int ABL>
-__global__ void __launch_bounds__(G::NT, G::MINB) gemm_kernel(Args a) {
+__global__ void __launch_bounds__(G::NT, 2) gemm_kernel(Args a) {
   constexpr int NPT = G::NPT, KS = G::KS, BK = G::BK, NW = G::NW, NST = G::NST, U4 = G::U4, MF = G::MF;
   constexpr bool kFold = !(ABL & 1), kDma = !(ABL & 2), kBar = !(ABL & 4), kPk = (ABL & 8) != 0, kPin = !(ABL & 16);
   constexpr bool kStore = !(ABL & 32);

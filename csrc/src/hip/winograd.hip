@@ -17,7 +17,6 @@
 
 #include "anx/ops.hpp"
 #include "anx/winograd_f35.hpp"
-#include "anx/winograd_f45.hpp"
 
 namespace anx::hip {
 namespace {
@@ -83,61 +82,9 @@ __global__ void __launch_bounds__(kT) wino_in2_kernel(const float* __restrict__ 
   }
 }
 
-// F(4x4,5x5) input transform: thread = (tile, channel); consecutive threads take consecutive channels
-// (coalesced 4-B loads and stores). The 8x8 patch streams through t = B^T d one input row at a time
-// (64 transform registers); rows / columns past the window (the 28th output row and column of the
-// 7x7 tile grid over 27x27) read zeros.
-__global__ void __launch_bounds__(kT) wino_in4_kernel(const float* __restrict__ x, float* __restrict__ V, int N, int Hq,
-                                                      int Wq, int C, int ty, int tx) {
-  namespace w4 = anx::wino45;
-  constexpr int n8 = w4::kN;
-  const int total = N * ty * tx * C;
-  for (int i = blockIdx.x * kT + threadIdx.x; i < total; i += gridDim.x * kT) {
-    const int c = i % C;
-    const int p = i / C;
-    const int tj = p % tx;
-    const int q = p / tx;
-    const int ti = q % ty;
-    const int n = q / ty;
-    float t[n8][n8];
-#pragma unroll
-    for (int a = 0; a < n8; ++a)
-#pragma unroll
-      for (int v = 0; v < n8; ++v) t[a][v] = 0.f;
-#pragma unroll
-    for (int u = 0; u < n8; ++u) {
-      const int yy = ti * w4::kM + u;
-      float row[n8];
-#pragma unroll
-      for (int v = 0; v < n8; ++v) {
-        const int xx = tj * w4::kM + v;
-        row[v] = (yy < Hq && xx < Wq) ? x[((static_cast<size_t>(n) * Hq + yy) * Wq + xx) * C + c] : 0.f;
-      }
-#pragma unroll
-      for (int a = 0; a < n8; ++a)
-        if (w4::kBT[a][u] != 0.f)
-#pragma unroll
-          for (int v = 0; v < n8; ++v) t[a][v] = fmaf(w4::kBT[a][u], row[v], t[a][v]);
-    }
-    float* out = V + static_cast<size_t>(p) * (n8 * n8) * C + c;
-#pragma unroll
-    for (int a = 0; a < n8; ++a)
-#pragma unroll
-      for (int b = 0; b < n8; ++b) {
-        float s1 = 0.f;
-#pragma unroll
-        for (int v = 0; v < n8; ++v)
-          if (w4::kBT[b][v] != 0.f) s1 = fmaf(w4::kBT[b][v], t[a][v], s1);
-        out[static_cast<size_t>(a * n8 + b) * C] = s1;
-      }
-  }
-}
-
 }  // namespace
 
-bool wino4_eligible(int C, int K, int groups) { return groups == 1 && C == 96 && K % 32 == 0; }
-
-WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups, int m) {
+WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups) {
   WinoPlan w{};
   w.N = N;
   w.Hq = Hq;
@@ -145,11 +92,10 @@ WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups, int m) 
   w.C = C;
   w.K = K;
   w.groups = groups;
-  w.m = m == 4 ? 4 : 3;
   w.Ho = Hq - (wino::kR - 1);
   w.Wo = Wq - (wino::kR - 1);
-  w.ty = (w.Ho + w.m - 1) / w.m;
-  w.tx = (w.Wo + w.m - 1) / w.m;
+  w.ty = (w.Ho + kM - 1) / kM;
+  w.tx = (w.Wo + kM - 1) / kM;
   w.P = N * w.ty * w.tx;
   return w;
 }
@@ -161,30 +107,29 @@ bool wino_eligible(int F, int S, int C, int K, int groups) {
   return (Cg == 96 || Cg == 48) && Kg % 64 == 0;
 }
 
-size_t wino_v_floats(const WinoPlan& w) { return static_cast<size_t>(w.P) * w.pts() * w.C; }
-size_t wino_u_floats(const WinoPlan& w) { return static_cast<size_t>(w.pts()) * w.K * (w.C / w.groups); }
+size_t wino_v_floats(const WinoPlan& w) { return static_cast<size_t>(w.P) * kN * kN * w.C; }
+size_t wino_u_floats(const WinoPlan& w) { return static_cast<size_t>(kN * kN) * w.K * (w.C / w.groups); }
 
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff) {
   // U[(ab*groups + g)*Kg + k][c] = (G g_{k,c} G^T)[a][b], computed in fp64 then rounded once.
-  const int Cg = w.C / w.groups, Kg = w.K / w.groups, R = wino::kR, kNt = w.n();
-  auto G = [&](int a, int u) { return w.m == 4 ? anx::wino45::kG[a][u] : wino::kG[a][u]; };
+  const int Cg = w.C / w.groups, Kg = w.K / w.groups, R = wino::kR;
   u_kcff.assign(wino_u_floats(w), 0.f);
   for (int g = 0; g < w.groups; ++g)
     for (int k = 0; k < Kg; ++k)
       for (int c = 0; c < Cg; ++c) {
         const float* f = w_kcff + ((static_cast<size_t>(g * Kg + k) * Cg + c) * R) * R;
-        double tmp[8][wino::kR];
-        for (int a = 0; a < kNt; ++a)
+        double tmp[kN][wino::kR];
+        for (int a = 0; a < kN; ++a)
           for (int v = 0; v < R; ++v) {
             double s = 0;
-            for (int u = 0; u < R; ++u) s += G(a, u) * f[u * R + v];
+            for (int u = 0; u < R; ++u) s += wino::kG[a][u] * f[u * R + v];
             tmp[a][v] = s;
           }
-        for (int a = 0; a < kNt; ++a)
-          for (int b = 0; b < kNt; ++b) {
+        for (int a = 0; a < kN; ++a)
+          for (int b = 0; b < kN; ++b) {
             double s = 0;
-            for (int v = 0; v < R; ++v) s += tmp[a][v] * G(b, v);
-            const int ab = a * kNt + b;
+            for (int v = 0; v < R; ++v) s += tmp[a][v] * wino::kG[b][v];
+            const int ab = a * kN + b;
             u_kcff[(static_cast<size_t>(ab * w.groups + g) * Kg + k) * Cg + c] = static_cast<float>(s);
           }
       }
@@ -193,12 +138,6 @@ void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::ve
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s) {
   const long n = static_cast<long>(w.P) * w.C;
   if (n >= (1L << 31) || w.C % 2) return hipErrorInvalidValue;
-  if (w.m == 4) {
-    const long g4 = (n + kT - 1) / kT;
-    const unsigned g4u = static_cast<unsigned>(g4 < (1 << 20) ? g4 : (1 << 20));
-    wino_in4_kernel<<<g4u, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
-    return hipGetLastError();
-  }
   const long g = (n / 2 + kT - 1) / kT;
   const unsigned gg = static_cast<unsigned>(g < (1 << 20) ? g : (1 << 20));
   wino_in2_kernel<<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
@@ -207,10 +146,6 @@ hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s
 
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,
                       hipStream_t s, const Knobs& k) {
-  if (w.m == 4) {
-    if (!wino4_eligible(w.C, w.K, w.groups)) return hipErrorInvalidValue;
-    return wino4_gemm_conv2(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.C, w.K, relu, s, k.conv2_occ);
-  }
   return wino_gemm_conv2(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.C, w.K, w.groups, relu, s, k.conv2_occ);
 }
 

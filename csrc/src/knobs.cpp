@@ -32,8 +32,6 @@ const Field kFields[] = {
     {"bf16_fc", &Knobs::bf16_fc, nullptr, 0, 1, "ANX_BF16_FC"},
     {"conv1_occ", &Knobs::conv1_occ, nullptr, 0, 8, "ANX_CONV1_OCC"},
     {"conv2_occ", &Knobs::conv2_occ, nullptr, 0, 8, "ANX_CONV2_OCC"},
-    {"conv1_tile", &Knobs::conv1_tile, nullptr, 3, 4, "ANX_CONV1_TILE"},
-    {"conv2_tile", &Knobs::conv2_tile, nullptr, 3, 4, "ANX_CONV2_TILE"},
 };
 
 const Field* find(const char* name) {

@@ -96,35 +96,8 @@ int main(int argc, char** argv) {
   // ---- Conv2: 31x31x96 window -> 27x27x256
   if (only != 1) {
     const hip::WinoPlan w = hip::make_wino_plan(images, 31, 31, 96, 256, 1);
-    const hip::WinoPlan w4 = hip::make_wino_plan(images, 31, 31, 96, 256, 1, 4);
-    // a real transform pipeline: random window (zero border of 2) and weights, V / U from them
-    std::vector<float> xh(static_cast<size_t>(images) * 31 * 31 * 96, 0.f), wh2(static_cast<size_t>(256) * 96 * 25);
-    {
-      std::mt19937 gx(1);
-      std::uniform_real_distribution<float> dx(0.f, 1.f), dw(-0.02f, 0.02f);
-      for (int n = 0; n < images; ++n)
-        for (int y = 2; y < 29; ++y)
-          for (int x0 = 2; x0 < 29; ++x0)
-            for (int c = 0; c < 96; ++c) xh[((static_cast<size_t>(n) * 31 + y) * 31 + x0) * 96 + c] = dx(gx);
-      for (auto& v : wh2) v = dw(gx);
-    }
-    float* xw = nullptr;
-    CHECK(hipMalloc(&xw, xh.size() * sizeof(float)));
-    CHECK(hipMemcpy(xw, xh.data(), xh.size() * sizeof(float), hipMemcpyHostToDevice));
-    std::vector<float> u3h, u4h;
-    hip::wino_transform_weights_host(w, wh2.data(), u3h);
-    hip::wino_transform_weights_host(w4, wh2.data(), u4h);
-    float *V = nullptr, *U = nullptr, *V4 = nullptr, *U4 = nullptr;
-    CHECK(hipMalloc(&V, hip::wino_v_floats(w) * sizeof(float)));
-    CHECK(hipMalloc(&V4, hip::wino_v_floats(w4) * sizeof(float)));
-    CHECK(hipMalloc(&U, u3h.size() * sizeof(float)));
-    CHECK(hipMalloc(&U4, u4h.size() * sizeof(float)));
-    CHECK(hipMemcpy(U, u3h.data(), u3h.size() * sizeof(float), hipMemcpyHostToDevice));
-    CHECK(hipMemcpy(U4, u4h.data(), u4h.size() * sizeof(float), hipMemcpyHostToDevice));
-    const double t_in3 = time_us([&] { return hip::wino_input(w, xw, V, nullptr); }, iters);
-    const double t_in4 = time_us([&] { return hip::wino_input(w4, xw, V4, nullptr); }, iters);
-    std::printf("{\"conv\": 2, \"images\": %d, \"arm\": \"input transform F3 / F4\", \"us\": %.1f, \"us4\": %.1f}\n",
-                images, t_in3, t_in4);
+    float* V = upload_random(hip::wino_v_floats(w), 1, -1.f, 1.f);
+    float* U = upload_random(hip::wino_u_floats(w), 2, -0.05f, 0.05f);
     float* b = upload_random(256, 3, 0.f, 0.1f);
     const size_t ny = static_cast<size_t>(images) * 27 * 27 * 256;
     float *y0 = nullptr, *y1 = nullptr;
@@ -132,12 +105,11 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&y1, ny * sizeof(float)));
     const double flop = 2.0 * w.P * 49 * 96 * 256;
     const hip::OutView o0{y0, 27, 27, 256, 0, 0, 0};
-    CHECK(hip::wino_input(w, xw, V, nullptr));
     const double t_old = time_us([&] { return hip::wino_conv2(w, V, U, b, o0, true, nullptr, kn); }, iters);
     const auto ref = download(y0, ny);
     std::printf("{\"conv\": 2, \"images\": %d, \"arm\": \"production wino_conv2\", \"us\": %.1f, \"tflops\": %.1f}\n",
                 images, t_old, flop / t_old * 1e-6);
-    for (int cfg = 0; cfg < 5; ++cfg)
+    for (int cfg = 0; cfg < 4; ++cfg)
       for (int abl : kAbl) {
         if (only_cfg >= 0 && cfg != only_cfg) continue;
         const hip::OutView ov{y1, 27, 27, 256, 0, 0, 0};
@@ -156,28 +128,7 @@ int main(int argc, char** argv) {
                     "%.1f, \"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
                     images, cfg, abl, t, flop / t * 1e-6, d, rmax);
       }
-    const double flop4 = 2.0 * w4.P * 64 * 96 * 256;
-    for (int cfg = 0; cfg < 3; ++cfg)
-      for (int abl : kAbl) {
-        if (only_cfg >= 0 && cfg != only_cfg) continue;
-        const hip::OutView ov{y1, 27, 27, 256, 0, 0, 0};
-        CHECK(hipMemset(y1, 0, ny * sizeof(float)));
-        if (hip::wino4_gemm_conv2(V4, U4, b, ov, w4.P, w4.ty, w4.tx, 27, 27, 96, 256, true, nullptr, occ, abl, cfg) ==
-            hipErrorInvalidValue)
-          continue;
-        const double t = time_us(
-            [&] {
-              return hip::wino4_gemm_conv2(V4, U4, b, ov, w4.P, w4.ty, w4.tx, 27, 27, 96, 256, true, nullptr, occ, abl,
-                                           cfg);
-            },
-            iters);
-        double rmax = 0;
-        const double d = max_abs_diff(download(y1, ny), ref, &rmax);
-        std::printf("{\"conv\": 2, \"images\": %d, \"arm\": \"F4 gemm16 cfg=%d abl=%d\", \"us\": %.1f, \"tflops\": "
-                    "%.1f, \"direct3_equiv_tflops\": %.1f, \"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
-                    images, cfg, abl, t, flop4 / t * 1e-6, flop / t * 1e-6, d, rmax);
-      }
-    for (float* p : {V, U, V4, U4, xw, b, y0, y1}) CHECK(hipFree(p));
+    for (float* p : {V, U, b, y0, y1}) CHECK(hipFree(p));
   }
 
   // ---- Conv1: 227x227x3 image -> 55x55x96 (polyphase F(3x3,3x3))
@@ -222,43 +173,6 @@ int main(int argc, char** argv) {
                     "\"tflops\": %.1f, \"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
                     images, cfg, abl, t, flop / t * 1e-6, dd, rmax);
       }
-    // F(4x4,3x3): the whole conv (transform + GEMM) and the GEMM alone per configuration
-    {
-      const hip::Conv1WinoPlan w4 = hip::make_conv1_wino_plan(images, 227, 227, 96, 11, 4);
-      std::vector<float> u4h;
-      hip::conv1_wino_weights_host(96, 11, wh.data(), u4h, 4);
-      float *U4 = nullptr, *V4 = nullptr;
-      CHECK(hipMalloc(&U4, u4h.size() * sizeof(float)));
-      CHECK(hipMemcpy(U4, u4h.data(), u4h.size() * sizeof(float), hipMemcpyHostToDevice));
-      CHECK(hipMalloc(&V4, hip::conv1_wino_v_floats(w4) * sizeof(float)));
-      CHECK(hipMemset(y1, 0, ny * sizeof(float)));
-      const double t4 = time_us([&] { return hip::conv1_wino(w4, x, V4, U4, b, o1, true, nullptr, kn); }, iters);
-      double rmax = 0;
-      const double dd = max_abs_diff(download(y1, ny), ref, &rmax);
-      std::printf("{\"conv\": 1, \"images\": %d, \"arm\": \"F4 conv1_wino (input transform + GEMM)\", \"us\": %.1f, "
-                  "\"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
-                  images, t4, dd, rmax);
-      const double flop4 = 2.0 * w4.P * 36 * 48 * 96;
-      for (int cfg = 0; cfg < 3; ++cfg)
-        for (int abl : kAbl) {
-          if (only_cfg >= 0 && cfg != only_cfg) continue;
-          CHECK(hipMemset(y1, 0, ny * sizeof(float)));
-          if (hip::wino4_gemm_conv1(V4, U4, b, o1, w4.P, w4.ty, w4.tx, 55, 55, 96, true, nullptr, occ, abl, cfg) ==
-              hipErrorInvalidValue)
-            continue;
-          const double t = time_us(
-              [&] {
-                return hip::wino4_gemm_conv1(V4, U4, b, o1, w4.P, w4.ty, w4.tx, 55, 55, 96, true, nullptr, occ, abl, cfg);
-              },
-              iters);
-          const double d4 = max_abs_diff(download(y1, ny), ref, &rmax);
-          std::printf("{\"conv\": 1, \"images\": %d, \"arm\": \"F4 gemm16 cfg=%d abl=%d (GEMM only)\", \"us\": %.1f, "
-                      "\"tflops\": %.1f, \"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
-                      images, cfg, abl, t, flop4 / t * 1e-6, d4, rmax);
-        }
-      CHECK(hipFree(U4));
-      CHECK(hipFree(V4));
-    }
     for (float* p : {x, U, b, V, y0, y1}) CHECK(hipFree(p));
   }
   return 0;

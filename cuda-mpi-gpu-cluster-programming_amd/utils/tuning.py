@@ -10,9 +10,8 @@ Names and values:
 * ``conv1_algo``: Conv1 (11x11, stride 4) — ``auto``/``winograd`` (polyphase Winograd F(3x3,3x3)) or
   ``direct``.
 * integer knobs: ``chunk1``, ``chunk2`` (images per launch), ``conv1_occ``, ``conv2_occ`` (Winograd
-  GEMM workgroups-per-CU caps), ``conv1_tile``, ``conv2_tile`` (Winograd output tile edge 3 or 4:
-  F(3x3,r) or F(4x4,r)), ``force_vec4``, ``force_scalar`` (direct GEMM tiles), and the bf16 full
-  model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``.
+  GEMM workgroups-per-CU caps), ``force_vec4``, ``force_scalar`` (direct GEMM tiles), and the bf16
+  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``.
 """
 from __future__ import annotations
 
@@ -22,7 +21,7 @@ from .. import _native as nat
 
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
-         "bf16_lrn_tile", "bf16_fc", "conv1_occ", "conv2_occ", "conv1_tile", "conv2_tile")
+         "bf16_lrn_tile", "bf16_fc", "conv1_occ", "conv2_occ")
 
 
 def knob_value(name: str, value) -> int:

@@ -18,9 +18,6 @@ pytestmark = pytest.mark.gpu
 # max 1.8-2.6e-6 (mean 8e-8), Conv1 max 1.0-1.3e-6 (mean 4.4e-8). A broken transform or fold is >=1e-3.
 BOUND_CONV2 = 1e-5
 BOUND_CONV1 = 4e-6
-# The 4x4-tile variants (knobs conv1_tile / conv2_tile = 4: F(4x4,5x5) on 8 points, polyphase
-# F(4x4,3x3) on 6) have fp32 error of the same order (emulated: 6.2e-7 / 6.5e-7 of Σ|x·w| vs 5.7e-7 /
-# 3.0e-7 for the 3x3 tiles, profiles/r03_f4_numerics.txt); the same bounds apply.
 
 
 def _rel_to_terms(y, x, w, b, S, P, groups=1):
@@ -31,12 +28,9 @@ def _rel_to_terms(y, x, w, b, S, P, groups=1):
     return rel.max().item()
 
 
-@pytest.mark.parametrize("N,groups,tile", [(12, 1, 3), (12, 2, 3), (9, 1, 3), (128, 1, 3), (140, 2, 3), (12, 1, 4),
-                                          (9, 1, 4), (128, 1, 4), (140, 1, 4)])
-def test_conv2_winograd_randn_he(cuda, monkeypatch, N, groups, tile):
-    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights; 3x3 and 4x4 tiles
-    (the 4x4 tile grid covers 28x28: its last row / column is computed and dropped)."""
-    monkeypatch.setenv("ANX_CONV2_TILE", str(tile))
+@pytest.mark.parametrize("N,groups", [(12, 1), (12, 2), (9, 1), (128, 1), (140, 2)])
+def test_conv2_winograd_randn_he(cuda, N, groups):
+    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights."""
     torch.manual_seed(21 + N)
     C, K = 96, 256
     x = torch.randn(N, 31, 31, C, device=cuda)
@@ -53,11 +47,9 @@ def test_conv2_winograd_randn_he(cuda, monkeypatch, N, groups, tile):
     assert _rel_to_terms(y, x, w.to(cuda), b, 1, 0, groups) < BOUND_CONV2
 
 
-@pytest.mark.parametrize("N,tile", [(5, 3), (70, 3), (5, 4), (70, 4), (33, 4)])
-def test_conv1_polyphase_winograd_randn_he(cuda, monkeypatch, N, tile):
-    """Conv1 (227x227x3, 11x11/4, 96 filters) on the polyphase Winograd path: randn inputs; 3x3 and
-    4x4 output tiles."""
-    monkeypatch.setenv("ANX_CONV1_TILE", str(tile))
+@pytest.mark.parametrize("N", [5, 70])
+def test_conv1_polyphase_winograd_randn_he(cuda, N):
+    """Conv1 (227x227x3, 11x11/4, 96 filters) on the polyphase Winograd path: randn inputs."""
     torch.manual_seed(31 + N)
     x = torch.randn(N, 227, 227, 3, device=cuda)
     w = torch.randn(96, 3, 11, 11) * math.sqrt(2.0 / (3 * 121))
@@ -69,15 +61,13 @@ def test_conv1_polyphase_winograd_randn_he(cuda, monkeypatch, N, tile):
     assert _rel_to_terms(y, x, w.to(cuda), b, 4, 0) < BOUND_CONV1
 
 
-@pytest.mark.parametrize("tiles", [(3, 3), (4, 4), (3, 4), (4, 3)])
-def test_full_blocks_randn_he_vs_oracle(cuda, tiles):
-    """The whole Blocks 1-2 engine (both Winograd convs, pools, LRN) at randn/He scale, for each
-    combination of the Winograd tile knobs."""
+def test_full_blocks_randn_he_vs_oracle(cuda):
+    """The whole Blocks 1-2 engine (both Winograd convs, pools, LRN) at randn/He scale."""
     torch.manual_seed(5)
     w1 = torch.randn(96, 3, 11, 11) * math.sqrt(2.0 / 363)
     w2 = torch.randn(256, 96, 5, 5) * math.sqrt(2.0 / 2400)
     ws = {"w1": w1, "b1": torch.randn(96) * 0.1, "w2": w2, "b2": torch.randn(256) * 0.1}
-    m = AlexNetBlocks(ws, device=cuda, max_batch=24, knobs={"conv1_tile": tiles[0], "conv2_tile": tiles[1]})
+    m = AlexNetBlocks(ws, device=cuda, max_batch=24)
     x = torch.randn(24, 227, 227, 3)
     y = m(x.to(cuda)).cpu().double()
     ref = blocks_forward(x, m.weights, m.b1, m.b2)
