@@ -8,6 +8,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <vector>
 
 #include "anx/knobs.hpp"
@@ -130,6 +131,17 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
                            int cfg = -1);
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
                            int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
+
+// A/B build only (anx_wgemm; defined under ANX_WGEMM_ABLATIONS): the same GEMMs on the bf16 matrix
+// cores with fp32-exact operands (wino_gemm_sb.hpp): U as three bf16 planes Ub[point][plane h/m/l][row]
+// [C/groups] (wino_split_planes_host: x = h + m + l exactly), V fp32 split in registers; nprod = 9
+// (every part product) or 6 (drops the three below 2^-21 |x*y|). Measured no faster than f32 MFMA.
+void wino_split_planes_host(const std::vector<float>& u, int npt, int rows, int cols, std::vector<uint16_t>& ub);
+hipError_t wino_sb_gemm_conv2(const float* V, const uint16_t* Ub, const float* bias, OutView out, int P, int ty, int tx,
+                              int Ho, int Wo, int C, int K, int groups, bool relu, hipStream_t s, int nprod = 9,
+                              int occ = 0, int abl = 0);
+hipError_t wino_sb_gemm_conv1(const float* V, const uint16_t* Ub, const float* bias, OutView out, int P, int ty, int tx,
+                              int Ho, int Wo, int K, bool relu, hipStream_t s, int nprod = 9, int occ = 0, int abl = 0);
 
 // Dynamic LDS bytes that cap a kernel at `wgs` workgroups per CU (160 KiB LDS per CU): the larger of
 // `natural` and just over 160 KiB / (wgs + 1). wgs <= 0: `natural`.
