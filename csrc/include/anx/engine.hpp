@@ -75,6 +75,9 @@ class BlocksEngine {
   hipError_t ensure_window(const TilePlan& t, int N, hipStream_t s);
   hipError_t conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s);
   hipError_t conv2_chunk(int n, const TilePlan& t, const float* qc, float* yc, hipStream_t s);
+  hipError_t pool2_chunk(int n, const TilePlan& t, float* yc, hipStream_t s);  // c2_ -> y (+LRN)
+  // Whether tile_forward of N images runs pool1 inside the Winograd input transform (Knobs::fuse_pool1)
+  bool fused_pool1(int N, const TilePlan& t) const;
 
   BlockSpec b1_, b2_;
   BlocksDims d_;

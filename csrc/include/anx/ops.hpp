@@ -101,6 +101,12 @@ size_t wino_u_floats(const WinoPlan& w);  // transformed weights [49][K][C/group
 // U[(ab*groups + g)*Kg + k][c] = (G g G^T)[a][b] in fp64, rounded once.
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s);
+// Pool1 (3x3 / 2 max) fused with the input transform: V straight from the conv1 output c1 [N][H1][W1][C]
+// (conv1 row c1_lo first). Window row R is pool1 row q_lo + R (zero outside [0, Hp)), window column c is
+// pool1 column c - P (zero outside [0, Wp)); every non-zero window row must be computable from c1's rows.
+// Bit-identical to maxpool + wino_input. C % 32 == 0, Wq <= 31.
+hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, int q_lo, int Hp, int Wp, int P,
+                           int c1_lo, float* V, hipStream_t s);
 // Fused batched GEMM + output transform + bias + optional ReLU into `out` (wino_gemm.hpp); Knobs:
 // conv2_occ (workgroups per CU cap).
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,

@@ -210,6 +210,10 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
     ANX_TRY(hip::conv2d_direct(qc, w2_, b2d_, c2_, n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, 0, k2.groups, true,
                                s));
   }
+  return pool2_chunk(n, t, yc, s);
+}
+
+hipError_t BlocksEngine::pool2_chunk(int n, const TilePlan& t, float* yc, hipStream_t s) {
   const LrnSpec& l = b2_.lrn;
   if (b2_.has_lrn) {
     if (impl_ == Impl::Mfma)
@@ -237,11 +241,43 @@ hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t 
   return hipSuccess;
 }
 
+bool BlocksEngine::fused_pool1(int N, const TilePlan& t) const {
+  if (impl_ != Impl::Mfma || !k_.fuse_pool1 || wv_ == nullptr || d_.C1 % 32 || wq_ > 31) return false;
+  // every pool1 row of the window (inside the pooled image) is computed by this tile
+  const int lo = std::max(t.q.lo, 0), hi = std::min(t.q.hi, d_.Hp1);
+  if (lo < t.p1.lo || hi > t.p1.hi) return false;
+  // and every launch chunk runs Conv2 as Winograd
+  const int chunk = std::min(chunk_, k_.chunk1 > 0 ? k_.chunk1 : chunk_);
+  const int last = N - (N - 1) / chunk * chunk;
+  return use_winograd(k_.conv2_algo, std::min(N, chunk), t.c2.size(), d_.H2) &&
+         use_winograd(k_.conv2_algo, last, t.c2.size(), d_.H2);
+}
+
 hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, float* y, hipStream_t s) {
   if (N > max_batch_) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
-  ANX_TRY(stage1(x, N, t, s));
-  return stage2(N, t, y, s);
+  if (!fused_pool1(N, t)) {
+    ANX_TRY(stage1(x, N, t, s));
+    return stage2(N, t, y, s);
+  }
+  // conv1 -> (pool1 + Winograd input transform) -> Winograd GEMM -> pool2 + LRN per chunk: the conv2
+  // window is never materialised (bit-identical to stage1 + stage2)
+  const ConvSpec& k2 = b2_.conv;
+  const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
+  const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
+  const int chunk = std::min(chunk_, k_.chunk1 > 0 ? k_.chunk1 : chunk_);
+  const hip::OutView c2v{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int n = std::min(chunk, N - n0);
+    ANX_TRY(conv1_chunk(x + n0 * in_img, n, t, s));
+    RoctxRange rx("anx pool1+conv2+pool2+lrn");
+    const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
+    if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
+    ANX_TRY(hip::wino_pool_input(w, c1_, t.c1.size(), d_.W1, t.q.lo, d_.Hp1, d_.Wp1, k2.P, t.c1.lo, wv_, s));
+    ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
+    ANX_TRY(pool2_chunk(n, t, y + n0 * y_img, s));
+  }
+  return hipSuccess;
 }
 
 hipError_t BlocksEngine::forward(const float* x, int N, float* y, hipStream_t s) {

@@ -22,6 +22,7 @@ namespace anx::hip {
 namespace {
 
 using f32x2 = __attribute__((ext_vector_type(2))) float;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
 constexpr int kT = 256;
 constexpr int kN = wino::kN, kM = wino::kM;
 
@@ -82,7 +83,114 @@ __global__ void __launch_bounds__(kT) wino_in2_kernel(const float* __restrict__ 
   }
 }
 
+// Pool1 (3x3 / 2 max) fused with the input transform: the conv2 window is never written. One
+// workgroup = (image, tile row, 32-channel group): it pools the 7 window rows of its tile row
+// straight from the conv1 output into LDS (zero border included), runs t = B^T d down each of the
+// window's columns in place, then B along each tile's 7 columns, and writes V. The fmaf sequences are
+// those of wino_in2_kernel (same zero skips, same order) and max is exact in any order, so V is
+// bit-identical to pool1 + wino_in2. The workgroups of one (image, channel group) share conv1 rows between adjacent
+// tile rows: they get equal blockIdx % 8 (one XCD under round-robin dispatch), so re-reads hit that
+// XCD's L2.
+constexpr int kPG = 32;     // channels per workgroup
+constexpr int kMaxWq = 31;  // window columns held in LDS
+__global__ void __launch_bounds__(kT) pool_wino_in_kernel(const float* __restrict__ c1, float* __restrict__ V, int groups,
+                                                          int H1, int W1, int C, int Hq, int Wq, int q_lo, int Hp,
+                                                          int Wp, int P, int c1_lo, int ty, int tx) {
+  __shared__ __attribute__((aligned(16))) float band[kN][kMaxWq][kPG];
+  const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+  const int grp = (j / ty) * 8 + xcd, ti = j % ty;
+  if (grp >= groups) return;  // whole workgroup, before any barrier
+  const int CG = C / kPG, n = grp / CG, cg = grp % CG;
+  const int tid = threadIdx.x;
+  // 1. pooled window rows 3ti .. 3ti+6 into LDS, zero outside the pooled image. A thread owns one
+  // (pooled column, 4-channel group) of the band: the row max of each conv1 row the band's 7 pooled
+  // rows touch (3 loads) is reused by the two pooled rows that share that conv1 row.
+  for (int it = tid; it < Wq * (kPG / 4); it += kT) {
+    const int c4 = it % (kPG / 4), col = it / (kPG / 4), pc = col - P;
+    const bool cin = pc >= 0 && pc < Wp;
+    const float* src = c1 + (static_cast<size_t>(n * H1) * W1 + 2 * pc) * C + cg * kPG + 4 * c4;
+    f32x4 prev = {0.f, 0.f, 0.f, 0.f};  // row max of conv1 row 2*pr (shared with pooled row pr - 1)
+    int prev_row = -1;
+#pragma unroll
+    for (int r = 0; r < kN; ++r) {
+      const int R = ti * kM + r, pr = q_lo + R;
+      f32x4 m = {0.f, 0.f, 0.f, 0.f};
+      if (cin && R < Hq && pr >= 0 && pr < Hp) {
+        f32x4 h[3];
+#pragma unroll
+        for (int fh = 0; fh < 3; ++fh) {
+          const int cr = 2 * pr + fh - c1_lo;  // local conv1 row
+          if (fh == 0 && cr == prev_row) {
+            h[0] = prev;
+            continue;
+          }
+          const float* q = src + static_cast<size_t>(cr) * W1 * C;
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(q), v1 = *reinterpret_cast<const f32x4*>(q + C),
+                      v2 = *reinterpret_cast<const f32x4*>(q + 2 * C);
+          h[fh] = f32x4{fmaxf(fmaxf(v0.x, v1.x), v2.x), fmaxf(fmaxf(v0.y, v1.y), v2.y), fmaxf(fmaxf(v0.z, v1.z), v2.z),
+                        fmaxf(fmaxf(v0.w, v1.w), v2.w)};
+        }
+        prev = h[2];
+        prev_row = 2 * pr + 2 - c1_lo;
+        m = f32x4{fmaxf(fmaxf(h[0].x, h[1].x), h[2].x), fmaxf(fmaxf(h[0].y, h[1].y), h[2].y),
+                  fmaxf(fmaxf(h[0].z, h[1].z), h[2].z), fmaxf(fmaxf(h[0].w, h[1].w), h[2].w)};
+      }
+      *reinterpret_cast<f32x4*>(&band[r][col][4 * c4]) = m;
+    }
+  }
+  __syncthreads();
+  // 2. t = B^T d down each column, in place (a thread owns one (column, 4-channel group))
+  for (int it = tid; it < Wq * (kPG / 4); it += kT) {
+    const int c4 = it % (kPG / 4), col = it / (kPG / 4);
+    f32x4 d[kN], t[kN];
+#pragma unroll
+    for (int u = 0; u < kN; ++u) d[u] = *reinterpret_cast<const f32x4*>(&band[u][col][4 * c4]);
+#pragma unroll
+    for (int a = 0; a < kN; ++a) {
+      t[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < kN; ++u)
+        if (wino::kBT[a][u] != 0.f)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[a][e] = fmaf(wino::kBT[a][u], d[u][e], t[a][e]);
+    }
+#pragma unroll
+    for (int a = 0; a < kN; ++a) *reinterpret_cast<f32x4*>(&band[a][col][4 * c4]) = t[a];
+  }
+  __syncthreads();
+  // 3. V[a][b] = sum_v B^T[b][v] t[a][3tj + v], one (tile, row a, 4-channel group) per thread: 16-B stores
+  for (int it = tid; it < tx * kN * (kPG / 4); it += kT) {
+    const int c4 = it % (kPG / 4), rest = it / (kPG / 4), a = rest % kN, tj = rest / kN;
+    f32x4 t[kN];
+#pragma unroll
+    for (int v = 0; v < kN; ++v)
+      t[v] = tj * kM + v < Wq ? *reinterpret_cast<const f32x4*>(&band[a][tj * kM + v][4 * c4]) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int p = (n * ty + ti) * tx + tj;
+    float* out = V + (static_cast<size_t>(p) * (kN * kN) + a * kN) * C + cg * kPG + 4 * c4;
+#pragma unroll
+    for (int bb = 0; bb < kN; ++bb) {
+      f32x4 s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int v = 0; v < kN; ++v)
+        if (wino::kBT[bb][v] != 0.f)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s1[e] = fmaf(wino::kBT[bb][v], t[v][e], s1[e]);
+      *reinterpret_cast<f32x4*>(out + static_cast<size_t>(bb) * C) = s1;
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, int q_lo, int Hp, int Wp, int P,
+                           int c1_lo, float* V, hipStream_t s) {
+  if (w.C % kPG || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * kN * kN >= (1L << 31)) return hipErrorInvalidValue;
+  if (w.P == 0) return hipSuccess;
+  const int groups = w.N * (w.C / kPG);
+  const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
+  pool_wino_in_kernel<<<grid, kT, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
+  return hipGetLastError();
+}
 
 WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups) {
   WinoPlan w{};

@@ -59,9 +59,10 @@ class AlexNetFull:
             raise ValueError("the bf16 full-AlexNet engine is GPU-only (use reference_forward on the CPU)")
         self._h = None
         self._cap = 0
-        self._ensure(max_batch)
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
+        per_lane = -(-max(1, max_batch) // lanes)
+        self._ensure(per_lane)  # lane 0's share; a forward of more images on lane 0 alone grows it
         # lanes > 1: the batch is split over engines on concurrent HIP streams (forked from / joined to
         # the caller's stream, as AlexNetBlocks does), so one lane's partial last rounds overlap the
         # other's kernels. Measured slower at 256 images (281k vs 305k img/s: half-size launches of
@@ -69,16 +70,19 @@ class AlexNetFull:
         # (profiles/r02_ab_full_lanes.txt)
         self._lanes: list[AlexNetFull] = []
         self._lane_streams: list[torch.cuda.Stream] = []
-        per_lane = -(-max(1, max_batch) // lanes)
         for _ in range(lanes - 1):
             self._lanes.append(AlexNetFull(self.weights, classes=classes, device=self.device, max_batch=per_lane,
                                            groups2=groups2, lrn_mode=lrn_mode, knobs=self.knobs))
             self._lane_streams.append(torch.cuda.Stream(self.device))
 
     def _ensure(self, n):
+        """Grow THIS engine to n images (the other lanes' engines are untouched)."""
         if self._h is not None and n <= self._cap:
             return
-        self.close()
+        if self._h is not None:
+            torch.cuda.synchronize(self.device)
+            nat.lib().anx_full_destroy(self._h)
+            self._h = None
         ws = (C.c_void_p * 8)(*[self.weights["w_" + k].data_ptr() for k in LAYERS])
         bs = (C.c_void_p * 8)(*[self.weights["b_" + k].data_ptr() for k in LAYERS])
         h = C.c_void_p()

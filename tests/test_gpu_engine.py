@@ -388,3 +388,31 @@ def test_forward_async_lanes_bit_identical(cuda, N):
     many.join()
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("N,chunk", [(9, 0), (64, 0), (130, 0), (40, 16)])
+def test_fused_pool1_bitwise(cuda, N, chunk):
+    """Pool1 fused into the Winograd input transform (knob fuse_pool1, the tile_forward default) is
+    bit-identical to the pool1 kernel + window + input transform, chunked launches included."""
+    x = init_input(N, "rand", seed=11).to(cuda)
+    kn = {**WINO1, **WINO2, "chunk1": chunk}
+    fused = AlexNetBlocks(device=cuda, init="rand", seed=11, max_batch=N, knobs={**kn, "fuse_pool1": 1})
+    plain = AlexNetBlocks(device=cuda, init="rand", seed=11, max_batch=N, knobs={**kn, "fuse_pool1": 0})
+    y = fused(x)
+    assert torch.equal(y, plain(x))
+    idx = [0, N - 1]
+    ref = blocks_forward(x[idx].cpu(), fused.weights, fused.b1, fused.b2)
+    torch.testing.assert_close(y[idx].cpu().double(), ref, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("np_", [2, 3, 5])
+def test_fused_pool1_row_tiles_bitwise(cuda, np_):
+    """Overlap row tiles compute every pool1 row of their conv2 window: fused and unfused agree bitwise."""
+    xd = init_input(12, "rand", seed=12).to(cuda)
+    fused = AlexNetBlocks(device=cuda, init="rand", seed=12, max_batch=12, knobs={**WINO1, **WINO2})
+    plain = AlexNetBlocks(device=cuda, init="rand", seed=12, max_batch=12, knobs={**WINO1, **WINO2, "fuse_pool1": 0})
+    for t in make_plan(227, 227, np_, OVERLAP).tiles:
+        if t.out.empty:
+            continue
+        xt = xd[:, t.inp.lo:t.inp.hi].contiguous()
+        assert torch.equal(fused.tile_forward(xt, t), plain.tile_forward(xt, t))
