@@ -103,6 +103,83 @@ __global__ void __launch_bounds__(kT) conv1_wino_in_kernel(const float* __restri
   }
 }
 
+// Band form of the input transform: one workgroup = (image, tile row). The 20 image rows of the tile
+// row (5 polyphase rows x 4 phases) are one contiguous run of the NHWC image: they are copied to LDS
+// with 16-B loads (each image row read once per tile row, not once per tile it touches), B^T runs down
+// each (phase row, float column) in place, then B along each tile's 5 polyphase columns. Same fmaf
+// expressions in the same order as conv1_wino_in_kernel, so V is bit-identical.
+constexpr int kBandRows = 5 * kPh;  // image rows per tile row
+constexpr int kMaxRowF = 684;       // LDS row stride (floats, 16-B multiple): image width <= 228
+constexpr int kTB = 512;
+__global__ void __launch_bounds__(kTB) conv1_wino_band_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
+                                                              int Hin, int rowf, int ty, int tx) {
+  __shared__ __attribute__((aligned(16))) float band[kBandRows * kMaxRowF];
+  const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+  const int n = (j / ty) * 8 + xcd, ti = j % ty;
+  if (n >= N) return;  // whole workgroup, before any barrier
+  const int tid = threadIdx.x, rowp = (rowf + 3) & ~3;
+  const int rows = min(kBandRows, Hin - ti * kPitch);  // image rows present (the last tile row runs past Hin)
+  const float* src = x + (static_cast<size_t>(n) * Hin + ti * kPitch) * rowf;
+  // 1. rows -> LDS (row stride rowp, zero past the image)
+  const int u4 = rowp / 4;
+  for (int it = tid; it < kBandRows * u4; it += kTB) {
+    const int r = it / u4, k = (it - r * u4) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (r < rows) {
+      const float* p = src + static_cast<size_t>(r) * rowf + k;
+      if (k + 4 <= rowf) {
+        v = *reinterpret_cast<const f32x4u*>(p);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (k + e < rowf) v[e] = p[e];
+      }
+    }
+    *reinterpret_cast<f32x4*>(&band[r * rowp + k]) = v;
+  }
+  __syncthreads();
+  // 2. t = B^T d over the 5 polyphase rows of each (phase row rh, float column), in place
+  for (int it = tid; it < kPh * rowp; it += kTB) {
+    const int f = it % rowp, rh = it / rowp;
+    float d[kN5], t[kN5];
+#pragma unroll
+    for (int u = 0; u < kN5; ++u) d[u] = band[(kPh * u + rh) * rowp + f];
+#pragma unroll
+    for (int a = 0; a < kN5; ++a) {
+      t[a] = 0.f;
+#pragma unroll
+      for (int u = 0; u < kN5; ++u)
+        if (w33::kBT[a][u] != 0.f) t[a] += w33::kBT[a][u] * d[u];
+    }
+#pragma unroll
+    for (int a = 0; a < kN5; ++a) band[(kPh * a + rh) * rowp + f] = t[a];
+  }
+  __syncthreads();
+  // 3. V[p][a*5 + b][rh*12 + 4q .. +3] = sum_v B^T[b][v] t[a][v]: one (tile, a, 16-B channel unit) per
+  // thread; the unit's 4 channels are 4 consecutive floats of the image row (rw, c)
+  for (int it = tid; it < tx * kN5 * 12; it += kTB) {
+    const int q = it % 12, rest = it / 12, a = rest % kN5, tj = rest / kN5;
+    const int rh = q / 3, jq = q - rh * 3;
+    const float* row = band + (kPh * a + rh) * rowp;
+    f32x4 t[kN5];
+#pragma unroll
+    for (int v = 0; v < kN5; ++v) {
+      const int o = (tj * kPitch + kPh * v) * 3 + 4 * jq;
+      t[v] = o < rowp ? *reinterpret_cast<const f32x4*>(row + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int p = (n * ty + ti) * tx + tj;
+    float* out = V + static_cast<size_t>(p) * kPts * kCh + a * kN5 * kCh + rh * 12 + 4 * jq;
+#pragma unroll
+    for (int bb = 0; bb < kN5; ++bb) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int v = 0; v < kN5; ++v)
+        if (w33::kBT[bb][v] != 0.f) s += w33::kBT[bb][v] * t[v];
+      *reinterpret_cast<f32x4*>(out + bb * kCh) = s;
+    }
+  }
+}
+
 }  // namespace
 
 bool conv1_wino_eligible(int C, int K, int F, int S, int P, int groups) {
@@ -162,10 +239,15 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
   if (w.K % kBN || static_cast<long>(w.P) * kPts * kCh >= (1L << 31) || static_cast<long>(w.P) * 12 >= (1L << 31) ||
       out.Cb % 4 || out.c_off % 4)  // 16-B epilogue stores
     return hipErrorInvalidValue;
-  const int total = w.P * 12;
-  long g = (total + kT - 1) / kT;
-  if (g > (1 << 20)) g = 1 << 20;
-  conv1_wino_in_kernel<<<static_cast<unsigned>(g), kT, 0, s>>>(x, V, total, w.Hin, w.W * 3, w.ty, w.tx);
+  if (kn.conv1_band && w.W * 3 <= kMaxRowF) {
+    const unsigned grid = static_cast<unsigned>((w.N + 7) / 8 * 8 * w.ty);
+    conv1_wino_band_kernel<<<grid, kTB, 0, s>>>(x, V, w.N, w.Hin, w.W * 3, w.ty, w.tx);
+  } else {
+    const int total = w.P * 12;
+    long g = (total + kT - 1) / kT;
+    if (g > (1 << 20)) g = 1 << 20;
+    conv1_wino_in_kernel<<<static_cast<unsigned>(g), kT, 0, s>>>(x, V, total, w.Hin, w.W * 3, w.ty, w.tx);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return wino_gemm_conv1(V, U, bias, out, w.P, w.ty, w.tx, w.H1, w.W1, w.K, relu, s, kn.conv1_occ);

@@ -416,3 +416,17 @@ def test_fused_pool1_row_tiles_bitwise(cuda, np_):
             continue
         xt = xd[:, t.inp.lo:t.inp.hi].contiguous()
         assert torch.equal(fused.tile_forward(xt, t), plain.tile_forward(xt, t))
+
+
+@pytest.mark.parametrize("N,np_", [(7, 1), (64, 1), (6, 3), (6, 5)])
+def test_conv1_band_transform_bitwise(cuda, N, np_):
+    """The band form of the Conv1 polyphase input transform (knob conv1_band, the default) gives the
+    same V as the per-tile gather kernel: whole images and overlap row tiles agree bitwise."""
+    xd = init_input(N, "rand", seed=13).to(cuda)
+    band = AlexNetBlocks(device=cuda, init="rand", seed=13, max_batch=N, knobs={**WINO1, **WINO2})
+    gath = AlexNetBlocks(device=cuda, init="rand", seed=13, max_batch=N, knobs={**WINO1, **WINO2, "conv1_band": 0})
+    for t in make_plan(227, 227, np_, OVERLAP).tiles:
+        if t.out.empty:
+            continue
+        xt = xd[:, t.inp.lo:t.inp.hi].contiguous()
+        assert torch.equal(band.tile_forward(xt, t), gath.tile_forward(xt, t))
