@@ -103,30 +103,34 @@ __global__ void __launch_bounds__(kT) conv1_wino_in_kernel(const float* __restri
   }
 }
 
-// Band form of the input transform: one workgroup = (image, tile row). The 20 image rows of the tile
-// row (5 polyphase rows x 4 phases) are one contiguous run of the NHWC image: they are copied to LDS
-// with 16-B loads (each image row read once per tile row, not once per tile it touches), B^T runs down
-// each (phase row, float column) in place, then B along each tile's 5 polyphase columns. Same fmaf
-// expressions in the same order as conv1_wino_in_kernel, so V is bit-identical.
-constexpr int kBandRows = 5 * kPh;  // image rows per tile row
-constexpr int kMaxRowF = 684;       // LDS row stride (floats, 16-B multiple): image width <= 228
-constexpr int kTB = 512;
-__global__ void __launch_bounds__(kTB) conv1_wino_band_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
-                                                              int Hin, int rowf, int ty, int tx) {
-  __shared__ __attribute__((aligned(16))) float band[kBandRows * kMaxRowF];
+// Band form of the input transform: one workgroup = (image, tile row, NRH of the 4 phase rows). The
+// tile row's image rows of those phases (5 polyphase rows x NRH) are copied to LDS with 16-B loads
+// (each image row read once per tile row, not once per tile it touches), B^T runs down each (phase
+// row, float column) in place, then B along each tile's 5 polyphase columns. Same fmaf expressions
+// in the same order as conv1_wino_in_kernel, so V is bit-identical. The launcher uses NRH = 2 (27 KiB
+// of LDS): with all 4 phase rows (54 KiB) a workgroup rarely fits beside a CU's Winograd GEMM
+// workgroups when stream lanes overlap them, and the bench step ran 236 k instead of 244 k images/s
+// (64 images per GPU: 199 k vs 216 k; profiles/r03_conv1_band2_*); with one phase row (14 KiB) the
+// extra workgroups cost more than the co-residency gains (237 k, profiles/r03_transform_lds_*).
+constexpr int kMaxRowF = 684;  // LDS row stride (floats, 16-B multiple): image width <= 228
+template <int NRH>
+__global__ void __launch_bounds__(kT) conv1_wino_band_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
+                                                             int Hin, int rowf, int ty, int tx) {
+  constexpr int RG = kPh / NRH, BR = kN5 * NRH;  // phase-row groups per tile row, LDS rows
+  __shared__ __attribute__((aligned(16))) float band[BR * kMaxRowF];
   const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-  const int n = (j / ty) * 8 + xcd, ti = j % ty;
+  const int n = (j / (ty * RG)) * 8 + xcd, rem = j % (ty * RG), ti = rem / RG, rg = rem % RG;
   if (n >= N) return;  // whole workgroup, before any barrier
   const int tid = threadIdx.x, rowp = (rowf + 3) & ~3;
-  const int rows = min(kBandRows, Hin - ti * kPitch);  // image rows present (the last tile row runs past Hin)
-  const float* src = x + (static_cast<size_t>(n) * Hin + ti * kPitch) * rowf;
-  // 1. rows -> LDS (row stride rowp, zero past the image)
+  const float* img = x + static_cast<size_t>(n) * Hin * rowf;
+  // 1. LDS row u*NRH + rl = image row ti*12 + 4u + rg*NRH + rl (zero past the image)
   const int u4 = rowp / 4;
-  for (int it = tid; it < kBandRows * u4; it += kTB) {
-    const int r = it / u4, k = (it - r * u4) * 4;
+  for (int it = tid; it < BR * u4; it += kT) {
+    const int lr = it / u4, k = (it - lr * u4) * 4;
+    const int row = ti * kPitch + kPh * (lr / NRH) + rg * NRH + lr % NRH;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (r < rows) {
-      const float* p = src + static_cast<size_t>(r) * rowf + k;
+    if (row < Hin) {
+      const float* p = img + static_cast<size_t>(row) * rowf + k;
       if (k + 4 <= rowf) {
         v = *reinterpret_cast<const f32x4u*>(p);
       } else {
@@ -135,15 +139,15 @@ __global__ void __launch_bounds__(kTB) conv1_wino_band_kernel(const float* __res
           if (k + e < rowf) v[e] = p[e];
       }
     }
-    *reinterpret_cast<f32x4*>(&band[r * rowp + k]) = v;
+    *reinterpret_cast<f32x4*>(&band[lr * rowp + k]) = v;
   }
   __syncthreads();
-  // 2. t = B^T d over the 5 polyphase rows of each (phase row rh, float column), in place
-  for (int it = tid; it < kPh * rowp; it += kTB) {
-    const int f = it % rowp, rh = it / rowp;
+  // 2. t = B^T d over the 5 polyphase rows of each (phase row, float column), in place
+  for (int it = tid; it < NRH * rowp; it += kT) {
+    const int f = it % rowp, rl = it / rowp;
     float d[kN5], t[kN5];
 #pragma unroll
-    for (int u = 0; u < kN5; ++u) d[u] = band[(kPh * u + rh) * rowp + f];
+    for (int u = 0; u < kN5; ++u) d[u] = band[(u * NRH + rl) * rowp + f];
 #pragma unroll
     for (int a = 0; a < kN5; ++a) {
       t[a] = 0.f;
@@ -152,15 +156,15 @@ __global__ void __launch_bounds__(kTB) conv1_wino_band_kernel(const float* __res
         if (w33::kBT[a][u] != 0.f) t[a] += w33::kBT[a][u] * d[u];
     }
 #pragma unroll
-    for (int a = 0; a < kN5; ++a) band[(kPh * a + rh) * rowp + f] = t[a];
+    for (int a = 0; a < kN5; ++a) band[(a * NRH + rl) * rowp + f] = t[a];
   }
   __syncthreads();
-  // 3. V[p][a*5 + b][rh*12 + 4q .. +3] = sum_v B^T[b][v] t[a][v]: one (tile, a, 16-B channel unit) per
+  // 3. V[p][a*5 + b][rh*12 + 4jq .. +3] = sum_v B^T[b][v] t[a][v]: one (tile, a, 16-B channel unit) per
   // thread; the unit's 4 channels are 4 consecutive floats of the image row (rw, c)
-  for (int it = tid; it < tx * kN5 * 12; it += kTB) {
-    const int q = it % 12, rest = it / 12, a = rest % kN5, tj = rest / kN5;
-    const int rh = q / 3, jq = q - rh * 3;
-    const float* row = band + (kPh * a + rh) * rowp;
+  for (int it = tid; it < tx * kN5 * 3 * NRH; it += kT) {
+    const int q = it % (3 * NRH), rest = it / (3 * NRH), a = rest % kN5, tj = rest / kN5;
+    const int rl = q / 3, jq = q - rl * 3, rh = rg * NRH + rl;
+    const float* row = band + (a * NRH + rl) * rowp;
     f32x4 t[kN5];
 #pragma unroll
     for (int v = 0; v < kN5; ++v) {
@@ -240,8 +244,9 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
       out.Cb % 4 || out.c_off % 4)  // 16-B epilogue stores
     return hipErrorInvalidValue;
   if (kn.conv1_band && w.W * 3 <= kMaxRowF) {
-    const unsigned grid = static_cast<unsigned>((w.N + 7) / 8 * 8 * w.ty);
-    conv1_wino_band_kernel<<<grid, kTB, 0, s>>>(x, V, w.N, w.Hin, w.W * 3, w.ty, w.tx);
+    constexpr int kNRH = 2;  // phase rows per workgroup: 27 KiB of LDS (1 and 4 ran slower under lanes)
+    const unsigned grid = static_cast<unsigned>((w.N + 7) / 8 * 8 * w.ty * (kPh / kNRH));
+    conv1_wino_band_kernel<kNRH><<<grid, kT, 0, s>>>(x, V, w.N, w.Hin, w.W * 3, w.ty, w.tx);
   } else {
     const int total = w.P * 12;
     long g = (total + kT - 1) / kT;

@@ -91,8 +91,8 @@ __global__ void __launch_bounds__(kT) wino_in2_kernel(const float* __restrict__ 
 // bit-identical to pool1 + wino_in2. The workgroups of one (image, channel group) share conv1 rows between adjacent
 // tile rows: they get equal blockIdx % 8 (one XCD under round-robin dispatch), so re-reads hit that
 // XCD's L2.
-constexpr int kPG = 32;     // channels per workgroup
 constexpr int kMaxWq = 31;  // window columns held in LDS
+template <int kPG>  // channels per workgroup
 __global__ void __launch_bounds__(kT) pool_wino_in_kernel(const float* __restrict__ c1, float* __restrict__ V, int groups,
                                                           int H1, int W1, int C, int Hq, int Wq, int q_lo, int Hp,
                                                           int Wp, int P, int c1_lo, int ty, int tx) {
@@ -184,11 +184,12 @@ __global__ void __launch_bounds__(kT) pool_wino_in_kernel(const float* __restric
 
 hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, int q_lo, int Hp, int Wp, int P,
                            int c1_lo, float* V, hipStream_t s) {
-  if (w.C % kPG || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * kN * kN >= (1L << 31)) return hipErrorInvalidValue;
+  constexpr int pg = 32;  // 16 channels (14 KiB of LDS) ran slower under lanes: profiles/r03_transform_lds_*
+  if (w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * kN * kN >= (1L << 31)) return hipErrorInvalidValue;
   if (w.P == 0) return hipSuccess;
-  const int groups = w.N * (w.C / kPG);
+  const int groups = w.N * (w.C / pg);
   const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
-  pool_wino_in_kernel<<<grid, kT, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
+  pool_wino_in_kernel<pg><<<grid, kT, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
   return hipGetLastError();
 }
 
