@@ -112,7 +112,8 @@ inline void split_host(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
 // ABL (A/B tool only; production instantiates 0): bit0 no fold, bit1 no DMA refills (times only).
 template <class G, int ABL>
 __global__ void __launch_bounds__(G::NT, G::MINB) sb_gemm_kernel(Args a) {
-  constexpr int NPT = G::NPT, KS = G::KS, BK = G::BK, NW = G::NW, NST = G::NST;
+  constexpr int NPT = G::NPT, KS = G::KS, NW = G::NW, NST = G::NST;
+  [[maybe_unused]] constexpr int BK = G::BK;  // device pass only
   constexpr bool kFold = !(ABL & 1), kDma = !(ABL & 2);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
