@@ -30,7 +30,8 @@ struct Knobs {
                            // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
   int conv1_occ = 0;       // cap on the Conv1 Winograd GEMM's workgroups per CU (LDS padding; 0 = none: 4)
-  int conv2_occ = 0;       // ... and Conv2's (0 = none: 2); a cap leaves room for a concurrent lane's kernels
+  int conv2_occ = -1;      // ... and Conv2's (0 = none: 2; -1 = auto: 1 when the launch has <= one workgroup per
+                           // CU); a cap leaves room for a concurrent lane's kernels
   int conv1_band = 1;      // Conv1 polyphase input transform: 1 = band kernel (image rows of 2 phase rows staged
                            // in LDS once per tile row), 0 = one thread per (tile, 4 channels) gathering from global memory
   int fuse_pool1 = 1;      // tile_forward of a tile that computes every pool1 row its conv2 window needs: pool1

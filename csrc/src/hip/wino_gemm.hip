@@ -10,6 +10,17 @@
 namespace anx::hip {
 namespace {
 
+int device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return cus;
+}
+
 template <class G, int ABL>
 hipError_t launch(const wg::Args& a0, hipStream_t s, int occ) {
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wg::gemm_kernel<G, ABL>),
@@ -19,6 +30,10 @@ hipError_t launch(const wg::Args& a0, hipStream_t s, int occ) {
   a.n_ptiles = (a.P + G::BM - 1) / G::BM;
   a.n_ntiles = a.kg / G::BN;
   if (a.kg % G::BN || a.n_ntiles < 1 || a.u_rows < a.n_ntiles * G::BN) return hipErrorInvalidValue;
+  // auto cap: a launch with no more workgroups than CUs runs one per CU, so the workgroups of a
+  // concurrent stream lane (and its transform kernels) find room on every CU (64 images per GPU as
+  // 2 lanes: 218-219 k vs 209-211 k images/s, profiles/r03_occ_bench_ab.jsonl)
+  if (occ < 0) occ = a.n_ptiles * a.n_ntiles <= device_cus() ? 1 : 0;
   const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
   wg::gemm_kernel<G, ABL><<<grid, G::NT, occupancy_lds(G::kLdsBytes, occ), s>>>(a);
   return hipGetLastError();
