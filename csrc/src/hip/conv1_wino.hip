@@ -113,8 +113,8 @@ __global__ void __launch_bounds__(kT) conv1_wino_in_kernel(const float* __restri
 // (64 images per GPU: 199 k vs 216 k; profiles/r03_conv1_band2_*); with one phase row (14 KiB) the
 // extra workgroups cost more than the co-residency gains (237 k, profiles/r03_transform_lds_*).
 constexpr int kMaxRowF = 684;  // LDS row stride (floats, 16-B multiple): image width <= 228
-template <int NRH>
-__global__ void __launch_bounds__(kT) conv1_wino_band_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
+template <int NRH, int NT>
+__global__ void __launch_bounds__(NT) conv1_wino_band_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
                                                              int Hin, int rowf, int ty, int tx) {
   constexpr int RG = kPh / NRH, BR = kN5 * NRH;  // phase-row groups per tile row, LDS rows
   __shared__ __attribute__((aligned(16))) float band[BR * kMaxRowF];
@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(kT) conv1_wino_band_kernel(const float* __rest
   const float* img = x + static_cast<size_t>(n) * Hin * rowf;
   // 1. LDS row u*NRH + rl = image row ti*12 + 4u + rg*NRH + rl (zero past the image)
   const int u4 = rowp / 4;
-  for (int it = tid; it < BR * u4; it += kT) {
+  for (int it = tid; it < BR * u4; it += NT) {
     const int lr = it / u4, k = (it - lr * u4) * 4;
     const int row = ti * kPitch + kPh * (lr / NRH) + rg * NRH + lr % NRH;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(kT) conv1_wino_band_kernel(const float* __rest
   }
   __syncthreads();
   // 2. t = B^T d over the 5 polyphase rows of each (phase row, float column), in place
-  for (int it = tid; it < NRH * rowp; it += kT) {
+  for (int it = tid; it < NRH * rowp; it += NT) {
     const int f = it % rowp, rl = it / rowp;
     float d[kN5], t[kN5];
 #pragma unroll
@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(kT) conv1_wino_band_kernel(const float* __rest
   __syncthreads();
   // 3. V[p][a*5 + b][rh*12 + 4jq .. +3] = sum_v B^T[b][v] t[a][v]: one (tile, a, 16-B channel unit) per
   // thread; the unit's 4 channels are 4 consecutive floats of the image row (rw, c)
-  for (int it = tid; it < tx * kN5 * 3 * NRH; it += kT) {
+  for (int it = tid; it < tx * kN5 * 3 * NRH; it += NT) {
     const int q = it % (3 * NRH), rest = it / (3 * NRH), a = rest % kN5, tj = rest / kN5;
     const int rl = q / 3, jq = q - rl * 3, rh = rg * NRH + rl;
     const float* row = band + (a * NRH + rl) * rowp;
@@ -246,7 +246,7 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
   if (kn.conv1_band && w.W * 3 <= kMaxRowF) {
     constexpr int kNRH = 2;  // phase rows per workgroup: 27 KiB of LDS (1 and 4 ran slower under lanes)
     const unsigned grid = static_cast<unsigned>((w.N + 7) / 8 * 8 * w.ty * (kPh / kNRH));
-    conv1_wino_band_kernel<kNRH><<<grid, kT, 0, s>>>(x, V, w.N, w.Hin, w.W * 3, w.ty, w.tx);
+    conv1_wino_band_kernel<kNRH, 512><<<grid, 512, 0, s>>>(x, V, w.N, w.Hin, w.W * 3, w.ty, w.tx);  // 8 waves
   } else {
     const int total = w.P * 12;
     long g = (total + kT - 1) / kT;

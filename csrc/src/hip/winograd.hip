@@ -92,8 +92,8 @@ __global__ void __launch_bounds__(kT) wino_in2_kernel(const float* __restrict__ 
 // tile rows: they get equal blockIdx % 8 (one XCD under round-robin dispatch), so re-reads hit that
 // XCD's L2.
 constexpr int kMaxWq = 31;  // window columns held in LDS
-template <int kPG>  // channels per workgroup
-__global__ void __launch_bounds__(kT) pool_wino_in_kernel(const float* __restrict__ c1, float* __restrict__ V, int groups,
+template <int kPG, int NT>  // channels, threads per workgroup
+__global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restrict__ c1, float* __restrict__ V, int groups,
                                                           int H1, int W1, int C, int Hq, int Wq, int q_lo, int Hp,
                                                           int Wp, int P, int c1_lo, int ty, int tx) {
   __shared__ __attribute__((aligned(16))) float band[kN][kMaxWq][kPG];
@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(kT) pool_wino_in_kernel(const float* __restric
   // 1. pooled window rows 3ti .. 3ti+6 into LDS, zero outside the pooled image. A thread owns one
   // (pooled column, 4-channel group) of the band: the row max of each conv1 row the band's 7 pooled
   // rows touch (3 loads) is reused by the two pooled rows that share that conv1 row.
-  for (int it = tid; it < Wq * (kPG / 4); it += kT) {
+  for (int it = tid; it < Wq * (kPG / 4); it += NT) {
     const int c4 = it % (kPG / 4), col = it / (kPG / 4), pc = col - P;
     const bool cin = pc >= 0 && pc < Wp;
     const float* src = c1 + (static_cast<size_t>(n * H1) * W1 + 2 * pc) * C + cg * kPG + 4 * c4;
@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(kT) pool_wino_in_kernel(const float* __restric
   }
   __syncthreads();
   // 2. t = B^T d down each column, in place (a thread owns one (column, 4-channel group))
-  for (int it = tid; it < Wq * (kPG / 4); it += kT) {
+  for (int it = tid; it < Wq * (kPG / 4); it += NT) {
     const int c4 = it % (kPG / 4), col = it / (kPG / 4);
     f32x4 d[kN], t[kN];
 #pragma unroll
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(kT) pool_wino_in_kernel(const float* __restric
   }
   __syncthreads();
   // 3. V[a][b] = sum_v B^T[b][v] t[a][3tj + v], one (tile, row a, 4-channel group) per thread: 16-B stores
-  for (int it = tid; it < tx * kN * (kPG / 4); it += kT) {
+  for (int it = tid; it < tx * kN * (kPG / 4); it += NT) {
     const int c4 = it % (kPG / 4), rest = it / (kPG / 4), a = rest % kN, tj = rest / kN;
     f32x4 t[kN];
 #pragma unroll
@@ -189,7 +189,9 @@ hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, i
   if (w.P == 0) return hipSuccess;
   const int groups = w.N * (w.C / pg);
   const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
-  pool_wino_in_kernel<pg><<<grid, kT, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
+  // 512 threads: 8 waves over the pooling walk and both transforms (bench step +2.7 % over 256 at 128
+  // images per GPU; profiles/r03_transform_threads_*)
+  pool_wino_in_kernel<pg, 512><<<grid, 512, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
   return hipGetLastError();
 }
 

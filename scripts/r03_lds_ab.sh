@@ -1,6 +1,6 @@
 #!/bin/bash
-# LDS footprint of the transform kernels under free-running lanes: conv1_band 1 / 2 (27 / 14 KiB) x
-# fuse_pool1 1 / 2 (27 / 14 KiB), bench step at 128 and 64 images (alternating arms), correctness
+# Transform-kernel variants under free-running lanes: conv1_band 1 / 2 x fuse_pool1 1 / 2 (256 / 512 threads;
+# earlier: 27 / 14 KiB of LDS), bench step at 128 and 64 images (alternating arms), correctness
 # of every arm against arm 0 (ab_variants max_abs_diff_vs_arm0).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
