@@ -32,8 +32,6 @@ struct Knobs {
   int conv1_occ = 0;       // cap on the Conv1 Winograd GEMM's workgroups per CU (LDS padding; 0 = none: 4)
   int conv2_occ = -1;      // ... and Conv2's (0 = none: 2; -1 = auto: 1 when the launch has <= one workgroup per
                            // CU); a cap leaves room for a concurrent lane's kernels
-  int conv2_wide = 0;      // Conv2 GEMM workgroup tile: 0 = 64 tiles x 64 filters (4 waves, 2 per CU), 1 = 64 x 128
-                           // (8 waves, 1 per CU: a quarter less operand traffic per FLOP)
   int conv1_band = 1;      // Conv1 polyphase input transform: 1 = band kernel (image rows of 2 phase rows staged
                            // in LDS once per tile row), 0 = one thread per (tile, 4 channels) gathering from global memory
   int fuse_pool1 = 1;      // tile_forward of a tile that computes every pool1 row its conv2 window needs: pool1
@@ -41,7 +39,7 @@ struct Knobs {
 };
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
-// ANX_BF16_GLDS, ANX_BF16_BIG, ANX_BF16_FC, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV2_WIDE, ANX_CONV1_BAND, ANX_FUSE_POOL1 when set.
+// ANX_BF16_GLDS, ANX_BF16_BIG, ANX_BF16_FC, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1 when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

@@ -43,9 +43,11 @@ hipError_t launch(const wg::Args& a0, hipStream_t s, int occ) {
 using C2 = wg::Cfg<49, 96, 2, 2, 48, 2>;    // Conv2: 64 tiles x 64 filters, 48 KiB ring, 2 workgroups per CU
 using C2g = wg::Cfg<49, 48, 2, 2, 48, 2>;   // Conv2 with 2 groups (48 channels per group)
 using C1 = wg::Cfg<25, 48, 2, 1, 48, 2>;    // Conv1: 64 tiles x 32 filters, 2 waves, 4 workgroups per CU
-using C2_64x128 = wg::Cfg<49, 96, 2, 4, 48, 2>;  // 64 tiles x 128 filters, 8 waves, 72 KiB ring (knob conv2_wide)
 #ifdef ANX_WGEMM_ABLATIONS
 using C2_32x4 = wg::Cfg<49, 96, 2, 2, 32, 4>;    // 64 KiB ring: 2 slices in flight behind the current one
+// 64 tiles x 128 filters, 8 waves, 72 KiB ring: a quarter less operand traffic per FLOP, but 636 vs 623 us
+// alone at 300 images and 246-247 k vs 255 k images/s in the bench step (profiles/r03_conv2_wide_*)
+using C2_64x128 = wg::Cfg<49, 96, 2, 4, 48, 2>;
 using C1_64x96 = wg::Cfg<25, 48, 2, 3, 48, 2>;   // 64 x 96 (every filter: V read once), 6 waves, 60 KiB ring
 using C1_32x96 = wg::Cfg<25, 48, 1, 3, 48, 2>;   // 32 x 96, 3 waves, 48 KiB ring
 using C1_48x2w4 = wg::Cfg<25, 48, 4, 1, 48, 2>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
@@ -97,9 +99,9 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
     else
       switch (cfg < 0 ? 0 : cfg) {
         case 0: e = launch_abl<C2>(a, s, occ, abl); break;
-        case 2: e = launch_abl<C2_64x128>(a, s, occ, abl); break;
 #ifdef ANX_WGEMM_ABLATIONS
         case 1: e = launch_abl<C2_32x4>(a, s, occ, abl); break;
+        case 2: e = launch_abl<C2_64x128>(a, s, occ, abl); break;
 #endif
         default: break;
       }

@@ -257,8 +257,7 @@ hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s
 
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,
                       hipStream_t s, const Knobs& k) {
-  return wino_gemm_conv2(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.C, w.K, w.groups, relu, s, k.conv2_occ, 0,
-                         k.conv2_wide && w.C / w.groups == 96 && (w.K / w.groups) % 128 == 0 ? 2 : -1);
+  return wino_gemm_conv2(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.C, w.K, w.groups, relu, s, k.conv2_occ);
 }
 
 }  // namespace anx::hip
