@@ -103,16 +103,21 @@ __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restric
   const int CG = C / kPG, n = grp / CG, cg = grp % CG;
   const int tid = threadIdx.x;
   // 1. pooled window rows 3ti .. 3ti+6 into LDS, zero outside the pooled image. A thread owns one
-  // (pooled column, 4-channel group) of the band: the row max of each conv1 row the band's 7 pooled
-  // rows touch (3 loads) is reused by the two pooled rows that share that conv1 row.
-  for (int it = tid; it < Wq * (kPG / 4); it += NT) {
-    const int c4 = it % (kPG / 4), col = it / (kPG / 4), pc = col - P;
+  // (pooled column, 4-channel group) of the band's upper (rows 0-3) or lower (rows 4-6) half: the row
+  // max of each conv1 row its pooled rows touch (3 loads) is reused by the two pooled rows that share
+  // that conv1 row. Two halves: every thread of the 512 has a walk, each walk half as long.
+  const int per_half = Wq * (kPG / 4);
+  for (int it = tid; it < 2 * per_half; it += NT) {
+    const int half = it / per_half, ih = it - half * per_half;
+    const int r0 = half ? 4 : 0, r1 = half ? kN : 4;
+    const int c4 = ih % (kPG / 4), col = ih / (kPG / 4), pc = col - P;
     const bool cin = pc >= 0 && pc < Wp;
     const float* src = c1 + (static_cast<size_t>(n * H1) * W1 + 2 * pc) * C + cg * kPG + 4 * c4;
     f32x4 prev = {0.f, 0.f, 0.f, 0.f};  // row max of conv1 row 2*pr (shared with pooled row pr - 1)
     int prev_row = -1;
 #pragma unroll
     for (int r = 0; r < kN; ++r) {
+      if (r < r0 || r >= r1) continue;
       const int R = ti * kM + r, pr = q_lo + R;
       f32x4 m = {0.f, 0.f, 0.f, 0.f};
       if (cin && R < Hq && pr >= 0 && pr < Hp) {
