@@ -103,6 +103,8 @@ def parse():
     ap.add_argument("--lane-priority", type=int, default=0, help="dp: HIP stream priority of the side lanes (-1 = high)")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
                     help="blocks model: engine knob override (anx.utils.tuning.KNOBS), repeatable; A/B only")
+    ap.add_argument("--stagger", action="store_true",
+                    help="dp: free-running lanes restart half a forward apart after a device sync (default: together)")
     ap.add_argument("--joined-lanes", action="store_true",
                     help="dp: join the stream lanes every step (AlexNetBlocks.forward) instead of free-running lanes "
                          "half a step apart (forward_async; the default with local input)")
@@ -197,6 +199,7 @@ def main():
         knobs = {k: int(v) if v.lstrip("-").isdigit() else v for k, v in (kv.split("=", 1) for kv in a.knob)}
         model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B, lanes=a.lanes,
                               lane_priority=a.lane_priority, knobs=knobs)
+        model.stagger = a.stagger
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
     else:
         GB = a.batch or DEFAULT_BATCH[a.workload]
@@ -336,7 +339,7 @@ def main():
                            "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
                            "gflop_per_image": round(flops / 1e9, 4), "tflops": round(imgs * flops / 1e12, 2),
                            "prewarm_steps": n_pw, "prewarm_ms": prewarm_ms, "lanes": a.full_lanes,
-                           "lane_sync": ("free-running lanes half a forward apart (forward_async)" if pipe.async_lanes
+                           "lane_sync": ("free-running lanes, staggered at a mid-forward event (forward_async)" if pipe.async_lanes
                                          else "lanes forked/joined every step" if a.full_lanes > 1 else "one lane")},
             }
             print(json.dumps(rec), flush=True)
@@ -359,7 +362,8 @@ def main():
             extra = {"input_source": a.input_source, "lanes": a.lanes, "hip_graph": use_graph, "knobs": a.knob,
                      "input_batches_rotated": len(rot) or 1,
                      "input_bytes_rotated": sum(t.numel() * 4 for t in rot) or pipe._xb[0].numel() * 4,
-                     "lane_sync": ("free-running lanes half a step apart, per-lane gathers (forward_async)"
+                     "lane_sync": ("free-running lanes (%s start), per-lane gathers (forward_async)"
+                                   % ("staggered" if a.stagger else "joint")
                                    if pipe.async_lanes else "lanes forked/joined every step")}
         else:
             par, scaling = f"{a.workload}-{a.decomp}{world}", "strong"

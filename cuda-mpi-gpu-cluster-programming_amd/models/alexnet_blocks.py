@@ -97,6 +97,12 @@ class AlexNetBlocks:
                 # lane_priority < 0: side lanes on high-priority streams (their waves dispatch first)
                 self._lane_streams.append(torch.cuda.Stream(self.device, priority=lane_priority))
         self._own_stream = None  # lane 0's stream in forward_async (the joined forward uses the current one)
+        # forward_async from idle lanes: all lanes start together (False, default) or lane i after lane
+        # i-1's stage 1, half a forward apart (True). With the fused transforms the staggered start no
+        # longer pays in steady state (257.2 / 256.0 k vs 258.3 / 257.5 k images/s over 200 steps) and
+        # its pipeline fill costs a short timed window ~1.5 % (20 steps: 250.5 / 249.6 k vs 253.0 /
+        # 254.4 k; profiles/r03_stagger_bench_ab.jsonl)
+        self.stagger = False
 
     @property
     def is_cuda(self) -> bool:
@@ -214,10 +220,10 @@ class AlexNetBlocks:
         """Throughput form of :meth:`forward` for a loop of forwards on the same buffers.
 
         Each lane enqueues its slice on its own stream and is NOT joined back: consecutive calls
-        pipeline, and the lanes stay half a forward apart (one lane's transforms and pools under the
-        other's GEMMs) instead of being realigned by a join every call. When every lane is idle (the
-        first call, or after any device synchronisation) the lanes fork from the current stream and
-        lane i >= 1 starts when lane i-1's stage 1 (Conv1 + Pool1) is done, which sets that phase.
+        pipeline instead of being realigned by a join every call. When every lane is idle (the first
+        call, or after any device synchronisation) the lanes fork from the current stream; with
+        ``stagger`` set, lane i >= 1 then starts when lane i-1's stage 1 (Conv1 + Pool1) is done, half
+        a forward apart (one lane's transforms and pools under the other's GEMMs), else together.
 
         Contract: ``out`` holds a call's results once :meth:`join` has made the current stream wait
         for the lanes (or after a device synchronisation); ``x`` and ``out`` must not be written by
@@ -252,7 +258,7 @@ class AlexNetBlocks:
                         st.wait_event(ev)
                 if pre_lane is not None:
                     pre_lane(i, lo, hi)
-                if fresh and i + 1 < L:
+                if fresh and i + 1 < L and self.stagger:
                     eng.stage1(x[lo:hi], plan)  # = tile_forward as stage1 + stage2, with the phase event between
                     ev = torch.cuda.Event()
                     ev.record(st)
