@@ -17,3 +17,7 @@ timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --kernel-trace \
   --output-format csv -d $O/v_pmc_write -o run -- python3 $BENCH > $O/v_pmc_write.log 2>&1 &&
 python3 tools/pmc_clock.py $O/v_pmc_fetch $O/v_pmc_write > $O/v_pmc_bytes_b128.md
+# lanes 2 / 3 / 4 at 128 images with the joint lane start (200 steps)
+for l in 2 3 4; do
+  timeout -k 10 200 python -u bench.py --lanes $l --steps 200 --warmup 10 --no-b1 >> $O/v_lanes.jsonl 2>> $O/v_lanes.err || exit $?
+done
