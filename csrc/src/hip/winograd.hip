@@ -92,7 +92,10 @@ __global__ void __launch_bounds__(kT) wino_in2_kernel(const float* __restrict__ 
 // tile rows: they get equal blockIdx % 8 (one XCD under round-robin dispatch), so re-reads hit that
 // XCD's L2.
 constexpr int kMaxWq = 31;  // window columns held in LDS
-template <int kPG, int NT>  // channels, threads per workgroup
+// POOL = false: the same kernel on a materialised conv2 window (`c1` = window [N][Hq][Wq][C], q_lo, Hp,
+// Wp, P, c1_lo unused): the window rows of the tile row are copied to LDS with 16-B loads (each
+// window row read once per tile row instead of once per tile it touches, as wino_in2_kernel does).
+template <int kPG, int NT, bool POOL = true>  // channels, threads per workgroup
 __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restrict__ c1, float* __restrict__ V, int groups,
                                                           int H1, int W1, int C, int Hq, int Wq, int q_lo, int Hp,
                                                           int Wp, int P, int c1_lo, int ty, int tx) {
@@ -106,8 +109,18 @@ __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restric
   // (pooled column, 4-channel group) of the band's upper (rows 0-3) or lower (rows 4-6) half: the row
   // max of each conv1 row its pooled rows touch (3 loads) is reused by the two pooled rows that share
   // that conv1 row. Two halves: every thread of the 512 has a walk, each walk half as long.
+  if constexpr (!POOL) {
+    for (int it = tid; it < kN * Wq * (kPG / 4); it += NT) {
+      const int c4 = it % (kPG / 4), rest = it / (kPG / 4), col = rest % Wq, r = rest / Wq;
+      const int R = ti * kM + r;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (R < Hq)
+        v = *reinterpret_cast<const f32x4*>(c1 + (static_cast<size_t>(n * Hq + R) * Wq + col) * C + cg * kPG + 4 * c4);
+      *reinterpret_cast<f32x4*>(&band[r][col][4 * c4]) = v;
+    }
+  }
   const int per_half = Wq * (kPG / 4);
-  for (int it = tid; it < 2 * per_half; it += NT) {
+  for (int it = tid; it < (POOL ? 2 * per_half : 0); it += NT) {
     const int half = it / per_half, ih = it - half * per_half;
     const int r0 = half ? 4 : 0, r1 = half ? kN : 4;
     const int c4 = ih % (kPG / 4), col = ih / (kPG / 4), pc = col - P;
@@ -254,6 +267,14 @@ void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::ve
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s) {
   const long n = static_cast<long>(w.P) * w.C;
   if (n >= (1L << 31) || w.C % 2) return hipErrorInvalidValue;
+  if (w.C % 32 == 0 && w.Wq <= kMaxWq && n * kN * kN < (1L << 31)) {  // band form (bit-identical V)
+    if (w.P == 0) return hipSuccess;
+    const int groups = w.N * (w.C / 32);
+    const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
+    pool_wino_in_kernel<32, 512, false>
+        <<<grid, 512, 0, s>>>(x, V, groups, 0, 0, w.C, w.Hq, w.Wq, 0, 0, 0, 0, 0, w.ty, w.tx);
+    return hipGetLastError();
+  }
   const long g = (n / 2 + kT - 1) / kT;
   const unsigned gg = static_cast<unsigned>(g < (1 << 20) ? g : (1 << 20));
   wino_in2_kernel<<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
