@@ -32,8 +32,9 @@ struct Knobs {
   int conv1_occ = 0;       // cap on the Conv1 Winograd GEMM's workgroups per CU (LDS padding; 0 = none: 4)
   int conv2_occ = -1;      // ... and Conv2's (0 = none: 2; -1 = auto: 1 when the launch has <= one workgroup per
                            // CU); a cap leaves room for a concurrent lane's kernels
-  int conv1_band = 1;      // Conv1 polyphase input transform: 1 = band kernel (image rows of 2 phase rows staged
-                           // in LDS once per tile row), 0 = one thread per (tile, 4 channels) gathering from global memory
+  int conv1_band = 2;      // Conv1 polyphase input transform, band kernel (a tile row's image rows staged in LDS):
+                           // 2 = all 4 phase rows x half the tile columns (each 192-B V segment written whole),
+                           // 1 = 2 phase rows x all columns, 0 = per-tile gathers from global memory
   int fuse_pool1 = 1;      // tile_forward of a tile that computes every pool1 row its conv2 window needs: pool1
                            // fused into the Winograd input transform (no window round trip), 0 = pool1 kernel
 };

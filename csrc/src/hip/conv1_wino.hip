@@ -113,16 +113,23 @@ __global__ void __launch_bounds__(kT) conv1_wino_in_kernel(const float* __restri
 // (64 images per GPU: 199 k vs 216 k; profiles/r03_conv1_band2_*); with one phase row (14 KiB) the
 // extra workgroups cost more than the co-residency gains (237 k, profiles/r03_transform_lds_*).
 constexpr int kMaxRowF = 684;  // LDS row stride (floats, 16-B multiple): image width <= 228
-template <int NRH, int NT>
+constexpr int kMaxSplitF = 384;  // column-split rows: <= 10 tiles per split (36 * 10 + 24 floats)
+template <int NRH, int NCS, int NT>  // phase rows, column splits, threads per workgroup
 __global__ void __launch_bounds__(NT) conv1_wino_band_kernel(const float* __restrict__ x, float* __restrict__ V, int N,
                                                              int Hin, int rowf, int ty, int tx) {
   constexpr int RG = kPh / NRH, BR = kN5 * NRH;  // phase-row groups per tile row, LDS rows
-  __shared__ __attribute__((aligned(16))) float band[BR * kMaxRowF];
+  constexpr int MAXF = NCS == 1 ? kMaxRowF : kMaxSplitF;
+  __shared__ __attribute__((aligned(16))) float band[BR * MAXF];
   const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-  const int n = (j / (ty * RG)) * 8 + xcd, rem = j % (ty * RG), ti = rem / RG, rg = rem % RG;
+  const int n = (j / (ty * RG * NCS)) * 8 + xcd, rem = j % (ty * RG * NCS);
+  const int ti = rem / (RG * NCS), rg = (rem / NCS) % RG, cs = rem % NCS;
   if (n >= N) return;  // whole workgroup, before any barrier
-  const int tid = threadIdx.x, rowp = (rowf + 3) & ~3;
-  const float* img = x + static_cast<size_t>(n) * Hin * rowf;
+  // this split's tiles [tj0, tj1) read image floats [f0, f0 + width) of each row (zero past the image)
+  const int tps = (tx + NCS - 1) / NCS, tj0 = cs * tps, tj1 = min(tx, tj0 + tps);
+  const int f0 = tj0 * kPitch * 3;
+  const int rowp = NCS == 1 ? (rowf + 3) & ~3 : (tps * kPitch + 2 * kPh) * 3;
+  const int tid = threadIdx.x;
+  const float* img = x + static_cast<size_t>(n) * Hin * rowf + f0;
   // 1. LDS row u*NRH + rl = image row ti*12 + 4u + rg*NRH + rl (zero past the image)
   const int u4 = rowp / 4;
   for (int it = tid; it < BR * u4; it += NT) {
@@ -131,12 +138,12 @@ __global__ void __launch_bounds__(NT) conv1_wino_band_kernel(const float* __rest
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (row < Hin) {
       const float* p = img + static_cast<size_t>(row) * rowf + k;
-      if (k + 4 <= rowf) {
+      if (f0 + k + 4 <= rowf) {
         v = *reinterpret_cast<const f32x4u*>(p);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (k + e < rowf) v[e] = p[e];
+          if (f0 + k + e < rowf) v[e] = p[e];
       }
     }
     *reinterpret_cast<f32x4*>(&band[lr * rowp + k]) = v;
@@ -161,14 +168,14 @@ __global__ void __launch_bounds__(NT) conv1_wino_band_kernel(const float* __rest
   __syncthreads();
   // 3. V[p][a*5 + b][rh*12 + 4jq .. +3] = sum_v B^T[b][v] t[a][v]: one (tile, a, 16-B channel unit) per
   // thread; the unit's 4 channels are 4 consecutive floats of the image row (rw, c)
-  for (int it = tid; it < tx * kN5 * 3 * NRH; it += NT) {
-    const int q = it % (3 * NRH), rest = it / (3 * NRH), a = rest % kN5, tj = rest / kN5;
+  for (int it = tid; it < (tj1 - tj0) * kN5 * 3 * NRH; it += NT) {
+    const int q = it % (3 * NRH), rest = it / (3 * NRH), a = rest % kN5, tj = tj0 + rest / kN5;
     const int rl = q / 3, jq = q - rl * 3, rh = rg * NRH + rl;
     const float* row = band + (a * NRH + rl) * rowp;
     f32x4 t[kN5];
 #pragma unroll
     for (int v = 0; v < kN5; ++v) {
-      const int o = (tj * kPitch + kPh * v) * 3 + 4 * jq;
+      const int o = ((tj - tj0) * kPitch + kPh * v) * 3 + 4 * jq;
       t[v] = o < rowp ? *reinterpret_cast<const f32x4*>(row + o) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const int p = (n * ty + ti) * tx + tj;
@@ -246,7 +253,12 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
   if (kn.conv1_band && w.W * 3 <= kMaxRowF) {
     constexpr int kNRH = 2;  // phase rows per workgroup: 27 KiB of LDS (1 and 4 ran slower under lanes)
     const unsigned grid = static_cast<unsigned>((w.N + 7) / 8 * 8 * w.ty * (kPh / kNRH));
-    conv1_wino_band_kernel<kNRH, 512><<<grid, 512, 0, s>>>(x, V, w.N, w.Hin, w.W * 3, w.ty, w.tx);  // 8 waves
+    if (kn.conv1_band == 2 && (w.tx + 1) / 2 * 36 + 24 <= kMaxSplitF) {  // all 4 phase rows, 2 column halves
+      const unsigned g2 = static_cast<unsigned>((w.N + 7) / 8 * 8 * w.ty * 2);
+      conv1_wino_band_kernel<4, 2, 512><<<g2, 512, 0, s>>>(x, V, w.N, w.Hin, w.W * 3, w.ty, w.tx);
+    } else {
+      conv1_wino_band_kernel<kNRH, 1, 512><<<grid, 512, 0, s>>>(x, V, w.N, w.Hin, w.W * 3, w.ty, w.tx);  // 8 waves
+    }
   } else {
     const int total = w.P * 12;
     long g = (total + kT - 1) / kT;

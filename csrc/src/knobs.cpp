@@ -32,7 +32,7 @@ const Field kFields[] = {
     {"bf16_fc", &Knobs::bf16_fc, nullptr, 0, 1, "ANX_BF16_FC"},
     {"conv1_occ", &Knobs::conv1_occ, nullptr, 0, 8, "ANX_CONV1_OCC"},
     {"conv2_occ", &Knobs::conv2_occ, nullptr, -1, 8, "ANX_CONV2_OCC"},
-    {"conv1_band", &Knobs::conv1_band, nullptr, 0, 1, "ANX_CONV1_BAND"},
+    {"conv1_band", &Knobs::conv1_band, nullptr, 0, 2, "ANX_CONV1_BAND"},
     {"fuse_pool1", &Knobs::fuse_pool1, nullptr, 0, 1, "ANX_FUSE_POOL1"},
 };
 

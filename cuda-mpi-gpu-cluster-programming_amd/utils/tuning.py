@@ -11,8 +11,9 @@ Names and values:
   ``direct``.
 * integer knobs: ``chunk1``, ``chunk2`` (images per launch), ``conv1_occ``, ``conv2_occ`` (Winograd
   GEMM workgroups-per-CU caps), ``force_vec4``, ``force_scalar`` (direct GEMM tiles), and the bf16
-  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``; ``conv1_band`` (1, the default: the
-  Conv1 input transform stages each tile row's image rows in LDS; 0: per-tile global gathers);
+  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``; ``conv1_band`` (2, the default: the
+  Conv1 input transform stages a tile row's image rows in LDS, all 4 phase rows x half the tile
+  columns per workgroup; 1: 2 phase rows x all columns; 0: per-tile global gathers);
   ``fuse_pool1`` (1, the
   default: a tile that computes all the pool1 rows its conv2 window needs runs pool1 inside the
   Winograd input transform; 0: the pool1 kernel and the window buffer).

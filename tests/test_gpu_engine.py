@@ -418,12 +418,13 @@ def test_fused_pool1_row_tiles_bitwise(cuda, np_):
         assert torch.equal(fused.tile_forward(xt, t), plain.tile_forward(xt, t))
 
 
-@pytest.mark.parametrize("N,np_", [(7, 1), (64, 1), (6, 3), (6, 5)])
-def test_conv1_band_transform_bitwise(cuda, N, np_):
-    """The band form of the Conv1 polyphase input transform (knob conv1_band, the default) gives the
-    same V as the per-tile gather kernel: whole images and overlap row tiles agree bitwise."""
+@pytest.mark.parametrize("N,np_,form", [(7, 1, 1), (64, 1, 1), (6, 3, 1), (6, 5, 1), (7, 1, 2), (6, 5, 2)])
+def test_conv1_band_transform_bitwise(cuda, N, np_, form):
+    """The band forms of the Conv1 polyphase input transform (knob conv1_band: 1 = 2 phase rows per
+    workgroup; 2 = 4 phase rows x half the tile columns, the default) give the same V as the per-tile
+    gather kernel: whole images and overlap row tiles agree bitwise."""
     xd = init_input(N, "rand", seed=13).to(cuda)
-    band = AlexNetBlocks(device=cuda, init="rand", seed=13, max_batch=N, knobs={**WINO1, **WINO2})
+    band = AlexNetBlocks(device=cuda, init="rand", seed=13, max_batch=N, knobs={**WINO1, **WINO2, "conv1_band": form})
     gath = AlexNetBlocks(device=cuda, init="rand", seed=13, max_batch=N, knobs={**WINO1, **WINO2, "conv1_band": 0})
     for t in make_plan(227, 227, np_, OVERLAP).tiles:
         if t.out.empty:
