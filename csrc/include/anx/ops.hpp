@@ -104,9 +104,10 @@ hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s
 // Pool1 (3x3 / 2 max) fused with the input transform: V straight from the conv1 output c1 [N][H1][W1][C]
 // (conv1 row c1_lo first). Window row R is pool1 row q_lo + R (zero outside [0, Hp)), window column c is
 // pool1 column c - P (zero outside [0, Wp)); every non-zero window row must be computable from c1's rows.
-// Bit-identical to maxpool + wino_input. C % 32 == 0, Wq <= 31.
+// Bit-identical to maxpool + wino_input. C % 32 == 0, Wq <= 31, and the pooling must be 3x3 / stride 2
+// (pool_F, pool_S; anything else returns hipErrorInvalidValue: the kernel's walk is written for 3/2).
 hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, int q_lo, int Hp, int Wp, int P,
-                           int c1_lo, float* V, hipStream_t s);
+                           int c1_lo, float* V, hipStream_t s, int pool_F = 3, int pool_S = 2);
 // Fused batched GEMM + output transform + bias + optional ReLU into `out` (wino_gemm.hpp); Knobs:
 // conv2_occ (workgroups per CU cap).
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,

@@ -243,6 +243,9 @@ hipError_t BlocksEngine::stage2(int N, const TilePlan& t, float* y, hipStream_t 
 
 bool BlocksEngine::fused_pool1(int N, const TilePlan& t) const {
   if (impl_ != Impl::Mfma || !k_.fuse_pool1 || wv_ == nullptr || d_.C1 % 32 || wq_ > 31) return false;
+  // the fused kernel's pooling walk is 3x3 / stride 2 (pool_wino_in_kernel); other pool1 shapes take
+  // the unfused maxpool + input transform
+  if (b1_.pool.F != 3 || b1_.pool.S != 2) return false;
   // every pool1 row of the window (inside the pooled image) is computed by this tile
   const int lo = std::max(t.q.lo, 0), hi = std::min(t.q.hi, d_.Hp1);
   if (lo < t.p1.lo || hi > t.p1.hi) return false;
@@ -273,7 +276,8 @@ hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, 
     RoctxRange rx("anx pool1+conv2+pool2+lrn");
     const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
     if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
-    ANX_TRY(hip::wino_pool_input(w, c1_, t.c1.size(), d_.W1, t.q.lo, d_.Hp1, d_.Wp1, k2.P, t.c1.lo, wv_, s));
+    ANX_TRY(hip::wino_pool_input(w, c1_, t.c1.size(), d_.W1, t.q.lo, d_.Hp1, d_.Wp1, k2.P, t.c1.lo, wv_, s,
+                                     b1_.pool.F, b1_.pool.S));
     ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
     ANX_TRY(pool2_chunk(n, t, y + n0 * y_img, s));
   }

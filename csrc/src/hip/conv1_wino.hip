@@ -103,15 +103,16 @@ __global__ void __launch_bounds__(kT) conv1_wino_in_kernel(const float* __restri
   }
 }
 
-// Band form of the input transform: one workgroup = (image, tile row, NRH of the 4 phase rows). The
-// tile row's image rows of those phases (5 polyphase rows x NRH) are copied to LDS with 16-B loads
-// (each image row read once per tile row, not once per tile it touches), B^T runs down each (phase
-// row, float column) in place, then B along each tile's 5 polyphase columns. Same fmaf expressions
-// in the same order as conv1_wino_in_kernel, so V is bit-identical. The launcher uses NRH = 2 (27 KiB
-// of LDS): with all 4 phase rows (54 KiB) a workgroup rarely fits beside a CU's Winograd GEMM
-// workgroups when stream lanes overlap them, and the bench step ran 236 k instead of 244 k images/s
-// (64 images per GPU: 199 k vs 216 k; profiles/r03_conv1_band2_*); with one phase row (14 KiB) the
-// extra workgroups cost more than the co-residency gains (237 k, profiles/r03_transform_lds_*).
+// Band form of the input transform: one workgroup = (image, tile row, NRH of the 4 phase rows, NCS
+// column splits). The tile row's image rows of those phases (5 polyphase rows x NRH) are copied to LDS
+// with 16-B loads (each image row read once per tile row, not once per tile it touches), B^T runs down
+// each (phase row, float column) in place, then B along each tile's 5 polyphase columns. Same fmaf
+// expressions in the same order as conv1_wino_in_kernel, so V is bit-identical. The launcher's default
+// (Knobs::conv1_band = 2) is NRH = 4 x NCS = 2: all 4 phase rows of half the tile columns, 30 KiB of
+// LDS, each 192-B V segment written whole (profiles/r03_band_split_*). conv1_band = 1 keeps NRH = 2 x
+// NCS = 1 (27 KiB). All 4 phase rows of a whole tile row (54 KiB) rarely fit beside a CU's Winograd
+// GEMM workgroups under stream lanes (236 k vs 244 k images/s, profiles/r03_conv1_band2_*); one phase
+// row (14 KiB) adds more workgroups than co-residency gains (profiles/r03_transform_lds_*).
 constexpr int kMaxRowF = 684;  // LDS row stride (floats, 16-B multiple): image width <= 228
 constexpr int kMaxSplitF = 384;  // column-split rows: <= 10 tiles per split (36 * 10 + 24 floats)
 template <int NRH, int NCS, int NT>  // phase rows, column splits, threads per workgroup

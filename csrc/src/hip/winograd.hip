@@ -201,8 +201,9 @@ __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restric
 }  // namespace
 
 hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, int q_lo, int Hp, int Wp, int P,
-                           int c1_lo, float* V, hipStream_t s) {
-  constexpr int pg = 32;  // 16 channels (14 KiB of LDS) ran slower under lanes: profiles/r03_transform_lds_*
+                           int c1_lo, float* V, hipStream_t s, int pool_F, int pool_S) {
+  constexpr int pg = 32;
+  if (pool_F != 3 || pool_S != 2) return hipErrorInvalidValue;  // the walk below is 3x3 / stride 2 only  // 16 channels (14 KiB of LDS) ran slower under lanes: profiles/r03_transform_lds_*
   if (w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * kN * kN >= (1L << 31)) return hipErrorInvalidValue;
   if (w.P == 0) return hipSuccess;
   const int groups = w.N * (w.C / pg);

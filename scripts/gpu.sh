@@ -12,7 +12,14 @@
 #   full     bf16 full-AlexNet bench + kernel trace     matrix  scripts/run_matrix.sh at batch 1 and 256
 #   peak     sustained f32 MFMA peak (anx_mfmapeak)     workloads  bench.py --workload v4 / v5 at N=1
 #   versions native V3/V4/V5 CLI (shared-GPU ranks)    markers rocprofv3 marker trace of a V5 peer run
-# Outputs land in gpurun_out/ (merged back by gpurun).
+#   benchab  bench.py arms alternated $BENCH_REPS times: BENCH_AB="conv1_band=1|conv1_band=2" (';' joins
+#            knobs of one arm), one JSON line per run into benchab.jsonl ($BENCH_STEPS timed steps)
+#   bytes    per-kernel HBM bytes, clock and MFMA busy of the bench step (FETCH / WRITE passes)
+#   wgemm    anx_wgemm Winograd GEMM A/B at 300 and 64 images; wgpmc: its clock / MFMA busy pass
+#   halo     V5 halo pipeline A/B on shared-GPU peer ranks: np {2,4} x chunks {1, auto} ($HALO_BATCH)
+#   tests_k  a subset of GPU tests: pytest -k "$TESTS_K" (one process)
+# Outputs land in gpurun_out/ (merged back by gpurun). This one script replaces the per-session
+# wrappers of rounds 1-3.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -70,6 +77,42 @@ for s in "$@"; do
     # the profiler wraps each rank (anxrun only forks; it never touches the GPU)
     markers) run markers 300 $B/anxrun -np 2 --timeout 240 -- rocprofv3 --marker-trace --kernel-trace --stats \
                -d "$O/markers" -o "rank_%pid%" -- $B/anx --version v5 --transport peer --batch 32 --iters 10 ;;
+    tests_k) run tests_k 900 python -u -m pytest tests -x -v -m gpu -k "${TESTS_K:?}" --timeout 240 --timeout-method thread ;;
+    benchab)
+      IFS='|' read -r -a arms <<< "${BENCH_AB:?BENCH_AB=arm|arm}"
+      for rep in $(seq "${BENCH_REPS:-3}"); do
+        for arm in "${arms[@]}"; do
+          kargs=()
+          IFS=';' read -r -a kvs <<< "$arm"
+          for kv in "${kvs[@]}"; do [ -n "$kv" ] && kargs+=(--knob "$kv"); done
+          echo "== benchab rep $rep arm '$arm'"
+          timeout -k 10 200 python -u bench.py --steps "${BENCH_STEPS:-20}" --warmup 5 --no-b1 $BARGS "${kargs[@]}" \
+            >> "$O/benchab.jsonl" 2>> "$O/benchab.err" || { echo "== benchab FAILED"; exit 1; }
+          tail -1 "$O/benchab.jsonl" | cut -c1-160
+        done
+      done ;;
+    bytes)
+      BYARGS="--lanes 1 --steps 6 --warmup 2 --no-b1 --prewarm-s 0 $BARGS"
+      timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --kernel-trace \
+        --output-format csv -d "$O/pmc_fetch" -o run -- python3 bench.py $BYARGS > "$O/pmc_fetch.log" 2>&1 &&
+      timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --kernel-trace \
+        --output-format csv -d "$O/pmc_write" -o run -- python3 bench.py $BYARGS > "$O/pmc_write.log" 2>&1 &&
+      python3 tools/pmc_clock.py "$O/pmc_fetch" "$O/pmc_write" > "$O/pmc_bytes.md" || { echo "== bytes FAILED"; exit 1; }
+      cat "$O/pmc_bytes.md" ;;
+    wgemm)
+      run wg300 120 $B/anx_wgemm --images 300 --iters 20
+      run wg64 120 $B/anx_wgemm --images 64 --iters 20 ;;
+    wgpmc)
+      timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+        --kernel-trace --output-format csv -d "$O/wgpmc" -o run -- $B/anx_wgemm --images 300 --iters 3 \
+        > "$O/wgpmc.log" 2>&1 && python3 tools/pmc_clock.py "$O/wgpmc" || { echo "== wgpmc FAILED"; exit 1; } ;;
+    halo)
+      for np in 2 4; do
+        for ch in 1 0; do
+          run "halo_np${np}_c${ch}" 240 $B/anxrun -np $np --timeout 200 -- $B/anx --version v5 --transport peer \
+            --batch "${HALO_BATCH:-512}" --iters 30 --init rand --chunks $ch
+        done
+      done ;;
     *) echo "unknown session $s"; exit 2 ;;
   esac
 done

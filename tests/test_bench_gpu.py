@@ -31,6 +31,9 @@ def test_bench_blocks_contract():
     c = rec["config"]
     assert rec["metric"] == metric and rec["dtype"] == "fp32" and c["global_batch"] == 64
     assert c["lanes"] == 2 and rec["vs_baseline"] > 1 and c["b1_warm_ms"] > 0
+    # vs_baseline is the like-for-like cold ratio (fresh process, one image), the warm one has its own key
+    assert rec["vs_baseline"] == c["b1_process_cold_vs_reference"] and "cold" in rec["vs_baseline_kind"]
+    assert c["b1_vs_reference_warm"] > rec["vs_baseline"]
     # unambiguous semantics: distinct input batches beyond the Infinity Cache, an engine-cold and a
     # process-cold (fresh `anx --version v3` process) batch-1 latency next to the reference's 610.661 ms
     assert c["input_batches_rotated"] >= 4 and c["input_bytes_rotated"] > (256 << 20)
@@ -52,6 +55,7 @@ def test_bench_workloads_one_gpu(workload):
     if workload == "v4":  # the native host-staged runtime: chunked per-rank DMA, link rate reported
         assert c["phases_ms"]["compute"] > 0 and c["h2d_gbps_link"] > 1 and 0 < c["h2d_bound_fraction"] < 1.5
         assert c["chunks"] >= 1 and c["runtime"].startswith("native")
+        assert "RCCL" not in c["pipeline"] and "per-rank chunked H2D" in c["pipeline"]
     else:  # the native runtime: critical-path phases, balanced layout, transport
         assert c["phases_ms"]["stage2"] > 0 and c["transport"] == "rccl" and c["imbalance"] == 1.0
 

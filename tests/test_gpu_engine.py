@@ -53,7 +53,8 @@ def test_engine_grouped_conv2(cuda):
 
 
 def test_engine_large_batch_variant(cuda):
-    """batch 256 takes the 128x128 / 128x96 MFMA tiles (small batches take 64x64)."""
+    """batch 256 runs the Winograd path in one launch per conv (both fused Winograd GEMMs at their
+    largest grids, the band transforms, pool1 fused into the Conv2 input transform)."""
     N = 256
     m = AlexNetBlocks(device=cuda, init="rand", seed=8, max_batch=N)
     x = init_input(N, "rand", seed=8)
@@ -403,6 +404,26 @@ def test_fused_pool1_bitwise(cuda, N, chunk):
     idx = [0, N - 1]
     ref = blocks_forward(x[idx].cpu(), fused.weights, fused.b1, fused.b2)
     torch.testing.assert_close(y[idx].cpu().double(), ref, rtol=2e-5, atol=2e-6)
+
+
+def test_fused_pool1_refuses_other_pool_shapes(cuda):
+    """The fused pool1 + input transform kernel walks 3x3 / stride-2 windows only. A block-1 pool of
+    another shape (2x2 / 2 also gives 27x27 here, so the rest of the engine is unchanged) must take
+    the unfused pool1 kernel + window path with fuse_pool1 on: both knob settings agree bitwise and
+    match the fp64 oracle of that spec."""
+    from dataclasses import replace
+    from anx.config import PoolSpec, blocks
+    b1, b2 = blocks()
+    b1 = replace(b1, pool=PoolSpec(2, 2))
+    N = 12
+    x = init_input(N, "rand", seed=14)
+    kn = {**WINO1, **WINO2}
+    on = AlexNetBlocks(device=cuda, init="rand", seed=14, max_batch=N, specs=(b1, b2), knobs={**kn, "fuse_pool1": 1})
+    off = AlexNetBlocks(device=cuda, init="rand", seed=14, max_batch=N, specs=(b1, b2), knobs={**kn, "fuse_pool1": 0})
+    y = on(x.to(cuda))
+    assert torch.equal(y, off(x.to(cuda)))
+    ref = blocks_forward(x[[0, N - 1]], on.weights, b1, b2)
+    torch.testing.assert_close(y[[0, N - 1]].cpu().double(), ref, rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.parametrize("np_", [2, 3, 5])
