@@ -16,13 +16,20 @@ MI355X". Workloads (--workload):
   input rows (halo included) over its own host link and its output rows back, in image chunks so
   H2D, compute and D2H overlap. The JSON reports the H2D GB/s in the step and the link's H2D-only
   rate (``h2d_bound_img_s``: what the H2D stage alone would allow).
-* ``v5``: BASELINE config "V5 GPU-aware, batch 1024": the same, device-resident, with per-layer
-  tiles and a pool1-halo exchange between the GPUs of a row group (README.md:157-166), run by the
-  native V5 runtime (anx/v5.hpp through libanx_dist: halo chunks pipelined against stage1, scatter
-  of the next step and gather of this one on a second stream, weights broadcast device to device).
-  --transport auto | rccl (one GPU per rank) | peer (IPC, ranks may share a GPU); --decomp auto
-  (default for v5: balanced batch groups x 2-way row split) | rows (the reference's row split over
-  every rank) | hybrid (batch first, rows only below one image per rank) | batch.
+* ``v5``: BASELINE config "V5 GPU-aware, batch 1024", device-resident "halo + gather": with
+  ``--input-source local`` (default) every rank's images x input rows are placed on its device once,
+  so a step moves only the per-layer pool1 halos of a row group and the gather (``root``: the
+  reference's data flow, the root scatters the batch every step). Run by the native V5 runtime
+  (anx/v5.hpp through libanx_dist: halo chunks pipelined against stage1, halo-free ranks as
+  free-running stream lanes, the gather of one step on a second stream under the next step's compute,
+  weights broadcast device to device). --transport auto | rccl (one GPU per rank) | peer / loopback
+  (ranks may share a GPU); --decomp auto (default: the cost model's pick, anx/cost.hpp) | rows (the
+  reference's row split over every rank) | hybrid (batch first, rows only below one image per rank) |
+  batch.
+
+Every workload's JSON carries ``model``: the modelled 1/2/4/8-GPU curve of its configuration
+(``"measured": false``; anx.parallel.cost), with this run's measured single-GPU rate in the model's
+throughput table when N = 1.
 
 Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
 bench.py --gpus N``. Rank 0 prints ONE JSON line.
@@ -81,8 +88,9 @@ def parse():
                     help="dp: images per GPU (default 128 for blocks; 256 for full = BASELINE's 2048 over 8 GPUs)")
     ap.add_argument("--batch", type=int, default=None, help="v4/v5: global batch (default 256 / 1024)")
     ap.add_argument("--decomp", default=None, choices=["auto", "rows", "hybrid", "batch"],
-                    help="v4/v5 decomposition (default: rows for v4, auto = balanced for v5)")
-    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer"], help="v5 device transport")
+                    help="v4/v5 decomposition (default on GPU: auto = the cost model's pick; rows on the CPU rehearsal)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer", "loopback"],
+                    help="v5 device transport")
     ap.add_argument("--chunks", type=int, default=0, help="v5: halo pipeline chunks per step (0 = auto)")
     ap.add_argument("--pipeline", type=int, default=-1, choices=[-1, 0, 1],
                     help="v5: next-step scatter / this-step gather on a second stream (-1 auto)")
@@ -94,7 +102,7 @@ def parse():
     ap.add_argument("--full-lanes", type=int, default=1,
                     help="--model full: concurrent stream lanes the batch is split over (AlexNetFull lanes)")
     ap.add_argument("--input-source", default="local", choices=["root", "local"],
-                    help="dp: local = per-rank synthetic shard; root = rank 0 scatters the batch")
+                    help="dp / v5: local = per-rank (device-resident) data; root = rank 0 scatters the batch every step")
     ap.add_argument("--no-gather", action="store_true", help="dp: leave outputs on their ranks")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu = gloo rehearsal (tests only)")
     ap.add_argument("--graph", type=int, default=0,
@@ -220,13 +228,14 @@ def main():
             from anx.utils.init import init_weights
             b1, b2 = anx.config.blocks()
             wl = NativeV5(GB, init_weights("rand", 1234, b1, b2) if rank == 0 else None, specs=(b1, b2),
-                          decomp=a.decomp, transport=a.transport, chunks=a.chunks, pipeline=a.pipeline, impl=a.impl)
+                          decomp=a.decomp, transport=a.transport, chunks=a.chunks, pipeline=a.pipeline, impl=a.impl,
+                          input_source=a.input_source, lanes=a.lanes)
             wl.fill((torch.rand((GB, d.H, d.W, d.C0), device=dev, generator=g) * 0.1) if rank == 0 else None)
         else:
-            from anx.parallel.plan import balanced_row_ways, make_hybrid_plan
+            from anx.parallel.plan import make_hybrid_plan, pick_row_ways
             from anx.parallel.workloads import RowsWorkload
             if a.decomp == "auto":
-                a.decomp = {world: "rows", 1: "batch"}.get(balanced_row_ways(world, GB), "rows")
+                a.decomp = {world: "rows", 1: "batch"}.get(pick_row_ways(world, GB, a.workload, "root"), "rows")
             # every rank holds an engine sized for the largest share any rank gets
             rw = {"rows": world, "hybrid": 0, "batch": 1}[a.decomp]
             hp = make_hybrid_plan(227, 227, world, GB, rw)
@@ -373,8 +382,10 @@ def main():
                         if a.workload == "v4" and cuda else
                         "root host -> gloo scatter -> overlap tiles -> gloo gather (CPU rehearsal)"
                         if a.workload == "v4" else
-                        "root device -> scatter -> stage1 (chunks) -> pool1 halo chunks -> stage2 -> gather "
-                        "(native V5 runtime; next scatter / this gather on a second stream)")
+                        ("device-resident input (placed once) -> " if a.input_source == "local" else
+                         "root device -> scatter (every step) -> ") +
+                        "stage1 (chunks) -> pool1 halo chunks -> stage2 (halo-free ranks: free-running lanes) -> "
+                        "gather (native V5 runtime; gather on a second stream under the next step)")
             extra = {**wl.describe(), "decomp": a.decomp, "phases_ms": phases}
             if a.workload == "v4" and cuda:
                 gbps = wl.probe_h2d_gbps()
@@ -386,6 +397,21 @@ def main():
                               "h2d_bound_fraction": round(imgs / (world * gbps * 1e9 / per_img), 3)})
             elif a.workload == "v4":
                 extra["lanes"] = a.lanes
+        # the modelled 1/2/4/8-GPU curve of this configuration (anx/cost.hpp; measured: false), with
+        # this run's measured rate in the throughput table when it ran on one GPU
+        model = None
+        if cuda:
+            from anx.parallel import cost
+            wl_name = "dp" if wl is None else a.workload
+            per_gpu = B if wl is None else GB
+            ov = {}
+            if world == 1 and wl_name in ("dp", "v5"):
+                pts = dict(cost.curve(wl_name, per_gpu)["params"]["rate"])
+                pts[B if wl is None else GB] = round(imgs)
+                ov["rate"] = ",".join(f"{k}:{v}" for k, v in sorted(pts.items()))
+            model = cost.curve(wl_name, per_gpu, input_source=a.input_source if wl_name != "v4" else "root",
+                               mode="per_layer", overrides=ov)
+            model.pop("steps", None)
         rec = {
             "metric": METRIC,
             "value": round(imgs, 2),
@@ -423,6 +449,7 @@ def main():
                 "mfma_tflops": round(imgs * mf / 1e12 / world, 2),
                 "mfma_tflops_note": "per GPU; fp32 matrix peak 157 TF/s (155 sustained)",
                 "vs_baseline_throughput": round(imgs / (1000.0 / BASELINE_V3_MS), 1),
+                "model": model,
                 **b1,
                 **b1p,
             },

@@ -40,6 +40,18 @@ int anx_make_plan(int H, int W, int np, int mode, const anx_block_c* b1, const a
                   int* owned_in, int* owned_p1, anx_xfer_c* in_halos, int* n_in_halos, anx_xfer_c* p1_halos,
                   int* n_p1_halos, int cap);
 
+/* ---- cost model (anx/cost.hpp): modelled, not measured ----
+ * workload: 0 dp (batch = images per GPU), 1 v4, 2 v5 (batch = global); input_source: 0 local, 1 root;
+ * mode: 0 overlap, 1 per_layer; row_ways: -1 = the model's pick; overrides: "name=value;..." over the
+ * default CostParams (rate=IMG:IPS,... for the rate table). anx_cost_curve writes the JSON curve over
+ * nps[0..n_nps) into buf; anx_cost_step one step's JSON; anx_cost_pick_row_ways the chosen split. */
+int anx_cost_curve(int workload, const int* nps, int n_nps, int batch, int row_ways, int input_source, int mode,
+                   const char* overrides, char* buf, size_t cap);
+int anx_cost_step(int workload, int np, int batch, int row_ways, int input_source, int mode, const char* overrides,
+                  char* buf, size_t cap);
+int anx_cost_pick_row_ways(int workload, int np, int batch, int input_source, int mode, const char* overrides,
+                           int* row_ways);
+
 /* ---- engine (Blocks 1-2) ---- */
 /* Hybrid batch x rows plan (anx/plan.hpp make_hybrid_plan). Per rank r (arrays of np):
    group[r], index[r] (position in its group), img[2r..2r+1] (its image range), tile[r] (its rows);
@@ -129,14 +141,18 @@ int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const
 /* ---- V5 device-resident runtime (libanx_dist.so: anx/v5.hpp) ----
  * anx_v5_create is collective over the `world` ranks (TCP bootstrap at master_addr:master_port, then
  * the transport: RCCL or peer IPC). Weights are read on rank 0 only (others may pass NULL).
- * mode: 0 overlap, 1 per_layer; row_ways: -1 balanced, 0 batch first, r > 0 groups of r ranks;
- * transport: "auto" | "rccl" | "peer"; chunks: 0 auto; pipeline: -1 auto, 0 off, 1 on;
- * peer_sync: "" | "flags" | "notes". */
+ * mode: 0 overlap, 1 per_layer; row_ways: -1 the cost model's pick, 0 batch first, r > 0 groups of r
+ * ranks; transport: "auto" | "rccl" | "peer" | "loopback"; chunks: 0 auto; pipeline: -1 auto, 0 off,
+ * 1 on; peer_sync: "" | "flags" | "notes"; input_source: 0 local (device-resident, placed once by
+ * set_input), 1 root (scattered every step); lanes: stream lanes of a halo-free rank (0 = default 2);
+ * keep_log: keep the transport's transfer log (anx_v5_log). */
 int anx_v5_create(void** out, int rank, int world, int local_rank, int local_world, int nnodes,
                   const char* master_addr, int master_port, double timeout_s, const anx_block_c* b1,
                   const anx_block_c* b2, int H, int W, const float* w1, const float* bias1, const float* w2,
                   const float* bias2, int batch, int row_ways, int mode, const char* transport, int chunks,
-                  int pipeline, int poison, int impl, const char* peer_sync);
+                  int pipeline, int poison, int impl, const char* peer_sync, int input_source, int lanes,
+                  int keep_log);
+int anx_v5_log(void* h, char* buf, size_t cap); /* this rank's issued transfers, one per line */
 int anx_v5_destroy(void* h);
 int anx_v5_set_input(void* h, const float* host_x); /* collective; rank 0's batch, others NULL */
 int anx_v5_step(void* h, int steps);                /* enqueue `steps` steps, no host sync */
@@ -145,15 +161,15 @@ int anx_v5_output(void* h, float* host_y);          /* rank 0: last step's outpu
 /* JSON objects into buf (truncated to cap): per-phase mean ms since the last reset / the layout */
 int anx_v5_phases(void* h, char* buf, size_t cap, int reset);
 int anx_v5_describe(void* h, char* buf, size_t cap);
-/* Record-only schedule, no GPU: rank < 0 -> every transfer of one step (scatter, halo chunks,
- * gather), else the transfers rank `rank`'s transport issues, in order; one per line. */
+/* Record-only schedule, no GPU: rank < 0 -> every transfer of one step (scatter with root input,
+ * halo chunks, gather), else the transfers rank `rank`'s transport issues, in order; one per line. */
 int anx_v5_schedule(int np, const anx_block_c* b1, const anx_block_c* b2, int H, int W, int batch, int row_ways,
-                    int mode, int chunks, int rank, const char* transport, char* buf, size_t cap);
+                    int mode, int chunks, int rank, const char* transport, int input_source, char* buf, size_t cap);
 
 /* ---- V4 host-staged runtime (libanx_dist.so: anx/v4.hpp) ----
  * Collective create; the batch and the output live in a shared pinned host segment every rank maps
  * (anx_v4_segment): write the input, call anx_v4_input_ready (collective), step, anx_v4_sync_all
- * (collective), read the output. row_ways: -1 balanced, 0 batch first, r > 0 groups of r ranks. */
+ * (collective), read the output. row_ways: -1 the cost model's pick, 0 batch first, r > 0 groups of r ranks. */
 int anx_v4_create(void** out, int rank, int world, int local_rank, int local_world, int nnodes,
                   const char* master_addr, int master_port, double timeout_s, const anx_block_c* b1,
                   const anx_block_c* b2, int H, int W, const float* w1, const float* bias1, const float* w2,

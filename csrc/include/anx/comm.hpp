@@ -6,9 +6,9 @@
 //                 to bootstrap RCCL. Point-to-point ops are queued in a group and progressed
 //                 together with poll(), so a halo exchange in both directions cannot deadlock
 //                 (the reference relies on MPI_Isend/Irecv + Waitall for the same).
-//   * DeviceComm — RCCL communicator over xGMI for device buffers (V5): broadcast, grouped
-//                 send/recv on a dedicated comm stream, ordered against the compute stream by
-//                 events.
+//   * DeviceComm — device-buffer communicator (V5): RCCL over xGMI, or a loopback implementation of
+//                 the same contract for ranks sharing one GPU; broadcast, grouped send/recv on a
+//                 dedicated comm stream, ordered against the compute stream by events.
 // Rank/world come from ANX_RANK/ANX_WORLD_SIZE (set by anxrun) or RANK/WORLD_SIZE (torchrun);
 // rendezvous at ANX_MASTER_ADDR:ANX_MASTER_PORT (or MASTER_ADDR/MASTER_PORT), default 127.0.0.1.
 #pragma once
@@ -68,28 +68,43 @@ class HostComm {
   std::vector<Op> ops_;
 };
 
-// RCCL communicator (V5). Built from a HostComm used only for the unique-id bootstrap.
+// Device communicator (V5): grouped send/recv and broadcast of device buffers on a dedicated comm
+// stream, ordered against compute streams by events. Two implementations behind one interface:
+//   rccl      — an RCCL communicator over xGMI (one GPU per rank);
+//   loopback  — the same contract for ranks that SHARE a GPU (RCCL refuses two ranks on one device):
+//               group_end matches the queued sends / receives through the host channel (the receiver
+//               sends the IPC handle + offset of each receive buffer), the sender's comm stream waits
+//               for the receiver's "posted" flag, copies straight into the receiver's IPC-mapped
+//               buffer (hipMemcpyAsync) and raises a "landed" flag the receiver's comm stream waits
+//               for (hipStreamWriteValue32 / hipStreamWaitValue32 on IPC-shared words). It exists so
+//               the RCCL transport's pack / staging / grouped P2P / unpack / two-communicator code
+//               runs unchanged, multi-rank, on a one-GPU box.
 class DeviceComm {
  public:
-  DeviceComm(HostComm& boot, int device);
-  ~DeviceComm();
-  DeviceComm(const DeviceComm&) = delete;
-  DeviceComm& operator=(const DeviceComm&) = delete;
-  hipStream_t stream() const { return stream_; }
-  void group_start();
-  void group_end();
-  void send(const void* buf, size_t bytes, int dst);
-  void recv(void* buf, size_t bytes, int src);
-  void bcast(void* buf, size_t bytes, int root);
-  // Make `other` wait for everything queued on the comm stream so far (and vice versa).
+  virtual ~DeviceComm() = default;
+  virtual const char* kind() const = 0;  // "rccl" | "loopback"
+  virtual hipStream_t stream() const = 0;
+  virtual void group_start() = 0;
+  virtual void group_end() = 0;
+  virtual void send(const void* buf, size_t bytes, int dst) = 0;
+  virtual void recv(void* buf, size_t bytes, int src) = 0;
+  virtual void bcast(void* buf, size_t bytes, int root) = 0;
+  // Make the comm stream wait for everything queued on `compute` so far / the reverse.
   void after(hipStream_t compute);   // comm stream waits for compute
   void before(hipStream_t compute);  // compute waits for comm stream
-  void abort();
+  // Make this comm stream wait for everything queued on `other`'s comm stream so far: two
+  // communicators of one rank then run in one total order, the same on every rank (their ops are
+  // issued in the same host order everywhere), so neither can wait on a peer that is itself stuck
+  // behind the other communicator.
+  void after_comm(DeviceComm& other);
+  virtual void abort() {}
 
- private:
-  void* comm_ = nullptr;  // ncclComm_t
-  hipStream_t stream_ = nullptr;
+ protected:
+  void init_sync();  // creates ev_ (call from the implementations' constructors)
   hipEvent_t ev_ = nullptr;
 };
+// Collective over `boot` (every rank constructs its communicators in the same order).
+std::unique_ptr<DeviceComm> make_rccl_comm(HostComm& boot, int device);
+std::unique_ptr<DeviceComm> make_loopback_comm(HostComm& boot, int device);
 
 }  // namespace anx

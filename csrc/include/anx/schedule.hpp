@@ -99,6 +99,8 @@ class Transport {
   // Record-only mode (no HIP / RCCL / socket call): every transfer is appended to log() — the
   // schedule the transport would execute, for tests and --dry-run.
   bool record_only = false;
+  // Keep the log in live mode too (tests: the transfers a live run issued == the record-only schedule).
+  bool keep_log = false;
   const std::vector<std::string>& log() const { return log_; }
   // transfers this rank took part in so far (every mode)
   size_t issued() const { return issued_; }
@@ -106,14 +108,15 @@ class Transport {
  protected:
   void note(const Transfer& x) {
     ++issued_;
-    if (record_only) log_.push_back(x.str());
+    if (record_only || keep_log) log_.push_back(x.str());
   }
   std::vector<std::string> log_;
   size_t issued_ = 0;
 };
 
-// `c` may be null for a record-only transport (no collective is issued then).
-std::unique_ptr<Transport> make_rccl_transport(HostComm* c, int device, int rank);
+// `c` may be null for a record-only transport (no collective is issued then). loopback: over the
+// loopback DeviceComm (ranks sharing one GPU) instead of an RCCL communicator; name "rccl-loopback".
+std::unique_ptr<Transport> make_rccl_transport(HostComm* c, int device, int rank, bool loopback = false);
 // Peer ordering: "flags" (default where the device supports hipStreamWaitValue32) = the sender's
 // stream writes a sequence number into the receiver's IPC-mapped flag word after its pushes and the
 // receiver's stream waits for it on the device (no host involvement per phase); "notes" = IPC

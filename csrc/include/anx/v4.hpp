@@ -28,7 +28,8 @@ namespace anx {
 
 struct V4Options {
   int batch = 256;
-  int row_ways = -1;  // -1 balanced (balanced_row_ways), 0 batch first, r > 0 groups of r ranks
+  int row_ways = -1;  // -1 the cost model's pick (anx/cost.hpp), 0 batch first, r > 0 groups of r ranks
+  std::string cost;   // cost-model overrides for that pick ("name=value;...")
   int chunks = 0;     // image chunks per rank and step (0 = auto)
   Impl impl = Impl::Mfma;
   Knobs knobs = default_knobs();

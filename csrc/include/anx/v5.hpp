@@ -3,16 +3,21 @@
 // C ABI that bench.py / anx.parallel.workloads drive.
 //
 // One step over a hybrid batch x rows plan (anx/plan.hpp):
-//   scatter   root X[images, tile.in rows] -> every rank's Tile             (transport, io stream)
+//   scatter   root X[images, tile.in rows] -> every rank's Tile             (root input only: io stream)
 //   stage1    conv1 + ReLU + pool1 into the conv2 window, chunk by chunk   (compute stream)
 //   halo_p1   pool1 rows between row neighbours, one transfer list per chunk (halo stream), so the
 //             halo of chunk c moves while stage1 computes chunk c+1 and stage2(c) waits only for it
 //   stage2    conv2 + ReLU + pool2 + LRN of each chunk                      (compute stream)
 //   gather    Y[images, tile.out rows] -> root YFull                        (transport, io stream)
-// Steady state is pipelined across steps: scatter(k+1) and gather(k) run on the io stream while the
-// compute stream runs step k; no stream is synchronised with the host inside a step. Weights reach
-// every rank by an RCCL broadcast from the root's device (reference M4/M5 MPI_Bcast,
-// v4_mpi_cuda/src/main_mpi_cuda.cpp:47-50).
+// With local input (the default, BASELINE.json's "device-resident RCCL/xGMI halo + gather") every
+// rank's images x input rows live on its device from set_input on: a step moves only halos and the
+// gather. A rank whose tile needs no halo (a row group of one rank, or overlap tiles) runs its images
+// as free-running stream lanes (the fused tile forward on each), joined only by the gather. Steady
+// state is pipelined across steps: scatter(k+1) and gather(k) run on the io stream while the compute
+// streams run step k; no stream is synchronised with the host inside a step. Weights reach every rank
+// by a device broadcast from the root (reference M4/M5 MPI_Bcast, v4_mpi_cuda/src/main_mpi_cuda.cpp:47-50).
+// The default row split is the cost model's (anx/cost.hpp), which weighs scatter / halo / gather bytes
+// against per-rank compute.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -22,6 +27,7 @@
 #include <vector>
 
 #include "anx/comm.hpp"
+#include "anx/cost.hpp"
 #include "anx/engine.hpp"
 #include "anx/plan.hpp"
 #include "anx/schedule.hpp"
@@ -30,16 +36,23 @@ namespace anx {
 
 struct V5Options {
   int batch = 1024;
-  // row split inside each group of ranks: -1 = auto (balanced_row_ways), 0 = batch first, rows only
-  // below one image per rank (make_hybrid_plan's auto), r > 0 = groups of r ranks (np = the
-  // reference's pure row split)
+  // row split inside each group of ranks: -1 = the cost model's pick (anx/cost.hpp pick_row_ways), 0 =
+  // batch first, rows only below one image per rank (make_hybrid_plan's auto), r > 0 = groups of r
+  // ranks (np = the reference's pure row split)
   int row_ways = -1;
   Decomp mode = Decomp::PerLayer;
-  std::string transport = "auto";  // auto | rccl | peer
+  // local (default): the BASELINE's device-resident V5 ("halo + gather"): every rank holds its images x
+  // input rows on its own device (placed once by set_input), so a step moves only pool1 halos and the
+  // gather; root: the reference's data flow, the root scatters the batch every step
+  InputSource input_source = InputSource::Local;
+  std::string transport = "auto";  // auto | rccl | peer | loopback (RCCL transport over the loopback comm)
   int chunks = 0;                  // halo pipeline chunks per step (0 = auto)
   int pipeline = -1;               // scatter(k+1) / gather(k) on the io stream: -1 auto, 0 off, 1 on
+  int lanes = 2;                   // stream lanes for a rank whose tile needs no halo (whole images, overlap tiles)
   bool poison = false;             // NaN-fill every consumed buffer after use (ordering tests)
+  bool keep_log = false;           // keep the transport's log of issued transfers (tests)
   std::string peer_sync;           // peer transport ordering: "" (default) | flags | notes
+  std::string cost;                // cost-model overrides for the row-split pick ("name=value;...")
   Impl impl = Impl::Mfma;
   Knobs knobs = default_knobs();
 };
@@ -52,26 +65,27 @@ struct PlanStats {
 };
 PlanStats plan_stats(const HybridPlan& p);
 
-// Row ways a balanced default uses for `batch` images over `np` ranks: the fewest row ways r (r | np)
-// whose per-rank work max / mean is within 1.1 (images split over np / r groups, 13 output rows over
-// r ranks), which keeps the halo exchange of the row split without the 8-way split's imbalance
-// (output rows 2,2,2,2,2,1,1,1: max / mean 1.23) and redundant Conv1. At least 2 when np > 1 so the
-// V5 halo path runs; batch < np / r images fall back to finer row splits.
-int balanced_row_ways(int np, int batch, int H = kInH, int W = kInW);
-
 // V5 transport by node: auto = RCCL when every rank of this node has its own GPU or the job spans
-// nodes, else peer (IPC, ranks share a GPU). Throws for a combination that cannot run.
+// nodes, else peer (IPC, ranks share a GPU); loopback = the RCCL transport over the loopback device
+// comm (ranks share a GPU; single node). Throws for a combination that cannot run.
 std::string pick_v5_transport(const std::string& want, const RankInfo& ri, int ndev, bool dry);
 
 // The plan, schedule and halo chunking of a V5 job: identical on every rank (a pure function of the
 // job shape), which is what keeps every rank's sequence of transport calls the same.
+struct RankBytes {  // bytes one rank sends / receives per step, by phase
+  double scatter_recv = 0, scatter_sent = 0, halo_sent = 0, halo_recv = 0, gather_sent = 0, gather_recv = 0;
+};
 struct V5Layout {
   HybridPlan plan;
   Schedule sched;
   int row_ways = 1, chunks = 1;
+  bool local_input = true;                          // no scatter inside a step (placed once by set_input)
   std::vector<std::vector<Transfer>> halo_chunks;  // chunk_of(P1Halo list, c, chunks)
-  // every transfer of one step in issue order: scatter, halo chunks, gather
+  // every transfer of one step in issue order: scatter (root input only), halo chunks, gather
   std::vector<Transfer> step_transfers() const;
+  // per rank, from step_transfers(); input_placement_bytes: the one-time placement of local input
+  std::vector<RankBytes> rank_bytes() const;
+  double input_placement_bytes() const;
 };
 V5Layout make_v5_layout(int np, const BlockSpec& b1, const BlockSpec& b2, int H, int W, const V5Options& o);
 
@@ -86,7 +100,8 @@ class V5Runtime {
   V5Runtime& operator=(const V5Runtime&) = delete;
 
   // Collective: the root's `host_x` (the global batch [batch, H, W, C0]) becomes the input of every
-  // following step (other ranks pass nullptr). Drains the pipeline first.
+  // following step (other ranks pass nullptr). Drains the pipeline first. Local input: the images x
+  // rows of every rank are placed on its device here, once (not part of a step).
   void set_input(const float* host_x);
   // Enqueue one step (pipelined with its neighbours when the pipeline is on). No host sync.
   void step();
@@ -96,7 +111,8 @@ class V5Runtime {
   void output(float* host_y);
   // Mean ms per step since the last reset, by phase, on the compute stream's critical path:
   // scatter (waiting for the input), stage1, halo_p1 (waiting for halo chunks), stage2, gather
-  // (end of stage2 to end of the gather). Syncs first.
+  // (end of stage2 to end of the gather), compute (= stage1 + halo_p1 + stage2; a rank without halos
+  // runs its tile as free-running stream lanes and reports its span as stage2). Syncs first.
   std::vector<std::pair<std::string, double>> phase_ms();
   void reset_phases();
 
@@ -106,6 +122,8 @@ class V5Runtime {
   bool pipelined() const { return pipeline_; }
   long steps() const;
   std::string describe_json() const;
+  // transfers this rank's transport issued since construction (V5Options::keep_log)
+  std::vector<std::string> transfer_log() const;
 
  private:
   struct Impl_;

@@ -4,11 +4,13 @@
 
 #include <cstring>
 #include <exception>
+#include <stdexcept>
 #include <string>
 #include <vector>
 #include <algorithm>
 
 #include "anx/bf16_ops.hpp"
+#include "anx/cost.hpp"
 #include "anx/cpu_engine.hpp"
 #include "anx/engine.hpp"
 #include "anx/ops.hpp"
@@ -536,3 +538,47 @@ int anx_rng_uniform(uint64_t seed, uint64_t stream, float* out, size_t n) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------- cost model
+namespace {
+int put_json(const std::string& j, char* buf, size_t cap) {
+  if (!buf || cap == 0) return fail("anx_cost: no output buffer");
+  if (j.size() + 1 > cap) return fail("anx_cost: output buffer too small (" + std::to_string(j.size() + 1) + " bytes)");
+  std::memcpy(buf, j.c_str(), j.size() + 1);
+  return 0;
+}
+anx::Workload wl_of(int w) {
+  if (w < 0 || w > 2) throw std::invalid_argument("workload must be 0 (dp), 1 (v4) or 2 (v5)");
+  return static_cast<anx::Workload>(w);
+}
+}  // namespace
+
+extern "C" int anx_cost_curve(int workload, const int* nps, int n_nps, int batch, int row_ways, int input_source,
+                              int mode, const char* overrides, char* buf, size_t cap) {
+  return guarded("anx_cost_curve", [&] {
+    std::vector<int> v(nps, nps + std::max(0, n_nps));
+    return put_json(anx::model_curve_json(wl_of(workload), v, batch, row_ways,
+                                          static_cast<anx::InputSource>(input_source != 0), static_cast<anx::Decomp>(mode),
+                                          anx::cost_params(overrides ? overrides : "")),
+                    buf, cap);
+  });
+}
+
+extern "C" int anx_cost_step(int workload, int np, int batch, int row_ways, int input_source, int mode,
+                             const char* overrides, char* buf, size_t cap) {
+  return guarded("anx_cost_step", [&] {
+    return put_json(anx::model_step(wl_of(workload), np, batch, row_ways, static_cast<anx::InputSource>(input_source != 0),
+                                    static_cast<anx::Decomp>(mode), anx::cost_params(overrides ? overrides : ""))
+                        .json(),
+                    buf, cap);
+  });
+}
+
+extern "C" int anx_cost_pick_row_ways(int workload, int np, int batch, int input_source, int mode, const char* overrides,
+                                      int* row_ways) {
+  return guarded("anx_cost_pick_row_ways", [&] {
+    *row_ways = anx::pick_row_ways(wl_of(workload), np, batch, static_cast<anx::InputSource>(input_source != 0),
+                                   static_cast<anx::Decomp>(mode), anx::cost_params(overrides ? overrides : ""));
+    return 0;
+  });
+}

@@ -52,13 +52,14 @@ int put(const std::string& s, char* buf, size_t cap) {
   return 0;
 }
 
-anx::V5Options options(int batch, int row_ways, int mode, const char* transport, int chunks) {
+anx::V5Options options(int batch, int row_ways, int mode, const char* transport, int chunks, int input_source) {
   anx::V5Options o;
   o.batch = batch;
   o.row_ways = row_ways;
   o.mode = mode ? anx::Decomp::PerLayer : anx::Decomp::Overlap;
   o.transport = transport ? transport : "auto";
   o.chunks = chunks;
+  o.input_source = input_source ? anx::InputSource::Root : anx::InputSource::Local;
   return o;
 }
 
@@ -121,11 +122,14 @@ int anx_v5_create(void** out, int rank, int world, int local_rank, int local_wor
                   const char* master_addr, int master_port, double timeout_s, const anx_block_c* b1,
                   const anx_block_c* b2, int H, int W, const float* w1, const float* bias1, const float* w2,
                   const float* bias2, int batch, int row_ways, int mode, const char* transport, int chunks,
-                  int pipeline, int poison, int impl, const char* peer_sync) {
+                  int pipeline, int poison, int impl, const char* peer_sync, int input_source, int lanes,
+                  int keep_log) {
   return guarded("anx_v5_create", [&] {
     if (!out || !b1 || !b2) throw std::invalid_argument("null argument");
     const anx::RankInfo ri = rank_info(rank, world, local_rank, local_world, nnodes, master_addr, master_port);
-    anx::V5Options o = options(batch, row_ways, mode, transport, chunks);
+    anx::V5Options o = options(batch, row_ways, mode, transport, chunks, input_source);
+    o.lanes = lanes > 0 ? lanes : o.lanes;
+    o.keep_log = keep_log != 0;
     o.pipeline = pipeline;
     o.poison = poison != 0;
     o.impl = impl ? anx::Impl::Direct : anx::Impl::Mfma;
@@ -189,17 +193,25 @@ int anx_v5_describe(void* h, char* buf, size_t cap) {
   return guarded("anx_v5_describe", [&] { return put(H(h)->rt->describe_json(), buf, cap); });
 }
 
+int anx_v5_log(void* h, char* buf, size_t cap) {
+  return guarded("anx_v5_log", [&] {
+    std::string s;
+    for (const std::string& l : H(h)->rt->transfer_log()) s += l + "\n";
+    return put(s, buf, cap);
+  });
+}
+
 int anx_v5_schedule(int np, const anx_block_c* b1, const anx_block_c* b2, int H, int W, int batch, int row_ways,
-                    int mode, int chunks, int rank, const char* transport, char* buf, size_t cap) {
+                    int mode, int chunks, int rank, const char* transport, int input_source, char* buf, size_t cap) {
   return guarded("anx_v5_schedule", [&] {
     if (!b1 || !b2) throw std::invalid_argument("null block spec");
-    const anx::V5Options o = options(batch, row_ways, mode, transport, chunks);
+    const anx::V5Options o = options(batch, row_ways, mode, transport, chunks, input_source);
     std::string s;
     if (rank < 0) {
       for (const anx::Transfer& x : anx::make_v5_layout(np, spec(*b1), spec(*b2), H, W, o).step_transfers())
         s += x.str() + "\n";
     } else {
-      const std::string tr = transport && std::string(transport) == "peer" ? "peer" : "rccl";
+      const std::string tr = transport ? transport : "rccl";
       for (const std::string& l : anx::v5_dry_schedule(rank, np, spec(*b1), spec(*b2), H, W, o, tr)) s += l + "\n";
     }
     return put(s, buf, cap);

@@ -130,18 +130,35 @@ struct DeviceBase : Transport {
 // 2-D copy each (allocated once per transfer and chunk). Two communicators: scatter / gather / weight
 // broadcast on one, the pool1 halos on the other, so a halo chunk never queues behind the previous
 // step's gather on one communicator stream.
+// `loopback`: the same transport over the loopback DeviceComm (ranks sharing one GPU; anx/comm.hpp), so
+// this code runs multi-rank on a one-GPU box exactly as it runs over RCCL. Ordering of the two
+// communicators ("chain", the default): each phase's comm stream first waits for the other
+// communicator's last queued op, so all device traffic of a rank is one total order, identical on
+// every rank (phases are issued in the same order everywhere); no communicator can wait on a peer
+// that is itself waiting behind the other one. "free" (ANX_V5_COMM_ORDER=free) lets them overlap.
 struct RcclTransport : DeviceBase {
   HostComm* hc_;
   int device_;
+  bool loopback_ = false, chain_ = true;
   std::unique_ptr<DeviceComm> dc_[2];
+  DeviceComm* last_ = nullptr;  // communicator of the previous phase
   std::map<std::tuple<int, int, int>, void*> stage_;  // (phase, chunk, transfer) -> contiguous staging
-  RcclTransport(HostComm* c, int device, int rank) : hc_(c), device_(device) { rank_ = rank; }
+  RcclTransport(HostComm* c, int device, int rank, bool loopback) : hc_(c), device_(device), loopback_(loopback) {
+    rank_ = rank;
+    const char* e = std::getenv("ANX_V5_COMM_ORDER");
+    if (e && std::string(e) != "chain" && std::string(e) != "free")
+      throw std::runtime_error("ANX_V5_COMM_ORDER must be chain or free");
+    chain_ = !(e && std::string(e) == "free");
+  }
   ~RcclTransport() override { close(); }
-  const char* name() const override { return "rccl"; }
-  const char* ordering() const override { return "events"; }
+  const char* name() const override { return loopback_ ? "rccl-loopback" : "rccl"; }
+  const char* ordering() const override { return chain_ ? "events, chained communicators" : "events"; }
   bool live() const { return !record_only && hc_ && hc_->size() > 1; }
+  std::unique_ptr<DeviceComm> make_comm() {
+    return loopback_ ? make_loopback_comm(*hc_, device_) : make_rccl_comm(*hc_, device_);
+  }
   void connect() {
-    if (live() && !dc_[0]) dc_[0] = std::make_unique<DeviceComm>(*hc_, device_);
+    if (live() && !dc_[0]) dc_[0] = make_comm();
   }
   void bcast(void* buf, size_t bytes, int root) override {
     if (!live()) return;
@@ -153,7 +170,7 @@ struct RcclTransport : DeviceBase {
     bind_bufs(bufs);
     if (!live()) return;
     connect();
-    if (!s.phase[static_cast<int>(Phase::P1Halo)].empty()) dc_[1] = std::make_unique<DeviceComm>(*hc_, device_);
+    if (!s.phase[static_cast<int>(Phase::P1Halo)].empty()) dc_[1] = make_comm();
   }
   void* staging(Phase ph, const Transfer& x, size_t i) {
     void*& p = stage_[{static_cast<int>(ph), x.chunk, x.seq >= 0 ? x.seq : static_cast<int>(i)}];
@@ -167,7 +184,11 @@ struct RcclTransport : DeviceBase {
     if (!any) return;
     DeviceComm* dc = record_only ? nullptr : dc_[ph == Phase::P1Halo && dc_[1] ? 1 : 0].get();
     hipStream_t cs = dc ? dc->stream() : nullptr;
-    if (dc) dc->after(compute);
+    if (dc) {
+      dc->after(compute);
+      if (chain_ && last_) dc->after_comm(*last_);
+      last_ = dc;
+    }
     std::vector<std::pair<const Transfer*, void*>> unpack;
     for (size_t i = 0; i < xs.size(); ++i) {  // pack
       const Transfer& x = xs[i];
@@ -198,6 +219,7 @@ struct RcclTransport : DeviceBase {
   void close() override {
     for (auto& kv : stage_) (void)hipFree(kv.second);
     stage_.clear();
+    last_ = nullptr;
     dc_[1].reset();
     dc_[0].reset();
   }
@@ -427,8 +449,8 @@ struct PeerTransport : DeviceBase {
 
 }  // namespace
 
-std::unique_ptr<Transport> make_rccl_transport(HostComm* c, int device, int rank) {
-  return std::make_unique<RcclTransport>(c, device, rank);
+std::unique_ptr<Transport> make_rccl_transport(HostComm* c, int device, int rank, bool loopback) {
+  return std::make_unique<RcclTransport>(c, device, rank, loopback);
 }
 std::unique_ptr<Transport> make_peer_transport(HostComm* c, int device, int rank, const std::string& sync) {
   return std::make_unique<PeerTransport>(c, device, rank, sync);

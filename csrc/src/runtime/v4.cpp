@@ -13,7 +13,8 @@
 #include <string>
 
 #include "anx/trace.hpp"
-#include "anx/v5.hpp"  // plan_stats, balanced_row_ways
+#include "anx/cost.hpp"
+#include "anx/v5.hpp"  // plan_stats
 
 namespace anx {
 
@@ -54,7 +55,28 @@ struct V4Runtime::Impl_ {
   double sums[3] = {0, 0, 0};
   long timed = 0;
 
+  bool created = false;  // rank 0 created the segment name and has not unlinked it yet
+
   Impl_(HostComm& cc, const RankInfo& r, const V4Options& oo) : c(cc), ri(r), o(oo) {}
+  // Frees whatever the constructor got to (it may have thrown half way): engine, device buffers,
+  // events, streams, the pinned registration, the mapping and (rank 0, before the others opened it)
+  // the segment name.
+  ~Impl_() {
+    eng.reset();
+    for (int p = 0; p < 2; ++p) {
+      if (d_in[p]) (void)hipFree(d_in[p]);
+      if (d_y[p]) (void)hipFree(d_y[p]);
+      for (auto* v : {&e_in[p], &e_cmp[p], &e_out[p]})
+        for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+    }
+    for (auto& e : ring)
+      for (hipEvent_t v : e) (void)hipEventDestroy(v);
+    for (hipStream_t s : {sh, st, sd})
+      if (s) (void)hipStreamDestroy(s);
+    if (registered) (void)hipHostUnregister(seg);
+    if (seg) munmap(seg, seg_bytes);
+    if (created) shm_unlink(shm_name.c_str());
+  }
   hipEvent_t event(bool timing = false) {
     hipEvent_t e = nullptr;
     hip_ok(hipEventCreateWithFlags(&e, timing ? hipEventDefault : hipEventDisableTiming), "hipEventCreate");
@@ -87,7 +109,11 @@ V4Runtime::V4Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const
   I.np = c.size();
   I.d = blocks_dims(H, W, b1, b2);
   if (ri.nnodes > 1) throw std::runtime_error("v4 shared host staging is single-node (one host segment)");
-  const int rw = o.row_ways < 0 ? balanced_row_ways(I.np, o.batch, H, W) : o.row_ways;
+  // default split: the cost model's (anx/cost.hpp): V4 is H2D-bound, so the batch split wins whenever
+  // every rank gets whole images (a row split adds the rows' receptive-field overlap to each H2D)
+  const int rw = o.row_ways < 0 ? pick_row_ways(Workload::V4, I.np, o.batch, InputSource::Root, Decomp::Overlap,
+                                                cost_params(o.cost), b1, b2, H, W)
+                                : o.row_ways;
   if (!make_hybrid_plan(H, W, I.np, o.batch, rw, Decomp::Overlap, I.plan, b1, b2))
     throw std::runtime_error("v4: invalid plan");
   I.t = I.plan.tile(I.rank);
@@ -127,21 +153,29 @@ V4Runtime::V4Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const
   std::snprintf(nb, sizeof nb, "%s", I.shm_name.c_str());
   c.bcast(nb, sizeof nb, 0);
   I.shm_name = nb;
-  int fd = -1;
+  struct Fd {  // closes the descriptor on every path out of here
+    int v = -1;
+    ~Fd() {
+      if (v >= 0) close(v);
+    }
+  } fd;
   if (I.rank == 0) {
-    fd = shm_open(I.shm_name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
-    if (fd < 0 || ftruncate(fd, static_cast<off_t>(I.seg_bytes)) != 0)
+    fd.v = shm_open(I.shm_name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd.v >= 0) I.created = true;
+    if (fd.v < 0 || ftruncate(fd.v, static_cast<off_t>(I.seg_bytes)) != 0)
       throw std::runtime_error("v4: cannot create shared segment " + I.shm_name + ": " + std::strerror(errno));
   }
   c.barrier();
-  if (I.rank != 0) fd = shm_open(I.shm_name.c_str(), O_RDWR, 0600);
-  if (fd < 0) throw std::runtime_error("v4: cannot open shared segment " + I.shm_name + ": " + std::strerror(errno));
-  void* m = mmap(nullptr, I.seg_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  close(fd);
+  if (I.rank != 0) fd.v = shm_open(I.shm_name.c_str(), O_RDWR, 0600);
+  if (fd.v < 0) throw std::runtime_error("v4: cannot open shared segment " + I.shm_name + ": " + std::strerror(errno));
+  void* m = mmap(nullptr, I.seg_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd.v, 0);
   if (m == MAP_FAILED) throw std::runtime_error(std::string("v4: mmap: ") + std::strerror(errno));
   I.seg = static_cast<char*>(m);
   c.barrier();
-  if (I.rank == 0) shm_unlink(I.shm_name.c_str());
+  if (I.rank == 0) {
+    shm_unlink(I.shm_name.c_str());
+    I.created = false;
+  }
   hip_ok(hipHostRegister(I.seg, I.seg_bytes, hipHostRegisterDefault), "hipHostRegister");
   I.registered = true;
 
@@ -169,25 +203,12 @@ V4Runtime::V4Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const
 
 V4Runtime::~V4Runtime() {
   if (!p_) return;
-  Impl_& I = *p_;
   (void)hipDeviceSynchronize();
   try {
-    I.c.barrier();
+    p_->c.barrier();  // every rank's copies out of / into the segment are done
   } catch (...) {
   }
-  I.eng.reset();
-  for (int p = 0; p < 2; ++p) {
-    if (I.d_in[p]) (void)hipFree(I.d_in[p]);
-    if (I.d_y[p]) (void)hipFree(I.d_y[p]);
-    for (auto* v : {&I.e_in[p], &I.e_cmp[p], &I.e_out[p]})
-      for (hipEvent_t e : *v) (void)hipEventDestroy(e);
-  }
-  for (auto& e : I.ring)
-    for (hipEvent_t v : e) (void)hipEventDestroy(v);
-  for (hipStream_t s : {I.sh, I.st, I.sd})
-    if (s) (void)hipStreamDestroy(s);
-  if (I.registered) (void)hipHostUnregister(I.seg);
-  if (I.seg) munmap(I.seg, I.seg_bytes);
+  p_.reset();  // Impl_'s destructor frees everything
 }
 
 float* V4Runtime::host_input() const { return reinterpret_cast<float*>(p_->seg); }

@@ -19,6 +19,8 @@ void hip_ok(hipError_t e, const char* what) {
 constexpr int kB = static_cast<int>(BufId::kCount);
 constexpr int kMaxChunks = 16;  // the peer transport's halo channels
 constexpr int kRing = 32;       // per-step timing event sets kept before they are folded in
+constexpr int kMaxLanes = 4;
+constexpr int kLaneMin = 16;    // images per lane below which a rank keeps one lane (Winograd needs > 8)
 const char* kPhase[5] = {"scatter", "stage1", "halo_p1", "stage2", "gather"};
 }  // namespace
 
@@ -43,27 +45,13 @@ PlanStats plan_stats(const HybridPlan& p) {
   return s;
 }
 
-int balanced_row_ways(int np, int batch, int H, int W) {
-  if (np <= 1) return 1;
-  int best = np;
-  double best_imb = 1e30;
-  for (int r = 2; r <= np; ++r) {
-    if (np % r) continue;
-    HybridPlan hp;
-    if (!make_hybrid_plan(H, W, np, batch, r, Decomp::PerLayer, hp)) continue;
-    const double imb = plan_stats(hp).imbalance;
-    if (imb <= 1.1) return r;
-    if (imb < best_imb - 1e-9) best_imb = imb, best = r;
-  }
-  return best;
-}
-
 std::string pick_v5_transport(const std::string& want, const RankInfo& ri, int ndev, bool dry) {
   const bool shared = !dry && ri.local_world > ndev;  // ranks of this node outnumber its GPUs
   const std::string tr = want == "auto" ? (shared && ri.nnodes == 1 ? "peer" : "rccl") : want;
-  if (tr != "rccl" && tr != "peer") throw std::runtime_error("--transport must be auto, rccl or peer");
-  if (tr == "peer" && ri.nnodes > 1)
-    throw std::runtime_error("the peer transport (IPC) is single-node: use --transport rccl across nodes");
+  if (tr != "rccl" && tr != "peer" && tr != "loopback")
+    throw std::runtime_error("--transport must be auto, rccl, peer or loopback");
+  if ((tr == "peer" || tr == "loopback") && ri.nnodes > 1)
+    throw std::runtime_error("the " + tr + " transport (IPC) is single-node: use --transport rccl across nodes");
   if (tr == "rccl" && shared)
     throw std::runtime_error("v5 over RCCL needs one GPU per rank on each node (" + std::to_string(ri.local_world) +
                              " ranks, " + std::to_string(ndev) + " GPUs here; --transport peer shares a GPU)");
@@ -72,7 +60,10 @@ std::string pick_v5_transport(const std::string& want, const RankInfo& ri, int n
 
 V5Layout make_v5_layout(int np, const BlockSpec& b1, const BlockSpec& b2, int H, int W, const V5Options& o) {
   V5Layout L;
-  L.row_ways = o.row_ways < 0 ? balanced_row_ways(np, o.batch, H, W) : o.row_ways;
+  L.local_input = o.input_source == InputSource::Local;
+  L.row_ways = o.row_ways < 0
+                   ? pick_row_ways(Workload::V5, np, o.batch, o.input_source, o.mode, cost_params(o.cost), b1, b2, H, W)
+                   : o.row_ways;
   if (!make_hybrid_plan(H, W, np, o.batch, L.row_ways, o.mode, L.plan, b1, b2))
     throw std::runtime_error("v5: invalid plan (row_ways " + std::to_string(L.row_ways) + " over " +
                              std::to_string(np) + " ranks)");
@@ -92,22 +83,45 @@ V5Layout make_v5_layout(int np, const BlockSpec& b1, const BlockSpec& b2, int H,
 }
 
 std::vector<Transfer> V5Layout::step_transfers() const {
-  std::vector<Transfer> v = sched.phase[static_cast<int>(Phase::Scatter)];
+  std::vector<Transfer> v;
+  if (!local_input) v = sched.phase[static_cast<int>(Phase::Scatter)];
   for (const auto& c : halo_chunks) v.insert(v.end(), c.begin(), c.end());
   const auto& g = sched.phase[static_cast<int>(Phase::Gather)];
   v.insert(v.end(), g.begin(), g.end());
   return v;
 }
 
+std::vector<RankBytes> V5Layout::rank_bytes() const {
+  std::vector<RankBytes> b(plan.np);
+  for (const Transfer& x : step_transfers()) {
+    if (x.src == x.dst) continue;
+    const double n = static_cast<double>(x.bytes());
+    switch (x.phase) {
+      case Phase::Scatter: b[x.src].scatter_sent += n, b[x.dst].scatter_recv += n; break;
+      case Phase::P1Halo: b[x.src].halo_sent += n, b[x.dst].halo_recv += n; break;
+      case Phase::Gather: b[x.src].gather_sent += n, b[x.dst].gather_recv += n; break;
+    }
+  }
+  return b;
+}
+
+double V5Layout::input_placement_bytes() const {
+  double n = 0;
+  if (local_input)
+    for (const Transfer& x : sched.phase[static_cast<int>(Phase::Scatter)])
+      if (x.src != x.dst) n += static_cast<double>(x.bytes());
+  return n;
+}
+
 std::vector<std::string> v5_dry_schedule(int rank, int np, const BlockSpec& b1, const BlockSpec& b2, int H, int W,
                                          const V5Options& o, const std::string& transport) {
   const V5Layout L = make_v5_layout(np, b1, b2, H, W, o);
-  std::unique_ptr<Transport> x =
-      transport == "rccl" ? make_rccl_transport(nullptr, 0, rank) : make_peer_transport(nullptr, 0, rank, o.peer_sync);
+  std::unique_ptr<Transport> x = transport == "peer" ? make_peer_transport(nullptr, 0, rank, o.peer_sync)
+                                                     : make_rccl_transport(nullptr, 0, rank, transport == "loopback");
   x->record_only = true;
   void* none[2][kB] = {};
   x->bind(L.sched, none, nullptr);
-  x->run_phase(Phase::Scatter, L.sched.phase[0], nullptr, 0);
+  if (!L.local_input) x->run_phase(Phase::Scatter, L.sched.phase[0], nullptr, 0);
   for (const auto& c : L.halo_chunks) x->run_phase(Phase::P1Halo, c, nullptr, 0);
   x->run_phase(Phase::Gather, L.sched.phase[2], nullptr, 0);
   return x->log();
@@ -126,6 +140,15 @@ struct V5Runtime::Impl_ {
   std::unique_ptr<BlocksEngine> eng;
   TilePlan t;
   int n = 0;  // images this rank computes
+  // lane path: a tile that needs no halo (a row group of one rank, or overlap tiles) runs as nl
+  // free-running stream lanes, lane i images [lb[i], lb[i+1]) on engine leng[i] / stream ls[i]
+  // (lane 0 = eng on st); only the gather joins them
+  bool lane_path = false, local = true;
+  int nl = 1;  // lanes
+  std::vector<int> lb;
+  std::vector<std::unique_ptr<BlocksEngine>> leng;
+  std::vector<hipStream_t> ls;
+  hipEvent_t e_lane[kMaxLanes][2] = {}, e_go[2] = {}, e_gdone[2] = {};
   std::vector<int> lo;  // this rank's chunk bounds (C + 1)
   size_t x_bytes = 0, yfull_bytes = 0, tile_bytes = 0, y_bytes = 0;
   float* d_x = nullptr;
@@ -195,6 +218,37 @@ struct V5Runtime::Impl_ {
     }
     if (o.poison && n && !alias_y) hip_ok(hipMemsetAsync(d_y[par], 0xff, y_bytes, on), "poison y");
   }
+  BlocksEngine& lane_engine(int i) { return i == 0 ? *eng : *leng[i - 1]; }
+  // Lane path: every lane waits for its step's input (`in_ev`: the scatter / the previous gather of
+  // this parity, both on io; or e_go on st when not pipelined) on its own stream and runs the fused
+  // tile forward of its slice; e_lane[i][par] marks it done (the gather waits for all of them).
+  void compute_lanes(long kk, std::vector<hipEvent_t>& e, hipEvent_t in_ev) {
+    const int par = static_cast<int>(kk & 1);
+    rec(e[2], st);
+    for (int cc = 0; cc < C; ++cc) rec(e[3 + 2 * cc], st), rec(e[4 + 2 * cc], st);  // no halo on this path
+    const size_t in_img = n ? tile_bytes / n : 0, out_img = n ? y_bytes / n : 0;
+    for (int i = 0; i < nl; ++i) {
+      hipStream_t s = ls[i];
+      const int a = lb[i], b = lb[i + 1];
+      if (i > 0 && in_ev) wait(s, in_ev);
+      if (b > a) {
+        RoctxRange r("v5 lane tile");
+        hip_ok(lane_engine(i).tile_forward(reinterpret_cast<float*>(reinterpret_cast<char*>(d_tile[par]) + a * in_img),
+                                           b - a, t,
+                                           reinterpret_cast<float*>(reinterpret_cast<char*>(d_y[par]) + a * out_img), s),
+               "tile_forward");
+        if (o.poison && !local && !alias_tile)
+          hip_ok(hipMemsetAsync(reinterpret_cast<char*>(d_tile[par]) + a * in_img, 0xff, (b - a) * in_img, s),
+                 "poison tile");
+      }
+      rec(e_lane[i][par], s);
+    }
+  }
+  // make `s` wait for every lane of step parity `par`
+  void join_lanes(hipStream_t s, int par) {
+    for (int i = 0; i < nl; ++i) wait(s, e_lane[i][par]);
+  }
+
   // stage1 chunks, halo chunks on hs, stage2 chunks; e: this step's timing events
   void compute(long kk, std::vector<hipEvent_t>& e) {
     const int par = static_cast<int>(kk & 1);
@@ -205,7 +259,7 @@ struct V5Runtime::Impl_ {
       if (n && lo[cc + 1] > lo[cc]) {
         RoctxRange r("v5 stage1");
         hip_ok(eng->stage1(d_tile[par], n, t, st, lo[cc], lo[cc + 1]), "stage1");
-        if (o.poison && !alias_tile) {
+        if (o.poison && !alias_tile && !local) {
           const size_t img = tile_bytes / n;
           hip_ok(hipMemsetAsync(reinterpret_cast<char*>(d_tile[par]) + lo[cc] * img, 0xff, (lo[cc + 1] - lo[cc]) * img,
                                 st),
@@ -228,7 +282,7 @@ struct V5Runtime::Impl_ {
       rec(e[4 + 2 * cc], st);
       if (!n || lo[cc + 1] <= lo[cc]) continue;
       RoctxRange r("v5 stage2");
-      if (per_layer) {
+      {
         hip_ok(eng->stage2(n, t, d_y[par], st, lo[cc], lo[cc + 1]), "stage2");
         if (o.poison)  // the halo rows this rank received: the next step must bring them again
           for (const Transfer& h : L.halo_chunks[cc])
@@ -236,9 +290,6 @@ struct V5Runtime::Impl_ {
               hip_ok(hipMemset2DAsync(reinterpret_cast<char*>(eng->q2_row_ptr(t, 0, t.q.lo)) + h.to.off, h.to.pitch,
                                       0xff, h.width, h.height, st),
                      "poison window");
-      } else {
-        hip_ok(eng->tile_forward(d_tile[par], n, t, d_y[par], st), "tile_forward");
-        if (o.poison && !alias_tile) hip_ok(hipMemsetAsync(d_tile[par], 0xff, tile_bytes, st), "poison tile");
       }
     }
     rec(e[3 + 2 * C], st);
@@ -260,8 +311,11 @@ V5Runtime::V5Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const
   I.tr = pick_v5_transport(o.transport, ri, ndev, false);
   I.dev = ri.local_rank % ndev;
   hip_ok(hipSetDevice(I.dev), "hipSetDevice");
-  I.x = I.tr == "rccl" ? make_rccl_transport(&c, I.dev, I.rank) : make_peer_transport(&c, I.dev, I.rank, o.peer_sync);
-  pipeline_ = I.pipeline = o.pipeline < 0 ? I.tr == "rccl" : o.pipeline > 0;
+  I.x = I.tr == "peer" ? make_peer_transport(&c, I.dev, I.rank, o.peer_sync)
+                       : make_rccl_transport(&c, I.dev, I.rank, I.tr == "loopback");
+  I.x->keep_log = o.keep_log;
+  pipeline_ = I.pipeline = o.pipeline < 0 ? I.tr != "peer" : o.pipeline > 0;
+  I.local = lay_.local_input;
 
   // weights: the root's host copy -> its device -> every rank's device (transport broadcast) -> host
   // (the engine packs / Winograd-transforms them once on the host)
@@ -299,10 +353,22 @@ V5Runtime::V5Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const
   const RowRange im = hp.images[hp.group_of[I.rank]];
   I.n = I.t.out.empty() ? 0 : im.size();
   for (int cc = 0; cc <= I.C; ++cc) I.lo.push_back(I.n * cc / I.C);
-  I.eng = std::make_unique<BlocksEngine>(b1, b2, H, W, hw, std::max(1, I.n), o.impl, o.knobs);
+  // no halo touches this rank: its tile runs as free-running stream lanes of the fused forward
+  I.lane_path = o.mode == Decomp::Overlap || hp.group_size[hp.group_of[I.rank]] == 1;
+  I.nl = I.lane_path ? std::max(1, std::min({o.lanes, kMaxLanes, I.n / kLaneMin})) : 1;
+  for (int i = 0; i <= I.nl; ++i) I.lb.push_back(I.n * i / I.nl);
+  I.eng = std::make_unique<BlocksEngine>(b1, b2, H, W, hw, std::max(1, I.lb[1] - I.lb[0]), o.impl, o.knobs);
+  for (int i = 1; i < I.nl; ++i)
+    I.leng.push_back(std::make_unique<BlocksEngine>(b1, b2, H, W, hw, std::max(1, I.lb[i + 1] - I.lb[i]), o.impl, o.knobs));
   hip_ok(hipStreamCreateWithFlags(&I.st, hipStreamNonBlocking), "hipStreamCreate");
   hip_ok(hipStreamCreateWithFlags(&I.io, hipStreamNonBlocking), "hipStreamCreate");
   hip_ok(hipStreamCreateWithFlags(&I.hs, hipStreamNonBlocking), "hipStreamCreate");
+  I.ls.push_back(I.st);
+  for (int i = 1; i < I.nl; ++i) {
+    hipStream_t s = nullptr;
+    hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    I.ls.push_back(s);
+  }
 
   const BlocksDims& d = I.d;
   const size_t in_img = static_cast<size_t>(H) * W * d.C0 * 4, out_img = static_cast<size_t>(d.Hp2) * d.Wp2 * d.C2 * 4;
@@ -326,7 +392,7 @@ V5Runtime::V5Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const
   }
   // the conv2 window exists once stage1 has seen this tile geometry: run it once on zeros
   float* d_win = nullptr;
-  if (I.n && o.mode == Decomp::PerLayer) {
+  if (I.n && !I.lane_path) {
     if (!I.alias_tile) hip_ok(hipMemsetAsync(I.d_tile[0], 0, I.tile_bytes, I.st), "hipMemset");
     hip_ok(I.eng->stage1(I.d_tile[0], I.n, I.t, I.st), "stage1");
     d_win = I.eng->q2_row_ptr(I.t, 0, I.t.q.lo);
@@ -341,7 +407,10 @@ V5Runtime::V5Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const
     bufs[p][static_cast<int>(BufId::YFull)] = I.d_yfull[p];
   }
   I.x->bind(lay_.sched, bufs, I.st);
-  for (int p = 0; p < 2; ++p) I.e_sc[p] = I.event(), I.e_s2[p] = I.event();
+  for (int p = 0; p < 2; ++p) {
+    I.e_sc[p] = I.event(), I.e_s2[p] = I.event(), I.e_go[p] = I.event(), I.e_gdone[p] = I.event();
+    for (int i = 0; i < I.nl; ++i) I.e_lane[i][p] = I.event();
+  }
   I.e_hdone = I.event();
   for (int cc = 0; cc < I.C; ++cc) I.e_s1.push_back(I.event()), I.e_h.push_back(I.event());
   I.ring.resize(kRing);
@@ -362,7 +431,15 @@ V5Runtime::~V5Runtime() {
   }
   I.x.reset();
   I.eng.reset();
+  I.leng.clear();
   for (float* p : I.owned) (void)hipFree(p);
+  for (int p = 0; p < 2; ++p) {
+    for (hipEvent_t v : {I.e_go[p], I.e_gdone[p]})
+      if (v) (void)hipEventDestroy(v);
+    for (int i = 0; i < kMaxLanes; ++i)
+      if (I.e_lane[i][p]) (void)hipEventDestroy(I.e_lane[i][p]);
+  }
+  for (size_t i = 1; i < I.ls.size(); ++i) (void)hipStreamDestroy(I.ls[i]);
   for (auto& e : I.ring)
     for (hipEvent_t v : e) (void)hipEventDestroy(v);
   for (hipEvent_t v : I.e_s1) (void)hipEventDestroy(v);
@@ -384,6 +461,16 @@ void V5Runtime::set_input(const float* host_x) {
     hip_ok(hipMemcpy(I.d_x, host_x, I.x_bytes, hipMemcpyHostToDevice), "H2D input");
   }
   I.prefetched = false;  // every rank drops its prefetched scatter: the next step scatters again
+  if (I.local) {
+    // device-resident input: every rank's images x input rows land on its device now, in both step
+    // parities' tile buffers; steps then move only halos and the gather
+    I.c.barrier();  // the root's X is complete before anyone pulls from it
+    for (int par = 0; par < 2; ++par) {
+      RoctxRange r("v5 input placement");
+      I.x->run_phase(Phase::Scatter, lay_.sched.phase[0], I.st, par);
+    }
+    hip_ok(hipStreamSynchronize(I.st), "hipStreamSynchronize");
+  }
   I.c.barrier();
 }
 
@@ -395,31 +482,53 @@ void V5Runtime::step() {
   I.fold(slot);
   std::vector<hipEvent_t>& e = I.ring[slot];
   I.ring_pos = (I.ring_pos + 1) % kRing;
-  if (!I.pipeline) {  // every phase on the compute stream
+  if (!I.pipeline) {  // every phase in step order on the compute stream (side lanes fork from it)
     I.rec(e[0], I.st);
-    I.scatter(k, I.st);
+    if (!I.local) I.scatter(k, I.st);
     I.rec(e[1], I.st);
-    I.compute(k, e);
+    if (I.lane_path) {
+      I.rec(I.e_go[par], I.st);
+      I.compute_lanes(k, e, I.e_go[par]);
+      I.join_lanes(I.st, par);
+      I.rec(e[3 + 2 * I.C], I.st);
+    } else {
+      I.compute(k, e);
+    }
     I.gather(k, I.st);
     I.rec(e.back(), I.st);
   } else {
-    // io runs scatter(k+1) while st computes step k, then gather(k) once stage2(k) is done; st starts
-    // step k+1 as soon as scatter(k+1) has landed. Every rank issues the phases in the same order
-    // (scatter k+1, gather k), as RCCL's in-order matching and the peer flag counters require.
-    if (!I.prefetched) {
+    // io runs scatter(k+1) while the compute stream(s) run step k, then gather(k) once step k's
+    // outputs are complete; compute starts step k+1 as soon as its input is there (scatter(k+1), or
+    // with local input the gather that last read this parity's outputs). Every rank issues the phases
+    // in the same order (scatter k+1, gather k), as RCCL's in-order matching and the peer flag
+    // counters require.
+    if (!I.local && !I.prefetched) {
       I.scatter(k, I.io);
       I.rec(I.e_sc[par], I.io);
     }
+    hipEvent_t in_ev = I.local ? I.e_gdone[par] : I.e_sc[par];
     I.rec(e[0], I.st);
-    I.wait(I.st, I.e_sc[par]);
+    I.wait(I.st, in_ev);
     I.rec(e[1], I.st);
-    I.compute(k, e);
-    I.rec(I.e_s2[par], I.st);
-    I.scatter(k + 1, I.io);
-    I.rec(I.e_sc[par ^ 1], I.io);
-    I.prefetched = true;
-    I.wait(I.io, I.e_s2[par]);
+    if (I.lane_path) {
+      I.compute_lanes(k, e, in_ev);
+    } else {
+      I.compute(k, e);
+      I.rec(I.e_s2[par], I.st);
+    }
+    if (!I.local) {
+      I.scatter(k + 1, I.io);
+      I.rec(I.e_sc[par ^ 1], I.io);
+      I.prefetched = true;
+    }
+    if (I.lane_path) {
+      I.join_lanes(I.io, par);
+      I.rec(e[3 + 2 * I.C], I.io);
+    } else {
+      I.wait(I.io, I.e_s2[par]);
+    }
     I.gather(k, I.io);
+    I.rec(I.e_gdone[par], I.io);
     I.rec(e.back(), I.io);
   }
   I.pending[slot] = true;
@@ -429,7 +538,10 @@ void V5Runtime::step() {
 void V5Runtime::sync() {
   Impl_& I = *p_;
   for (hipStream_t s : {I.st, I.io, I.hs}) hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize");
+  for (size_t i = 1; i < I.ls.size(); ++i) hip_ok(hipStreamSynchronize(I.ls[i]), "hipStreamSynchronize");
 }
+
+std::vector<std::string> V5Runtime::transfer_log() const { return p_->x->log(); }
 
 void V5Runtime::output(float* host_y) {
   Impl_& I = *p_;
@@ -445,6 +557,7 @@ std::vector<std::pair<std::string, double>> V5Runtime::phase_ms() {
   for (int i = 0; i < kRing; ++i) I.fold(i);
   std::vector<std::pair<std::string, double>> v;
   for (int i = 0; i < 5; ++i) v.push_back({kPhase[i], I.timed ? I.sums[i] / I.timed : 0.0});
+  v.push_back({"compute", v[1].second + v[2].second + v[3].second});
   return v;
 }
 
@@ -459,17 +572,34 @@ void V5Runtime::reset_phases() {
 std::string V5Runtime::describe_json() const {
   const Impl_& I = *p_;
   const PlanStats s = stats();
-  char b[768];
+  char b[1024];
   std::snprintf(b, sizeof b,
                 "{\"transport\": \"%s\", \"ordering\": \"%s\", \"pipeline\": %s, \"chunks\": %d, \"groups\": %d, "
                 "\"row_ways\": %d, \"out_rows_max\": %g, \"out_rows_mean\": %.4f, \"imbalance\": %.4f, "
                 "\"conv1_redundancy\": %.4f, \"images_per_rank_max\": %g, \"transfers_per_step\": %zu, "
-                "\"decomp\": \"%s\", \"device\": %d}",
-                I.x->name(), I.x->ordering(),
-                pipeline_ ? "true" : "false", lay_.chunks, s.groups, s.row_ways, s.rows_max, s.rows_mean, s.imbalance,
-                s.conv1_redundancy, s.images_max, lay_.step_transfers().size(),
-                I.o.mode == Decomp::PerLayer ? "per_layer" : "overlap", I.dev);
-  return b;
+                "\"decomp\": \"%s\", \"device\": %d, \"input_source\": \"%s\", \"lanes\": %d, "
+                "\"lane_path\": %s, \"input_placement_bytes\": %.0f, ",
+                I.x->name(), I.x->ordering(), pipeline_ ? "true" : "false", lay_.chunks, s.groups, s.row_ways, s.rows_max,
+                s.rows_mean, s.imbalance, s.conv1_redundancy, s.images_max, lay_.step_transfers().size(),
+                I.o.mode == Decomp::PerLayer ? "per_layer" : "overlap", I.dev, I.local ? "local" : "root", I.nl,
+                I.lane_path ? "true" : "false", lay_.input_placement_bytes());
+  // bytes per step by phase: per rank (arrays over ranks) and the root's / busiest rank's totals
+  const std::vector<RankBytes> rb = lay_.rank_bytes();
+  std::string j = b;
+  auto arr = [&](const char* name, double RankBytes::*f) {
+    std::string a = "\"" + std::string(name) + "\": [";
+    char t[32];
+    for (size_t r = 0; r < rb.size(); ++r) {
+      std::snprintf(t, sizeof t, "%s%.0f", r ? ", " : "", rb[r].*f);
+      a += t;
+    }
+    return a + "]";
+  };
+  j += "\"bytes_per_step\": {" + arr("scatter_recv", &RankBytes::scatter_recv) + ", " +
+       arr("scatter_sent", &RankBytes::scatter_sent) + ", " + arr("halo_sent", &RankBytes::halo_sent) + ", " +
+       arr("halo_recv", &RankBytes::halo_recv) + ", " + arr("gather_sent", &RankBytes::gather_sent) + ", " +
+       arr("gather_recv", &RankBytes::gather_recv) + "}}";
+  return j;
 }
 
 }  // namespace anx

@@ -53,8 +53,10 @@ struct Options {
   std::string impl = "mfma";
   std::string conv2_algo = "auto";  // auto | direct | winograd
   std::string conv1_algo = "auto";  // auto | direct | winograd
-  std::string transport = "auto";   // v5 device traffic: auto | rccl | peer (IPC + hipMemcpy2DAsync)
-  std::string split = "auto";       // v5 decomposition: auto (balanced) | rows (reference) | hybrid | batch
+  std::string transport = "auto";   // v5 device traffic: auto | rccl | peer (IPC + hipMemcpy2DAsync) | loopback
+  std::string split = "auto";       // v5 decomposition: auto (cost model) | rows (reference) | hybrid | batch
+  std::string input_source = "local";  // v5: local (device-resident, placed once) | root (scattered every step)
+  int lanes = 0;                    // v5: stream lanes of a halo-free rank (0 = the runtime's default)
   int chunks = 0;                   // v5: halo pipeline chunks per step (0 = auto)
   std::string peer_sync;            // v5 peer transport ordering: flags | notes ("" = default)
   bool dry_run = false;             // v5: print the transfer schedule (record-only transports, no GPU)
@@ -70,8 +72,9 @@ struct Options {
                "%s\nusage: anx --version v1|v2.1|v2.2|v3|v4|v5 [--batch N] [--init const|rand] [--seed S]\n"
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
                "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd]\n"
-               "           [--conv1-algo auto|direct|winograd] [--transport auto|rccl|peer] [--check]\n"
+               "           [--conv1-algo auto|direct|winograd] [--transport auto|rccl|peer|loopback] [--check]\n"
                "           [--split auto|rows|hybrid|batch] [--chunks K] [--peer-sync flags|notes]\n"
+               "           [--input-source local|root] [--lanes L]\n"
                "           [--dry-run] [--pipeline auto|on|off] [--poison]\n"
                "           [--weights DIR] [--no-json]\n",
                msg);
@@ -99,6 +102,8 @@ Options parse(int argc, char** argv) {
     else if (a == "--conv1-algo") o.conv1_algo = val();
     else if (a == "--transport") o.transport = val();
     else if (a == "--split") o.split = val();
+    else if (a == "--input-source") o.input_source = val();
+    else if (a == "--lanes") o.lanes = std::atoi(val().c_str());
     else if (a == "--chunks") o.chunks = std::atoi(val().c_str());
     else if (a == "--peer-sync") o.peer_sync = val();
     else if (a == "--dry-run") o.dry_run = true;
@@ -119,6 +124,8 @@ Options parse(int argc, char** argv) {
   if (o.batch < 1) usage("--batch must be >= 1");
   if (o.split != "auto" && o.split != "rows" && o.split != "hybrid" && o.split != "batch") usage("bad --split");
   if (o.chunks < 0) usage("--chunks must be >= 0");
+  if (o.input_source != "local" && o.input_source != "root") usage("--input-source must be local or root");
+  if (o.lanes < 0) usage("--lanes must be >= 0");
   if (!o.peer_sync.empty() && o.peer_sync != "flags" && o.peer_sync != "notes") usage("--peer-sync must be flags or notes");
   return o;
 }
@@ -652,12 +659,13 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
 }
 
 // ------------------------------------------------------------------------------ V5 (device-resident)
-// The V5 runtime (anx/v5.hpp): one transfer schedule per step (scatter of images x input rows, pool1
-// halos inside each row group cut into image chunks that move while stage1 computes the next chunk,
-// gather of output rows), executed by a pluggable transport:
-//   rccl  grouped ncclSend/ncclRecv over xGMI (one GPU per rank),
-//   peer  one hipMemcpy2DAsync per transfer into the receiver's IPC-mapped buffer, ordered by
-//         device-side flags (ranks may share a GPU: the configuration the one-GPU test box can run).
+// The V5 runtime (anx/v5.hpp): one transfer schedule per step (with --input-source root a scatter of
+// images x input rows; pool1 halos inside each row group cut into image chunks that move while stage1
+// computes the next chunk; gather of output rows), executed by a pluggable transport:
+//   rccl      grouped ncclSend/ncclRecv over xGMI (one GPU per rank),
+//   loopback  the same RCCL transport code over the loopback device comm (ranks share a GPU),
+//   peer      one hipMemcpy2DAsync per transfer into the receiver's IPC-mapped buffer, ordered by
+//             device-side flags (ranks may share a GPU: the configuration the one-GPU test box can run).
 // Steady-state steps never synchronise a stream with the host. Phase times are the compute stream's
 // critical path (scatter / halo_p1 = time spent waiting for data). --dry-run prints the schedule each
 // rank's transport would execute (record-only, no GPU) as ANX_SCHEDULE lines.
@@ -674,6 +682,8 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
   o.impl = s.o.impl == "direct" ? Impl::Direct : Impl::Mfma;
   o.knobs = s.k;
   o.peer_sync = s.o.peer_sync;
+  o.input_source = s.o.input_source == "root" ? InputSource::Root : InputSource::Local;
+  if (s.o.lanes > 0) o.lanes = s.o.lanes;
   if (dry) {  // the schedule this rank's transport would execute, one step
     const std::string tr = pick_v5_transport(o.transport, s.ri, 0, true);
     const std::vector<std::string> log = v5_dry_schedule(rank, np, s.b1, s.b2, s.d.H, s.d.W, o, tr);

@@ -2,7 +2,8 @@
 
   run      run one staged version (v1 v2.1 v2.2 v3 v4 v5) in this process / torchrun rank
   launch   start N ranks of ``run`` on this node (the reference's ``mpirun -np N ./template``)
-  plan     print the exact row decomposition for np ranks
+  plan     print the exact row decomposition for np ranks, or (--model dp|v4|v5) the modelled
+           1/2/4/8-GPU scaling curve of a workload
   bench    shortcut for the headline benchmark (bench.py)
 """
 from __future__ import annotations
@@ -80,13 +81,36 @@ def cmd_launch(a, rest):
 
 
 def cmd_plan(a):
-    from .parallel.plan import balanced_row_ways, conv1_redundancy, make_hybrid_plan, make_plan, plan_stats
+    from .parallel.plan import conv1_redundancy, make_hybrid_plan, make_plan, pick_row_ways, plan_stats
+    if a.model:  # the modelled 1/2/4/8-GPU curve of a workload (anx/cost.hpp; not a measurement)
+        from .parallel import cost
+        batch = a.batch or {"dp": 128, "v4": 256, "v5": 1024}[a.model]
+        src = "root" if a.model == "v4" else a.input_source
+        c = cost.curve(a.model, batch, row_ways=a.row_ways, input_source=src,
+                       mode="overlap" if a.model == "v4" else a.decomp, overrides=a.cost)
+        if a.json:
+            print(json.dumps(c))
+            return
+        unit = "images per GPU (weak scaling)" if a.model == "dp" else "images in all (strong scaling)"
+        print(f"MODELLED (not measured) {a.model} {batch} {unit}, input {src}:")
+        print(cost.table(c))
+        for st in c["steps"]:
+            b = st["bytes"]
+            print(f"N={st['np']}: compute {st['compute_ms']:.3f} ms, egress {st['egress_ms']:.3f}, ingress "
+                  f"{st['ingress_ms']:.3f}, halo {st['halo_ms']:.3f} (exposed {st['halo_exposed_ms']:.3f}), h2d "
+                  f"{st['h2d_ms']:.3f}; root egress {b['root_egress'] / 1e6:.1f} MB, root ingress "
+                  f"{b['root_ingress'] / 1e6:.1f} MB, max rank h2d {b['max_rank_h2d'] / 1e6:.1f} MB, max rank halo "
+                  f"{b['max_rank_halo'] / 1e6:.2f} MB")
+        p = c["params"]
+        print(f"params: xGMI {p['xgmi_gbps']} GB/s per link (assumed), H2D {p['h2d_gbps']} GB/s (measured), "
+              f"host {p['host_gbps']} GB/s (assumed), root ingest slowdown {p['ingest_slowdown']}")
+        return
     if a.batch is not None:  # hybrid batch x rows plan
-        rw = balanced_row_ways(a.np, a.batch) if a.row_ways < 0 else a.row_ways
+        rw = pick_row_ways(a.np, a.batch, "v5", a.input_source, a.decomp) if a.row_ways < 0 else a.row_ways
         hp = make_hybrid_plan(227, 227, a.np, a.batch, rw, a.decomp)
         st = plan_stats(hp)
         print(f"np {a.np} batch {a.batch}: {hp.groups} group(s) of {st['row_ways']} rank(s) (row_ways {rw}"
-              f"{' = balanced default' if a.row_ways < 0 else ''}); output rows per rank max {st['out_rows_max']} / "
+              f"{' = the cost model pick' if a.row_ways < 0 else ''}); output rows per rank max {st['out_rows_max']} / "
               f"mean {st['out_rows_mean']:.3f}; work max/mean {st['imbalance']:.3f}; redundant conv1 rows "
               f"{100 * st['conv1_redundancy']:.1f}% of one device's")
         for r in range(a.np):
@@ -118,7 +142,13 @@ def main(argv=None):
     pp.add_argument("--decomp", default="overlap", choices=["overlap", "per_layer"])
     pp.add_argument("--batch", "-b", type=int, default=None, help="hybrid batch x rows plan for this many images")
     pp.add_argument("--row-ways", type=int, default=-1,
-                    help="ranks per image group (-1 = the V4/V5 runtimes' balanced default, 0 = batch first)")
+                    help="ranks per image group (-1 = the V4/V5 runtimes' default: the cost model's pick, 0 = batch first)")
+    pp.add_argument("--model", default=None, choices=["dp", "v4", "v5"],
+                    help="print the MODELLED 1/2/4/8-GPU scaling curve of a workload (anx/cost.hpp)")
+    pp.add_argument("--input-source", default="local", choices=["local", "root"],
+                    help="v5 / dp input: device-resident (local) or scattered by the root every step")
+    pp.add_argument("--cost", default="", help="cost-model overrides, name=value;... (e.g. xgmi_gbps=64)")
+    pp.add_argument("--json", action="store_true", help="--model: print the curve as JSON")
     sub.add_parser("bench")
     if argv and argv[0] == "launch":
         a, rest = ap.parse_known_args(argv)

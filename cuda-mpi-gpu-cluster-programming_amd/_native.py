@@ -61,6 +61,9 @@ _SIGS = {
     "anx_make_hybrid_plan": (_I, [_I, _I, _I, _I, _I, _I, C.POINTER(BlockC), C.POINTER(BlockC), C.POINTER(_I),
                                   C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), C.POINTER(TileC),
                                   C.POINTER(C.c_double)]),
+    "anx_cost_curve": (_I, [_I, C.POINTER(_I), _I, _I, _I, _I, _I, C.c_char_p, C.c_char_p, _SZ]),
+    "anx_cost_step": (_I, [_I, _I, _I, _I, _I, _I, C.c_char_p, C.c_char_p, _SZ]),
+    "anx_cost_pick_row_ways": (_I, [_I, _I, _I, _I, _I, C.c_char_p, C.POINTER(_I)]),
     "anx_engine_create": (_I, [C.POINTER(_P), C.POINTER(BlockC), C.POINTER(BlockC), _I, _I, _P, _P, _P, _P, _I, _I]),
     "anx_engine_destroy": (_I, [_P]),
     "anx_engine_forward": (_I, [_P, _P, _I, _P, _P]),
@@ -110,7 +113,8 @@ _SIGS = {
 _DIST_SIGS = {
     "anx_v5_create": (_I, [C.POINTER(_P), _I, _I, _I, _I, _I, C.c_char_p, _I, C.c_double, C.POINTER(BlockC),
                            C.POINTER(BlockC), _I, _I, _P, _P, _P, _P, _I, _I, _I, C.c_char_p, _I, _I, _I, _I,
-                           C.c_char_p]),
+                           C.c_char_p, _I, _I, _I]),
+    "anx_v5_log": (_I, [_P, C.c_char_p, _SZ]),
     "anx_v5_destroy": (_I, [_P]),
     "anx_v5_set_input": (_I, [_P, _P]),
     "anx_v5_step": (_I, [_P, _I]),
@@ -129,7 +133,7 @@ _DIST_SIGS = {
     "anx_v4_describe": (_I, [_P, C.c_char_p, _SZ]),
     "anx_v4_probe_h2d": (_I, [_P, _I, C.POINTER(C.c_double)]),
     "anx_v5_schedule": (_I, [_I, C.POINTER(BlockC), C.POINTER(BlockC), _I, _I, _I, _I, _I, _I, _I, C.c_char_p,
-                             C.c_char_p, _SZ]),
+                             _I, C.c_char_p, _SZ]),
 }
 
 

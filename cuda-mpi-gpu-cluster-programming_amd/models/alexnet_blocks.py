@@ -196,11 +196,15 @@ class AlexNetBlocks:
     def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """Full images: [N,H,W,3] -> [N,Hp2,Wp2,K2]."""
         plan = full_plan(self.H, self.W, self.b1, self.b2)
+        if plan.inp.size != self.H and x.dim() == 4 and x.shape[1] == self.H:
+            # a spec whose receptive field skips the last input rows (e.g. a 2x2 pool1): the tile reads
+            # exactly the rows it needs
+            x = x[:, plan.inp.lo:plan.inp.hi].contiguous()
         L = 1 + len(self._lanes)
         N = x.shape[0] if x.dim() == 4 else 0
         if L == 1 or N < L * LANE_MIN:
             return self.tile_forward(x, plan, out)
-        self._check_in(x, self.H)
+        self._check_in(x, plan.inp.size)
         y = self._out(out, N)
         bounds = [N * i // L for i in range(L + 1)]
         cur = torch.cuda.current_stream(self.device)

@@ -241,7 +241,7 @@ def check_plan(p: DecompPlan, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) ->
 
 
 # ----------------------------------------------------------------------------- V5 step schedule
-# Mirror of anx::plan_stats / balanced_row_ways / make_v5_layout (csrc/src/runtime/v5.cpp) and of
+# Mirror of anx::plan_stats / make_v5_layout (csrc/src/runtime/v5.cpp) and of
 # anx::make_step_schedule / chunk_of (csrc/src/runtime/schedule.cpp): tests/test_v5_runtime.py checks
 # that the native runtime issues exactly this transfer list.
 
@@ -259,22 +259,12 @@ def plan_stats(p: HybridPlan) -> dict:
             "conv1_redundancy": hybrid_conv1_redundancy(p), "images_per_rank_max": max(imgs)}
 
 
-def balanced_row_ways(np_: int, batch: int, H: int = 227, W: int = 227) -> int:
-    """Fewest row ways r >= 2 (r | np) whose images x rows work is within 10% of the mean (np = 8,
-    batch 1024: r = 2, four groups of 256 images split 7 / 6 output rows, max / mean 1.077); else the
-    most balanced r."""
-    if np_ <= 1:
-        return 1
-    best, best_imb = np_, float("inf")
-    for r in range(2, np_ + 1):
-        if np_ % r:
-            continue
-        imb = plan_stats(make_hybrid_plan(H, W, np_, batch, r, PER_LAYER))["imbalance"]
-        if imb <= 1.1:
-            return r
-        if imb < best_imb - 1e-9:
-            best, best_imb = r, imb
-    return best
+def pick_row_ways(np_: int, batch: int, workload: str = "v5", input_source: str = "local",
+                  mode: str = PER_LAYER) -> int:
+    """The runtimes' default row split: the native cost model's lowest modelled step over the divisors
+    of np (anx/cost.hpp; :mod:`anx.parallel.cost`)."""
+    from .cost import pick_row_ways as native_pick
+    return native_pick(workload, np_, batch, input_source, "per_layer" if mode == PER_LAYER else "overlap")
 
 
 def _xfer(phase, src, dst, frm, to, width, height):
@@ -282,10 +272,12 @@ def _xfer(phase, src, dst, frm, to, width, height):
             f"to={to[0]}+{to[1]}/{to[2]}")
 
 
-def step_schedule(p: HybridPlan, chunks: int = 0, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> list[str]:
-    """Every transfer of one V5 step in issue order (scatter, pool1-halo chunks, gather), in the
-    native Transfer::str() format: a 2-D block of `h` images x `w` bytes between buffer regions
-    (X / Tile / Win / Y / YFull + byte offset / image pitch)."""
+def step_schedule(p: HybridPlan, chunks: int = 0, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2,
+                  input_source: str = "root") -> list[str]:
+    """Every transfer of one V5 step in issue order (scatter with root input, pool1-halo chunks,
+    gather), in the native Transfer::str() format: a 2-D block of `h` images x `w` bytes between buffer
+    regions (X / Tile / Win / Y / YFull + byte offset / image pitch). With local input the scatter is
+    the one-time placement of set_input, not part of a step."""
     d = blocks_dims(p.row_plans[0].H, p.row_plans[0].W, b1, b2)
     in_row, out_row = d.W * d.C0 * 4, d.Wp2 * d.C2 * 4
     win_row = (d.Wp1 + 2 * b2.conv.P) * d.C1 * 4
@@ -311,7 +303,7 @@ def step_schedule(p: HybridPlan, chunks: int = 0, b1: BlockSpec = BLOCK1, b2: Bl
     if halos:
         least = min(x[6] for x in halos)
         chunks = max(1, min(chunks if chunks > 0 else max(1, min(4, least // 128)), least, MAX_CHUNKS))
-    out = [_xfer(*x) for x in scatter]
+    out = [_xfer(*x) for x in scatter] if input_source == "root" else []
     for c in range(chunks if halos else 0):
         for ph, s, t, frm, to, w, hgt in halos:
             lo, hi = hgt * c // chunks, hgt * (c + 1) // chunks

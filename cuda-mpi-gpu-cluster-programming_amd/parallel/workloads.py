@@ -6,25 +6,26 @@ The reference's V4 (final_project/v4_mpi_cuda/src/main_mpi_cuda.cpp:52-130) keep
 planned V5 (README.md:157-166) keeps every byte on the device and exchanges per-layer halos between
 GPUs.
 
-* :class:`NativeV5` — V5 on GPUs: a thin client of the native V5 runtime (``anx/v5.hpp`` through
-  ``libanx_dist``'s C ABI). The runtime owns the plan, the buffers, the streams and the transport
-  (RCCL over xGMI, or the peer IPC transport with device-side flags when ranks share a GPU); Python
-  only passes the job shape and the root's weights / batch and reads back the output, the phase
-  times and the layout. Its transfer list is :func:`anx.parallel.plan.step_schedule` exactly
-  (tests/test_v5_runtime.py).
-* :class:`RowsWorkload` — V4 on GPUs and the CPU (gloo) rehearsal of both versions, over
-  torch.distributed: a fixed global batch split by the hybrid planner
-  (:func:`anx.parallel.plan.make_hybrid_plan`: ``rows`` = the reference's pure row split over all
-  ranks, ``hybrid`` = batch first, rows only below one image per rank, ``batch`` = images only)::
+* :class:`NativeV5` / :class:`NativeV4` — the GPU programs: thin clients of the native runtimes
+  (``anx/v5.hpp`` / ``anx/v4.hpp`` through ``libanx_dist``'s C ABI). The runtimes own the plan, the
+  buffers, the streams and the transport (RCCL over xGMI; the RCCL transport over the loopback device
+  comm, or the peer IPC transport with device-side flags, when ranks share a GPU); Python only passes
+  the job shape and the root's weights / batch and reads back the output, the phase times and the
+  layout. The V5 transfer list is :func:`anx.parallel.plan.step_schedule` exactly
+  (tests/test_v5_runtime.py). Default row split: the native cost model's pick (anx/cost.hpp).
+* :class:`RowsWorkload` — a SEPARATE, Python-level gloo/CPU rehearsal of the same two programs over
+  torch.distributed (``bench.py --device cpu``, tests/test_dist_cpu.py). It shares the planner and
+  the engines with the native runtimes but not their scatter / halo / gather code: its transfers are
+  torch.distributed P2P ops issued from Python. The GPU benchmarks never run it::
 
-    v4  root pinned host --H2D--> root GPU --RCCL scatter (images x input rows incl. halo)--> ranks
-        --tile_forward (overlap tiles: no mid-network exchange)--> RCCL gather --D2H--> root pinned host
+    v4  root host --H2D--> root device --scatter (images x input rows incl. halo)--> ranks
+        --tile_forward (overlap tiles: no mid-network exchange)--> gather --D2H--> root host
     v5  root --scatter--> ranks --stage1 (conv1+pool1)--> pool1-halo exchange inside each row group
         (per_layer tiles) --stage2 (conv2+pool2+LRN)--> gather --> root
 
-  Every transfer is a grouped point-to-point op (RCCL has no Scatterv/Gatherv). Buffers are allocated
-  once. Each phase ends with an event on the compute stream (no host sync inside a step), so the
-  per-phase times come from event pairs after the timed loop.
+  Every transfer is a grouped point-to-point op (no Scatterv/Gatherv). Buffers are allocated once.
+  Each phase ends with an event on the compute stream (no host sync inside a step), so the per-phase
+  times come from event pairs after the timed loop.
 """
 from __future__ import annotations
 
@@ -42,7 +43,7 @@ from .comm import world
 from .plan import OVERLAP, PER_LAYER, HybridPlan, make_hybrid_plan
 
 DECOMPS = {"rows": None, "hybrid": 0, "batch": 1}  # row_ways (None = all ranks)
-V5_DECOMPS = {"auto": -1, "rows": None, "hybrid": 0, "batch": 1}  # -1: balanced (anx::balanced_row_ways)
+V5_DECOMPS = {"auto": -1, "rows": None, "hybrid": 0, "batch": 1}  # -1: the cost model's pick (anx/cost.hpp)
 PHASES = ("h2d", "scatter", "stage1", "halo_p1", "compute", "gather", "d2h")
 
 
@@ -63,9 +64,9 @@ class RowsWorkload:
         self.layer = layer or (OVERLAP if version == "v4" else PER_LAYER)
         if version == "v4" and self.layer != OVERLAP:
             raise ValueError("v4 runs overlap tiles (host-staged, no mid-network exchange)")
-        if decomp == "auto":  # the balanced default of the native runtime (anx::balanced_row_ways)
-            from .plan import balanced_row_ways
-            rw = balanced_row_ways(self.world, batch, model.H, model.W)
+        if decomp == "auto":  # the native runtimes' default: the cost model's pick
+            from .plan import pick_row_ways
+            rw = pick_row_ways(self.world, batch, version, "root", self.layer)
         else:
             rw = DECOMPS[decomp]
         self.plan: HybridPlan = make_hybrid_plan(model.H, model.W, self.world, batch,
@@ -293,11 +294,14 @@ class NativeV5:
     def __init__(self, batch: int, weights: dict | None, *, specs=(BLOCK1, BLOCK2), H: int = 227, W: int = 227,
                  decomp: str = "auto", layer: str = PER_LAYER, transport: str = "auto", chunks: int = 0,
                  pipeline: int = -1, poison: bool = False, impl: str = "mfma", peer_sync: str = "",
-                 port: int | None = None, timeout_s: float = 300.0):
+                 port: int | None = None, timeout_s: float = 300.0, input_source: str = "local", lanes: int = 0,
+                 keep_log: bool = False):
         if decomp not in V5_DECOMPS:
             raise ValueError(f"decomp must be one of {sorted(V5_DECOMPS)}")
         if layer not in (OVERLAP, PER_LAYER):
             raise ValueError("layer must be overlap or per_layer")
+        if input_source not in ("local", "root"):
+            raise ValueError("input_source must be local or root")
         self.rank, self.world, local_rank, local_world, nnodes, port = _launch(port)
         self.batch, self.b1, self.b2, self.H, self.W = batch, specs[0], specs[1], H, W
         self.dims = blocks_dims(H, W, *specs)
@@ -309,9 +313,10 @@ class NativeV5:
         nat.dist_call("anx_v5_create", C.byref(h), self.rank, self.world, local_rank, local_world, nnodes, addr, port,
                       timeout_s, C.byref(nat.block_c(self.b1)), C.byref(nat.block_c(self.b2)), H, W, *ptrs, batch, rw,
                       1 if layer == PER_LAYER else 0, transport.encode(), chunks, pipeline, int(poison),
-                      0 if impl == "mfma" else 1, peer_sync.encode())
+                      0 if impl == "mfma" else 1, peer_sync.encode(), 1 if input_source == "root" else 0, lanes,
+                      int(keep_log))
         self._h = h
-        self.version, self.layer = "v5", layer
+        self.version, self.layer, self.input_source = "v5", layer, input_source
 
     # ------------------------------------------------------------------ data
     def fill(self, x: torch.Tensor | None) -> None:
@@ -342,9 +347,15 @@ class NativeV5:
         nat.dist_call("anx_v5_sync", self._h)
 
     def _json(self, name, *extra) -> dict:
-        buf = C.create_string_buffer(4096)
+        buf = C.create_string_buffer(1 << 16)
         nat.dist_call(name, self._h, buf, len(buf), *extra)
         return json.loads(buf.value.decode())
+
+    def transfer_log(self) -> list[str]:
+        """Every transfer this rank's transport issued since construction (``keep_log=True``)."""
+        buf = C.create_string_buffer(1 << 22)
+        nat.dist_call("anx_v5_log", self._h, buf, len(buf))
+        return [l for l in buf.value.decode().splitlines() if l]
 
     def phase_ms(self, reset: bool = False) -> dict:
         """Mean ms per step since the last reset on the compute stream's critical path (syncs)."""
@@ -370,13 +381,14 @@ class NativeV5:
 
 def native_schedule(np_: int, batch: int, row_ways: int = -1, layer: str = PER_LAYER, chunks: int = 0,
                     rank: int = -1, transport: str = "rccl", specs=(BLOCK1, BLOCK2), H: int = 227,
-                    W: int = 227) -> list[str]:
+                    W: int = 227, input_source: str = "root") -> list[str]:
     """The native runtime's record-only schedule (no GPU): rank < 0 -> every transfer of one step in
     issue order; else what rank `rank`'s transport issues."""
     buf = C.create_string_buffer(1 << 22)
     nat.check(nat.dist().anx_v5_schedule(np_, C.byref(nat.block_c(specs[0])), C.byref(nat.block_c(specs[1])), H, W,
                                          batch, row_ways, 1 if layer == PER_LAYER else 0, chunks, rank,
-                                         transport.encode(), buf, len(buf)), "anx_v5_schedule")
+                                         transport.encode(), 1 if input_source == "root" else 0, buf, len(buf)),
+              "anx_v5_schedule")
     return [l for l in buf.value.decode().splitlines() if l]
 
 
@@ -384,7 +396,11 @@ class NativeV4:
     """V4 on GPUs through the native host-staged runtime (anx/v4.hpp; construction is collective):
     the batch and the output live in one shared pinned host segment, every rank DMAs its own images x
     input rows (halo included) from it and its output rows back, chunked so H2D / compute / D2H
-    overlap. ``x_host`` / ``y_host`` are zero-copy views of the segment."""
+    overlap.
+
+    ``x_host`` / ``y_host`` are zero-copy views of the segment, valid until :meth:`close`: ``close``
+    unmaps it, after which the properties raise and any view or slice kept from them points at
+    unmapped memory (take ``.clone()`` of what must outlive the runtime; :meth:`output` does)."""
 
     def __init__(self, batch: int, weights: dict | None, *, specs=(BLOCK1, BLOCK2), H: int = 227, W: int = 227,
                  decomp: str = "auto", chunks: int = 0, impl: str = "mfma", port: int | None = None,
@@ -406,9 +422,21 @@ class NativeV4:
         self._h = h
         pin, pout = C.POINTER(C.c_float)(), C.POINTER(C.c_float)()
         nat.dist_call("anx_v4_segment", h, C.byref(pin), C.byref(pout))
-        self.x_host = torch.from_numpy(np.ctypeslib.as_array(pin, shape=(batch, H, W, d.C0)))
-        self.y_host = torch.from_numpy(np.ctypeslib.as_array(pout, shape=(batch, d.Hp2, d.Wp2, d.C2)))
+        self._x_host = torch.from_numpy(np.ctypeslib.as_array(pin, shape=(batch, H, W, d.C0)))
+        self._y_host = torch.from_numpy(np.ctypeslib.as_array(pout, shape=(batch, d.Hp2, d.Wp2, d.C2)))
         self.version, self.layer = "v4", OVERLAP
+
+    @property
+    def x_host(self) -> torch.Tensor:
+        if self._x_host is None:
+            raise RuntimeError("NativeV4 is closed: its shared segment is unmapped")
+        return self._x_host
+
+    @property
+    def y_host(self) -> torch.Tensor:
+        if self._y_host is None:
+            raise RuntimeError("NativeV4 is closed: its shared segment is unmapped")
+        return self._y_host
 
     def fill(self, x: torch.Tensor | None) -> None:
         """Collective: rank 0 writes the global batch into the shared segment."""
@@ -450,7 +478,7 @@ class NativeV4:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            self.x_host = self.y_host = None
+            self._x_host = self._y_host = None
             nat.dist_call("anx_v4_destroy", self._h)
             self._h = None
 

@@ -110,21 +110,22 @@ def test_native_v4_shared_gpu(cuda, np_):
     assert rec["max_abs_err"] < 1e-3
 
 
-def _schedule(np_, transport, split, batch=3, decomp="per_layer"):
+def _schedule(np_, transport, split, batch=3, decomp="per_layer", src="root"):
     _, out = native(["--version", "v5", "--dry-run", "--transport", transport, "--split", split, "--batch",
-                     str(batch), "--decomp", decomp], np_)
+                     str(batch), "--decomp", decomp, "--input-source", src], np_)
     return sorted(l.split(" ", 2)[2] for l in out.stdout.splitlines() if l.startswith("ANX_SCHEDULE "))
 
 
 @pytest.mark.parametrize("np_,split", [(2, "rows"), (3, "rows"), (4, "rows"), (4, "hybrid"), (3, "batch")])
-def test_v5_transports_issue_identical_transfers(np_, split):
-    """The RCCL and peer transports execute the same transfer list (record-only dry run: each logs
-    every transfer at the point it would issue it), so the shared-GPU peer tests cover the RCCL
-    schedule."""
-    rccl, peer = _schedule(np_, "rccl", split), _schedule(np_, "peer", split)
-    assert rccl == peer and len(rccl) > 0
+@pytest.mark.parametrize("src", ["root", "local"])
+def test_v5_transports_issue_identical_transfers(np_, split, src):
+    """The RCCL, loopback and peer transports execute the same transfer list (record-only dry run:
+    each logs every transfer at the point it would issue it), so the shared-GPU peer / loopback tests
+    cover the RCCL schedule. Device-resident (local) input moves no scatter inside a step."""
+    rccl, peer = _schedule(np_, "rccl", split, src=src), _schedule(np_, "peer", split, src=src)
+    assert rccl == peer == _schedule(np_, "loopback", split, src=src) and len(rccl) > 0
     phases = {l.split(" ")[2].split("#")[0] for l in rccl}
-    assert {"scatter", "gather"} <= phases
+    assert "gather" in phases and ("scatter" in phases) == (src == "root")
     assert ("halo_p1" in phases) == (split == "rows" or np_ > 3)
 
 
@@ -148,7 +149,7 @@ def test_native_v5_peer_transport(cuda, np_, decomp, split, extra):
         rec, out = native(["--version", "v5", "--transport", "peer", "--decomp", decomp, "--split", split, "--init",
                            "rand", "--seed", "6", "--batch", "3", "--iters", "4", "--lrn-alpha-mode", "raw",
                            "--pipeline", pipe, "--poison", *extra, *d], np_)
-        assert set(rec["phases_warm"]) == {"scatter", "stage1", "halo_p1", "stage2", "gather"}
+        assert set(rec["phases_warm"]) == {"scatter", "stage1", "halo_p1", "stage2", "gather", "compute"}
         assert "Final Output Shape: 13x13x256" in out.stdout or rec["shape"] == [13, 13, 256]
         assert rec["checksum"] == ref["checksum"], pipe
         assert rec["v5"]["ordering"] == ("notes" if "notes" in extra else "flags")
