@@ -104,6 +104,8 @@ int anx_memcpy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch,
 int anx_conv2d_direct(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C, int K,
                       int F, int S, int P, int groups, int relu, void* stream);
 int anx_relu(float* x, size_t n, void* stream);
+/* copy on exactly `workgroups` workgroups (tools/probe_ingest.py); bytes % 16 == 0, 16-B aligned */
+int anx_channel_copy(void* dst, const void* src, size_t bytes, int workgroups, void* stream);
 int anx_maxpool_direct(const float* x, float* y, int N, int H, int W, int C, int F, int S, void* stream);
 int anx_lrn_direct(const float* x, float* y, int N, int H, int W, int C, int size, float alpha, float beta, float k,
                    int mode, void* stream);

@@ -73,7 +73,8 @@ class BlocksEngine {
 
  private:
   hipError_t ensure_window(const TilePlan& t, int N, hipStream_t s);
-  hipError_t conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s);
+  // conv1 (+ReLU) of n images into c1_ starting at image c1_img0
+  hipError_t conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s, int c1_img0 = 0);
   hipError_t conv2_chunk(int n, const TilePlan& t, const float* qc, float* yc, hipStream_t s);
   hipError_t pool2_chunk(int n, const TilePlan& t, float* yc, hipStream_t s);  // c2_ -> y (+LRN)
   // Whether tile_forward of N images runs pool1 inside the Winograd input transform (Knobs::fuse_pool1)

@@ -162,6 +162,9 @@ hipError_t maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int
 
 // Zero the rows of an NHWC buffer outside [row_lo, row_hi) and the W border (halo buffers).
 hipError_t fill(float* x, size_t n, float v, hipStream_t s);
+// 16-B-vector copy on exactly `workgroups` workgroups (the ingest probe's stand-in for a collective's
+// receive channels: tools/probe_ingest.py). bytes % 16 == 0, both pointers 16-B aligned.
+hipError_t channel_copy(void* dst, const void* src, size_t bytes, int workgroups, hipStream_t s);
 
 }  // namespace hip
 }  // namespace anx

@@ -353,6 +353,9 @@ int anx_conv2d_direct(const float* x, const float* w, const float* b, float* y, 
 }
 
 int anx_relu(float* x, size_t n, void* stream) { return hip_status(anx::hip::relu(x, n, S(stream)), "relu"); }
+int anx_channel_copy(void* dst, const void* src, size_t bytes, int workgroups, void* stream) {
+  return hip_status(anx::hip::channel_copy(dst, src, bytes, workgroups, S(stream)), "channel_copy");
+}
 
 int anx_maxpool_direct(const float* x, float* y, int N, int H, int W, int C, int F, int S_, void* stream) {
   return hip_status(anx::hip::maxpool_direct(x, y, N, H, W, C, F, S_, S(stream)), "maxpool_direct");

@@ -132,10 +132,11 @@ float* BlocksEngine::q2_row_ptr(const TilePlan& t, int n, int r) {
   return q2_ + static_cast<size_t>(n) * q2_image_stride_floats(t) + static_cast<size_t>(r - t.q.lo) * q2_row_floats();
 }
 
-hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s) {
+hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s, int c1_img0) {
   RoctxRange rx("anx conv1");
   const ConvSpec& k1 = b1_.conv;
-  const hip::OutView c1v{c1_, t.c1.size(), d_.W1, d_.C1, 0, 0, 0};
+  const hip::OutView c1v{c1_ + static_cast<size_t>(c1_img0) * t.c1.size() * d_.W1 * d_.C1, t.c1.size(), d_.W1, d_.C1,
+                         0, 0, 0};
   if (impl_ == Impl::Mfma && wv1_ != nullptr && use_winograd(k_.conv1_algo, n, t.c1.size(), d_.H1)) {
     const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
     if (hip::conv1_wino_v_floats(w) > wv1_cap_) return hipErrorInvalidValue;
@@ -249,11 +250,15 @@ bool BlocksEngine::fused_pool1(int N, const TilePlan& t) const {
   // every pool1 row of the window (inside the pooled image) is computed by this tile
   const int lo = std::max(t.q.lo, 0), hi = std::min(t.q.hi, d_.Hp1);
   if (lo < t.p1.lo || hi > t.p1.hi) return false;
-  // and every launch chunk runs Conv2 as Winograd
+  // and every Conv2 launch (chunk, or sub-chunk of one) runs Winograd
   const int chunk = std::min(chunk_, k_.chunk1 > 0 ? k_.chunk1 : chunk_);
-  const int last = N - (N - 1) / chunk * chunk;
-  return use_winograd(k_.conv2_algo, std::min(N, chunk), t.c2.size(), d_.H2) &&
-         use_winograd(k_.conv2_algo, last, t.c2.size(), d_.H2);
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int n = std::min(chunk, N - n0), sub = k_.conv2_sub > 0 ? std::min(n, k_.conv2_sub) : n;
+    if (!use_winograd(k_.conv2_algo, sub, t.c2.size(), d_.H2) ||
+        !use_winograd(k_.conv2_algo, n - (n - 1) / sub * sub, t.c2.size(), d_.H2))
+      return false;
+  }
+  return true;
 }
 
 hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, float* y, hipStream_t s) {
@@ -269,16 +274,26 @@ hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, 
   const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
   const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
   const int chunk = std::min(chunk_, k_.chunk1 > 0 ? k_.chunk1 : chunk_);
-  const hip::OutView c2v{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
+  const size_t c1_img = static_cast<size_t>(t.c1.size()) * d_.W1 * d_.C1;
+  const size_t c2_img = static_cast<size_t>(t.c2.size()) * d_.W2 * d_.C2;
   for (int n0 = 0; n0 < N; n0 += chunk) {
     const int n = std::min(chunk, N - n0);
-    ANX_TRY(conv1_chunk(x + n0 * in_img, n, t, s));
+    // Conv1 in sub-chunks (Knobs::conv1_sub): each rewrites the same V workspace, which a small
+    // sub-chunk keeps inside the Infinity Cache between the transform and the GEMM
+    const int s1 = k_.conv1_sub > 0 ? std::min(n, k_.conv1_sub) : n;
+    for (int a0 = 0; a0 < n; a0 += s1)
+      ANX_TRY(conv1_chunk(x + (n0 + a0) * in_img, std::min(s1, n - a0), t, s, a0));
     RoctxRange rx("anx pool1+conv2+pool2+lrn");
-    const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
-    if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
-    ANX_TRY(hip::wino_pool_input(w, c1_, t.c1.size(), d_.W1, t.q.lo, d_.Hp1, d_.Wp1, k2.P, t.c1.lo, wv_, s,
-                                     b1_.pool.F, b1_.pool.S));
-    ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
+    const int s2 = k_.conv2_sub > 0 ? std::min(n, k_.conv2_sub) : n;
+    for (int b0 = 0; b0 < n; b0 += s2) {
+      const int m = std::min(s2, n - b0);
+      const hip::WinoPlan w = hip::make_wino_plan(m, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
+      if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
+      ANX_TRY(hip::wino_pool_input(w, c1_ + b0 * c1_img, t.c1.size(), d_.W1, t.q.lo, d_.Hp1, d_.Wp1, k2.P, t.c1.lo,
+                                   wv_, s, b1_.pool.F, b1_.pool.S));
+      const hip::OutView c2v{c2_ + b0 * c2_img, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
+      ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
+    }
     ANX_TRY(pool2_chunk(n, t, y + n0 * y_img, s));
   }
   return hipSuccess;

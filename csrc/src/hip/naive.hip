@@ -117,7 +117,25 @@ __global__ void __launch_bounds__(kBlock) fill_kernel(float* __restrict__ x, siz
     x[i] = v;
 }
 
+// Copy with a fixed number of workgroups (the receive-side work of a collective that owns that many
+// CUs: RCCL's receive channels copying from their FIFOs into the user buffer). 16-B vectors, grid-stride.
+__global__ void __launch_bounds__(kBlock) channel_copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                              size_t n4) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n4;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x)
+    dst[i] = src[i];
+}
+
 }  // namespace
+
+hipError_t channel_copy(void* dst, const void* src, size_t bytes, int workgroups, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if (bytes % 16 || workgroups < 1 || reinterpret_cast<uintptr_t>(dst) % 16 || reinterpret_cast<uintptr_t>(src) % 16)
+    return hipErrorInvalidValue;
+  channel_copy_kernel<<<static_cast<unsigned>(workgroups), kBlock, 0, s>>>(static_cast<const float4*>(src),
+                                                                          static_cast<float4*>(dst), bytes / 16);
+  return hipGetLastError();
+}
 
 hipError_t conv2d_direct(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C,
                          int K, int F, int S, int P, int groups, bool relu, hipStream_t s) {

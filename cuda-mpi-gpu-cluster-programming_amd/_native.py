@@ -61,6 +61,7 @@ _SIGS = {
     "anx_make_hybrid_plan": (_I, [_I, _I, _I, _I, _I, _I, C.POINTER(BlockC), C.POINTER(BlockC), C.POINTER(_I),
                                   C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), C.POINTER(TileC),
                                   C.POINTER(C.c_double)]),
+    "anx_channel_copy": (_I, [_P, _P, _SZ, _I, _P]),
     "anx_cost_curve": (_I, [_I, C.POINTER(_I), _I, _I, _I, _I, _I, C.c_char_p, C.c_char_p, _SZ]),
     "anx_cost_step": (_I, [_I, _I, _I, _I, _I, _I, C.c_char_p, C.c_char_p, _SZ]),
     "anx_cost_pick_row_ways": (_I, [_I, _I, _I, _I, _I, C.c_char_p, C.POINTER(_I)]),

@@ -18,6 +18,7 @@
 #   wgemm    anx_wgemm Winograd GEMM A/B at 300 and 64 images; wgpmc: its clock / MFMA busy pass
 #   halo     V5 halo pipeline A/B on shared-GPU peer ranks: np {2,4} x chunks {1, auto} ($HALO_BATCH)
 #   tests_k  a subset of GPU tests: pytest -k "$TESTS_K" (one process)
+#   ingest   tools/probe_ingest.py: the bench step with a concurrent 155 MB/step receive-side copy
 # Outputs land in gpurun_out/ (merged back by gpurun). This one script replaces the per-session
 # wrappers of rounds 1-3.
 set -o pipefail
@@ -50,7 +51,8 @@ for s in "$@"; do
     tests) run tests 900 python -u -m pytest tests -x -q -m gpu --timeout 240 --timeout-method thread ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 $BARGS ;;
-    sweep) run sweep 600 python tools/sweep_batch.py --batches ${SWEEP:-64,128,256,300,600} --rounds 3 --iters 10 ;;
+    sweep) run sweep 600 python tools/sweep_batch.py --batches ${SWEEP:-64,128,256,300,600} --rounds 3 --iters 10 \
+             ${SWEEP_ARGS:-} ;;
     ab) run ab 900 python tools/ab_variants.py --arms "${AB_ARMS:-|conv1_occ=3}" --batch "${AB_BATCH:-300}" \
           --lanes "${AB_LANES:-1}" --rounds "${AB_ROUNDS:-5}" ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 10 --warmup 3 $BARGS ;;
@@ -69,7 +71,9 @@ for s in "$@"; do
     peak) run peak 120 bash -c "$B/anx_mfmapeak --waves 1 && $B/anx_mfmapeak --waves 2 && $B/anx_mfmapeak --waves 4" ;;
     workloads)
       run wl_v4 300 python bench.py --workload v4 --steps 10 --warmup 3
-      run wl_v5 300 python bench.py --workload v5 --steps 10 --warmup 3 ;;
+      run wl_v5 300 python bench.py --workload v5 --steps 10 --warmup 3
+      run wl_v5_root 300 python bench.py --workload v5 --input-source root --steps 10 --warmup 3 --no-b1 ;;
+    ingest) run probe_ingest 600 python tools/probe_ingest.py ${INGEST_ARGS:-} ;;
     versions)
       run v3_b1 120 $B/anx --version v3 --iters 20 --check
       run v4_np2 180 $B/anxrun -np 2 --timeout 150 -- $B/anx --version v4 --batch 8 --iters 5 --check

@@ -406,6 +406,16 @@ def test_fused_pool1_bitwise(cuda, N, chunk):
     torch.testing.assert_close(y[idx].cpu().double(), ref, rtol=2e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("N,sub1,sub2", [(64, 16, 0), (64, 0, 24), (40, 16, 16), (20, 9, 12)])
+def test_sub_chunks_bitwise(cuda, N, sub1, sub2):
+    """Conv1 / Conv2 in sub-chunks (knobs conv1_sub / conv2_sub: the V workspace rewritten in place per
+    sub-chunk) give the same bits as whole launches."""
+    x = init_input(N, "rand", seed=15).to(cuda)
+    whole = AlexNetBlocks(device=cuda, init="rand", seed=15, max_batch=N)
+    sub = AlexNetBlocks(device=cuda, init="rand", seed=15, max_batch=N, knobs={"conv1_sub": sub1, "conv2_sub": sub2})
+    assert torch.equal(whole(x), sub(x))
+
+
 def test_fused_pool1_refuses_other_pool_shapes(cuda):
     """The fused pool1 + input transform kernel walks 3x3 / stride-2 windows only. A block-1 pool of
     another shape (2x2 / 2 also gives 27x27 here, so the rest of the engine is unchanged) must take
