@@ -37,6 +37,8 @@ struct Knobs {
                            // 1 = 2 phase rows x all columns, 0 = per-tile gathers from global memory
   int fuse_pool1 = 1;      // tile_forward of a tile that computes every pool1 row its conv2 window needs: pool1
                            // fused into the Winograd input transform (no window round trip), 0 = pool1 kernel
+  int conv1_fused = 0;     // Conv1 as one kernel (conv1_fused.hip: V built in LDS inside the GEMM, 64 tiles x 96
+                           // filters per workgroup) instead of the band transform kernel + GEMM
   int conv1_sub = 0;       // fused tile_forward: images per Conv1 (input transform + GEMM) launch pair inside a
                            // chunk (0 = the whole chunk); the V workspace is rewritten in place per sub-chunk, so
                            // a small one is written and re-read inside the 256 MB Infinity Cache
@@ -45,7 +47,7 @@ struct Knobs {
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
 // ANX_BF16_GLDS, ANX_BF16_BIG, ANX_BF16_FC, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1,
-// ANX_CONV1_SUB, ANX_CONV2_SUB when set.
+// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

@@ -1,0 +1,318 @@
+// Conv1 as ONE kernel: polyphase Winograd F(3x3,3x3) with the input transform generated in LDS
+// inside the GEMM (conv1_wino.hip explains the polyphase rewrite and the two-kernel form).
+//
+// The two-kernel form writes V [P][25][48] to HBM (1.73 MB per image, 2.8x the image) and the GEMM
+// reads it back: 237 MB written + read per 128 images, ~29 % of the fp32 step's HBM traffic
+// (profiles/r03_pmc_bytes_b128_after.md). Here a workgroup owns 64 tiles x ALL 96 filters, so each
+// tile's V is built once, by the workgroup, from the image rows in L2:
+//
+//   a-step a (5 per workgroup): V_a[b][tile][ch] = sum_v B^T[b][v] t[v],
+//                               t[v] = sum_u B^T[a][u] X'[tile][u][v][ch]   (same fmaf order as the
+//                               band kernel, so V is bit-identical to the two-kernel form's)
+//   point (a, b): M = V_ab[64 x 48] . U_ab[48 x 96] on v_mfma_f32_16x16x4_f32, folded into the 3x3
+//                 outputs in registers: Y[i][j] += A^T[i][a] A^T[j][b] M.
+//
+// V_{a+1} is built (global loads of X' from L2 into registers, VALU) while the MFMAs of a-step a run
+// and stored at its end; the two V buffers (5 points x 32 tiles x 48 ch, row stride 56 floats:
+// conflict-free ds_read_b128 fragments) alternate by a-step. U_ab (18 KB per point) streams through a
+// 2-slot LDS ring by buffer_load ... lds, one barrier per point (it also publishes V). 12 waves (3 per
+// SIMD): wave (wm, wn) computes tiles 16 wm .. +15 x filters 16 wn .. +15 as one 16x16x4 MFMA block,
+// so the fold keeps 36 registers (9 outputs x 4 values) and three waves fit a SIMD with room for the
+// V build. Bias + ReLU + the NHWC store through an LDS transpose (each 384-B output row of 96 filters
+// written by 24 lanes, 16 B each).
+//
+// Reference op: convKernel (v3_cuda_only/src/layers_cuda.cu:20-46), one thread per output.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "anx/ops.hpp"
+#include "anx/winograd_f33.hpp"
+
+namespace anx::hip {
+namespace {
+
+namespace w33 = anx::wino33;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using lds_f32 = __attribute__((address_space(3))) float;
+using lds_void = __attribute__((address_space(3))) void;
+
+constexpr int kPh = 4, kCh = 48, kN5 = 5, kPts = 25, kPitch = 12;
+constexpr int kK = 96;                     // filters per workgroup (all of Conv1's)
+constexpr int kTiles = 32;                 // tiles per workgroup
+constexpr int kWaves = 12, kNT = 64 * kWaves;
+constexpr int kVS = 56;                    // LDS row stride of V (floats): conflict-free b128 fragment reads
+constexpr int kVBuf = kN5 * kTiles * kVS;  // floats per a-step V buffer
+constexpr int kUSlot = kK * kCh;           // floats per U ring slot (one point)
+constexpr int kUPieces = kUSlot / 256;     // 1-KiB DMA pieces per slot
+constexpr int kOS = kK + 4;                // epilogue transpose row stride (floats)
+constexpr int kLdsFloats = 2 * kVBuf + 2 * kUSlot;
+constexpr size_t kLds = kLdsFloats * sizeof(float);
+static_assert(kLds <= 160 * 1024, "LDS");
+static_assert(kUSlot % 256 == 0 && kUPieces <= 2 * kWaves, "U ring pieces");
+static_assert(kTiles * kOS <= kLdsFloats, "epilogue scratch");
+static_assert(kTiles * 24 == kNT, "V build: one (tile, channel pair) per thread");
+
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+// 16-B unit u of U row r sits at unit u ^ swz(r) of its LDS row (12 units per row): conflict-free
+// ds_read_b128 of the B fragments (16 filter rows x 4 units per lane group; (r >> 2) & 3 left 2-way
+// conflicts for this access pattern)
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 3; }
+
+struct Conv1FusedArgs {
+  const float* x;     // [N][Hin][W][3] image rows of the tile
+  const float* U;     // [25][96][48] transformed filters
+  const float* bias;  // [96]
+  OutView out;
+  int P, ty, tx, Ho, Wo, Hin, rowf;  // rowf = W * 3 floats per image row
+  int xbytes, ubytes;                // buffer-resource extents (< 2^31)
+  int n_ptiles, per_xcd;
+  int relu;
+};
+
+__global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: the DMA M0 values stay scalar
+  const int wm = wave & 1, wn = wave >> 1;
+  // consecutive tile blocks on one XCD (they read overlapping image rows: L2 reuse; speed only)
+  const int pt = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
+  if (pt >= a.n_ptiles) return;  // whole workgroup, before any barrier
+  const int p0 = pt * kTiles;
+#if __HIP_DEVICE_COMPILE__
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), 0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
+#endif
+  lds_f32* lds3 = (lds_f32*)(lds);
+  float* const vbuf = lds;                // [2][5][kTiles][kVS]
+  lds_f32* const uring = lds3 + 2 * kVBuf;  // [2][kK][kCh], swizzled units
+
+  // ---- U ring: point ab into slot ab & 1 (pieces q = wave, wave + 12 of the slot)
+  int uoff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave + kWaves * i, U = (q < kUPieces ? q : 0) * 64 + lane;
+    const int row = U / 12, u = (U - row * 12) ^ swz(row);
+    uoff[i] = (row * kCh + 4 * u) * 4;
+  }
+  auto issue_u = [&](int ab) {
+#if __HIP_DEVICE_COMPILE__
+    lds_f32* st = uring + (ab & 1) * kUSlot;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (wave + kWaves * i < kUPieces)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + (wave + kWaves * i) * 256), 16, uoff[i],
+                                                 ab * kUSlot * 4, 0, 0);
+#endif
+  };
+
+  // ---- the V build slot of this thread: tile bt, channels 2 bc, 2 bc + 1 (phase row rh, floats 2 bc % 12
+  // .. +1 of the 12-float (rw, c) run)
+  const int bt = tid / 24, bc = tid - bt * 24, rh = (2 * bc) / 12, bf2 = 2 * bc - rh * 12;
+  const int bp = p0 + bt;
+  const bool bval = bp < a.P;
+  int btj = 0, bti = 0, bn = 0;
+  if (bval) {
+    btj = bp % a.tx;
+    const int pq = bp / a.tx;
+    bti = pq % a.ty;
+    bn = pq / a.ty;
+  }
+  const int row0 = bti * kPitch + rh;               // image row of u = 0 (this slot's phase row)
+  const int col0 = btj * kPitch * 3 + bf2;          // float of v = 0 inside the row
+  const int xoff = ((bn * a.Hin + row0) * a.rowf + col0) * 4;
+  // X'[u][v] (2 channels): image row 12 ti + 4u + rh, floats (12 tj + 4v) * 3 + bf2 .. +1 (zero outside)
+  auto load_x = [&](int u, int v) -> f32x2 {
+    f32x2 d = {0.f, 0.f};
+#if __HIP_DEVICE_COMPILE__
+    const int o = col0 + 12 * v;
+    const int so = (kPh * u * a.rowf + 12 * v) * 4;
+    if (bval && row0 + kPh * u < a.Hin) {
+      if (o + 2 <= a.rowf)
+        d = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, xoff, so, 0));
+      else if (o < a.rowf)
+        d.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff, so, 0));
+    }
+#endif
+    return d;
+  };
+  f32x2 t[kN5];
+  auto t_zero = [&]() {
+#pragma unroll
+    for (int v = 0; v < kN5; ++v) t[v] = f32x2{0.f, 0.f};
+  };
+  // t = B^T d over u, then V = t B over v: the fmaf expressions and order of conv1_wino_band_kernel
+  auto t_add = [&](auto A, auto Uc, const f32x2 (&d)[kN5]) {
+    constexpr int av = decltype(A)::value, u = decltype(Uc)::value;
+    constexpr float c = w33::kBT[av][u];
+    if constexpr (c != 0.f)
+#pragma unroll
+      for (int v = 0; v < kN5; ++v) {
+        t[v].x = __builtin_fmaf(c, d[v].x, t[v].x);
+        t[v].y = __builtin_fmaf(c, d[v].y, t[v].y);
+      }
+  };
+  auto v_store = [&](int buf) {
+    float* vb = vbuf + buf * kVBuf + bt * kVS + 2 * bc;
+    sfor<0, kN5>([&](auto Bc) {
+      constexpr int b = decltype(Bc)::value;
+      f32x2 s = {0.f, 0.f};
+      sfor<0, kN5>([&](auto Vc) {
+        constexpr int v = decltype(Vc)::value;
+        constexpr float c = w33::kBT[b][v];
+        if constexpr (c != 0.f) {
+          s.x = __builtin_fmaf(c, t[v].x, s.x);
+          s.y = __builtin_fmaf(c, t[v].y, s.y);
+        }
+      });
+      *reinterpret_cast<f32x2*>(vb + b * kTiles * kVS) = s;
+    });
+  };
+
+  // ---- MFMA fragments (v_mfma_f32_16x16x4_f32): A[row = lane & 15][k = lane >> 4], B[k = lane >> 4][col =
+  // lane & 15]; k-step 4g + i uses channel 16g + 4(lane >> 4) + i (one ds_read_b128 per operand per g)
+  const int r16 = lane & 15, h4 = lane >> 4;
+  const int a_off = (wm * 16 + r16) * kVS + 4 * h4;
+  const int brow = wn * 16 + r16;
+  int b_off[3];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) b_off[g] = brow * kCh + 4 * ((4 * g + h4) ^ swz(brow));
+  f32x4 Y[9];  // Y[q]: output q of the block's 4 accumulator rows
+#pragma unroll
+  for (int q = 0; q < 9; ++q) Y[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: U of point 0 in flight, V_0 built and stored
+  issue_u(0);
+  t_zero();
+  sfor<0, kN5>([&](auto Uc) {
+    constexpr int u = decltype(Uc)::value;
+    if constexpr (w33::kBT[0][u] != 0.f) {
+      f32x2 d[kN5];
+#pragma unroll
+      for (int v = 0; v < kN5; ++v) d[v] = load_x(u, v);
+      t_add(std::integral_constant<int, 0>{}, Uc, d);
+    }
+  });
+  v_store(0);
+
+  sfor<0, kN5>([&](auto Ac) {
+    constexpr int av = decltype(Ac)::value;
+    constexpr int an = av + 1 < kN5 ? av + 1 : 0;  // the a-step whose V this one builds (when av < 4)
+    const float* vb = vbuf + (av & 1) * kVBuf;
+    if constexpr (av + 1 < kN5) t_zero();
+    sfor<0, kN5>([&](auto Bc) {
+      constexpr int b = decltype(Bc)::value, ab = av * kN5 + b;
+      // U_ab landed (this wave's DMA: vmcnt; everyone's: the barrier), V_a stored (ds: barrier)
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (ab + 1 < kPts) issue_u(ab + 1);  // the slot read at point ab - 1: free after the barrier
+      // X' of V_{a+1}'s u = b row: issued now, consumed after this point's MFMAs
+      constexpr bool part = av + 1 < kN5 && w33::kBT[an][b] != 0.f;
+      f32x2 d[kN5];
+      if constexpr (part)
+#pragma unroll
+        for (int v = 0; v < kN5; ++v) d[v] = load_x(b, v);
+      const float* vp = vb + b * kTiles * kVS + a_off;
+      const float* up = reinterpret_cast<const float*>(lds + 2 * kVBuf + (ab & 1) * kUSlot);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const f32x4 af = *reinterpret_cast<const f32x4*>(vp + 16 * g);
+        const f32x4 bf = *reinterpret_cast<const f32x4*>(up + b_off[g]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[i], acc, 0, 0, 0);
+      }
+      // fold: Y[i][j] += A^T[i][a] A^T[j][b] M_ab (compile-time coefficients; zero ones skipped)
+      sfor<0, 9>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        constexpr float c = w33::kAT[q / 3][av] * w33::kAT[q % 3][b];
+        if constexpr (c != 0.f)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) Y[q][i] = __builtin_fmaf(c, acc[i], Y[q][i]);  // scalar v_fma_f32
+      });
+      if constexpr (part) t_add(std::integral_constant<int, an>{}, Bc, d);
+    });
+    // V_{a+1} into the other buffer (last read in a-step a - 1, before this a-step's first barrier);
+    // published by the barrier of point (a + 1, 0)
+    if constexpr (av + 1 < kN5) v_store((av + 1) & 1);
+  });
+
+  // ---- epilogue: per output position q, bias + ReLU into an LDS image [32 tiles][96 filters], then
+  // 16-B row-contiguous stores. D layout: lane holds col = lane & 15 (filter), rows 4 (lane >> 4) + i.
+  const int f = wn * 16 + r16;
+  const float bv = a.bias ? a.bias[f] : 0.f;
+  const OutView o = a.out;
+  float* tr = lds;
+  const int st = tid / (kK / 4), sq = tid - st * (kK / 4);  // this thread's store: tile st, filters 4 sq .. +3
+  const int sp = p0 + st;
+  int sn = 0, sti = 0, stj = 0;
+  if (sp < a.P) {
+    stj = sp % a.tx;
+    const int pq = sp / a.tx;
+    sti = pq % a.ty;
+    sn = pq / a.ty;
+  }
+  __syncthreads();  // every wave's last fragment reads are done: the LDS is scratch now
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = Y[q][i] + bv;
+      if (a.relu) v = fmaxf(v, 0.f);
+      tr[(wm * 16 + 4 * h4 + i) * kOS + f] = v;
+    }
+    __syncthreads();
+    const int oy = sti * 3 + q / 3, ox = stj * 3 + q % 3;
+    if (sp < a.P && oy < a.Ho && ox < a.Wo)
+      *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(sn * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
+                                o.c_off + 4 * sq) = *reinterpret_cast<const f32x4*>(tr + st * kOS + 4 * sq);
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+bool conv1_fused_eligible(const Conv1WinoPlan& w, const OutView& out) {
+  return w.K == kK && w.W * 3 >= 4 && out.Cb % 4 == 0 && out.c_off % 4 == 0 &&
+         static_cast<long>(w.N) * w.Hin * w.W * 3 * 4 < (1L << 31);
+}
+
+hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out, bool relu,
+                       hipStream_t s) {
+  if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
+  if (!conv1_fused_eligible(w, out)) return hipErrorInvalidValue;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_fused_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  Conv1FusedArgs a{};
+  a.x = x;
+  a.U = U;
+  a.bias = bias;
+  a.out = out;
+  a.P = w.P;
+  a.ty = w.ty;
+  a.tx = w.tx;
+  a.Ho = w.H1;
+  a.Wo = w.W1;
+  a.Hin = w.Hin;
+  a.rowf = w.W * 3;
+  a.xbytes = static_cast<int>(static_cast<long>(w.N) * w.Hin * w.W * 3 * 4);
+  a.ubytes = kPts * kK * kCh * 4;
+  a.n_ptiles = (w.P + kTiles - 1) / kTiles;
+  a.per_xcd = (a.n_ptiles + 7) / 8;
+  a.relu = relu ? 1 : 0;
+  conv1_fused_kernel<<<static_cast<unsigned>(a.per_xcd * 8), kNT, kLds, s>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace anx::hip

@@ -18,7 +18,8 @@ Names and values:
   default: a tile that computes all the pool1 rows its conv2 window needs runs pool1 inside the
   Winograd input transform; 0: the pool1 kernel and the window buffer); ``conv1_sub`` / ``conv2_sub``
   (images per Conv1 / Conv2 transform + GEMM launch pair inside a fused forward; 0 = whole launch: a
-  small sub-chunk rewrites the V workspace in place, inside the Infinity Cache).
+  small sub-chunk rewrites the V workspace in place, inside the Infinity Cache); ``conv1_fused`` (1: Conv1
+  as one kernel, the polyphase input transform built in LDS inside the Winograd GEMM).
 """
 from __future__ import annotations
 
@@ -28,7 +29,8 @@ from .. import _native as nat
 
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
-         "bf16_lrn_tile", "bf16_fc", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub")
+         "bf16_lrn_tile", "bf16_fc", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
+         "conv1_fused")
 
 
 def knob_value(name: str, value) -> int:
