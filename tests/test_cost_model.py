@@ -104,3 +104,30 @@ def test_readme_scaling_section_is_the_model():
     m = re.search(r"<!-- scaling-model:begin -->\n(.*?)<!-- scaling-model:end -->", text, re.S)
     assert m, "README lacks the generated scaling section"
     assert m.group(1) == render()
+
+
+@pytest.mark.parametrize("np_,batch,rw", [(8, 1024, 1), (8, 1024, 2), (4, 256, 2), (2, 64, 2), (4, 6, 4)])
+@pytest.mark.parametrize("src", ["root", "local"])
+def test_model_bytes_are_the_runtime_schedule(np_, batch, rw, src):
+    """The model's root egress / ingress and busiest-rank halo bytes equal the sums over the native V5
+    runtime's own transfer schedule (libanx_dist record-only schedule; no GPU)."""
+    from anx.parallel.workloads import native_schedule
+    sched = native_schedule(np_, batch, rw, input_source=src)
+    sent, recv = {}, {}
+    egress = ingress = 0
+    for l in sched:
+        ph, edge, w, h = l.split(" ")[:4]
+        s, d = (int(v) for v in edge.split("->"))
+        if s == d:
+            continue
+        b = int(w[2:]) * int(h[2:])
+        if ph.startswith("scatter"):
+            egress += b
+        elif ph.startswith("gather"):
+            ingress += b
+        else:
+            sent[s] = sent.get(s, 0) + b
+            recv[d] = recv.get(d, 0) + b
+    m = cost.step("v5", np_, batch, rw, input_source=src)["bytes"]
+    assert m["root_egress"] == egress and m["root_ingress"] == ingress
+    assert m["max_rank_halo"] == max([0, *sent.values(), *recv.values()])
