@@ -104,6 +104,9 @@ def parse():
     ap.add_argument("--input-source", default="local", choices=["root", "local"],
                     help="dp / v5: local = per-rank (device-resident) data; root = rank 0 scatters the batch every step")
     ap.add_argument("--no-gather", action="store_true", help="dp: leave outputs on their ranks")
+    ap.add_argument("--root-batch", type=int, default=-1,
+                    help="dp, local input, N>1: images rank 0 computes per step while it also receives the gather "
+                         "(-1 = the cost model's shed share on GPUs / off on the CPU rehearsal, 0 = off, >0 = that many)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu = gloo rehearsal (tests only)")
     ap.add_argument("--graph", type=int, default=0,
                     help="dp, 1 GPU: the step as one captured HIP graph replayed each step (1), eager (0, default; "
@@ -249,8 +252,16 @@ def main():
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
 
     use_graph = False
+    root_b = B
+    if wl is None and a.model == "blocks" and world > 1 and a.input_source == "local" and not a.no_gather:
+        if a.root_batch > 0:
+            root_b = min(B, a.root_batch)
+        elif a.root_batch < 0 and cuda:
+            from anx.parallel import cost
+            root_b = cost.dp_root_batch(world, B)
     if wl is None:
         cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather,
+                             root_batch=root_b,
                              prefetch=not a.no_prefetch,
                              async_lanes=not a.joined_lanes and a.graph == 0
                              and (a.full_lanes if a.model == "full" else a.lanes) > 1)
@@ -334,7 +345,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ms = el * 1e3 / a.steps
-    per_step = B if wl is not None else B * world  # images per step over the whole job
+    per_step = B if wl is not None else B * (world - 1) + root_b  # images per step over the whole job
     imgs = per_step * a.steps / el
     phases = wl.phase_ms() if wl is not None else None
 
@@ -370,6 +381,9 @@ def main():
                 if world > 1 else "single GPU"
             rot = pipe.inputs or []
             extra = {"input_source": a.input_source, "lanes": a.lanes, "hip_graph": use_graph, "knobs": a.knob,
+                     "batch_per_gpu": B, "root_batch": root_b,
+                     "root_batch_note": ("rank 0 sheds the share its gather ingest costs it (cost model "
+                                         "dp_root_batch; tools/probe_ingest.py)") if root_b != B else None,
                      "input_batches_rotated": len(rot) or 1,
                      "input_bytes_rotated": sum(t.numel() * 4 for t in rot) or pipe._xb[0].numel() * 4,
                      "lane_sync": ("free-running lanes (%s start), per-lane gathers (forward_async)"

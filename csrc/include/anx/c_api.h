@@ -51,6 +51,8 @@ int anx_cost_step(int workload, int np, int batch, int row_ways, int input_sourc
                   char* buf, size_t cap);
 int anx_cost_pick_row_ways(int workload, int np, int batch, int input_source, int mode, const char* overrides,
                            int* row_ways);
+/* dp: images rank 0 computes per step when every peer has `batch` (its ingest slowdown shed). */
+int anx_cost_dp_root_batch(int np, int batch, const char* overrides, int* root_batch);
 
 /* ---- engine (Blocks 1-2) ---- */
 /* Hybrid batch x rows plan (anx/plan.hpp make_hybrid_plan). Per rank r (arrays of np):

@@ -11,8 +11,9 @@
 //             in whole-image equivalents, at the measured single-GPU rate for that many images
 //             (CostParams::rate, interpolated in log2(images)); row tiles of the per-layer split pay
 //             split_penalty (pool1 not fused into the Conv2 input transform, window materialised);
-//             the root's compute slows by ingest_slowdown while it receives the gather (measured on
-//             one GPU by tools/probe_ingest.py).
+//             the root's compute slows by ingest_slowdown (per 155 MB received per step) while it
+//             receives the gather (measured on one GPU by tools/probe_ingest.py); in dp the root then
+//             takes a proportionally smaller share of the images (dp_root_shed).
 //   egress    root -> peers (the scatter of a root-held batch): each peer's bytes over its own xGMI
 //             link, all links in parallel: max over peers / xgmi_gbps.
 //   ingress   peers -> root (the output gather): likewise.
@@ -50,7 +51,11 @@ struct CostParams {
   double h2d_gbps = 56.7;        // one GPU's host link, measured (profiles/r03_v4_chunks.jsonl)
   double d2h_gbps = 56.7;        // assumed equal to H2D
   double host_gbps = 400.0;      // host memory feeding all H2D streams at once (assumed)
-  double ingest_slowdown = 0.0;  // root compute slowdown while receiving the gather (tools/probe_ingest.py)
+  // root compute slowdown while it receives the gather, per 155.06 MB per step (the dp N=8 volume),
+  // linear in the bytes received: 0.15 measured by tools/probe_ingest.py (the bench step beside a
+  // 155 MB/step receive-side copy: +11 % on all CUs, +18 % on 64 workgroups; profiles/r04_probe_ingest.jsonl)
+  double ingest_slowdown = 0.15;
+  int dp_root_shed = 1;          // dp: the root computes B / (1 + its slowdown) images (even), the peers B
   double phase_latency_ms = 0.02;  // per transport phase (RCCL group launch / flag round trip)
   double v4_fill = 0.1;          // exposed share of V4's non-bottleneck stages (see above)
   int v5_chunks = 0;             // V5 halo chunks (0 = the runtime's auto rule)
@@ -67,12 +72,14 @@ struct StepCost {
   double root_egress_bytes = 0, root_ingress_bytes = 0, max_peer_egress_bytes = 0, max_peer_ingress_bytes = 0;
   double max_rank_h2d_bytes = 0, max_rank_d2h_bytes = 0, total_h2d_bytes = 0, max_rank_halo_bytes = 0;
   double max_rank_work = 0;  // whole-image equivalents of the busiest rank
+  int root_batch = 0;        // images the root computes per step (dp: after shedding)
+  int images = 0;            // images per step over all ranks
   std::string bound;         // compute | egress | ingress | io | halo | h2d | d2h | host
   std::string json() const;
 };
 
-// dp: `batch` = images per GPU (weak scaling; a step moves np x batch images); v4 / v5: the global batch
-// (strong scaling). row_ways: as make_hybrid_plan (0 = batch first) or -1 = pick_row_ways.
+// dp: `batch` = images per GPU (weak scaling; a step moves np x batch images, less the root's shed
+// share); v4 / v5: the global batch (strong scaling). row_ways: as make_hybrid_plan (0 = batch first) or -1 = pick_row_ways.
 StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource src, Decomp mode,
                     const CostParams& p = CostParams{}, const BlockSpec& b1 = kBlock1, const BlockSpec& b2 = kBlock2,
                     int H = kInH, int W = kInW);
@@ -80,6 +87,10 @@ StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource sr
 // CostParams from "name=value;..." overrides of the defaults (names: the fields above; rate=IMG:IPS,IMG:IPS,...
 // replaces the rate table). Throws std::invalid_argument for an unknown name or a malformed value.
 CostParams cost_params(const std::string& overrides);
+
+// dp: images the root computes per step when every rank has `batch` (its ingest slowdown shed; even,
+// so two lanes split it equally); = batch when shedding is off or np == 1.
+int dp_root_batch(int np, int batch, const CostParams& p = CostParams{}, int H = kInH, int W = kInW);
 
 // The row split with the lowest modelled step over the divisors r of np (ties: fewer row ways). For V4
 // this is the batch split whenever the step is H2D-bound (a row split adds the rows' receptive-field

@@ -585,3 +585,10 @@ extern "C" int anx_cost_pick_row_ways(int workload, int np, int batch, int input
     return 0;
   });
 }
+
+extern "C" int anx_cost_dp_root_batch(int np, int batch, const char* overrides, int* root_batch) {
+  return guarded("anx_cost_dp_root_batch", [&] {
+    *root_batch = anx::dp_root_batch(np, batch, anx::cost_params(overrides ? overrides : ""));
+    return 0;
+  });
+}

@@ -50,12 +50,12 @@ std::string StepCost::json() const {
       "\"egress_ms\": %.4f, \"ingress_ms\": %.4f, \"halo_ms\": %.4f, \"halo_exposed_ms\": %.4f, \"h2d_ms\": %.4f, "
       "\"d2h_ms\": %.4f, \"bytes\": {\"root_egress\": %.0f, \"root_ingress\": %.0f, \"max_peer_egress\": %.0f, "
       "\"max_peer_ingress\": %.0f, \"max_rank_h2d\": %.0f, \"max_rank_d2h\": %.0f, \"total_h2d\": %.0f, "
-      "\"max_rank_halo\": %.0f}, \"max_rank_work_images\": %.3f}",
+      "\"max_rank_halo\": %.0f}, \"max_rank_work_images\": %.3f, \"root_batch\": %d, \"images\": %d}",
       wl_name(wl), np, batch, row_ways, groups, src == InputSource::Local ? "local" : "root",
       mode == Decomp::PerLayer ? "per_layer" : "overlap", step_ms, images_per_s, bound.c_str(), compute_ms, egress_ms,
       ingress_ms, halo_ms, halo_exposed_ms, h2d_ms, d2h_ms, root_egress_bytes, root_ingress_bytes, max_peer_egress_bytes,
       max_peer_ingress_bytes, max_rank_h2d_bytes, max_rank_d2h_bytes, total_h2d_bytes, max_rank_halo_bytes,
-      max_rank_work);
+      max_rank_work, root_batch, images);
   return b;
 }
 
@@ -101,6 +101,7 @@ CostParams cost_params(const std::string& overrides) {
     else if (k == "ingest_slowdown") p.ingest_slowdown = x;
     else if (k == "phase_latency_ms") p.phase_latency_ms = x;
     else if (k == "min_step_ms") p.min_step_ms = x;
+    else if (k == "dp_root_shed") p.dp_root_shed = static_cast<int>(x);
     else if (k == "v4_fill") p.v4_fill = x;
     else if (k == "v5_chunks") p.v5_chunks = static_cast<int>(x);
     else throw std::invalid_argument("cost model: unknown parameter '" + k + "'");
@@ -108,6 +109,19 @@ CostParams cost_params(const std::string& overrides) {
   if (p.xgmi_gbps <= 0 || p.h2d_gbps <= 0 || p.d2h_gbps <= 0 || p.host_gbps <= 0)
     throw std::invalid_argument("cost model: link rates must be positive");
   return p;
+}
+
+namespace {
+constexpr double kProbeBytes = 155.06e6;  // the probe's receive volume per step (7 x 128 x 173,056 B)
+double root_slowdown(const CostParams& p, double ingress_bytes) { return p.ingest_slowdown * ingress_bytes / kProbeBytes; }
+}  // namespace
+
+int dp_root_batch(int np, int batch, const CostParams& p, int H, int W) {
+  if (np <= 1 || !p.dp_root_shed) return batch;
+  const BlocksDims d = blocks_dims(H, W);
+  const double ingress = static_cast<double>(np - 1) * batch * d.Hp2 * d.Wp2 * d.C2 * 4;
+  const int b0 = 2 * static_cast<int>(std::lround(batch / (1 + root_slowdown(p, ingress)) / 2));
+  return std::max(2, std::min(batch, b0));
 }
 
 StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource src, Decomp mode, const CostParams& p,
@@ -123,6 +137,7 @@ StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource sr
   if (wl == Workload::V4) mode = Decomp::Overlap;
   c.mode = mode;
   c.row_ways = row_ways;
+  const int root_b = wl == Workload::DP ? dp_root_batch(np, batch, p, H, W) : batch;
   const int global = wl == Workload::DP ? np * batch : batch;
   HybridPlan hp;
   if (!make_hybrid_plan(H, W, np, global, row_ways, mode, hp, b1, b2))
@@ -137,7 +152,10 @@ StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource sr
   double compute_max = 0, root_compute = 0;
   for (int r = 0; r < np; ++r) {
     const TilePlan& t = hp.tile(r);
-    const int n = t.out.empty() ? 0 : hp.images[hp.group_of[r]].size();
+    int n = t.out.empty() ? 0 : hp.images[hp.group_of[r]].size();
+    if (wl == Workload::DP && r == 0) n = root_b;  // the root's shed share
+    if (r == 0) c.root_batch = n;
+    c.images += n;
     if (n == 0) continue;
     const bool whole = t.in.size() == H && t.out.size() == d.Hp2;
     const double eq = n * (p.stage1_share * t.c1.size() / d.H1 + (1 - p.stage1_share) * t.c2.size() / d.H2);
@@ -181,7 +199,7 @@ StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource sr
   c.egress_ms = c.max_peer_egress_bytes / link;
   c.ingress_ms = c.max_peer_ingress_bytes / link;
   if (np > 1 && c.root_ingress_bytes > 0)  // the root computes while its links receive the gather
-    c.compute_ms = std::max(compute_max, root_compute * (1 + p.ingest_slowdown));
+    c.compute_ms = std::max(compute_max, root_compute * (1 + root_slowdown(p, c.root_ingress_bytes)));
   if (wl == Workload::V4) {
     c.h2d_ms = std::max(c.max_rank_h2d_bytes / (p.h2d_gbps * 1e6), c.total_h2d_bytes / (p.host_gbps * 1e6));
     c.d2h_ms = c.max_rank_d2h_bytes / (p.d2h_gbps * 1e6);
@@ -211,7 +229,7 @@ StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource sr
               : c.egress_ms > 0 ? (c.egress_ms >= c.ingress_ms ? "egress" : "ingress")
                                 : "ingress";
   }
-  c.images_per_s = c.step_ms > 0 ? global / c.step_ms * 1e3 : 0;
+  c.images_per_s = c.step_ms > 0 ? c.images / c.step_ms * 1e3 : 0;
   return c;
 }
 
@@ -268,9 +286,9 @@ std::string model_curve_json(Workload wl, const std::vector<int>& nps, int batch
   char b[1024];
   std::snprintf(b, sizeof b,
                 "], \"params\": {%s\"xgmi_gbps\": %g, \"h2d_gbps\": %g, \"d2h_gbps\": %g, \"host_gbps\": %g, "
-                "\"ingest_slowdown\": %g, \"stage1_share\": %g, \"split_penalty\": %g, \"phase_latency_ms\": %g, "
+                "\"ingest_slowdown\": %g, \"dp_root_shed\": %d, \"stage1_share\": %g, \"split_penalty\": %g, \"phase_latency_ms\": %g, "
                 "\"v4_fill\": %g, \"v5_chunks\": %d}}",
-                rate.c_str(), p.xgmi_gbps, p.h2d_gbps, p.d2h_gbps, p.host_gbps, p.ingest_slowdown, p.stage1_share, p.split_penalty,
+                rate.c_str(), p.xgmi_gbps, p.h2d_gbps, p.d2h_gbps, p.host_gbps, p.ingest_slowdown, p.dp_root_shed, p.stage1_share, p.split_penalty,
                 p.phase_latency_ms, p.v4_fill, p.v5_chunks);
   return s + b;
 }

@@ -38,7 +38,8 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 using lds_f32 = __attribute__((address_space(3))) float;
 using lds_void = __attribute__((address_space(3))) void;
 
-constexpr int kPh = 4, kCh = 48, kN5 = 5, kPts = 25, kPitch = 12;
+[[maybe_unused]] constexpr int kPh = 4;
+constexpr int kCh = 48, kN5 = 5, kPts = 25, kPitch = 12;
 constexpr int kK = 96;                     // filters per workgroup (all of Conv1's)
 constexpr int kTiles = 32;                 // tiles per workgroup
 constexpr int kWaves = 12, kNT = 64 * kWaves;
@@ -93,7 +94,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 #endif
   lds_f32* lds3 = (lds_f32*)(lds);
   float* const vbuf = lds;                // [2][5][kTiles][kVS]
-  lds_f32* const uring = lds3 + 2 * kVBuf;  // [2][kK][kCh], swizzled units
+  [[maybe_unused]] lds_f32* const uring = lds3 + 2 * kVBuf;  // [2][kK][kCh], swizzled units
 
   // ---- U ring: point ab into slot ab & 1 (pieces q = wave, wave + 12 of the slot)
   int uoff[2];
@@ -128,7 +129,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   }
   const int row0 = bti * kPitch + rh;               // image row of u = 0 (this slot's phase row)
   const int col0 = btj * kPitch * 3 + bf2;          // float of v = 0 inside the row
-  const int xoff = ((bn * a.Hin + row0) * a.rowf + col0) * 4;
+  [[maybe_unused]] const int xoff = ((bn * a.Hin + row0) * a.rowf + col0) * 4;
   // X'[u][v] (2 channels): image row 12 ti + 4u + rh, floats (12 tj + 4v) * 3 + bf2 .. +1 (zero outside)
   auto load_x = [&](int u, int v) -> f32x2 {
     f32x2 d = {0.f, 0.f};

@@ -65,6 +65,7 @@ _SIGS = {
     "anx_cost_curve": (_I, [_I, C.POINTER(_I), _I, _I, _I, _I, _I, C.c_char_p, C.c_char_p, _SZ]),
     "anx_cost_step": (_I, [_I, _I, _I, _I, _I, _I, C.c_char_p, C.c_char_p, _SZ]),
     "anx_cost_pick_row_ways": (_I, [_I, _I, _I, _I, _I, C.c_char_p, C.POINTER(_I)]),
+    "anx_cost_dp_root_batch": (_I, [_I, _I, C.c_char_p, C.POINTER(_I)]),
     "anx_engine_create": (_I, [C.POINTER(_P), C.POINTER(BlockC), C.POINTER(BlockC), _I, _I, _P, _P, _P, _P, _I, _I]),
     "anx_engine_destroy": (_I, [_P]),
     "anx_engine_forward": (_I, [_P, _P, _I, _P, _P]),

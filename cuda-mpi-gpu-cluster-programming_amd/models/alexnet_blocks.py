@@ -249,7 +249,7 @@ class AlexNetBlocks:
         streams = [self._own_stream, *self._lane_streams]
         engines = [self, *self._lanes]
         plan = full_plan(self.H, self.W, self.b1, self.b2)
-        bounds = [N * i // L for i in range(L + 1)]
+        bounds = self.lane_bounds(N)
         fresh = all(st.query() for st in streams)
         cur = torch.cuda.current_stream(self.device)
         ev = None
@@ -272,6 +272,13 @@ class AlexNetBlocks:
                 if on_lane is not None:
                     on_lane(i, lo, hi)
         return out
+
+    def lane_bounds(self, n: int) -> list[int]:
+        """Image boundaries [0, ..., n] of the lanes :meth:`forward_async` runs ``n`` images on."""
+        L = 1 + len(self._lanes)
+        if L == 1 or n < L * LANE_MIN or not self.is_cuda:
+            return [0, n]
+        return [n * i // L for i in range(L + 1)]
 
     def join(self) -> None:
         """Make the current stream wait for every lane of :meth:`forward_async`."""

@@ -11,7 +11,7 @@ The same model picks the runtimes' default row split (``pick_row_ways``): the V4
 it natively, so what ``python -m anx plan --model`` prints is what they run.
 
 Overrides: ``"name=value;..."`` over the defaults (``xgmi_gbps``, ``h2d_gbps``, ``d2h_gbps``,
-``host_gbps``, ``ingest_slowdown``, ``stage1_share``, ``split_penalty``, ``phase_latency_ms``,
+``host_gbps``, ``ingest_slowdown`` (per 155 MB received per step), ``dp_root_shed``, ``stage1_share``, ``split_penalty``, ``phase_latency_ms``,
 ``v4_fill``, ``v5_chunks``; ``rate=IMAGES:IMG_PER_S,...`` replaces the throughput table).
 """
 from __future__ import annotations
@@ -58,6 +58,14 @@ def pick_row_ways(workload: str, np_: int, batch: int, input_source: str = "loca
     r = C.c_int()
     nat.call("anx_cost_pick_row_ways", WORKLOADS[workload], np_, batch, SOURCES[input_source], MODES[mode],
              _ov(overrides), C.byref(r))
+    return r.value
+
+
+def dp_root_batch(np_: int, batch: int, overrides=None) -> int:
+    """dp: the images rank 0 computes per step while each peer computes ``batch`` -- the root's share
+    shrunk by its modelled slowdown while it receives the gather (ingest_slowdown x bytes / 155 MB)."""
+    r = C.c_int()
+    nat.call("anx_cost_dp_root_batch", np_, batch, _ov(overrides), C.byref(r))
     return r.value
 
 

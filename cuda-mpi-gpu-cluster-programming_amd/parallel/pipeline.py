@@ -21,6 +21,15 @@ batch scale and MI355X-first:
   slice from its own stream; a lane waits, on its stream, for the gather that read the same output
   buffer two steps earlier. ``drain()`` joins the lanes.
 
+``root_batch`` (local input, dp): rank 0 computes only that many images per step while every peer
+computes ``batch_per_rank`` -- the root also receives the whole gather, and that receive costs it
+compute (11-18 % at the 8-GPU volume, tools/probe_ingest.py), so it sheds the share the cost model
+prices (:func:`anx.parallel.cost.dp_root_batch`). The reference's root likewise gets its own
+Scatterv count (final_project/v4_mpi_cuda/src/main_mpi_cuda.cpp:52-75, counts per rank). Unequal
+slices cannot use ``gather``, so each segment goes point to point: peers ``isend`` their segment,
+the root ``irecv``s every peer's segment in one batch into ``y_global[r, seg]`` and copies its own
+slice into ``y_global[0]`` (rows past ``root_batch`` of ``y_global[0]`` are unused).
+
 ``inputs`` (local input only): a list of input batches used round-robin, step k computing
 ``inputs[k % len(inputs)]`` — a benchmark streams distinct data through the engine instead of one
 cache-resident batch.
@@ -58,6 +67,7 @@ class PipelineConfig:
     gather: bool = True    # outputs are gathered to rank 0
     prefetch: bool = False  # scatter step k+1 while step k computes (double-buffered x and y)
     async_lanes: bool = False  # free-running model lanes (forward_async) with per-lane gathers; local input only
+    root_batch: int | None = None  # images rank 0 computes per step (local input; None = batch_per_rank)
 
 
 class ScatterComputeGather:
@@ -71,7 +81,17 @@ class ScatterComputeGather:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         B = cfg.batch_per_rank
-        self.splits = micro_splits(B, cfg.micro if self.world > 1 else 1)
+        rb = B if cfg.root_batch is None or self.world == 1 else cfg.root_batch
+        if rb != B and (cfg.scatter or not 0 < rb <= B):
+            raise ValueError(f"root_batch {rb} needs local input and 0 < root_batch <= batch_per_rank {B}")
+        self.root_batch, self.shed = rb, rb != B
+        M = cfg.micro if self.world > 1 else 1
+        if self.shed and min(M, rb) != min(M, B):
+            raise ValueError(f"root_batch {rb} must give the root as many micro-batches ({M}) as its peers")
+        self.peer_splits = micro_splits(B, M)  # a peer's micro-batches (the root receives these)
+        if self.rank == 0:
+            B = rb
+        self.splits = micro_splits(B, M)
         self.prefetch = cfg.prefetch and self.world > 1
         nbuf = 2 if self.prefetch else 1
         self._xb = [torch.empty((B, *in_shape), device=self.device) for _ in range(nbuf)]
@@ -83,13 +103,31 @@ class ScatterComputeGather:
         # single rank: no scatter/gather buffers at all (the V3 shape: compute on resident data)
         root = self.rank == 0 and self.world > 1
         self.x_global = torch.empty((self.world, B, *in_shape), device=self.device) if root and cfg.scatter else None
-        self.y_global = torch.empty((self.world, B, *out_shape), device=self.device) if root and cfg.gather else None
+        self.y_global = (torch.empty((self.world, cfg.batch_per_rank, *out_shape), device=self.device)
+                         if root and cfg.gather else None)
         self.async_lanes = cfg.async_lanes and not cfg.scatter and hasattr(model, "forward_async")
         if self.async_lanes and self.world > 1 and cfg.gather and nbuf < 2:  # a gather may still read y[k-1]
             self._yb.append(torch.empty_like(self._yb[0]))
             self._gather_pending.append(None)
         self._lane_gathers = [dict() for _ in self._yb]  # per output buffer: lane -> gather work reading it
         self.inputs: list | None = None  # local input only: batches used round-robin (see module doc)
+
+    def _gather(self, y, seg: int, lo: int, hi: int):
+        """Collect micro-batch / lane segment ``seg`` (this rank's rows [lo, hi) of ``y``) at rank 0."""
+        root = self.rank == 0
+        if not self.shed:
+            dst = [self.y_global[r, lo:hi] for r in range(self.world)] if root else None
+            return dist.gather(y[lo:hi], dst, dst=0, group=self.group, async_op=True)
+        if not root:
+            ops = [dist.P2POp(dist.isend, y[lo:hi], dist.get_global_rank(self.group, 0) if self.group else 0,
+                              self.group)]
+        else:
+            self.y_global[0, lo:hi].copy_(y[lo:hi])
+            plo, phi = self._peer_seg[seg]
+            ops = [dist.P2POp(dist.irecv, self.y_global[r, plo:phi],
+                              dist.get_global_rank(self.group, r) if self.group else r, self.group)
+                   for r in range(1, self.world)]
+        return _Works(dist.batch_isend_irecv(ops))
 
     def _local_input(self, default):
         if self.inputs and not self.cfg.scatter:
@@ -119,11 +157,11 @@ class ScatterComputeGather:
             for w in self._gather_pending[cur]:
                 w.wait()
         gw = []
-        for lo, hi in self.splits:
+        self._peer_seg = self.peer_splits
+        for j, (lo, hi) in enumerate(self.splits):
             self.model(x[lo:hi], out=y[lo:hi])
             if self.cfg.gather:
-                dst = [self.y_global[r, lo:hi] for r in range(self.world)] if self.rank == 0 else None
-                gw.append(dist.gather(y[lo:hi], dst, dst=0, group=self.group, async_op=True))
+                gw.append(self._gather(y, j, lo, hi))
         self._gather_pending[cur] = gw
         # Order the prefetch's read of x_global before anything the caller enqueues next (e.g. writing
         # the following batch into x_global). Enqueued after this step's compute, so it delays
@@ -145,10 +183,15 @@ class ScatterComputeGather:
 
         def on_lane(i, lo, hi):  # on lane i's stream: gather its slice as soon as it is computed
             if gather:
-                dst = [self.y_global[r, lo:hi] for r in range(self.world)] if self.rank == 0 else None
-                pend[i] = dist.gather(y[lo:hi], dst, dst=0, group=self.group, async_op=True)
+                pend[i] = self._gather(y, i, lo, hi)
 
-        self.model.forward_async(self._local_input(self.x), y, on_lane=on_lane, pre_lane=pre_lane)
+        x = self._local_input(self.x)
+        if self.shed:  # the root's lanes split fewer images: it receives the peers' lane slices
+            lanes = _lane_bounds(self.model, self.root_batch)
+            if lanes != len(peer := _lane_bounds(self.model, self.cfg.batch_per_rank, bounds=True)) - 1:
+                raise ValueError(f"root_batch {self.root_batch} runs {lanes} lanes, a peer's batch {len(peer) - 1}")
+            self._peer_seg = list(zip(peer[:-1], peer[1:]))
+        self.model.forward_async(x, y, on_lane=on_lane, pre_lane=pre_lane)
         self.y = y
         self._k += 1
 
@@ -178,17 +221,34 @@ class ScatterComputeGather:
                 self.y_global[0].copy_(self.y)
             self._k += 1
             return
-        root = self.rank == 0
         sw = self._scatter(self.x) if self.cfg.scatter else []
         gw = []
         x = self._local_input(self.x)
+        self._peer_seg = self.peer_splits
         for i, (lo, hi) in enumerate(self.splits):
             if sw:
                 sw[i].wait()
             self.model(x[lo:hi], out=self.y[lo:hi])
             if self.cfg.gather:
-                dst = [self.y_global[r, lo:hi] for r in range(self.world)] if root else None
-                gw.append(dist.gather(self.y[lo:hi], dst, dst=0, group=self.group, async_op=True))
+                gw.append(self._gather(self.y, i, lo, hi))
         for w in gw:
             w.wait()
         self._k += 1
+
+
+class _Works:
+    """The works of one batched point-to-point exchange, waited as one (a gather's work stand-in)."""
+
+    def __init__(self, works):
+        self.works = works or []
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
+def _lane_bounds(model, n: int, bounds: bool = False):
+    """How ``model.forward_async`` splits ``n`` images over its lanes: the lane count, or (bounds=True)
+    the lane boundaries [0, ..., n]."""
+    b = model.lane_bounds(n) if hasattr(model, "lane_bounds") else [0, n]
+    return b if bounds else len(b) - 1

@@ -84,16 +84,37 @@ def test_curve_contract(wl, batch):
 def test_dp_ingest_and_overrides():
     """dp at 8 GPUs: rank 0 ingests 7 x 128 images of output per step (155 MB); with slower links the
     step turns ingress-bound, with a measured ingest slowdown the root's compute grows."""
-    s = cost.step("dp", 8, 128)
+    flat = {"ingest_slowdown": 0, "dp_root_shed": 0}
+    s = cost.step("dp", 8, 128, overrides=flat)
     assert s["bytes"]["root_ingress"] == 7 * 128 * OUT_IMG
-    slow = cost.step("dp", 8, 128, overrides="xgmi_gbps=20")
+    slow = cost.step("dp", 8, 128, overrides=dict(flat, xgmi_gbps=20))
     assert slow["bound"] == "ingress" and slow["step_ms"] > s["step_ms"]
-    probe = cost.step("dp", 8, 128, overrides={"ingest_slowdown": 0.1})
-    assert probe["compute_ms"] == pytest.approx(s["compute_ms"] * 1.1, rel=1e-6)
+    probe = cost.step("dp", 8, 128, overrides={"ingest_slowdown": 0.1, "dp_root_shed": 0})
+    # the slowdown is per 155.06 MB received per step: 7 x 128 images of output is that volume
+    assert probe["compute_ms"] == pytest.approx(s["compute_ms"] * (1 + 0.1 * 7 * 128 * OUT_IMG / 155.06e6), rel=1e-3)
+    two = cost.step("dp", 2, 128, overrides={"ingest_slowdown": 0.1, "dp_root_shed": 0})
+    base2 = cost.step("dp", 2, 128, overrides=flat)
+    assert two["compute_ms"] == pytest.approx(base2["compute_ms"] * (1 + 0.1 * 128 * OUT_IMG / 155.06e6), rel=1e-3)
     r = cost.curve("dp", 128, overrides="rate=64:100000,128:200000")
     assert r["images_per_s"][0] == pytest.approx(200000, rel=1e-6)
     with pytest.raises(Exception, match="unknown parameter"):
         cost.step("dp", 2, 128, overrides="nope=1")
+
+
+def test_dp_root_shed():
+    """dp: rank 0 computes B / (1 + its ingest slowdown) images (even), the peers B; the job's images
+    per step and the modelled rate count the shed share."""
+    assert cost.dp_root_batch(1, 128) == 128
+    assert cost.dp_root_batch(8, 128) == 2 * round(128 / (1 + 0.15 * 7 * 128 * OUT_IMG / 155.06e6) / 2) == 112
+    assert cost.dp_root_batch(8, 128, overrides="dp_root_shed=0") == 128
+    assert cost.dp_root_batch(2, 128) == 126 and cost.dp_root_batch(8, 2) == 2
+    s = cost.step("dp", 8, 128)
+    assert s["root_batch"] == 112 and s["images"] == 7 * 128 + 112
+    assert s["bytes"]["root_ingress"] == 7 * 128 * OUT_IMG  # peers still send full batches
+    assert s["images_per_s"] == pytest.approx(s["images"] / s["step_ms"] * 1e3, rel=1e-3)
+    noshed = cost.step("dp", 8, 128, overrides="dp_root_shed=0")
+    assert noshed["root_batch"] == 128 and s["step_ms"] < noshed["step_ms"]
+    assert s["images_per_s"] > noshed["images_per_s"]
 
 
 def test_readme_scaling_section_is_the_model():

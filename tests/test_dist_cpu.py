@@ -114,6 +114,56 @@ def test_async_lanes_pipeline_gloo():
     torch.testing.assert_close(y.view_as(ref), ref, rtol=0, atol=0)
 
 
+def _shed_worker(rank, world, port, q, mode):
+    sys.path.insert(0, ROOT)
+    import anx  # noqa: F401
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.parallel.pipeline import PipelineConfig, ScatterComputeGather
+    from anx.utils.init import init_input
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    d = anx.blocks_dims()
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    cfg = PipelineConfig(2, micro=1, scatter=False, prefetch=mode != "plain", async_lanes=mode == "async", root_batch=1)
+    pipe = ScatterComputeGather(m, cfg, (d.H, d.W, d.C0), (d.Hp2, d.Wp2, d.C2), "cpu")
+    assert pipe.shed and pipe.x.shape[0] == (1 if rank == 0 else 2)
+    xs = init_input(2 * world, "rand", seed=2)
+    for xb in pipe._xb:
+        xb.copy_(xs[2 * rank:2 * rank + pipe.x.shape[0]])
+    for _ in range(3):
+        pipe.step()
+    pipe.drain()
+    if rank == 0:
+        q.put(pipe.y_global.clone())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["async", "prefetch", "plain"])
+def test_root_batch_shed_gloo(mode):
+    """dp with rank 0 shedding images (root_batch < batch_per_rank): the point-to-point gather puts
+    every peer's full batch and the root's smaller one where the single-process result has them."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_shed_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    y = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, ROOT)
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.utils.init import init_input
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    ref = m(init_input(2 * world, "rand", seed=2)).view(world, 2, *y.shape[2:])
+    torch.testing.assert_close(y[0, :1], ref[0, :1], rtol=0, atol=0)
+    torch.testing.assert_close(y[1:], ref[1:], rtol=0, atol=0)
+
+
 def _prefetch_changing_worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     import anx  # noqa: F401
@@ -242,3 +292,17 @@ def test_bench_contract_gloo():
               "vs_baseline", "dtype", "data", "config"):
         assert k in rec
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 4 and rec["value"] > 0
+
+
+def test_bench_root_batch_gloo():
+    """bench.py --root-batch (gloo/CPU rehearsal): the JSON counts the root's shed share in the job."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "2", "--root-batch", "1", "--device", "cpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["config"]["global_batch"] == 3 and rec["config"]["root_batch"] == 1
+    assert rec["config"]["batch_per_gpu"] == 2
