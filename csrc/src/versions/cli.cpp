@@ -58,6 +58,7 @@ struct Options {
   std::string input_source = "local";  // v5: local (device-resident, placed once) | root (scattered every step)
   int lanes = 0;                    // v5: stream lanes of a halo-free rank (0 = the runtime's default)
   int chunks = 0;                   // v5: halo pipeline chunks per step (0 = auto)
+  int row_ways = 0;                 // v5: explicit row split (ranks per row group; 0 = from --split)
   std::string peer_sync;            // v5 peer transport ordering: flags | notes ("" = default)
   bool dry_run = false;             // v5: print the transfer schedule (record-only transports, no GPU)
   std::string pipeline = "auto";    // v5: scatter / gather on a second stream (auto: on over RCCL)
@@ -73,7 +74,7 @@ struct Options {
                "           [--lrn-alpha-mode div_n|raw] [--groups 1|2] [--decomp overlap|per_layer]\n"
                "           [--iters K] [--impl mfma|direct] [--conv2-algo auto|direct|winograd]\n"
                "           [--conv1-algo auto|direct|winograd] [--transport auto|rccl|peer|loopback] [--check]\n"
-               "           [--split auto|rows|hybrid|batch] [--chunks K] [--peer-sync flags|notes]\n"
+               "           [--split auto|rows|hybrid|batch] [--row-ways R] [--chunks K] [--peer-sync flags|notes]\n"
                "           [--input-source local|root] [--lanes L]\n"
                "           [--dry-run] [--pipeline auto|on|off] [--poison]\n"
                "           [--weights DIR] [--no-json]\n",
@@ -102,6 +103,7 @@ Options parse(int argc, char** argv) {
     else if (a == "--conv1-algo") o.conv1_algo = val();
     else if (a == "--transport") o.transport = val();
     else if (a == "--split") o.split = val();
+    else if (a == "--row-ways") o.row_ways = std::atoi(val().c_str());
     else if (a == "--input-source") o.input_source = val();
     else if (a == "--lanes") o.lanes = std::atoi(val().c_str());
     else if (a == "--chunks") o.chunks = std::atoi(val().c_str());
@@ -124,6 +126,7 @@ Options parse(int argc, char** argv) {
   if (o.batch < 1) usage("--batch must be >= 1");
   if (o.split != "auto" && o.split != "rows" && o.split != "hybrid" && o.split != "batch") usage("bad --split");
   if (o.chunks < 0) usage("--chunks must be >= 0");
+  if (o.row_ways < 0) usage("--row-ways must be >= 0");
   if (o.input_source != "local" && o.input_source != "root") usage("--input-source must be local or root");
   if (o.lanes < 0) usage("--lanes must be >= 0");
   if (!o.peer_sync.empty() && o.peer_sync != "flags" && o.peer_sync != "notes") usage("--peer-sync must be flags or notes");
@@ -674,6 +677,10 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
   V5Options o;
   o.batch = N;
   o.row_ways = s.o.split == "rows" ? np : s.o.split == "hybrid" ? 0 : s.o.split == "batch" ? 1 : -1;
+  if (s.o.row_ways > 0) {
+    if (np % s.o.row_ways) throw std::invalid_argument("--row-ways must divide the rank count");
+    o.row_ways = s.o.row_ways;
+  }
   o.mode = s.o.decomp == "overlap" ? Decomp::Overlap : Decomp::PerLayer;
   o.transport = s.o.transport;
   o.chunks = s.o.chunks;

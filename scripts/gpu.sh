@@ -16,7 +16,7 @@
 #            knobs of one arm), one JSON line per run into benchab.jsonl ($BENCH_STEPS timed steps)
 #   bytes    per-kernel HBM bytes, clock and MFMA busy of the bench step (FETCH / WRITE passes)
 #   wgemm    anx_wgemm Winograd GEMM A/B at 300 and 64 images; wgpmc: its clock / MFMA busy pass
-#   halo     V5 halo pipeline A/B on shared-GPU peer ranks: np {2,4} x chunks {1, auto} ($HALO_BATCH)
+#   halo     V5 halo pipeline A/B on shared-GPU peer ranks, 2-way rows: np {2,4} x chunks {1, auto}
 #   tests_k  a subset of GPU tests: pytest -k "$TESTS_K" (one process)
 #   ingest   tools/probe_ingest.py: the bench step with a concurrent 155 MB/step receive-side copy
 # Outputs land in gpurun_out/ (merged back by gpurun). This one script replaces the per-session
@@ -110,11 +110,11 @@ for s in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
         --kernel-trace --output-format csv -d "$O/wgpmc" -o run -- $B/anx_wgemm --images 300 --iters 3 \
         > "$O/wgpmc.log" 2>&1 && python3 tools/pmc_clock.py "$O/wgpmc" || { echo "== wgpmc FAILED"; exit 1; } ;;
-    halo)
+    halo)  # the BASELINE V5 share: 256 images per 2-way row group (np 2: 256 images, np 4: 512)
       for np in 2 4; do
         for ch in 1 0; do
           run "halo_np${np}_c${ch}" 240 $B/anxrun -np $np --timeout 200 -- $B/anx --version v5 --transport peer \
-            --batch "${HALO_BATCH:-512}" --iters 30 --init rand --chunks $ch
+            --batch $((np * ${HALO_SHARE:-128})) --row-ways 2 --iters 30 --init rand --chunks $ch
         done
       done ;;
     *) echo "unknown session $s"; exit 2 ;;

@@ -129,6 +129,17 @@ def test_v5_transports_issue_identical_transfers(np_, split, src):
     assert ("halo_p1" in phases) == (split == "rows" or np_ > 3)
 
 
+def test_v5_explicit_row_ways():
+    """--row-ways R: R ranks per row group (4 ranks, 2-way rows = 2 groups, halos inside each group);
+    it must divide the rank count."""
+    _, out = native(["--version", "v5", "--dry-run", "--transport", "peer", "--row-ways", "2", "--batch", "8",
+                     "--input-source", "local"], 4)
+    halos = [l for l in out.stdout.splitlines() if l.startswith("ANX_SCHEDULE ") and " halo_p1" in l]
+    pairs = {tuple(sorted(int(t) for t in l.split(" ")[5].split("->"))) for l in halos}
+    assert pairs and pairs <= {(0, 1), (2, 3)}
+    native(["--version", "v5", "--dry-run", "--row-ways", "3", "--batch", "8"], 4, expect="nonzero")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("np_,decomp,split,extra", [(2, "per_layer", "rows", []), (3, "per_layer", "rows", []),
                                                     (4, "per_layer", "rows", ["--chunks", "2"]),
