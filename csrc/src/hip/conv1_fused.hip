@@ -15,11 +15,14 @@
 // V_{a+1} is built (global loads of X' from L2 into registers, VALU) while the MFMAs of a-step a run
 // and stored at its end; the two V buffers (5 points x 32 tiles x 48 ch, row stride 56 floats:
 // conflict-free ds_read_b128 fragments) alternate by a-step. U_ab (18 KB per point) streams through a
-// 2-slot LDS ring by buffer_load ... lds, one barrier per point (it also publishes V). 12 waves (3 per
-// SIMD): wave (wm, wn) computes tiles 16 wm .. +15 x filters 16 wn .. +15 as one 16x16x4 MFMA block,
-// so the fold keeps 36 registers (9 outputs x 4 values) and three waves fit a SIMD with room for the
-// V build. Bias + ReLU + the NHWC store through an LDS transpose (each 384-B output row of 96 filters
-// written by 24 lanes, 16 B each).
+// 3-slot LDS ring by buffer_load ... lds, one barrier per point (it also publishes V). Latency: U is
+// issued two points ahead and each X' row one point before the point that consumes it, with every
+// wait a compile-time vmcnt (the first form waited for everything at every point and ran the MFMA
+// pipe ~29 % busy alone, 37 % of wave cycles in waits). 12 waves (3 per SIMD): wave (wm, wn) computes
+// tiles 16 wm .. +15 x filters 16 wn .. +15 as one 16x16x4 MFMA block, so the fold keeps 36
+// registers (9 outputs x 4 values) and three waves fit a SIMD with room for the V build. Bias + ReLU +
+// the NHWC store through an LDS transpose (each 384-B output row of 96 filters written by 24 lanes,
+// 16 B each).
 //
 // Reference op: convKernel (v3_cuda_only/src/layers_cuda.cu:20-46), one thread per output.
 #include <hip/hip_runtime.h>
@@ -47,11 +50,23 @@ constexpr int kVS = 56;                    // LDS row stride of V (floats): conf
 constexpr int kVBuf = kN5 * kTiles * kVS;  // floats per a-step V buffer
 constexpr int kUSlot = kK * kCh;           // floats per U ring slot (one point)
 constexpr int kUPieces = kUSlot / 256;     // 1-KiB DMA pieces per slot
+constexpr int kUSlots = 3;                 // U ring slots: U_{p+2} is in flight while point p computes
+constexpr int kOOB = 0x7ffffff0;           // a buffer offset past any extent: the load returns 0
 constexpr int kOS = kK + 4;                // epilogue transpose row stride (floats)
-constexpr int kLdsFloats = 2 * kVBuf + 2 * kUSlot;
+constexpr int kDummy = 2 * kVBuf + kUSlots * kUSlot;  // 1-KiB scratch for the dummy DMAs
+constexpr int kLdsFloats = kDummy + 256;
 constexpr size_t kLds = kLdsFloats * sizeof(float);
 static_assert(kLds <= 160 * 1024, "LDS");
-static_assert(kUSlot % 256 == 0 && kUPieces <= 2 * kWaves, "U ring pieces");
+static_assert(kUSlot % 256 == 0 && kUPieces <= 2 * kWaves && kUPieces >= kWaves, "U ring pieces: 1 or 2 per wave");
+
+// V_a's X' row u is loaded (kN5 loads) iff B^T[a][u] != 0
+constexpr bool needs_row(int av, int u) { return av < kN5 && w33::kBT[av][u] != 0.f; }
+// does point p = 5a + b load an X' row (the one consumed at the end of point p + 1: row b + 1 of V_{a+1},
+// or row 0 of V_{a+2} at b = 4; p = -1 is the prologue)?
+constexpr bool loads_at(int p) {
+  const int av = p < 0 ? 0 : p / kN5, b = p < 0 ? kN5 - 1 : p % kN5;
+  return b + 1 < kN5 ? needs_row(av + 1, b + 1) : needs_row(av + (p < 0 ? 1 : 2), 0);
+}
 static_assert(kTiles * kOS <= kLdsFloats, "epilogue scratch");
 static_assert(kTiles * 24 == kNT, "V build: one (tile, channel pair) per thread");
 
@@ -93,25 +108,28 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
 #endif
   lds_f32* lds3 = (lds_f32*)(lds);
-  float* const vbuf = lds;                // [2][5][kTiles][kVS]
-  [[maybe_unused]] lds_f32* const uring = lds3 + 2 * kVBuf;  // [2][kK][kCh], swizzled units
+  float* const vbuf = lds;                                   // [2][5][kTiles][kVS]
+  [[maybe_unused]] lds_f32* const uring = lds3 + 2 * kVBuf;  // [kUSlots][kK][kCh], swizzled units
 
-  // ---- U ring: point ab into slot ab & 1 (pieces q = wave, wave + 12 of the slot)
+  // ---- U ring: point ab into slot ab % kUSlots, issued two points ahead (pieces q = wave, wave + 12)
   int uoff[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = wave + kWaves * i, U = (q < kUPieces ? q : 0) * 64 + lane;
     const int row = U / 12, u = (U - row * 12) ^ swz(row);
-    uoff[i] = (row * kCh + 4 * u) * 4;
+    uoff[i] = q < kUPieces ? (row * kCh + 4 * u) * 4 : kOOB;  // no second piece: the dummy reads zeros
   }
-  auto issue_u = [&](int ab) {
+  // Every wave issues exactly 2 vector-memory ops per point, unconditionally: the waves without a
+  // second 1-KiB piece DMA zeros (out-of-range source) into a 1-KiB scratch row instead, so the compiler's (and the schedule's)
+  // vmcnt values count the same ops on every wave (with a conditional second piece the compiler
+  // assumed none and its waits for the X' rows also waited for the U DMA just issued).
+  auto issue_u = [&](auto AB) {
+    [[maybe_unused]] constexpr int ab = decltype(AB)::value;
 #if __HIP_DEVICE_COMPILE__
-    lds_f32* st = uring + (ab & 1) * kUSlot;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (wave + kWaves * i < kUPieces)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + (wave + kWaves * i) * 256), 16, uoff[i],
-                                                 ab * kUSlot * 4, 0, 0);
+    lds_f32* st = uring + (ab % kUSlots) * kUSlot;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + wave * 256), 16, uoff[0], ab * kUSlot * 4, 0, 0);
+    lds_f32* st2 = wave + kWaves < kUPieces ? st + (wave + kWaves) * 256 : lds3 + kDummy;  // scalar select
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)st2, 16, uoff[1], ab * kUSlot * 4, 0, 0);
 #endif
   };
 
@@ -130,21 +148,28 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   const int row0 = bti * kPitch + rh;               // image row of u = 0 (this slot's phase row)
   const int col0 = btj * kPitch * 3 + bf2;          // float of v = 0 inside the row
   [[maybe_unused]] const int xoff = ((bn * a.Hin + row0) * a.rowf + col0) * 4;
-  // X'[u][v] (2 channels): image row 12 ti + 4u + rh, floats (12 tj + 4v) * 3 + bf2 .. +1 (zero outside)
+  // X'[u][v] (2 channels): image row 12 ti + 4u + rh, floats (12 tj + 4v) * 3 + bf2 .. +1 (zero outside).
+  // Every load is issued by every lane (a lane outside the image reads past the buffer's extent, which
+  // returns 0), so each X' row is exactly kN5 vector-memory ops per wave and the schedule's vmcnt
+  // values are compile-time. At the row's last float (o + 1 == rowf) the pair is loaded from o - 1.
+  bool rok[kN5], cok[kN5], cpart[kN5];
+#pragma unroll
+  for (int i = 0; i < kN5; ++i) {
+    const int o = col0 + 12 * i;
+    rok[i] = bval && row0 + kPh * i < a.Hin;
+    cok[i] = o < a.rowf;
+    cpart[i] = o + 2 > a.rowf;
+  }
   auto load_x = [&](int u, int v) -> f32x2 {
     f32x2 d = {0.f, 0.f};
 #if __HIP_DEVICE_COMPILE__
-    const int o = col0 + 12 * v;
     const int so = (kPh * u * a.rowf + 12 * v) * 4;
-    if (bval && row0 + kPh * u < a.Hin) {
-      if (o + 2 <= a.rowf)
-        d = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, xoff, so, 0));
-      else if (o < a.rowf)
-        d.x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff, so, 0));
-    }
+    const int vo = rok[u] && cok[v] ? xoff - (cpart[v] ? 4 : 0) : kOOB;
+    d = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, vo, so, 0));
 #endif
-    return d;
+    return d;  // raw: x_fix() at the consumer (a select here would wait for the load at its issue)
   };
+  auto x_fix = [&](int v, f32x2 d) { return cpart[v] ? f32x2{d.y, 0.f} : d; };
   f32x2 t[kN5];
   auto t_zero = [&]() {
 #pragma unroll
@@ -157,8 +182,9 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
     if constexpr (c != 0.f)
 #pragma unroll
       for (int v = 0; v < kN5; ++v) {
-        t[v].x = __builtin_fmaf(c, d[v].x, t[v].x);
-        t[v].y = __builtin_fmaf(c, d[v].y, t[v].y);
+        const f32x2 e = x_fix(v, d[v]);
+        t[v].x = __builtin_fmaf(c, e.x, t[v].x);
+        t[v].y = __builtin_fmaf(c, e.y, t[v].y);
       }
   };
   auto v_store = [&](int buf) {
@@ -190,8 +216,16 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 #pragma unroll
   for (int q = 0; q < 9; ++q) Y[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: U of point 0 in flight, V_0 built and stored
-  issue_u(0);
+  // Schedule (points p = 5a + b in order). At point p a wave: waits for U_p (its own DMA: vmcnt; every
+  // wave's: the barrier, which also publishes V_a), issues U_{p+2} (two points of MFMAs cover its
+  // latency) and the X' row consumed at the end of point p + 1, runs point p's MFMAs and fold, then
+  // adds the X' row loaded at point p - 1 into t (V_{a+1}, row b). V_{a+1} is stored at the end of
+  // a-step a. vmcnt is in order, so the wait at point p leaves exactly the ops issued at point p - 1
+  // in flight (2 U ops per wave, then kN5 X' loads when that point loads a row).
+  f32x2 dq[2][kN5];  // X' rows in flight, by the parity of the point that loaded them
+  // prologue: U_0, U_1 in flight, V_0 built and stored (its loads waited here), X' for point 0
+  issue_u(std::integral_constant<int, 0>{});
+  issue_u(std::integral_constant<int, 1>{});
   t_zero();
   sfor<0, kN5>([&](auto Uc) {
     constexpr int u = decltype(Uc)::value;
@@ -203,28 +237,31 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
     }
   });
   v_store(0);
+  t_zero();
+  if constexpr (loads_at(-1))
+#pragma unroll
+    for (int v = 0; v < kN5; ++v) dq[1][v] = load_x(0, v);
 
   sfor<0, kN5>([&](auto Ac) {
     constexpr int av = decltype(Ac)::value;
-    constexpr int an = av + 1 < kN5 ? av + 1 : 0;  // the a-step whose V this one builds (when av < 4)
     const float* vb = vbuf + (av & 1) * kVBuf;
-    if constexpr (av + 1 < kN5) t_zero();
     sfor<0, kN5>([&](auto Bc) {
-      constexpr int b = decltype(Bc)::value, ab = av * kN5 + b;
-      // U_ab landed (this wave's DMA: vmcnt; everyone's: the barrier), V_a stored (ds: barrier)
+      constexpr int b = decltype(Bc)::value, p = av * kN5 + b;
+      constexpr int inflight = (p + 1 < kPts ? 2 : 0) + (loads_at(p - 1) ? kN5 : 0);
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(inflight) : "memory");
+      __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (ab + 1 < kPts) issue_u(ab + 1);  // the slot read at point ab - 1: free after the barrier
-      // X' of V_{a+1}'s u = b row: issued now, consumed after this point's MFMAs
-      constexpr bool part = av + 1 < kN5 && w33::kBT[an][b] != 0.f;
-      f32x2 d[kN5];
-      if constexpr (part)
+      asm volatile("" ::: "memory");
+      if constexpr (p + 2 < kPts) issue_u(std::integral_constant<int, p + 2>{});  // slot of point p - 1: free
+      if constexpr (loads_at(p)) {
+        constexpr int r = b + 1 < kN5 ? b + 1 : 0;  // the X' row consumed at the end of point p + 1
 #pragma unroll
-        for (int v = 0; v < kN5; ++v) d[v] = load_x(b, v);
+        for (int v = 0; v < kN5; ++v) dq[p & 1][v] = load_x(r, v);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // loads issued before the MFMAs
       const float* vp = vb + b * kTiles * kVS + a_off;
-      const float* up = reinterpret_cast<const float*>(lds + 2 * kVBuf + (ab & 1) * kUSlot);
+      const float* up = reinterpret_cast<const float*>(lds + 2 * kVBuf + (p % kUSlots) * kUSlot);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
@@ -241,11 +278,22 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) Y[q][i] = __builtin_fmaf(c, acc[i], Y[q][i]);  // scalar v_fma_f32
       });
-      if constexpr (part) t_add(std::integral_constant<int, an>{}, Bc, d);
+      // pinned here (the empty asm takes t and Y as operands: the DAG scheduler had sunk the adds to the
+      // a-step's end, where their in-order vmcnt also waited for the U DMA just issued)
+      if constexpr (needs_row(av + 1, b)) {
+        t_add(std::integral_constant<int, av + 1>{}, Bc, dq[(p + 1) & 1]);
+#pragma unroll
+        for (int v = 0; v < kN5; ++v) asm volatile("" : "+v"(t[v]));
+      }
+#pragma unroll
+      for (int q = 0; q < 9; ++q) asm volatile("" : "+v"(Y[q]));
+      if constexpr (b == kN5 - 1 && av + 1 < kN5) {
+        // V_{a+1} into the other buffer (last read in a-step a - 1, before this a-step's first barrier);
+        // published by the barrier of point (a + 1, 0)
+        v_store((av + 1) & 1);
+        t_zero();
+      }
     });
-    // V_{a+1} into the other buffer (last read in a-step a - 1, before this a-step's first barrier);
-    // published by the barrier of point (a + 1, 0)
-    if constexpr (av + 1 < kN5) v_store((av + 1) & 1);
   });
 
   // ---- epilogue: per output position q, bias + ReLU into an LDS image [32 tiles][96 filters], then

@@ -18,8 +18,9 @@ Names and values:
   default: a tile that computes all the pool1 rows its conv2 window needs runs pool1 inside the
   Winograd input transform; 0: the pool1 kernel and the window buffer); ``conv1_sub`` / ``conv2_sub``
   (images per Conv1 / Conv2 transform + GEMM launch pair inside a fused forward; 0 = whole launch: a
-  small sub-chunk rewrites the V workspace in place, inside the Infinity Cache); ``conv1_fused`` (1: Conv1
-  as one kernel, the polyphase input transform built in LDS inside the Winograd GEMM).
+  small sub-chunk rewrites the V workspace in place, inside the Infinity Cache); ``conv1_fused`` (1, the
+  default: Conv1 as one kernel, the polyphase input transform built in LDS inside the Winograd GEMM;
+  0: the band transform kernel + GEMM).
 """
 from __future__ import annotations
 
