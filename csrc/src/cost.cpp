@@ -213,12 +213,7 @@ StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource sr
   } else {
     if (c.max_rank_halo_bytes > 0) {
       int chunks = p.v5_chunks;
-      if (chunks <= 0) {  // the runtime's auto rule (make_v5_layout): chunks of >= 128 images, at most 4
-        int least = 1 << 30;
-        for (int g = 0; g < hp.groups; ++g)
-          if (hp.group_size[g] > 1 && hp.images[g].size() > 0) least = std::min(least, hp.images[g].size());
-        chunks = std::max(1, std::min(4, least / 128));
-      }
+      if (chunks <= 0) chunks = 1;  // the runtime's auto rule (make_v5_layout): one chunk
       c.halo_ms = c.max_rank_halo_bytes / link;
       c.halo_exposed_ms = c.halo_ms / chunks + p.phase_latency_ms * chunks;
     }

@@ -74,9 +74,11 @@ V5Layout make_v5_layout(int np, const BlockSpec& b1, const BlockSpec& b2, int H,
   const auto& halos = L.sched.phase[static_cast<int>(Phase::P1Halo)];
   int min_imgs = 1 << 30;
   for (const Transfer& x : halos) min_imgs = std::min(min_imgs, static_cast<int>(x.height));
-  // auto: chunks of >= 128 images, at most 4 (halo c moves while stage1 computes c+1; smaller launches
-  // lose more to wave quantization than the exposed halo costs: profiles/r03_v5_halo.log)
-  const int auto_chunks = std::max(1, std::min(4, min_imgs / 128));
+  // auto: one chunk. Chunking (halo c moves while stage1 computes c+1) never paid: at the BASELINE
+  // share (256 images per 2-way row group) 1.207 vs 1.226 ms at np 2 and 2.645 vs 2.646 ms at np 4 for
+  // 1 vs 2 chunks, stage1's smaller launches losing what the hidden halo gains
+  // (profiles/r04_halo/, profiles/r03_v5_halo.log); --chunks K keeps the pipeline for other links
+  const int auto_chunks = 1;
   L.chunks = halos.empty() ? 1 : std::max(1, std::min({o.chunks > 0 ? o.chunks : auto_chunks, min_imgs, kMaxChunks}));
   for (int c = 0; c < L.chunks; ++c) L.halo_chunks.push_back(chunk_of(halos, c, L.chunks));
   return L;

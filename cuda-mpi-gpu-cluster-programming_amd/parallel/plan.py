@@ -302,7 +302,7 @@ def step_schedule(p: HybridPlan, chunks: int = 0, b1: BlockSpec = BLOCK1, b2: Bl
                           ("Win", (h.rows.lo - td.q.lo) * win_row, td.q.size * win_row), h.rows.size * win_row, n))
     if halos:
         least = min(x[6] for x in halos)
-        chunks = max(1, min(chunks if chunks > 0 else max(1, min(4, least // 128)), least, MAX_CHUNKS))
+        chunks = max(1, min(chunks if chunks > 0 else 1, least, MAX_CHUNKS))  # auto: 1 (the runtime's rule)
     out = [_xfer(*x) for x in scatter] if input_source == "root" else []
     for c in range(chunks if halos else 0):
         for ph, s, t, frm, to, w, hgt in halos:
