@@ -38,8 +38,8 @@ struct Knobs {
   int fuse_pool1 = 1;      // tile_forward of a tile that computes every pool1 row its conv2 window needs: pool1
                            // fused into the Winograd input transform (no window round trip), 0 = pool1 kernel
   int conv1_fused = 1;     // Conv1 as one kernel (conv1_fused.hip: V built in LDS inside the GEMM, 32 tiles x 96
-                           // filters per workgroup; bench step 273-275 k vs 253-256 k images/s,
-                           // profiles/r04_conv1_fused_v2_bench_ab.jsonl), 0 = the band transform kernel + GEMM
+                           // filters per workgroup; bench step 277-278 k vs 252-254 k images/s,
+                           // profiles/r04_conv1_fused_v3_bench_ab.jsonl), 2 = U fragments in registers (A/B), 0 = the band transform kernel + GEMM
   int conv1_sub = 0;       // fused tile_forward: images per Conv1 (input transform + GEMM) launch pair inside a
                            // chunk (0 = the whole chunk); the V workspace is rewritten in place per sub-chunk, so
                            // a small one is written and re-read inside the 256 MB Infinity Cache

@@ -125,14 +125,15 @@ size_t conv1_wino_v_floats(const Conv1WinoPlan& w);  // V workspace [P][25][48]
 size_t conv1_wino_u_floats(int K);                   // transformed weights [25][K][48]
 void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<float>& u);
 // x: [N, Hin, W, 3] image rows; writes conv1 (+bias, optional ReLU) through `out`. Knobs: conv1_occ,
-// conv1_band, conv1_fused (1: the one-kernel form below instead of transform kernel + GEMM).
+// conv1_band, conv1_fused (1 / 2: the one-kernel form below instead of transform kernel + GEMM).
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
                       bool relu, hipStream_t s, const Knobs& k);
 // The one-kernel form (conv1_fused.hip): the input transform generated in LDS inside the GEMM, each
-// workgroup 64 tiles x all 96 filters (V never reaches HBM). Eligible for K == 96.
+// workgroup 32 tiles x all 96 filters (V never reaches HBM). Eligible for K == 96. mode 1: U through
+// an LDS ring; mode 2: U fragments straight into registers (one barrier per a-step).
 bool conv1_fused_eligible(const Conv1WinoPlan& w, const OutView& out);
 hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out, bool relu,
-                       hipStream_t s);
+                       hipStream_t s, int mode = 1);
 
 // The fused Winograd GEMM + output transform (wino_gemm.hip). V [P][points][C], U [points][K][C/groups]
 // (row = filter), bias + optional ReLU, NHWC store through `out` (Cb, c_off multiples of 4). P tiles of

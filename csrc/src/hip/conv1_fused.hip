@@ -94,6 +94,9 @@ struct Conv1FusedArgs {
   int relu;
 };
 
+// UM = 0: U through the 3-slot LDS ring (a barrier per point); UM = 1: each wave loads its own B
+// fragments of U straight into registers two points ahead (no LDS for U: one barrier per a-step).
+template <int UM>
 __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -123,9 +126,18 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // second 1-KiB piece DMA zeros (out-of-range source) into a 1-KiB scratch row instead, so the compiler's (and the schedule's)
   // vmcnt values count the same ops on every wave (with a conditional second piece the compiler
   // assumed none and its waits for the X' rows also waited for the U DMA just issued).
+  [[maybe_unused]] f32x4 ureg[kUSlots][3];  // UM 1: B fragments of points p, p + 1, p + 2 (slot p % 3)
+  [[maybe_unused]] const int ureg_off = ((wave >> 1) * 16 + (lane & 15)) * kCh * 4 + 16 * (lane >> 4);
   auto issue_u = [&](auto AB) {
     [[maybe_unused]] constexpr int ab = decltype(AB)::value;
 #if __HIP_DEVICE_COMPILE__
+    if constexpr (UM == 1) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        ureg[ab % kUSlots][g] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ur, ureg_off, (ab * kUSlot + 16 * g) * 4, 0));
+      return;
+    }
     lds_f32* st = uring + (ab % kUSlots) * kUSlot;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + wave * 256), 16, uoff[0], ab * kUSlot * 4, 0, 0);
     lds_f32* st2 = wave + kWaves < kUPieces ? st + (wave + kWaves) * 256 : lds3 + kDummy;  // scalar select
@@ -151,25 +163,26 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // X'[u][v] (2 channels): image row 12 ti + 4u + rh, floats (12 tj + 4v) * 3 + bf2 .. +1 (zero outside).
   // Every load is issued by every lane (a lane outside the image reads past the buffer's extent, which
   // returns 0), so each X' row is exactly kN5 vector-memory ops per wave and the schedule's vmcnt
-  // values are compile-time. At the row's last float (o + 1 == rowf) the pair is loaded from o - 1.
-  bool rok[kN5], cok[kN5], cpart[kN5];
+  // values are compile-time. At the row's last float (o + 1 == rowf) the pair's .y is the next row's
+  // first float (or, past the buffer, 0: the range check is per dword): t's .y for that column is
+  // zeroed once per a-step before V is formed (vpart), instead of a select per load.
+  bool rok[kN5], cpart[kN5];
+  int offv[kN5];  // per column v: this lane's byte offset, or past the extent (zeros)
 #pragma unroll
   for (int i = 0; i < kN5; ++i) {
     const int o = col0 + 12 * i;
     rok[i] = bval && row0 + kPh * i < a.Hin;
-    cok[i] = o < a.rowf;
-    cpart[i] = o + 2 > a.rowf;
+    offv[i] = o < a.rowf ? xoff : kOOB;
+    cpart[i] = o + 1 == a.rowf;
   }
   auto load_x = [&](int u, int v) -> f32x2 {
     f32x2 d = {0.f, 0.f};
 #if __HIP_DEVICE_COMPILE__
     const int so = (kPh * u * a.rowf + 12 * v) * 4;
-    const int vo = rok[u] && cok[v] ? xoff - (cpart[v] ? 4 : 0) : kOOB;
-    d = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, vo, so, 0));
+    d = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, rok[u] ? offv[v] : kOOB, so, 0));
 #endif
-    return d;  // raw: x_fix() at the consumer (a select here would wait for the load at its issue)
+    return d;
   };
-  auto x_fix = [&](int v, f32x2 d) { return cpart[v] ? f32x2{d.y, 0.f} : d; };
   f32x2 t[kN5];
   auto t_zero = [&]() {
 #pragma unroll
@@ -182,12 +195,13 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
     if constexpr (c != 0.f)
 #pragma unroll
       for (int v = 0; v < kN5; ++v) {
-        const f32x2 e = x_fix(v, d[v]);
-        t[v].x = __builtin_fmaf(c, e.x, t[v].x);
-        t[v].y = __builtin_fmaf(c, e.y, t[v].y);
+        t[v].x = __builtin_fmaf(c, d[v].x, t[v].x);
+        t[v].y = __builtin_fmaf(c, d[v].y, t[v].y);
       }
   };
   auto v_store = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < kN5; ++v) t[v].y = cpart[v] ? 0.f : t[v].y;  // the row's last float has no pair
     float* vb = vbuf + buf * kVBuf + bt * kVS + 2 * bc;
     sfor<0, kN5>([&](auto Bc) {
       constexpr int b = decltype(Bc)::value;
@@ -215,6 +229,9 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   f32x4 Y[9];  // Y[q]: output q of the block's 4 accumulator rows
 #pragma unroll
   for (int q = 0; q < 9; ++q) Y[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // separable fold: T[j] = sum_b A^T[j][b] M_ab over the a-step's points, then Y[i][j] += A^T[i][a] T[j]
+  // at its end (352 instead of 484 FMAs per wave and tile block)
+  f32x4 T[3];
 
   // Schedule (points p = 5a + b in order). At point p a wave: waits for U_p (its own DMA: vmcnt; every
   // wave's: the barrier, which also publishes V_a), issues U_{p+2} (two points of MFMAs cover its
@@ -245,14 +262,21 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   sfor<0, kN5>([&](auto Ac) {
     constexpr int av = decltype(Ac)::value;
     const float* vb = vbuf + (av & 1) * kVBuf;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) T[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     sfor<0, kN5>([&](auto Bc) {
       constexpr int b = decltype(Bc)::value, p = av * kN5 + b;
       constexpr int inflight = (p + 1 < kPts ? 2 : 0) + (loads_at(p - 1) ? kN5 : 0);
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(inflight) : "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("" ::: "memory");
+      if constexpr (UM == 0 || b == 0) {  // UM 1: only V_a needs publishing (and V_{a-1}'s readers done)
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (UM == 0)
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(inflight) : "memory");
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+      }
       if constexpr (p + 2 < kPts) issue_u(std::integral_constant<int, p + 2>{});  // slot of point p - 1: free
       if constexpr (loads_at(p)) {
         constexpr int r = b + 1 < kN5 ? b + 1 : 0;  // the X' row consumed at the end of point p + 1
@@ -266,19 +290,23 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
         const f32x4 af = *reinterpret_cast<const f32x4*>(vp + 16 * g);
-        const f32x4 bf = *reinterpret_cast<const f32x4*>(up + b_off[g]);
+        f32x4 bf;
+        if constexpr (UM == 1)
+          bf = ureg[p % kUSlots][g];
+        else
+          bf = *reinterpret_cast<const f32x4*>(up + b_off[g]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[i], acc, 0, 0, 0);
       }
-      // fold: Y[i][j] += A^T[i][a] A^T[j][b] M_ab (compile-time coefficients; zero ones skipped)
-      sfor<0, 9>([&](auto Qc) {
-        constexpr int q = decltype(Qc)::value;
-        constexpr float c = w33::kAT[q / 3][av] * w33::kAT[q % 3][b];
+      // fold, first half: T[j] += A^T[j][b] M_ab (compile-time coefficients; zero ones skipped)
+      sfor<0, 3>([&](auto Jc) {
+        constexpr int j = decltype(Jc)::value;
+        constexpr float c = w33::kAT[j][b];
         if constexpr (c != 0.f)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) Y[q][i] = __builtin_fmaf(c, acc[i], Y[q][i]);  // scalar v_fma_f32
+          for (int i = 0; i < 4; ++i) T[j][i] = __builtin_fmaf(c, acc[i], T[j][i]);  // scalar v_fma_f32
       });
-      // pinned here (the empty asm takes t and Y as operands: the DAG scheduler had sunk the adds to the
+      // pinned here (the empty asm takes t and T as operands: the DAG scheduler had sunk the adds to the
       // a-step's end, where their in-order vmcnt also waited for the U DMA just issued)
       if constexpr (needs_row(av + 1, b)) {
         t_add(std::integral_constant<int, av + 1>{}, Bc, dq[(p + 1) & 1]);
@@ -286,7 +314,18 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         for (int v = 0; v < kN5; ++v) asm volatile("" : "+v"(t[v]));
       }
 #pragma unroll
-      for (int q = 0; q < 9; ++q) asm volatile("" : "+v"(Y[q]));
+      for (int j = 0; j < 3; ++j) asm volatile("" : "+v"(T[j]));
+      if constexpr (b == kN5 - 1) {  // fold, second half: Y[i][j] += A^T[i][a] T[j]
+        sfor<0, 9>([&](auto Qc) {
+          constexpr int q = decltype(Qc)::value;
+          constexpr float c = w33::kAT[q / 3][av];
+          if constexpr (c != 0.f)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Y[q][i] = __builtin_fmaf(c, T[q % 3][i], Y[q][i]);
+        });
+#pragma unroll
+        for (int q = 0; q < 9; ++q) asm volatile("" : "+v"(Y[q]));
+      }
       if constexpr (b == kN5 - 1 && av + 1 < kN5) {
         // V_{a+1} into the other buffer (last read in a-step a - 1, before this a-step's first barrier);
         // published by the barrier of point (a + 1, 0)
@@ -337,11 +376,17 @@ bool conv1_fused_eligible(const Conv1WinoPlan& w, const OutView& out) {
 }
 
 hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out, bool relu,
-                       hipStream_t s) {
+                       hipStream_t s, int mode) {
   if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
   if (!conv1_fused_eligible(w, out)) return hipErrorInvalidValue;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_fused_kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const hipError_t attr = [] {
+    for (const void* k : {reinterpret_cast<const void*>(conv1_fused_kernel<0>),
+                          reinterpret_cast<const void*>(conv1_fused_kernel<1>)}) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }();
   if (attr != hipSuccess) return attr;
   Conv1FusedArgs a{};
   a.x = x;
@@ -360,7 +405,10 @@ hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, c
   a.n_ptiles = (w.P + kTiles - 1) / kTiles;
   a.per_xcd = (a.n_ptiles + 7) / 8;
   a.relu = relu ? 1 : 0;
-  conv1_fused_kernel<<<static_cast<unsigned>(a.per_xcd * 8), kNT, kLds, s>>>(a);
+  if (mode == 2)
+    conv1_fused_kernel<1><<<static_cast<unsigned>(a.per_xcd * 8), kNT, 2 * kVBuf * sizeof(float), s>>>(a);
+  else
+    conv1_fused_kernel<0><<<static_cast<unsigned>(a.per_xcd * 8), kNT, kLds, s>>>(a);
   return hipGetLastError();
 }
 
