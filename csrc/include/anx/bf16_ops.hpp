@@ -85,6 +85,13 @@ hipError_t f32_to_bf16(const float* x, void* y, size_t n, hipStream_t s);
 // Conv1 polyphase input (space-to-depth by the stride 4) fused with the bf16 conversion:
 // y[n][i][j][(rh*4+rw)*3+c] = x[n][4i+rh][4j+rw][c] (0 past the image), y = [N, ceil(H/4), ceil(W/4), 48].
 hipError_t f32_to_bf16_s2d4(const float* x, void* y, int N, int H, int W, hipStream_t s);
+// Conv1 on the polyphase image as a persistent row-band kernel (conv1_bf16_ring.hip): x' [N,57,57,48]
+// bf16, weights packed by pack_conv1_ring_weights from the polyphase fp32 filters [96][48][3][3]
+// (conv1_ring_weight_bytes() bytes), bias + ReLU (relu must be true), bf16 NHWC out (55x55x96 view).
+void pack_conv1_ring_weights(const float* w_k48_33, std::vector<uint16_t>& out);
+size_t conv1_ring_weight_bytes();
+hipError_t conv1_bf16_ring(const void* xpoly, int N, const void* wpacked, const float* bias, OutViewB out, bool relu,
+                           hipStream_t s, int cus = 256);
 
 }  // namespace hip
 
@@ -139,6 +146,7 @@ class FullEngine {
   int cus_ = 256;  // compute units (the wide-tile kernel's cost model)
   LrnMode lrn_;
   bool poly1_ = false;  // Conv1 as a stride-1 3x3 conv over the 48-channel polyphase image (ANX_FULL_CONV1)
+  void* w1ring_ = nullptr;  // Conv1 weights packed for conv1_bf16_ring (poly1_ only)
   void *xb_ = nullptr, *c1_ = nullptr, *q2_ = nullptr, *c2_ = nullptr, *q3_ = nullptr, *q4_ = nullptr,
        *q5_ = nullptr, *c5_ = nullptr, *f6_ = nullptr, *f7_ = nullptr, *f8_ = nullptr;
   float* ws_ = nullptr;  // split-K partial slabs of the FC layers (sized for every batch <= chunk_)

@@ -82,6 +82,10 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
     L.C = 48;
     L.F = 3;
     L.S = 1;
+    std::vector<uint16_t> rp;
+    hip::pack_conv1_ring_weights(L.host.data(), rp);
+    w1ring_ = dalloc(rp.size() * 2);
+    check(hipMemcpy(w1ring_, rp.data(), rp.size() * 2, hipMemcpyHostToDevice), "H2D conv1 ring weights");
   }
   {
     int dev = 0;
@@ -124,7 +128,7 @@ FullEngine::~FullEngine() {
   for (Layer& L : L_)
     for (void* p : {L.wp, L.wfc, static_cast<void*>(L.koff), static_cast<void*>(L.bias)})
       if (p) (void)hipFree(p);
-  for (void* p : {xb_, c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_, static_cast<void*>(ws_)})
+  for (void* p : {xb_, c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_, static_cast<void*>(ws_), w1ring_})
     if (p) (void)hipFree(p);
 }
 
@@ -193,7 +197,10 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
     const float* xn = x + static_cast<size_t>(n0) * 227 * 227 * 3;
     if (poly1_) {
       ANX_TRY(hip::f32_to_bf16_s2d4(xn, xb_, n, 227, 227, s));
-      ANX_TRY(conv(L_[0], n, 57, 57, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
+      if (k_.bf16_conv1 == 1)
+        ANX_TRY(hip::conv1_bf16_ring(xb_, n, w1ring_, L_[0].bias, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, true, s, cus_));
+      else
+        ANX_TRY(conv(L_[0], n, 57, 57, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
     } else {
       ANX_TRY(hip::f32_to_bf16(xn, xb_, static_cast<size_t>(n) * 227 * 227 * 3, s));
       ANX_TRY(conv(L_[0], n, 227, 227, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));

@@ -1,0 +1,245 @@
+// Conv1 of the bf16 full AlexNet (extension, BASELINE config 5) as a persistent row-band kernel.
+//
+// Conv1 runs on the polyphase input (space-to-depth by the stride: 11x11/4 over 3 channels becomes
+// 3x3/1 over 48, full_engine.cpp), x' [N][57][57][48] bf16, 96 filters, 55x55 outputs. As an
+// implicit GEMM over 96-row tiles (conv_bf16_big.hip, 8067 workgroups of 96 pixels x 96 filters)
+// every K tile gathers its A rows from L2 again: 9 taps x 48 channels per pixel, i.e. the image is
+// fetched 9 times over (1.3 GB of L2 -> LDS traffic at 256 images), and the layer ran 113 us
+// (profiles/r03_full_bf16_kernels_b256.md) against ~46 us for its HBM bytes.
+//
+// Here one workgroup (4 waves, one per SIMD) walks an image in tiles of two output rows:
+//   * the polyphase rows it needs live in an 8-slot LDS ring (slot = row & 7, 6 KiB each: a row is
+//     57 x 48 bf16 = 5472 B, one contiguous LDS-DMA copy); tile t reads rows 2t .. 2t+3 and the
+//     DMAs of rows 2t+6, 2t+7 (tile t+2) fly behind its MFMAs, so each input row crosses HBM once;
+//   * all 96 filters' weights stay in LDS for the kernel's lifetime ([96][440] bf16, row stride 880
+//     B: the 32 rows of a 32x32x16 operand read hit distinct bank quads);
+//   * wave w owns pixels 32w .. 32w+31 of the tile (110 valid of 128) x all 96 filters: per K step
+//     (16 of the 432) one pixel fragment and three filter fragments feed three
+//     v_mfma_f32_32x32x16_bf16 (filters as the A operand, so each lane ends up holding 4
+//     consecutive filters of one pixel: 8-B stores, no LDS transpose);
+//   * bias + ReLU + bf16 in the epilogue, straight into the NHWC output.
+// Fragments are read one K step ahead of their MFMAs (registers double-buffered).
+//
+// Reference op: convKernel (final_project/v3_cuda_only/src/layers_cuda.cu:20-46); the full-network
+// tail is the extension's own.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+#include <vector>
+
+#include "anx/bf16_ops.hpp"
+
+namespace anx::hip {
+namespace {
+
+using bf16 = __bf16;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+using u32x2 = __attribute__((ext_vector_type(2))) unsigned;
+using lds_b16 = __attribute__((address_space(3))) bf16;
+using lds_void = __attribute__((address_space(3))) void;
+
+constexpr int kP = 57, kCh = 48, kRowB = kP * kCh * 2;  // polyphase rows: 57 x 48 bf16 = 5472 B
+constexpr int kHo = 55, kWo = 55, kK = 96, kKd = 432;  // output rows / cols, filters, GEMM K
+constexpr int kSlots = 8, kSlotB = 6144;                // ring: 8 rows, 6 KiB apart (6 DMA pieces)
+constexpr int kPieces = kSlotB / 1024;
+constexpr int kWRow = 440;                              // weight row stride (bf16): 880 B
+constexpr int kWBytes = 83 * 1024;                      // [96][440] bf16 = 84,480 B, padded to whole DMA pieces
+constexpr int kRing = kSlots * kSlotB;                  // 49,152 B
+constexpr int kBias = kRing + kWBytes;
+constexpr size_t kLds = kBias + kK * 4;                 // 134,528 B
+constexpr int kTilesPerImage = (kHo + 1) / 2;           // 28 (the last holds one row)
+constexpr int kNT = 256;
+constexpr int kKS = kKd / 16;                           // 27 K steps (3 per tap)
+constexpr int kOOB = 0x7ffffff0;
+static_assert(kK * kWRow * 2 <= kWBytes && kRowB <= kSlotB, "LDS layout");
+static_assert(2 * kPieces % 4 == 0, "the two rows' DMA pieces split evenly over the 4 waves");
+
+struct Args {
+  const bf16* x;      // [N][57][57][48]
+  const bf16* w;      // [96][440] (K = tap * 48 + channel, zero past 432), kWBytes bytes
+  const float* bias;  // [96]
+  bf16* out;          // NHWC through the view
+  int Hb, Wb, Cb, h_off, w_off, c_off;
+  int N, segs;        // segments per image (workgroups sharing one image's tiles)
+  int xbytes, obytes;
+};
+
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+__global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = blockIdx.x / a.segs, seg = blockIdx.x - n * a.segs;
+  const int t0 = seg * kTilesPerImage / a.segs, t1 = (seg + 1) * kTilesPerImage / a.segs;
+  if (n >= a.N || t0 >= t1) return;  // whole workgroup, before any barrier
+#if __HIP_DEVICE_COMPILE__
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.w), 0, kWBytes, 0x00020000);
+#endif
+  lds_b16* lds3 = (lds_b16*)(lds);
+
+  // ---- one polyphase row into its ring slot: pieces 3 wave .. 3 wave + 2 of the two rows of a
+  // tile (each wave issues exactly 3 DMAs per tile: the vmcnt values below are compile-time)
+  [[maybe_unused]] auto issue_rows = [&](int row0) {  // rows row0, row0 + 1 (zeros past the image)
+#if __HIP_DEVICE_COMPILE__
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int q = wave * 3 + i, r = row0 + q / kPieces, pc = q % kPieces;  // wave-uniform
+      const int src = r < kP ? ((n * kP + r) * kRowB + pc * 1024 + lane * 16) : kOOB;
+      lds_b16* dst = lds3 + ((r & (kSlots - 1)) * kSlotB + pc * 1024) / 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)dst, 16, src, 0, 0, 0);
+    }
+#endif
+  };
+
+  // ---- prologue: weights + bias, the first tile's 4 rows and the next tile's 2
+#if __HIP_DEVICE_COMPILE__
+  for (int q = wave; q < kWBytes / 1024; q += 4)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(lds3 + (kRing + q * 1024) / 2), 16, q * 1024 + lane * 16, 0,
+                                             0, 0);
+#endif
+  if (tid < kK) reinterpret_cast<float*>(lds + kBias)[tid] = a.bias[tid];
+  issue_rows(2 * t0);
+  issue_rows(2 * t0 + 2);
+  issue_rows(2 * t0 + 4);  // tile t0 + 1's new rows
+
+  // ---- per-lane fragment addressing. Pixel operand: lane (r, h) reads pixel m = 32 wave + r,
+  // channels 16 c + 8 h .. +7 of tap (qh, qw); filter operand: filter 32 nb + r, K 16 ks + 8 h .. +7.
+  const int r = lane & 31, h = lane >> 5;
+  const int m = 32 * wave + r;
+  const int mrow = m < 2 * kWo ? m / kWo : 0, ox = m < 2 * kWo ? m - mrow * kWo : 0;
+  const int wbase = kRing + r * (kWRow * 2) + h * 16;
+  const int pcol = ox * (kCh * 2) + h * 16;
+  f32x16 acc[3];
+  bf16x8 pf[2], wf[2][3];
+
+#if __HIP_DEVICE_COMPILE__
+  const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.obytes, 0x00020000);
+#endif
+  for (int t = t0; t < t1; ++t) {
+    // Rows 2t .. 2t+3 landed: this wave's DMAs by a counted vmcnt (vmcnt is in order; every wave
+    // issues exactly 3 row DMAs per tile and 12 output stores per tile, so the ops issued after tile
+    // t's rows are: tile t-2's stores, tile t+1's rows (when that tile exists), tile t-1's stores),
+    // every wave's by the barrier, which also retires tile t-1's reads of the slots refilled below.
+    const int k = (t - t0 >= 2 ? 2 : t - t0) * 2 + (t + 1 < t1 ? 1 : 0);
+    switch (k) {
+      case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(27) lgkmcnt(0)" ::: "memory"); break;
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < t1) issue_rows(2 * t + 6);  // tile t+2's new rows, into tile t-1's slots
+    const int sb0 = ((2 * t + mrow) & (kSlots - 1)) * kSlotB + pcol;
+    const int sb1 = ((2 * t + mrow + 1) & (kSlots - 1)) * kSlotB + pcol;
+    const int sb2 = ((2 * t + mrow + 2) & (kSlots - 1)) * kSlotB + pcol;
+    auto pix = [&](int ks) -> bf16x8 {  // ks compile-time after unrolling
+      const int tap = ks / 3, qh = tap / 3, qw = tap - 3 * qh, c16 = ks - 3 * tap;
+      const int base = qh == 0 ? sb0 : qh == 1 ? sb1 : sb2;
+      return *reinterpret_cast<const bf16x8*>(lds + base + qw * (kCh * 2) + c16 * 32);
+    };
+    auto wgt = [&](int ks, int nb) -> bf16x8 {
+      return *reinterpret_cast<const bf16x8*>(lds + wbase + nb * 32 * (kWRow * 2) + ks * 32);
+    };
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb) acc[nb] = f32x16{};
+    pf[0] = pix(0);
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb) wf[0][nb] = wgt(0, nb);
+    sfor<0, kKS>([&](auto KS) {
+      constexpr int ks = decltype(KS)::value, cur = ks & 1;
+      if constexpr (ks + 1 < kKS) {
+        pf[cur ^ 1] = pix(ks + 1);
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb) wf[cur ^ 1][nb] = wgt(ks + 1, nb);
+      }
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb)
+        acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cur][nb], pf[cur], acc[nb], 0, 0, 0);
+    });
+
+    // ---- epilogue: lane holds pixel m, filters 32 nb + 8 j + 4 h + (0..3) in acc[nb][4 j .. 4 j + 3].
+    // 12 buffer stores per lane, always issued (a pixel outside the tile stores past the extent,
+    // which drops the write), so the vmcnt counts above hold on every wave.
+    const int oy = 2 * t + mrow;
+    const bool ok = m < 2 * kWo && oy < kHo;
+    [[maybe_unused]] const int obase =
+        ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off) * 2 : kOOB;
+    const float* bs = reinterpret_cast<const float*>(lds + kBias);
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int f = 32 * nb + 8 * j + 4 * h;
+        const f32x4 b = *reinterpret_cast<const f32x4*>(bs + f);
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[nb][4 * j + i] + b[i], 0.f));
+#if __HIP_DEVICE_COMPILE__
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f * 2, 0);
+#endif
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+}
+
+}  // namespace
+
+void pack_conv1_ring_weights(const float* w_k48_33, std::vector<uint16_t>& out) {
+  out.assign(kWBytes / 2, 0);
+  for (int k = 0; k < kK; ++k)
+    for (int c = 0; c < kCh; ++c)
+      for (int qh = 0; qh < 3; ++qh)
+        for (int qw = 0; qw < 3; ++qw)
+          out[static_cast<size_t>(k) * kWRow + (qh * 3 + qw) * kCh + c] =
+              f32_to_bf16_bits(w_k48_33[((static_cast<size_t>(k) * kCh + c) * 3 + qh) * 3 + qw]);
+}
+
+size_t conv1_ring_weight_bytes() { return kWBytes; }
+
+hipError_t conv1_bf16_ring(const void* xpoly, int N, const void* wpacked, const float* bias, OutViewB out, bool relu,
+                           hipStream_t s, int cus) {
+  if (N <= 0) return hipSuccess;
+  if (!relu || !out.base || out.Cb % 4 || out.c_off % 4 || static_cast<long>(N) * kP * kRowB >= (1L << 31) ||
+      static_cast<long>(N) * out.Hb * out.Wb * out.Cb * 2 >= (1L << 31) || out.Hb < kHo + out.h_off ||
+      out.Wb < kWo + out.w_off || out.Cb < kK + out.c_off)
+    return hipErrorInvalidValue;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_bf16_ring_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  Args a{};
+  a.x = static_cast<const bf16*>(xpoly);
+  a.w = static_cast<const bf16*>(wpacked);
+  a.bias = bias;
+  a.out = out.base;
+  a.Hb = out.Hb;
+  a.Wb = out.Wb;
+  a.Cb = out.Cb;
+  a.h_off = out.h_off;
+  a.w_off = out.w_off;
+  a.c_off = out.c_off;
+  a.N = N;
+  // one image per workgroup when the batch fills the CUs; else each image's 28 tiles split over
+  // segments (each re-stages its first 4 rows)
+  a.segs = std::max(1, std::min(kTilesPerImage / 4, (std::max(1, cus) + N - 1) / N));
+  a.xbytes = static_cast<int>(static_cast<long>(N) * kP * kRowB);
+  a.obytes = static_cast<int>(static_cast<long>(N) * out.Hb * out.Wb * out.Cb * 2);
+  conv1_bf16_ring_kernel<<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace anx::hip

@@ -11,7 +11,8 @@ Names and values:
   ``direct``.
 * integer knobs: ``chunk1``, ``chunk2`` (images per launch), ``conv1_occ``, ``conv2_occ`` (Winograd
   GEMM workgroups-per-CU caps), ``force_vec4``, ``force_scalar`` (direct GEMM tiles), and the bf16
-  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``; ``conv1_band`` (2, the default: the
+  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``, ``bf16_conv1`` (1, the default:
+  Conv1 as the persistent row-band kernel; 0: the implicit-GEMM tiles); ``conv1_band`` (2, the default: the
   Conv1 input transform stages a tile row's image rows in LDS, all 4 phase rows x half the tile
   columns per workgroup; 1: 2 phase rows x all columns; 0: per-tile global gathers);
   ``fuse_pool1`` (1, the
@@ -30,7 +31,7 @@ from .. import _native as nat
 
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
-         "bf16_lrn_tile", "bf16_fc", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
+         "bf16_lrn_tile", "bf16_fc", "bf16_conv1", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
          "conv1_fused")
 
 

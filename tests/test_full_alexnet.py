@@ -191,6 +191,27 @@ def test_full_conv1_polyphase_matches_taps8(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 3, 40, 300])
+def test_conv1_ring_kernel_matches_tile_kernels(cuda, N):
+    """Conv1 as the persistent row-band kernel (knob bf16_conv1=1: polyphase rows in an LDS ring,
+    weights resident, 32x32x16 MFMA) against the implicit-GEMM tile kernels (bf16_conv1=0): the same
+    bf16 products in another fp32 summation order, so conv1 outputs agree to about one bf16 ulp; the
+    segment split (N < CUs: an image's 28 row tiles over several workgroups) and the one-image-per-
+    workgroup form are both covered."""
+    x = (torch.randn(N, 227, 227, 3, generator=torch.Generator().manual_seed(N)) * 3).to(cuda)
+    m = AlexNetFull(seed=19, device=cuda, max_batch=N, knobs={"bf16_conv1": 1})
+    y = m(x).clone()
+    c1 = m.tap(0, N).double()
+    m.set_knob("bf16_conv1", 0)
+    y0 = m(x)
+    r1 = m.tap(0, N).double()
+    torch.cuda.synchronize()
+    assert (c1 - r1).abs().max().item() <= 1.6e-2 * r1.abs().max().item()
+    assert ((c1 - r1).norm() / r1.norm()).item() < 4e-3
+    assert ((y - y0).norm() / y0.norm()).item() < 1e-2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("lrn", ["div_n", "raw"])
 def test_bf16_pool_lrn_wave_kernel_bitwise(cuda, lrn):
     """Pool2+LRN2 as half-wave pixels (bpermute neighbours, default) against the LDS-tile kernel
