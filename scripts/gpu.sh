@@ -63,8 +63,8 @@ for s in "$@"; do
       pmc pmc4 FETCH_SIZE
       pmc pmc5 WRITE_SIZE ;;
     full)
-      run full_bench 300 python bench.py --model full --steps 20 --warmup 5
-      run full_prof 300 rocprofv3 --kernel-trace --stats -d "$O/full_prof" -o run -- python3 bench.py --model full --steps 10 --warmup 3 ;;
+      run full_bench 300 python bench.py --model full --steps 20 --warmup 5 $BARGS
+      run full_prof 300 rocprofv3 --kernel-trace --stats -d "$O/full_prof" -o run -- python3 bench.py --model full --steps 10 --warmup 3 $BARGS ;;
     matrix)
       run matrix_b1 400 bash scripts/run_matrix.sh --no-build --batch 1 --iters 3 --out "$O/matrix"
       run matrix_b256 600 bash scripts/run_matrix.sh --no-build --batch 256 --iters 1 --out "$O/matrix" ;;
