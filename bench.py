@@ -201,14 +201,14 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     wl = None
+    knobs = {k: int(v) if v.lstrip("-").isdigit() else v for k, v in (kv.split("=", 1) for kv in a.knob)}
     if a.model == "full":  # extension config: full AlexNet bf16 (BASELINE.json config 5)
         from anx.models.alexnet_full import FLOPS_PER_IMAGE, AlexNetFull
         B = a.batch_per_gpu or 256
-        model = AlexNetFull(seed=1234, device=dev, max_batch=B, lanes=a.full_lanes)
+        model = AlexNetFull(seed=1234, device=dev, max_batch=B, lanes=a.full_lanes, knobs=knobs)
         out_shape, flops = (1000,), FLOPS_PER_IMAGE
     elif a.workload == "dp":
         B = a.batch_per_gpu or DEFAULT_BATCH["dp"]
-        knobs = {k: int(v) if v.lstrip("-").isdigit() else v for k, v in (kv.split("=", 1) for kv in a.knob)}
         model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=B, lanes=a.lanes,
                               lane_priority=a.lane_priority, knobs=knobs)
         model.stagger = a.stagger
@@ -359,7 +359,7 @@ def main():
                 "config": {"model": "AlexNet full (reference Blocks1-2 + Conv3-5 + FC6-8, 1000 classes)",
                            "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
                            "gflop_per_image": round(flops / 1e9, 4), "tflops": round(imgs * flops / 1e12, 2),
-                           "prewarm_steps": n_pw, "prewarm_ms": prewarm_ms, "lanes": a.full_lanes,
+                           "prewarm_steps": n_pw, "prewarm_ms": prewarm_ms, "lanes": a.full_lanes, "knobs": a.knob,
                            "lane_sync": ("free-running lanes, staggered at a mid-forward event (forward_async)" if pipe.async_lanes
                                          else "lanes forked/joined every step" if a.full_lanes > 1 else "one lane")},
             }

@@ -7,13 +7,13 @@
 // fetched 9 times over (1.3 GB of L2 -> LDS traffic at 256 images), and the layer ran 113 us
 // (profiles/r03_full_bf16_kernels_b256.md) against ~46 us for its HBM bytes.
 //
-// Here one workgroup (4 waves, one per SIMD) walks an image in tiles of two output rows:
-//   * the polyphase rows it needs live in an 8-slot LDS ring (slot = row & 7, 6 KiB each: a row is
-//     57 x 48 bf16 = 5472 B, one contiguous LDS-DMA copy); tile t reads rows 2t .. 2t+3 and the
-//     DMAs of rows 2t+6, 2t+7 (tile t+2) fly behind its MFMAs, so each input row crosses HBM once;
+// Here one workgroup (8 waves, two per SIMD) walks an image in tiles of four output rows:
+//   * the polyphase rows it needs live in a 10-slot LDS ring (slot = row % 10, 6 KiB each: a row is
+//     57 x 48 bf16 = 5472 B, one contiguous LDS-DMA copy); tile t reads rows 4t .. 4t+5 and the
+//     DMAs of rows 4t+6 .. 4t+9 (tile t+1) fly behind its MFMAs, so each input row crosses HBM once;
 //   * all 96 filters' weights stay in LDS for the kernel's lifetime ([96][440] bf16, row stride 880
 //     B: the 32 rows of a 32x32x16 operand read hit distinct bank quads);
-//   * wave w owns pixels 32w .. 32w+31 of the tile (110 valid of 128) x all 96 filters: per K step
+//   * wave w owns pixels 32w .. 32w+31 of the tile (220 valid of 256) x all 96 filters: per K step
 //     (16 of the 432) one pixel fragment and three filter fragments feed three
 //     v_mfma_f32_32x32x16_bf16 (filters as the A operand, so each lane ends up holding 4
 //     consecutive filters of one pixel: 8-B stores, no LDS transpose);
@@ -44,19 +44,22 @@ using lds_void = __attribute__((address_space(3))) void;
 
 constexpr int kP = 57, kCh = 48, kRowB = kP * kCh * 2;  // polyphase rows: 57 x 48 bf16 = 5472 B
 constexpr int kHo = 55, kWo = 55, kK = 96, kKd = 432;  // output rows / cols, filters, GEMM K
-constexpr int kSlots = 8, kSlotB = 6144;                // ring: 8 rows, 6 KiB apart (6 DMA pieces)
+constexpr int kSlots = 10, kSlotB = 6144;               // ring: 10 rows, 6 KiB apart (6 DMA pieces)
 constexpr int kPieces = kSlotB / 1024;
 constexpr int kWRow = 440;                              // weight row stride (bf16): 880 B
 constexpr int kWBytes = 83 * 1024;                      // [96][440] bf16 = 84,480 B, padded to whole DMA pieces
 constexpr int kRing = kSlots * kSlotB;                  // 49,152 B
 constexpr int kBias = kRing + kWBytes;
 constexpr size_t kLds = kBias + kK * 4;                 // 134,528 B
-constexpr int kTilesPerImage = (kHo + 1) / 2;           // 28 (the last holds one row)
-constexpr int kNT = 256;
+constexpr int kRT = 4;                                  // output rows per tile
+constexpr int kTilesPerImage = (kHo + kRT - 1) / kRT;   // 14 (the last holds three rows)
+constexpr int kNT = 512, kWaves = kNT / 64;
 constexpr int kKS = kKd / 16;                           // 27 K steps (3 per tap)
+constexpr int kAhead = 2;                               // K steps of fragments in flight
 constexpr int kOOB = 0x7ffffff0;
 static_assert(kK * kWRow * 2 <= kWBytes && kRowB <= kSlotB, "LDS layout");
-static_assert(2 * kPieces % 4 == 0, "the two rows' DMA pieces split evenly over the 4 waves");
+static_assert(kRT * kPieces % kWaves == 0, "a tile's row DMAs split evenly over the waves");
+constexpr int kDPW = kRT * kPieces / kWaves;            // row DMAs per wave per tile (3)
 
 struct Args {
   const bf16* x;      // [N][57][57][48]
@@ -89,64 +92,58 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
 #endif
   lds_b16* lds3 = (lds_b16*)(lds);
 
-  // ---- one polyphase row into its ring slot: pieces 3 wave .. 3 wave + 2 of the two rows of a
-  // tile (each wave issues exactly 3 DMAs per tile: the vmcnt values below are compile-time)
-  [[maybe_unused]] auto issue_rows = [&](int row0) {  // rows row0, row0 + 1 (zeros past the image)
+  // ---- kRT polyphase rows into their ring slots: pieces kDPW wave .. +kDPW-1 of the group (each
+  // wave issues exactly kDPW DMAs per group: the vmcnt values below are compile-time)
+  [[maybe_unused]] auto issue_rows = [&](int row0) {  // rows row0 .. row0 + kRT - 1 (zeros past the image)
 #if __HIP_DEVICE_COMPILE__
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int q = wave * 3 + i, r = row0 + q / kPieces, pc = q % kPieces;  // wave-uniform
+    for (int i = 0; i < kDPW; ++i) {
+      const int q = wave * kDPW + i, r = row0 + q / kPieces, pc = q % kPieces;  // wave-uniform
       const int src = r < kP ? ((n * kP + r) * kRowB + pc * 1024 + lane * 16) : kOOB;
-      lds_b16* dst = lds3 + ((r & (kSlots - 1)) * kSlotB + pc * 1024) / 2;
+      lds_b16* dst = lds3 + ((r % kSlots) * kSlotB + pc * 1024) / 2;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)dst, 16, src, 0, 0, 0);
     }
 #endif
   };
 
-  // ---- prologue: weights + bias, the first tile's 4 rows and the next tile's 2
+  // ---- prologue: weights + bias, the first tile's 6 rows (two groups)
 #if __HIP_DEVICE_COMPILE__
-  for (int q = wave; q < kWBytes / 1024; q += 4)
+  for (int q = wave; q < kWBytes / 1024; q += kWaves)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(lds3 + (kRing + q * 1024) / 2), 16, q * 1024 + lane * 16, 0,
                                              0, 0);
 #endif
   if (tid < kK) reinterpret_cast<float*>(lds + kBias)[tid] = a.bias[tid];
-  issue_rows(2 * t0);
-  issue_rows(2 * t0 + 2);
-  issue_rows(2 * t0 + 4);  // tile t0 + 1's new rows
+  issue_rows(kRT * t0);
+  issue_rows(kRT * t0 + kRT);
 
   // ---- per-lane fragment addressing. Pixel operand: lane (r, h) reads pixel m = 32 wave + r,
   // channels 16 c + 8 h .. +7 of tap (qh, qw); filter operand: filter 32 nb + r, K 16 ks + 8 h .. +7.
   const int r = lane & 31, h = lane >> 5;
   const int m = 32 * wave + r;
-  const int mrow = m < 2 * kWo ? m / kWo : 0, ox = m < 2 * kWo ? m - mrow * kWo : 0;
+  const int mrow = m < kRT * kWo ? m / kWo : 0, ox = m < kRT * kWo ? m - mrow * kWo : 0;
   const int wbase = kRing + r * (kWRow * 2) + h * 16;
   const int pcol = ox * (kCh * 2) + h * 16;
   f32x16 acc[3];
-  bf16x8 pf[2], wf[2][3];
+  bf16x8 pf[kAhead + 1], wf[kAhead + 1][3];
 
 #if __HIP_DEVICE_COMPILE__
   const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.obytes, 0x00020000);
 #endif
   for (int t = t0; t < t1; ++t) {
-    // Rows 2t .. 2t+3 landed: this wave's DMAs by a counted vmcnt (vmcnt is in order; every wave
-    // issues exactly 3 row DMAs per tile and 12 output stores per tile, so the ops issued after tile
-    // t's rows are: tile t-2's stores, tile t+1's rows (when that tile exists), tile t-1's stores),
-    // every wave's by the barrier, which also retires tile t-1's reads of the slots refilled below.
-    const int k = (t - t0 >= 2 ? 2 : t - t0) * 2 + (t + 1 < t1 ? 1 : 0);
-    switch (k) {
-      case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
-      case 1: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory"); break;
-      case 2: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory"); break;
-      case 3: asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory"); break;
-      case 4: asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory"); break;
-      default: asm volatile("s_waitcnt vmcnt(27) lgkmcnt(0)" ::: "memory"); break;
-    }
+    // Rows 4t .. 4t+5 landed: this wave's DMAs by a counted vmcnt (vmcnt is in order; the last group,
+    // rows 4t+2 .. 4t+5, was issued at tile t-1's start and only tile t-1's 12 output stores per wave
+    // followed it; the first tile waits for the prologue), every wave's by the barrier, which also
+    // retires tile t-1's reads of the slots refilled below.
+    if (t == t0)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < t1) issue_rows(2 * t + 6);  // tile t+2's new rows, into tile t-1's slots
-    const int sb0 = ((2 * t + mrow) & (kSlots - 1)) * kSlotB + pcol;
-    const int sb1 = ((2 * t + mrow + 1) & (kSlots - 1)) * kSlotB + pcol;
-    const int sb2 = ((2 * t + mrow + 2) & (kSlots - 1)) * kSlotB + pcol;
+    if (t + 1 < t1) issue_rows(kRT * t + 6);  // tile t+1's new rows, into tile t-1's first slots
+    const int sb0 = ((kRT * t + mrow) % kSlots) * kSlotB + pcol;
+    const int sb1 = ((kRT * t + mrow + 1) % kSlots) * kSlotB + pcol;
+    const int sb2 = ((kRT * t + mrow + 2) % kSlots) * kSlotB + pcol;
     auto pix = [&](int ks) -> bf16x8 {  // ks compile-time after unrolling
       const int tap = ks / 3, qh = tap / 3, qw = tap - 3 * qh, c16 = ks - 3 * tap;
       const int base = qh == 0 ? sb0 : qh == 1 ? sb1 : sb2;
@@ -157,26 +154,38 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     };
 #pragma unroll
     for (int nb = 0; nb < 3; ++nb) acc[nb] = f32x16{};
-    pf[0] = pix(0);
+    // fragments two K steps ahead (3 register sets), each step's reads pinned above the previous
+    // step's MFMAs: left alone, the compiler re-read right before each MFMA and waited on it
+    sfor<0, kAhead>([&](auto KS) {
+      constexpr int ks = decltype(KS)::value;
+      pf[ks] = pix(ks);
 #pragma unroll
-    for (int nb = 0; nb < 3; ++nb) wf[0][nb] = wgt(0, nb);
+      for (int nb = 0; nb < 3; ++nb) wf[ks][nb] = wgt(ks, nb);
+    });
     sfor<0, kKS>([&](auto KS) {
-      constexpr int ks = decltype(KS)::value, cur = ks & 1;
-      if constexpr (ks + 1 < kKS) {
-        pf[cur ^ 1] = pix(ks + 1);
+      constexpr int ks = decltype(KS)::value, cur = ks % (kAhead + 1), nxt = (ks + kAhead) % (kAhead + 1);
+      if constexpr (ks + kAhead < kKS) {
+        pf[nxt] = pix(ks + kAhead);
 #pragma unroll
-        for (int nb = 0; nb < 3; ++nb) wf[cur ^ 1][nb] = wgt(ks + 1, nb);
+        for (int nb = 0; nb < 3; ++nb) wf[nxt][nb] = wgt(ks + kAhead, nb);
       }
+      // this step's fragments landed (the reads of the steps ahead may fly)
+      if constexpr (ks + kAhead < kKS)
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(4 * kAhead) : "memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(4 * (kKS - 1 - ks)) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int nb = 0; nb < 3; ++nb)
         acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cur][nb], pf[cur], acc[nb], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     });
 
     // ---- epilogue: lane holds pixel m, filters 32 nb + 8 j + 4 h + (0..3) in acc[nb][4 j .. 4 j + 3].
     // 12 buffer stores per lane, always issued (a pixel outside the tile stores past the extent,
     // which drops the write), so the vmcnt counts above hold on every wave.
-    const int oy = 2 * t + mrow;
-    const bool ok = m < 2 * kWo && oy < kHo;
+    const int oy = kRT * t + mrow;
+    const bool ok = m < kRT * kWo && oy < kHo;
     [[maybe_unused]] const int obase =
         ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off) * 2 : kOOB;
     const float* bs = reinterpret_cast<const float*>(lds + kBias);
@@ -233,9 +242,9 @@ hipError_t conv1_bf16_ring(const void* xpoly, int N, const void* wpacked, const 
   a.w_off = out.w_off;
   a.c_off = out.c_off;
   a.N = N;
-  // one image per workgroup when the batch fills the CUs; else each image's 28 tiles split over
-  // segments (each re-stages its first 4 rows)
-  a.segs = std::max(1, std::min(kTilesPerImage / 4, (std::max(1, cus) + N - 1) / N));
+  // one image per workgroup when the batch fills the CUs; else each image's 14 tiles split over
+  // segments (each re-stages its first rows)
+  a.segs = std::max(1, std::min(kTilesPerImage / 2, (std::max(1, cus) + N - 1) / N));
   a.xbytes = static_cast<int>(static_cast<long>(N) * kP * kRowB);
   a.obytes = static_cast<int>(static_cast<long>(N) * out.Hb * out.Wb * out.Cb * 2);
   conv1_bf16_ring_kernel<<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
