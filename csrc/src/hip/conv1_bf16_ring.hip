@@ -7,18 +7,22 @@
 // fetched 9 times over (1.3 GB of L2 -> LDS traffic at 256 images), and the layer ran 113 us
 // (profiles/r03_full_bf16_kernels_b256.md) against ~46 us for its HBM bytes.
 //
-// Here one workgroup (8 waves, two per SIMD) walks an image in tiles of four output rows:
-//   * the polyphase rows it needs live in a 10-slot LDS ring (slot = row % 10, 6 KiB each: a row is
-//     57 x 48 bf16 = 5472 B, one contiguous LDS-DMA copy); tile t reads rows 4t .. 4t+5 and the
-//     DMAs of rows 4t+6 .. 4t+9 (tile t+1) fly behind its MFMAs, so each input row crosses HBM once;
+// Here one workgroup (4 waves, one per SIMD) walks an image in tiles of four output rows:
+//   * the polyphase rows it needs live in a 10-slot LDS ring (slot = row % 10; a row is 57 x 48 bf16
+//     = 5472 B, one LDS-DMA copy of 6 pieces); tile t reads rows 4t .. 4t+5 and the DMAs of rows
+//     4t+6 .. 4t+9 (tile t+1) fly behind its MFMAs, so each input row crosses HBM once;
 //   * all 96 filters' weights stay in LDS for the kernel's lifetime ([96][440] bf16, row stride 880
 //     B: the 32 rows of a 32x32x16 operand read hit distinct bank quads);
-//   * wave w owns pixels 32w .. 32w+31 of the tile (220 valid of 256) x all 96 filters: per K step
-//     (16 of the 432) one pixel fragment and three filter fragments feed three
+//   * wave w owns pixels 64w .. 64w+63 of the tile (220 valid of 256) x all 96 filters: per K step
+//     (16 of the 432) two pixel fragments and three filter fragments feed six
 //     v_mfma_f32_32x32x16_bf16 (filters as the A operand, so each lane ends up holding 4
-//     consecutive filters of one pixel: 8-B stores, no LDS transpose);
+//     consecutive filters of one pixel: 8-B stores, no LDS transpose). 5 fragment reads per 6 MFMAs
+//     keep the LDS at ~40 % of its rate (the 8-wave 32-pixel form read 4 per 3 and ran the MFMA pipe
+//     28 % busy with 21 % of LDS cycles in bank conflicts);
+//   * a polyphase column's six 16-B channel units are stored in the order k ^ ((column >> 3) & 1)
+//     (applied on the DMA's source side), which halves the pixel reads' bank conflicts;
 //   * bias + ReLU + bf16 in the epilogue, straight into the NHWC output.
-// Fragments are read one K step ahead of their MFMAs (registers double-buffered).
+// Fragments are read two K steps ahead of their MFMAs (registers triple-buffered).
 //
 // Reference op: convKernel (final_project/v3_cuda_only/src/layers_cuda.cu:20-46); the full-network
 // tail is the extension's own.
@@ -44,8 +48,8 @@ using lds_void = __attribute__((address_space(3))) void;
 
 constexpr int kP = 57, kCh = 48, kRowB = kP * kCh * 2;  // polyphase rows: 57 x 48 bf16 = 5472 B
 constexpr int kHo = 55, kWo = 55, kK = 96, kKd = 432;  // output rows / cols, filters, GEMM K
-constexpr int kSlots = 10, kSlotB = 6144;               // ring: 10 rows, 6 KiB apart (6 DMA pieces)
-constexpr int kPieces = kSlotB / 1024;
+constexpr int kSlots = 10, kPieces = 6;                 // ring: 10 rows of 6 DMA pieces (6 KiB)
+constexpr int kSlotB = kPieces * 1024 + 16;             // + one 16-B unit: a slot change shifts the banks
 constexpr int kWRow = 440;                              // weight row stride (bf16): 880 B
 constexpr int kWBytes = 83 * 1024;                      // [96][440] bf16 = 84,480 B, padded to whole DMA pieces
 constexpr int kRing = kSlots * kSlotB;                  // 49,152 B
@@ -53,13 +57,15 @@ constexpr int kBias = kRing + kWBytes;
 constexpr size_t kLds = kBias + kK * 4;                 // 134,528 B
 constexpr int kRT = 4;                                  // output rows per tile
 constexpr int kTilesPerImage = (kHo + kRT - 1) / kRT;   // 14 (the last holds three rows)
-constexpr int kNT = 512, kWaves = kNT / 64;
+constexpr int kNT = 256, kWaves = kNT / 64, kPB = 2;   // waves, 32-pixel blocks per wave
 constexpr int kKS = kKd / 16;                           // 27 K steps (3 per tap)
 constexpr int kAhead = 2;                               // K steps of fragments in flight
 constexpr int kOOB = 0x7ffffff0;
-static_assert(kK * kWRow * 2 <= kWBytes && kRowB <= kSlotB, "LDS layout");
+static_assert(kK * kWRow * 2 <= kWBytes && kRowB <= kPieces * 1024 && kRing % 16 == 0, "LDS layout");
+static_assert(kWaves * kPB * 32 >= kRT * kWo, "a tile's pixels fit the waves' blocks");
 static_assert(kRT * kPieces % kWaves == 0, "a tile's row DMAs split evenly over the waves");
-constexpr int kDPW = kRT * kPieces / kWaves;            // row DMAs per wave per tile (3)
+constexpr int kDPW = kRT * kPieces / kWaves;            // row DMAs per wave per tile (6)
+constexpr int kSPW = kPB * 12;                          // output stores per wave per tile (24)
 
 struct Args {
   const bf16* x;      // [N][57][57][48]
@@ -90,7 +96,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.w), 0, kWBytes, 0x00020000);
 #endif
-  lds_b16* lds3 = (lds_b16*)(lds);
+  [[maybe_unused]] lds_b16* lds3 = (lds_b16*)(lds);
 
   // ---- kRT polyphase rows into their ring slots: pieces kDPW wave .. +kDPW-1 of the group (each
   // wave issues exactly kDPW DMAs per group: the vmcnt values below are compile-time)
@@ -99,7 +105,9 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
 #pragma unroll
     for (int i = 0; i < kDPW; ++i) {
       const int q = wave * kDPW + i, r = row0 + q / kPieces, pc = q % kPieces;  // wave-uniform
-      const int src = r < kP ? ((n * kP + r) * kRowB + pc * 1024 + lane * 16) : kOOB;
+      // LDS unit u of the slot holds column u / 6, channel unit (u % 6) ^ ((column >> 3) & 1)
+      const int u = pc * 64 + lane, col = u / 6, k = (u - col * 6) ^ ((col >> 3) & 1);
+      const int src = r < kP && u < kP * 6 ? ((n * kP + r) * kRowB + col * (kCh * 2) + k * 16) : kOOB;
       lds_b16* dst = lds3 + ((r % kSlots) * kSlotB + pc * 1024) / 2;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)dst, 16, src, 0, 0, 0);
     }
@@ -116,92 +124,108 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
   issue_rows(kRT * t0);
   issue_rows(kRT * t0 + kRT);
 
-  // ---- per-lane fragment addressing. Pixel operand: lane (r, h) reads pixel m = 32 wave + r,
-  // channels 16 c + 8 h .. +7 of tap (qh, qw); filter operand: filter 32 nb + r, K 16 ks + 8 h .. +7.
+  // ---- per-lane fragment addressing. Pixel operand: lane (r, h) reads pixel m = 64 wave + 32 b + r,
+  // channels 16 c + 8 h .. +7 of tap (qh, qw) (unit 2c + h, swizzled); filter operand: filter
+  // 32 nb + r, K 16 ks + 8 h .. +7.
   const int r = lane & 31, h = lane >> 5;
-  const int m = 32 * wave + r;
-  const int mrow = m < kRT * kWo ? m / kWo : 0, ox = m < kRT * kWo ? m - mrow * kWo : 0;
+  int mrow[kPB], ox[kPB], po[kPB][3];
+#pragma unroll
+  for (int b = 0; b < kPB; ++b) {
+    const int m = 64 * wave + 32 * b + r;
+    mrow[b] = m < kRT * kWo ? m / kWo : 0;
+    ox[b] = m < kRT * kWo ? m - mrow[b] * kWo : 0;
+#pragma unroll
+    for (int qw = 0; qw < 3; ++qw) {
+      const int c = ox[b] + qw;
+      po[b][qw] = c * (kCh * 2) + (h ^ ((c >> 3) & 1)) * 16;
+    }
+  }
   const int wbase = kRing + r * (kWRow * 2) + h * 16;
-  const int pcol = ox * (kCh * 2) + h * 16;
-  f32x16 acc[3];
-  bf16x8 pf[kAhead + 1], wf[kAhead + 1][3];
+  f32x16 acc[kPB][3];
+  bf16x8 pf[kAhead + 1][kPB], wf[kAhead + 1][3];
 
 #if __HIP_DEVICE_COMPILE__
   const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.obytes, 0x00020000);
 #endif
   for (int t = t0; t < t1; ++t) {
     // Rows 4t .. 4t+5 landed: this wave's DMAs by a counted vmcnt (vmcnt is in order; the last group,
-    // rows 4t+2 .. 4t+5, was issued at tile t-1's start and only tile t-1's 12 output stores per wave
-    // followed it; the first tile waits for the prologue), every wave's by the barrier, which also
-    // retires tile t-1's reads of the slots refilled below.
+    // rows 4t+2 .. 4t+5, was issued at tile t-1's start and only tile t-1's kSPW output stores per
+    // wave followed it; the first tile waits for the prologue), every wave's by the barrier, which
+    // also retires tile t-1's reads of the slots refilled below.
     if (t == t0)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     else
-      asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kSPW) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (t + 1 < t1) issue_rows(kRT * t + 6);  // tile t+1's new rows, into tile t-1's first slots
-    const int sb0 = ((kRT * t + mrow) % kSlots) * kSlotB + pcol;
-    const int sb1 = ((kRT * t + mrow + 1) % kSlots) * kSlotB + pcol;
-    const int sb2 = ((kRT * t + mrow + 2) % kSlots) * kSlotB + pcol;
-    auto pix = [&](int ks) -> bf16x8 {  // ks compile-time after unrolling
+    int sb[kPB][3];
+#pragma unroll
+    for (int b = 0; b < kPB; ++b)
+#pragma unroll
+      for (int qh = 0; qh < 3; ++qh) sb[b][qh] = ((kRT * t + mrow[b] + qh) % kSlots) * kSlotB;
+    auto pix = [&](int ks, int b) -> bf16x8 {  // ks compile-time after unrolling
       const int tap = ks / 3, qh = tap / 3, qw = tap - 3 * qh, c16 = ks - 3 * tap;
-      const int base = qh == 0 ? sb0 : qh == 1 ? sb1 : sb2;
-      return *reinterpret_cast<const bf16x8*>(lds + base + qw * (kCh * 2) + c16 * 32);
+      return *reinterpret_cast<const bf16x8*>(lds + sb[b][qh] + po[b][qw] + c16 * 32);
     };
     auto wgt = [&](int ks, int nb) -> bf16x8 {
       return *reinterpret_cast<const bf16x8*>(lds + wbase + nb * 32 * (kWRow * 2) + ks * 32);
     };
+    auto load_step = [&](int ks, int set) {
 #pragma unroll
-    for (int nb = 0; nb < 3; ++nb) acc[nb] = f32x16{};
-    // fragments two K steps ahead (3 register sets), each step's reads pinned above the previous
-    // step's MFMAs: left alone, the compiler re-read right before each MFMA and waited on it
-    sfor<0, kAhead>([&](auto KS) {
-      constexpr int ks = decltype(KS)::value;
-      pf[ks] = pix(ks);
+      for (int b = 0; b < kPB; ++b) pf[set][b] = pix(ks, b);
 #pragma unroll
-      for (int nb = 0; nb < 3; ++nb) wf[ks][nb] = wgt(ks, nb);
-    });
+      for (int nb = 0; nb < 3; ++nb) wf[set][nb] = wgt(ks, nb);
+    };
+#pragma unroll
+    for (int b = 0; b < kPB; ++b)
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) acc[b][nb] = f32x16{};
+    // fragments kAhead K steps ahead, each step's reads pinned above the previous step's MFMAs
+    // (left alone, the compiler re-read right before each MFMA and waited on it)
+    sfor<0, kAhead>([&](auto KS) { load_step(decltype(KS)::value, decltype(KS)::value); });
     sfor<0, kKS>([&](auto KS) {
       constexpr int ks = decltype(KS)::value, cur = ks % (kAhead + 1), nxt = (ks + kAhead) % (kAhead + 1);
-      if constexpr (ks + kAhead < kKS) {
-        pf[nxt] = pix(ks + kAhead);
-#pragma unroll
-        for (int nb = 0; nb < 3; ++nb) wf[nxt][nb] = wgt(ks + kAhead, nb);
-      }
+      constexpr int per = kPB + 3;  // fragment reads per step
+      if constexpr (ks + kAhead < kKS) load_step(ks + kAhead, nxt);
       // this step's fragments landed (the reads of the steps ahead may fly)
       if constexpr (ks + kAhead < kKS)
-        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(4 * kAhead) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(per * kAhead) : "memory");
       else
-        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(4 * (kKS - 1 - ks)) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(per * (kKS - 1 - ks)) : "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int nb = 0; nb < 3; ++nb)
-        acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cur][nb], pf[cur], acc[nb], 0, 0, 0);
+      for (int b = 0; b < kPB; ++b)
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb)
+          acc[b][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cur][nb], pf[cur][b], acc[b][nb], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     });
 
-    // ---- epilogue: lane holds pixel m, filters 32 nb + 8 j + 4 h + (0..3) in acc[nb][4 j .. 4 j + 3].
-    // 12 buffer stores per lane, always issued (a pixel outside the tile stores past the extent,
+    // ---- epilogue: lane holds pixel m, filters 32 nb + 8 j + 4 h + (0..3) in acc[b][nb][4 j .. 4 j + 3].
+    // kSPW buffer stores per lane, always issued (a pixel outside the tile stores past the extent,
     // which drops the write), so the vmcnt counts above hold on every wave.
-    const int oy = kRT * t + mrow;
-    const bool ok = m < kRT * kWo && oy < kHo;
-    [[maybe_unused]] const int obase =
-        ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox + a.w_off) * a.Cb + a.c_off) * 2 : kOOB;
     const float* bs = reinterpret_cast<const float*>(lds + kBias);
 #pragma unroll
-    for (int nb = 0; nb < 3; ++nb)
+    for (int b = 0; b < kPB; ++b) {
+      const int m = 64 * wave + 32 * b + r, oy = kRT * t + mrow[b];
+      const bool ok = m < kRT * kWo && oy < kHo;
+      [[maybe_unused]] const int obase =
+          ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox[b] + a.w_off) * a.Cb + a.c_off) * 2 : kOOB;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f = 32 * nb + 8 * j + 4 * h;
-        const f32x4 b = *reinterpret_cast<const f32x4*>(bs + f);
-        bf16x4 v;
+      for (int nb = 0; nb < 3; ++nb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[nb][4 * j + i] + b[i], 0.f));
+        for (int j = 0; j < 4; ++j) {
+          const int f = 32 * nb + 8 * j + 4 * h;
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(bs + f);
+          bf16x4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
 #if __HIP_DEVICE_COMPILE__
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f * 2, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f * 2, 0);
 #endif
-      }
+        }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
 }
