@@ -64,7 +64,7 @@ constexpr int kOOB = 0x7ffffff0;
 static_assert(kK * kWRow * 2 <= kWBytes && kRowB <= kPieces * 1024 && kRing % 16 == 0, "LDS layout");
 static_assert(kWaves * kPB * 32 >= kRT * kWo, "a tile's pixels fit the waves' blocks");
 static_assert(kRT * kPieces % kWaves == 0, "a tile's row DMAs split evenly over the waves");
-constexpr int kDPW = kRT * kPieces / kWaves;            // row DMAs per wave per tile (6)
+[[maybe_unused]] constexpr int kDPW = kRT * kPieces / kWaves;            // row DMAs per wave per tile (6)
 constexpr int kSPW = kPB * 12;                          // output stores per wave per tile (24)
 
 struct Args {
