@@ -90,8 +90,10 @@ hipError_t f32_to_bf16_s2d4(const float* x, void* y, int N, int H, int W, hipStr
 // (conv1_ring_weight_bytes() bytes), bias + ReLU (relu must be true), bf16 NHWC out (55x55x96 view).
 void pack_conv1_ring_weights(const float* w_k48_33, std::vector<uint16_t>& out);
 size_t conv1_ring_weight_bytes();
-hipError_t conv1_bf16_ring(const void* xpoly, int N, const void* wpacked, const float* bias, OutViewB out, bool relu,
-                           hipStream_t s, int cus = 256);
+// f32_input: x is the fp32 NHWC image [N,227,227,3] (space-to-depth + bf16 conversion inside the
+// kernel, no polyphase copy); else the polyphase bf16 image of f32_to_bf16_s2d4.
+hipError_t conv1_bf16_ring(const void* x, int N, const void* wpacked, const float* bias, OutViewB out, bool relu,
+                           hipStream_t s, int cus = 256, bool f32_input = false);
 
 }  // namespace hip
 

@@ -30,7 +30,8 @@ struct Knobs {
                            // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
   int bf16_conv1 = 0;      // bf16 Conv1 (polyphase): 1 = the persistent row-band kernel (conv1_bf16_ring.hip:
-                           // input rows in an LDS ring, weights resident), 0 = the implicit-GEMM tile kernels
+                           // input rows in an LDS ring, weights resident), 2 = the same on the fp32 image
+                           // (space-to-depth inside, no s2d4 pass), 0 = s2d4 + the implicit-GEMM tile kernels
   int conv1_occ = 0;       // cap on the Conv1 Winograd GEMM's workgroups per CU (LDS padding; 0 = none: 4)
   int conv2_occ = -1;      // ... and Conv2's (0 = none: 2; -1 = auto: 1 when the launch has <= one workgroup per
                            // CU); a cap leaves room for a concurrent lane's kernels

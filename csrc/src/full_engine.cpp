@@ -196,11 +196,16 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
     const int n = std::min(chunk_, N - n0);
     const float* xn = x + static_cast<size_t>(n0) * 227 * 227 * 3;
     if (poly1_) {
-      ANX_TRY(hip::f32_to_bf16_s2d4(xn, xb_, n, 227, 227, s));
-      if (k_.bf16_conv1 == 1)
-        ANX_TRY(hip::conv1_bf16_ring(xb_, n, w1ring_, L_[0].bias, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, true, s, cus_));
-      else
-        ANX_TRY(conv(L_[0], n, 57, 57, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
+      if (k_.bf16_conv1 == 2) {  // the fp32 image straight into the row-band kernel (no polyphase copy)
+        ANX_TRY(hip::conv1_bf16_ring(xn, n, w1ring_, L_[0].bias, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, true, s, cus_,
+                                     true));
+      } else {
+        ANX_TRY(hip::f32_to_bf16_s2d4(xn, xb_, n, 227, 227, s));
+        if (k_.bf16_conv1 == 1)
+          ANX_TRY(hip::conv1_bf16_ring(xb_, n, w1ring_, L_[0].bias, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, true, s, cus_));
+        else
+          ANX_TRY(conv(L_[0], n, 57, 57, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
+      }
     } else {
       ANX_TRY(hip::f32_to_bf16(xn, xb_, static_cast<size_t>(n) * 227 * 227 * 3, s));
       ANX_TRY(conv(L_[0], n, 227, 227, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));

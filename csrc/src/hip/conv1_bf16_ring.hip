@@ -68,7 +68,7 @@ static_assert(kRT * kPieces % kWaves == 0, "a tile's row DMAs split evenly over 
 constexpr int kSPW = kPB * 12;                          // output stores per wave per tile (24)
 
 struct Args {
-  const bf16* x;      // [N][57][57][48]
+  const void* x;      // F32IN: [N][227][227][3] fp32 images; else [N][57][57][48] bf16 polyphase
   const bf16* w;      // [96][440] (K = tap * 48 + channel, zero past 432), kWBytes bytes
   const float* bias;  // [96]
   bf16* out;          // NHWC through the view
@@ -85,6 +85,12 @@ __device__ __forceinline__ void sfor(F&& f) {
   }
 }
 
+// F32IN: the space-to-depth and bf16 conversion happen here (the image's fp32 rows are loaded to
+// registers one tile ahead and written into the ring converted and swizzled), so neither the
+// s2d4 kernel nor its 80 MB polyphase copy runs.
+constexpr int kUnitsPerRow = 4 * kP;                     // a polyphase row: 4 image rows x 57 (12-float) units
+constexpr int kUPT = (kRT * kUnitsPerRow + kNT - 1) / kNT;  // units per thread per tile (4)
+template <bool F32IN>
 __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -93,7 +99,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
   const int t0 = seg * kTilesPerImage / a.segs, t1 = (seg + 1) * kTilesPerImage / a.segs;
   if (n >= a.N || t0 >= t1) return;  // whole workgroup, before any barrier
 #if __HIP_DEVICE_COMPILE__
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.w), 0, kWBytes, 0x00020000);
 #endif
   [[maybe_unused]] lds_b16* lds3 = (lds_b16*)(lds);
@@ -114,6 +120,43 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
 #endif
   };
 
+  // ---- F32IN: polyphase rows from the fp32 image. Unit e of a group of kRT rows = (row j, phase
+  // row rh, column c): 12 floats (4 image columns x 3 channels) -> 12 bf16 at channels 12 rh .. +11
+  // of column c, written as three 8-B pieces at their swizzled 16-B units.
+  [[maybe_unused]] float xu[kUPT][12];
+  [[maybe_unused]] auto load_units = [&](int row0) {  // rows row0 .. row0 + kRT - 1 into xu
+#if __HIP_DEVICE_COMPILE__
+#pragma unroll
+    for (int i = 0; i < kUPT; ++i) {
+      const int e = tid + kNT * i, j = e / kUnitsPerRow, rem = e - j * kUnitsPerRow;
+      const int rh = rem / kP, c = rem - rh * kP, pr = row0 + j, row = 4 * pr + rh;
+      const bool ok = e < kRT * kUnitsPerRow && pr < kP && row < 227;
+      const int base = ok ? ((n * 227 + row) * 227 + 4 * c) * 3 * 4 : kOOB;
+#pragma unroll
+      for (int f = 0; f < 12; ++f)  // column 227 (c = 56, f >= 9) does not exist: past the extent
+        xu[i][f] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(xr, c == kP - 1 && f >= 9 ? kOOB : base, f * 4, 0));
+    }
+#endif
+  };
+  [[maybe_unused]] auto store_units = [&](int row0) {
+#pragma unroll
+    for (int i = 0; i < kUPT; ++i) {
+      const int e = tid + kNT * i, j = e / kUnitsPerRow, rem = e - j * kUnitsPerRow;
+      if (e >= kRT * kUnitsPerRow) continue;
+      const int rh = rem / kP, c = rem - rh * kP, sw = (c >> 3) & 1;
+      char* col = lds + ((row0 + j) % kSlots) * kSlotB + c * (kCh * 2);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int lb = rh * 24 + q * 8;  // logical byte in the column's 96
+        bf16x4 v;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) v[f] = static_cast<bf16>(xu[i][4 * q + f]);
+        *reinterpret_cast<bf16x4*>(col + (((lb >> 4) ^ sw) << 4) + (lb & 15)) = v;
+      }
+    }
+  };
+
   // ---- prologue: weights + bias, the first tile's 6 rows (two groups)
 #if __HIP_DEVICE_COMPILE__
   for (int q = wave; q < kWBytes / 1024; q += kWaves)
@@ -121,8 +164,15 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
                                              0, 0);
 #endif
   if (tid < kK) reinterpret_cast<float*>(lds + kBias)[tid] = a.bias[tid];
-  issue_rows(kRT * t0);
-  issue_rows(kRT * t0 + kRT);
+  if constexpr (F32IN) {
+    load_units(kRT * t0);
+    store_units(kRT * t0);
+    load_units(kRT * t0 + kRT);
+    store_units(kRT * t0 + kRT);
+  } else {
+    issue_rows(kRT * t0);
+    issue_rows(kRT * t0 + kRT);
+  }
 
   // ---- per-lane fragment addressing. Pixel operand: lane (r, h) reads pixel m = 64 wave + 32 b + r,
   // channels 16 c + 8 h .. +7 of tap (qh, qw) (unit 2c + h, swizzled); filter operand: filter
@@ -154,11 +204,18 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     // also retires tile t-1's reads of the slots refilled below.
     if (t == t0)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if constexpr (F32IN)  // the rows were written by ds_write at tile t-1's end
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kSPW) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 1 < t1) issue_rows(kRT * t + 6);  // tile t+1's new rows, into tile t-1's first slots
+    if (t + 1 < t1) {  // tile t+1's new rows, into tile t-1's first slots
+      if constexpr (F32IN)
+        load_units(kRT * t + 6);
+      else
+        issue_rows(kRT * t + 6);
+    }
     int sb[kPB][3];
 #pragma unroll
     for (int b = 0; b < kPB; ++b)
@@ -226,6 +283,10 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
 #endif
         }
     }
+    // F32IN: tile t+1's new rows (loaded at this tile's start) into tile t-1's slots, which no wave
+    // reads in tile t; the next tile's barrier publishes them
+    if constexpr (F32IN)
+      if (t + 1 < t1) store_units(kRT * t + 6);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
 }
@@ -244,18 +305,24 @@ void pack_conv1_ring_weights(const float* w_k48_33, std::vector<uint16_t>& out) 
 
 size_t conv1_ring_weight_bytes() { return kWBytes; }
 
-hipError_t conv1_bf16_ring(const void* xpoly, int N, const void* wpacked, const float* bias, OutViewB out, bool relu,
-                           hipStream_t s, int cus) {
+hipError_t conv1_bf16_ring(const void* xin, int N, const void* wpacked, const float* bias, OutViewB out, bool relu,
+                           hipStream_t s, int cus, bool f32_input) {
   if (N <= 0) return hipSuccess;
   if (!relu || !out.base || out.Cb % 4 || out.c_off % 4 || static_cast<long>(N) * kP * kRowB >= (1L << 31) ||
       static_cast<long>(N) * out.Hb * out.Wb * out.Cb * 2 >= (1L << 31) || out.Hb < kHo + out.h_off ||
       out.Wb < kWo + out.w_off || out.Cb < kK + out.c_off)
     return hipErrorInvalidValue;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_bf16_ring_kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const hipError_t attr = [] {
+    for (const void* k : {reinterpret_cast<const void*>(conv1_bf16_ring_kernel<false>),
+                          reinterpret_cast<const void*>(conv1_bf16_ring_kernel<true>)}) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }();
   if (attr != hipSuccess) return attr;
   Args a{};
-  a.x = static_cast<const bf16*>(xpoly);
+  a.x = xin;
   a.w = static_cast<const bf16*>(wpacked);
   a.bias = bias;
   a.out = out.base;
@@ -269,9 +336,14 @@ hipError_t conv1_bf16_ring(const void* xpoly, int N, const void* wpacked, const 
   // one image per workgroup when the batch fills the CUs; else each image's 14 tiles split over
   // segments (each re-stages its first rows)
   a.segs = std::max(1, std::min(kTilesPerImage / 2, (std::max(1, cus) + N - 1) / N));
-  a.xbytes = static_cast<int>(static_cast<long>(N) * kP * kRowB);
+  const long xb = f32_input ? static_cast<long>(N) * 227 * 227 * 3 * 4 : static_cast<long>(N) * kP * kRowB;
+  if (xb >= (1L << 31)) return hipErrorInvalidValue;
+  a.xbytes = static_cast<int>(xb);
   a.obytes = static_cast<int>(static_cast<long>(N) * out.Hb * out.Wb * out.Cb * 2);
-  conv1_bf16_ring_kernel<<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
+  if (f32_input)
+    conv1_bf16_ring_kernel<true><<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
+  else
+    conv1_bf16_ring_kernel<false><<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
   return hipGetLastError();
 }
 

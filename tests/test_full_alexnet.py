@@ -191,15 +191,17 @@ def test_full_conv1_polyphase_matches_taps8(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("N", [1, 3, 40, 300])
-def test_conv1_ring_kernel_matches_tile_kernels(cuda, N):
+def test_conv1_ring_kernel_matches_tile_kernels(cuda, N, mode):
     """Conv1 as the persistent row-band kernel (knob bf16_conv1=1: polyphase rows in an LDS ring,
-    weights resident, 32x32x16 MFMA) against the implicit-GEMM tile kernels (bf16_conv1=0): the same
-    bf16 products in another fp32 summation order, so conv1 outputs agree to about one bf16 ulp; the
-    segment split (N < CUs: an image's 28 row tiles over several workgroups) and the one-image-per-
-    workgroup form are both covered."""
+    weights resident, 32x32x16 MFMA; 2: the same reading the fp32 image, space-to-depth + bf16
+    inside) against s2d4 + the implicit-GEMM tile kernels (bf16_conv1=0): the same bf16 products in
+    another fp32 summation order, so conv1 outputs agree to about one bf16 ulp; the segment split
+    (N < CUs: an image's 14 row tiles over several workgroups) and the one-image-per-workgroup form
+    are both covered."""
     x = (torch.randn(N, 227, 227, 3, generator=torch.Generator().manual_seed(N)) * 3).to(cuda)
-    m = AlexNetFull(seed=19, device=cuda, max_batch=N, knobs={"bf16_conv1": 1})
+    m = AlexNetFull(seed=19, device=cuda, max_batch=N, knobs={"bf16_conv1": mode})
     y = m(x).clone()
     c1 = m.tap(0, N).double()
     m.set_knob("bf16_conv1", 0)
