@@ -48,6 +48,9 @@ using C2_32x4 = wg::Cfg<49, 96, 2, 2, 32, 4>;    // 64 KiB ring: 2 slices in fli
 // 64 tiles x 128 filters, 8 waves, 72 KiB ring: a quarter less operand traffic per FLOP, but 636 vs 623 us
 // alone at 300 images and 246-247 k vs 255 k images/s in the bench step (profiles/r03_conv2_wide_*)
 using C2_64x128 = wg::Cfg<49, 96, 2, 4, 48, 2>;
+using C2_64x64s3 = wg::Cfg<49, 96, 2, 2, 48, 3>;  // 64 x 64, 3-slot ring (72 KiB: still 2 workgroups per CU)
+using C2_64x128s3 = wg::Cfg<49, 96, 2, 4, 48, 3>; // 64 x 128, 8 waves, 3-slot ring (108 KiB)
+using C2_128x64 = wg::Cfg<49, 96, 4, 2, 48, 2>;   // 128 tiles x 64 filters, 8 waves (V read by 4 workgroups, U by half as many)
 using C1_64x96 = wg::Cfg<25, 48, 2, 3, 48, 2>;   // 64 x 96 (every filter: V read once), 6 waves, 60 KiB ring
 using C1_32x96 = wg::Cfg<25, 48, 1, 3, 48, 2>;   // 32 x 96, 3 waves, 48 KiB ring
 using C1_48x2w4 = wg::Cfg<25, 48, 4, 1, 48, 2>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
@@ -102,6 +105,9 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
 #ifdef ANX_WGEMM_ABLATIONS
         case 1: e = launch_abl<C2_32x4>(a, s, occ, abl); break;
         case 2: e = launch_abl<C2_64x128>(a, s, occ, abl); break;
+        case 3: e = launch_abl<C2_64x64s3>(a, s, occ, abl); break;
+        case 4: e = launch_abl<C2_64x128s3>(a, s, occ, abl); break;
+        case 5: e = launch_abl<C2_128x64>(a, s, occ, abl); break;
 #endif
         default: break;
       }

@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
     const auto ref = download(y0, ny);
     std::printf("{\"conv\": 2, \"images\": %d, \"arm\": \"production wino_conv2\", \"us\": %.1f, \"tflops\": %.1f}\n",
                 images, t_old, flop / t_old * 1e-6);
-    for (int cfg = 0; cfg < 4; ++cfg)
+    for (int cfg = 0; cfg < 6; ++cfg)
       for (int abl : kAbl) {
         if (only_cfg >= 0 && cfg != only_cfg) continue;
         const hip::OutView ov{y1, 27, 27, 256, 0, 0, 0};
