@@ -164,6 +164,45 @@ def test_root_batch_shed_gloo(mode):
     torch.testing.assert_close(y[1:], ref[1:], rtol=0, atol=0)
 
 
+def _shed_reject_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import anx  # noqa: F401
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.parallel.pipeline import PipelineConfig, ScatterComputeGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d = anx.blocks_dims()
+    m = AlexNetBlocks(init="rand", seed=2, device="cpu")
+    errs = []
+    for cfg in (PipelineConfig(2, scatter=True, root_batch=1),     # the root's input is scattered
+                PipelineConfig(4, micro=2, scatter=False, root_batch=1),  # fewer micro-batches on the root
+                PipelineConfig(2, scatter=False, root_batch=3)):  # more than a peer's batch
+        try:
+            ScatterComputeGather(m, cfg, (d.H, d.W, d.C0), (d.Hp2, d.Wp2, d.C2), "cpu")
+            errs.append(None)
+        except ValueError as e:
+            errs.append(str(e))
+    q.put(errs)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_root_batch_rejects_unsupported_shapes():
+    """root_batch needs local input, the peers' micro-batch count and at most a peer's batch."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_shed_reject_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    errs = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for e in errs:
+        assert all(x is not None for x in e), e
+
+
 def _prefetch_changing_worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     import anx  # noqa: F401
