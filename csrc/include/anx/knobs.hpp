@@ -28,6 +28,7 @@ struct Knobs {
                            // picks the config, -2 off (the 128x128 kernels above), 0.. force that config
   int bf16_fc = 0;         // bf16 FC layers: 1 = activation-streaming kernel (fc_bf16; measured slower than the
                            // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
+  int bf16_fc_cfg = -1;    // bf16 FC layers: force this wide-tile config (A/B; -1 = cfg 8, 256x64 3-stage)
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
   int bf16_conv1 = 0;      // bf16 Conv1 (polyphase): 1 = the persistent row-band kernel (conv1_bf16_ring.hip:
                            // input rows in an LDS ring, weights resident), 2 = the same on the fp32 image

@@ -214,6 +214,25 @@ def test_conv1_ring_kernel_matches_tile_kernels(cuda, N, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 1, 5])
+def test_fc_forced_wide_tile_configs(cuda, cfg):
+    """FC6-8 on a forced wide-tile config (knob bf16_fc_cfg, its own K split <= 16 slabs) against the
+    default cfg 8: the same bf16 products summed in another order."""
+    N = 40
+    x = (init_input(N, "rand", seed=23) * 10).to(cuda)
+    m = AlexNetFull(seed=23, device=cuda, max_batch=N)
+    ref = m(x).clone()
+    ref_taps = [m.tap(i, N).double() for i in (8, 9)]
+    m.set_knob("bf16_fc_cfg", cfg)
+    got = m(x)
+    torch.cuda.synchronize()
+    for i, r in zip((8, 9), ref_taps):
+        t = m.tap(i, N).double()
+        assert ((t - r).norm() / r.norm()).item() < 1e-2, i
+    assert ((got - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("lrn", ["div_n", "raw"])
 def test_bf16_pool_lrn_wave_kernel_bitwise(cuda, lrn):
     """Pool2+LRN2 as half-wave pixels (bpermute neighbours, default) against the LDS-tile kernel
