@@ -264,6 +264,7 @@ std::string model_curve_json(Workload wl, const std::vector<int>& nps, int batch
                   (weak ? "weak" : "strong") + "\", ";
   s += "\"N\": " + arr([](const StepCost& c) { return c.np; }, "%d") + ", ";
   s += "\"row_ways\": " + arr([](const StepCost& c) { return c.row_ways; }, "%d") + ", ";
+  s += "\"root_batch\": " + arr([](const StepCost& c) { return c.root_batch; }, "%d") + ", ";
   s += "\"step_ms\": " + arr([](const StepCost& c) { return c.step_ms; }, "%.4f") + ", ";
   s += "\"images_per_s\": " + arr([](const StepCost& c) { return c.images_per_s; }, "%.0f") + ", ";
   s += "\"speedup\": " +

@@ -70,9 +70,13 @@ def dp_root_batch(np_: int, batch: int, overrides=None) -> int:
 
 
 def table(c: dict) -> str:
-    """Markdown table of a curve (the README's scaling section is generated from these)."""
-    lines = ["| N | row ways | step ms | images/s | speedup | efficiency | bound |", "|---:|---:|---:|---:|---:|---:|---|"]
+    """Markdown table of a curve (the README's scaling section is generated from these); dp curves add
+    the images rank 0 computes per step (its shed share)."""
+    dp = c.get("workload") == "dp"
+    head = "| N | row ways | " + ("rank-0 images | " if dp else "") + "step ms | images/s | speedup | efficiency | bound |"
+    lines = [head, "|---:|---:|" + ("---:|" if dp else "") + "---:|---:|---:|---:|---|"]
     for i, n in enumerate(c["N"]):
-        lines.append(f"| {n} | {c['row_ways'][i]} | {c['step_ms'][i]:.3f} | {c['images_per_s'][i]:,.0f} | "
+        root = f"{c['root_batch'][i]} | " if dp else ""
+        lines.append(f"| {n} | {c['row_ways'][i]} | {root}{c['step_ms'][i]:.3f} | {c['images_per_s'][i]:,.0f} | "
                      f"{c['speedup'][i]:.2f} | {c['efficiency'][i]:.2f} | {c['bound'][i]} |")
     return "\n".join(lines)

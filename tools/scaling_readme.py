@@ -30,8 +30,8 @@ def render() -> str:
         out.append(f"**{title}** (modelled, not measured)\n\n{cost.table(c)}\n")
     p = cost.curve("dp", 128)["params"]
     out.append(f"Model inputs: single-GPU throughput vs images per launch {p['rate']} (measured); H2D "
-               f"{p['h2d_gbps']} GB/s per GPU (measured); root ingest slowdown {p['ingest_slowdown']} (measured, "
-               f"tools/probe_ingest.py); xGMI {p['xgmi_gbps']} GB/s per link and direction and host memory "
+               f"{p['h2d_gbps']} GB/s per GPU (measured); root ingest slowdown {p['ingest_slowdown']} per 155 MB received "
+               f"per step (measured, tools/probe_ingest.py; dp rank 0 sheds that share); xGMI {p['xgmi_gbps']} GB/s per link and direction and host memory "
                f"{p['host_gbps']} GB/s (assumed). `python -m anx plan --model dp|v4|v5` prints the per-term "
                f"breakdown.\n")
     return "\n".join(out)
