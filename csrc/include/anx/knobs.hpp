@@ -30,9 +30,10 @@ struct Knobs {
                            // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
   int bf16_fc_cfg = -1;    // bf16 FC layers: force this wide-tile config (A/B; -1 = cfg 8, 256x64 3-stage)
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
-  int bf16_conv1 = 0;      // bf16 Conv1 (polyphase): 1 = the persistent row-band kernel (conv1_bf16_ring.hip:
-                           // input rows in an LDS ring, weights resident), 2 = the same on the fp32 image
-                           // (space-to-depth inside, no s2d4 pass), 0 = s2d4 + the implicit-GEMM tile kernels
+  int bf16_conv1 = 2;      // bf16 Conv1 (polyphase): 2 = the persistent row-band kernel on the fp32 image
+                           // (conv1_bf16_ring.hip: space-to-depth + bf16 inside, rows in an LDS ring, weights
+                           // resident; 362 k vs 343 k images/s, profiles/r04_bf16_ring_v2_bench_ab.jsonl),
+                           // 1 = the same on the s2d4 polyphase copy, 0 = s2d4 + the implicit-GEMM tile kernels
   int conv1_occ = 0;       // cap on the Conv1 Winograd GEMM's workgroups per CU (LDS padding; 0 = none: 4)
   int conv2_occ = -1;      // ... and Conv2's (0 = none: 2; -1 = auto: 1 when the launch has <= one workgroup per
                            // CU); a cap leaves room for a concurrent lane's kernels

@@ -267,19 +267,22 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     for (int b = 0; b < kPB; ++b) {
       const int m = 64 * wave + 32 * b + r, oy = kRT * t + mrow[b];
       const bool ok = m < kRT * kWo && oy < kHo;
+      // the lane's filter half (4 h) rides in the VGPR offset: the SGPR offset must be wave-uniform,
+      // or the compiler runs each store as a two-pass waterfall loop (twice the store instructions,
+      // which also broke the vmcnt counts above)
       [[maybe_unused]] const int obase =
-          ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox[b] + a.w_off) * a.Cb + a.c_off) * 2 : kOOB;
+          ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox[b] + a.w_off) * a.Cb + a.c_off + 4 * h) * 2 : kOOB;
 #pragma unroll
       for (int nb = 0; nb < 3; ++nb)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int f = 32 * nb + 8 * j + 4 * h;
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(bs + f);
+          const int f0 = 32 * nb + 8 * j;  // wave-uniform
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(bs + f0 + 4 * h);
           bf16x4 v;
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
 #if __HIP_DEVICE_COMPILE__
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f * 2, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f0 * 2, 0);
 #endif
         }
     }

@@ -66,7 +66,7 @@ def test_s2d4_polyphase_input_exact(cuda):
     column, [N, 57, 57, (rh*4 + rw)*3 + c] — bit-exact against the same rearrangement in torch (one
     round-to-nearest-even conversion on both sides)."""
     N = 5
-    m = AlexNetFull(seed=3, device=cuda, max_batch=N)
+    m = AlexNetFull(seed=3, device=cuda, max_batch=N, knobs={"bf16_conv1": 0})  # the s2d4 pass writes tap 10
     x = (torch.randn(N, 227, 227, 3, generator=torch.Generator().manual_seed(4)) * 3).to(cuda)
     m(x)
     xq = F.pad(x.to(torch.bfloat16), (0, 0, 0, 1, 0, 1))  # 228 x 228
