@@ -88,8 +88,7 @@ __device__ __forceinline__ void sfor(F&& f) {
 // F32IN: the space-to-depth and bf16 conversion happen here (the image's fp32 rows are loaded to
 // registers one tile ahead and written into the ring converted and swizzled), so neither the
 // s2d4 kernel nor its 80 MB polyphase copy runs.
-constexpr int kUnitsPerRow = 4 * kP;                     // a polyphase row: 4 image rows x 57 (12-float) units
-constexpr int kUPT = (kRT * kUnitsPerRow + kNT - 1) / kNT;  // units per thread per tile (4)
+static_assert(kWaves == 4, "F32IN: wave w loads the image rows of phase w");
 template <bool F32IN>
 __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -120,38 +119,54 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
 #endif
   };
 
-  // ---- F32IN: polyphase rows from the fp32 image. Unit e of a group of kRT rows = (row j, phase
-  // row rh, column c): 12 floats (4 image columns x 3 channels) -> 12 bf16 at channels 12 rh .. +11
-  // of column c, written as three 8-B pieces at their swizzled 16-B units.
-  [[maybe_unused]] float xu[kUPT][12];
-  [[maybe_unused]] auto load_units = [&](int row0) {  // rows row0 .. row0 + kRT - 1 into xu
+  // ---- F32IN: polyphase rows from the fp32 image. A group of kRT polyphase rows is 16 image rows;
+  // wave w loads the rows with phase rh = w (one per polyphase row j), lane c = polyphase column c
+  // (57 of 64 lanes): 12 floats (4 image columns x 3 channels) -> 12 bf16 at channels 12 rh .. +11
+  // of column c, written as three 8-B pieces at their swizzled 16-B units. The 12 floats are three
+  // 16-B loads at 4-B alignment (HSA runs buffer accesses in unaligned mode); column 56 has 9 floats
+  // and its third load takes the row's last 16 B (floats 5..8), so no load reaches past the tensor.
+  [[maybe_unused]] f32x4 xw[kRT][3];
+  [[maybe_unused]] auto row_of = [&](int row0, int jj, int& row, bool& ok) {
+    const int pr = row0 + jj;
+    row = 4 * pr + wave;
+    ok = pr < kP && row < 227;
+  };
+  [[maybe_unused]] auto load_units = [&](int row0) {  // polyphase rows row0 .. row0 + kRT - 1 into xw
 #if __HIP_DEVICE_COMPILE__
+    const int c = lane;
 #pragma unroll
-    for (int i = 0; i < kUPT; ++i) {
-      const int e = tid + kNT * i, j = e / kUnitsPerRow, rem = e - j * kUnitsPerRow;
-      const int rh = rem / kP, c = rem - rh * kP, pr = row0 + j, row = 4 * pr + rh;
-      const bool ok = e < kRT * kUnitsPerRow && pr < kP && row < 227;
-      const int base = ok ? ((n * 227 + row) * 227 + 4 * c) * 3 * 4 : kOOB;
-#pragma unroll
-      for (int f = 0; f < 12; ++f)  // column 227 (c = 56, f >= 9) does not exist: past the extent
-        xu[i][f] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(xr, c == kP - 1 && f >= 9 ? kOOB : base, f * 4, 0));
+    for (int jj = 0; jj < kRT; ++jj) {
+      int row;
+      bool ok;
+      row_of(row0, jj, row, ok);
+      const int b = ok && c < kP ? ((n * 227 + row) * 681 + 12 * c) * 4 : kOOB;
+      xw[jj][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, b, 0, 0));
+      xw[jj][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, b, 16, 0));
+      xw[jj][2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, b + (c == kP - 1 ? 20 : 32), 0, 0));
     }
 #endif
   };
   [[maybe_unused]] auto store_units = [&](int row0) {
+    const int c = lane, sw = (c >> 3) & 1;
+    if (c >= kP) return;
 #pragma unroll
-    for (int i = 0; i < kUPT; ++i) {
-      const int e = tid + kNT * i, j = e / kUnitsPerRow, rem = e - j * kUnitsPerRow;
-      if (e >= kRT * kUnitsPerRow) continue;
-      const int rh = rem / kP, c = rem - rh * kP, sw = (c >> 3) & 1;
-      char* col = lds + ((row0 + j) % kSlots) * kSlotB + c * (kCh * 2);
+    for (int jj = 0; jj < kRT; ++jj) {
+      int row;
+      bool ok;
+      row_of(row0, jj, row, ok);
+      float u[12];
+#pragma unroll
+      for (int f = 0; f < 12; ++f) u[f] = xw[jj][f >> 2][f & 3];
+      u[8] = c == kP - 1 ? xw[jj][2][3] : u[8];
+#pragma unroll
+      for (int f = 0; f < 12; ++f) u[f] = ok && !(c == kP - 1 && f >= 9) ? u[f] : 0.f;  // column 227 / past the image
+      char* col = lds + ((row0 + jj) % kSlots) * kSlotB + c * (kCh * 2);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        const int lb = rh * 24 + q * 8;  // logical byte in the column's 96
+        const int lb = wave * 24 + q * 8;  // logical byte in the column's 96 (rh = wave)
         bf16x4 v;
 #pragma unroll
-        for (int f = 0; f < 4; ++f) v[f] = static_cast<bf16>(xu[i][4 * q + f]);
+        for (int f = 0; f < 4; ++f) v[f] = static_cast<bf16>(u[4 * q + f]);
         *reinterpret_cast<bf16x4*>(col + (((lb >> 4) ^ sw) << 4) + (lb & 15)) = v;
       }
     }
@@ -326,6 +341,7 @@ hipError_t conv1_bf16_ring(const void* xin, int N, const void* wpacked, const fl
   if (attr != hipSuccess) return attr;
   Args a{};
   a.x = xin;
+  if (f32_input && (reinterpret_cast<uintptr_t>(xin) & 3)) return hipErrorInvalidValue;
   a.w = static_cast<const bf16*>(wpacked);
   a.bias = bias;
   a.out = out.base;

@@ -214,6 +214,26 @@ def test_conv1_ring_kernel_matches_tile_kernels(cuda, N, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_conv1_ring_fp32_input_interior_pointer(cuda, shift):
+    """The fused-input ring (bf16_conv1=2) reads the fp32 image with aligned 16-B window loads from the
+    granule holding x: an input that starts `shift` floats into a granule (a lane's x[lo:hi] slice or
+    any interior view) gives the same Conv1 as an aligned copy, including the batch's last row, which
+    takes the dword path."""
+    N = 5
+    flat = torch.randn(N * 227 * 227 * 3 + 8, generator=torch.Generator().manual_seed(shift)).to(cuda) * 3
+    x = flat[shift:shift + N * 227 * 227 * 3].view(N, 227, 227, 3)
+    assert (x.data_ptr() // 4) % 4 == shift % 4
+    m = AlexNetFull(seed=29, device=cuda, max_batch=N, knobs={"bf16_conv1": 2})
+    m(x)
+    c_view = m.tap(0, N).clone()
+    m(x.clone())
+    c_copy = m.tap(0, N)
+    torch.cuda.synchronize()
+    assert torch.equal(c_view, c_copy)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [0, 1, 5])
 def test_fc_forced_wide_tile_configs(cuda, cfg):
     """FC6-8 on a forced wide-tile config (knob bf16_fc_cfg, its own K split <= 16 slabs) against the
