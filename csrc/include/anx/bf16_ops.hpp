@@ -94,8 +94,11 @@ void pack_conv1_ring_weights(const float* w_k48_33, std::vector<uint16_t>& out);
 size_t conv1_ring_weight_bytes();
 // f32_input: x is the fp32 NHWC image [N,227,227,3] (space-to-depth + bf16 conversion inside the
 // kernel, no polyphase copy); else the polyphase bf16 image of f32_to_bf16_s2d4.
+// pool_out: also max-pool 3x3/2 into this 27x27x96 view (pool1). With f32_input and one workgroup
+// per image (N >= cus) the pool runs in the kernel's epilogue and `out` is NOT written (the 55x55
+// map never reaches HBM); otherwise Conv1 writes `out` (dense 55x55x96) and maxpool_bf16 follows.
 hipError_t conv1_bf16_ring(const void* x, int N, const void* wpacked, const float* bias, OutViewB out, bool relu,
-                           hipStream_t s, int cus = 256, bool f32_input = false);
+                           hipStream_t s, int cus = 256, bool f32_input = false, const OutViewB* pool_out = nullptr);
 
 }  // namespace hip
 

@@ -34,6 +34,8 @@ struct Knobs {
                            // (conv1_bf16_ring.hip: space-to-depth + bf16 inside, rows in an LDS ring, weights
                            // resident; 362 k vs 343 k images/s, profiles/r04_bf16_ring_v2_bench_ab.jsonl),
                            // 1 = the same on the s2d4 polyphase copy, 0 = s2d4 + the implicit-GEMM tile kernels
+  int bf16_pool1 = 1;      // bf16 pool1: 1 = in the Conv1 ring kernel's epilogue (bf16_conv1 2, one workgroup per
+                           // image: the 55x55 map never reaches HBM), 0 = Conv1 writes it and maxpool_bf16 reads it
   int conv1_occ = 0;       // cap on the Conv1 Winograd GEMM's workgroups per CU (LDS padding; 0 = none: 4)
   int conv2_occ = -1;      // ... and Conv2's (0 = none: 2; -1 = auto: 1 when the launch has <= one workgroup per
                            // CU); a cap leaves room for a concurrent lane's kernels

@@ -197,10 +197,13 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
   for (int n0 = 0; n0 < N; n0 += chunk_) {
     const int n = std::min(chunk_, N - n0);
     const float* xn = x + static_cast<size_t>(n0) * 227 * 227 * 3;
+    bool pooled = false;  // pool1 done with Conv1
     if (poly1_) {
       if (k_.bf16_conv1 == 2) {  // the fp32 image straight into the row-band kernel (no polyphase copy)
+        const OutViewB q2v{B(q2_), 31, 31, 96, 2, 2, 0};
         ANX_TRY(hip::conv1_bf16_ring(xn, n, w1ring_, L_[0].bias, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, true, s, cus_,
-                                     true));
+                                     true, k_.bf16_pool1 ? &q2v : nullptr));
+        pooled = k_.bf16_pool1 != 0;
       } else {
         ANX_TRY(hip::f32_to_bf16_s2d4(xn, xb_, n, 227, 227, s));
         if (k_.bf16_conv1 == 1)
@@ -212,7 +215,7 @@ hipError_t FullEngine::forward(const float* x, int N, float* logits, hipStream_t
       ANX_TRY(hip::f32_to_bf16(xn, xb_, static_cast<size_t>(n) * 227 * 227 * 3, s));
       ANX_TRY(conv(L_[0], n, 227, 227, xb_, OutViewB{B(c1_), 55, 55, 96, 0, 0, 0}, nullptr, true, s));
     }
-    ANX_TRY(hip::maxpool_bf16(c1_, n, 55, 55, 96, 3, 2, OutViewB{B(q2_), 31, 31, 96, 2, 2, 0}, s));
+    if (!pooled) ANX_TRY(hip::maxpool_bf16(c1_, n, 55, 55, 96, 3, 2, OutViewB{B(q2_), 31, 31, 96, 2, 2, 0}, s));
     ANX_TRY(conv(L_[1], n, 31, 31, q2_, OutViewB{B(c2_), 27, 27, 256, 0, 0, 0}, nullptr, true, s));
     ANX_TRY(hip::maxpool_lrn_bf16(c2_, n, 27, 27, 256, 3, 2, 5, 1e-4f, 0.75f, 2.0f, lrn_,
                                   OutViewB{B(q3_), 15, 15, 256, 1, 1, 0}, s, k_.bf16_lrn_tile));

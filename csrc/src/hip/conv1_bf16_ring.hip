@@ -43,6 +43,7 @@ using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 using u32x2 = __attribute__((ext_vector_type(2))) unsigned;
+using u16x8 = __attribute__((ext_vector_type(8))) unsigned short;
 using lds_b16 = __attribute__((address_space(3))) bf16;
 using lds_void = __attribute__((address_space(3))) void;
 
@@ -54,7 +55,9 @@ constexpr int kWRow = 440;                              // weight row stride (bf
 constexpr int kWBytes = 83 * 1024;                      // [96][440] bf16 = 84,480 B, padded to whole DMA pieces
 constexpr int kRing = kSlots * kSlotB;                  // 49,152 B
 constexpr int kBias = kRing + kWBytes;
-constexpr size_t kLds = kBias + kK * 4;                 // 134,528 B
+constexpr size_t kLds = kBias + kK * 4;                 // 146,976 B
+constexpr int kPw = 27, kCarryB = kPw * kK * 2;         // pool1: a pooled row's running max, 5184 B
+constexpr size_t kLdsPool = kLds + 2 * kCarryB;         // + two carry rows: 157,344 B
 constexpr int kRT = 4;                                  // output rows per tile
 constexpr int kTilesPerImage = (kHo + kRT - 1) / kRT;   // 14 (the last holds three rows)
 constexpr int kNT = 256, kWaves = kNT / 64, kPB = 2;   // waves, 32-pixel blocks per wave
@@ -62,6 +65,7 @@ constexpr int kKS = kKd / 16;                           // 27 K steps (3 per tap
 constexpr int kAhead = 2;                               // K steps of fragments in flight
 constexpr int kOOB = 0x7ffffff0;
 static_assert(kK * kWRow * 2 <= kWBytes && kRowB <= kPieces * 1024 && kRing % 16 == 0, "LDS layout");
+static_assert(kLdsPool <= 160 * 1024 && kWo * kCh * 2 <= kSlotB, "pool1: carry rows fit; a 48-filter output row fits a slot");
 static_assert(kWaves * kPB * 32 >= kRT * kWo, "a tile's pixels fit the waves' blocks");
 static_assert(kRT * kPieces % kWaves == 0, "a tile's row DMAs split evenly over the waves");
 [[maybe_unused]] constexpr int kDPW = kRT * kPieces / kWaves;            // row DMAs per wave per tile (6)
@@ -75,6 +79,9 @@ struct Args {
   int Hb, Wb, Cb, h_off, w_off, c_off;
   int N, segs;        // segments per image (workgroups sharing one image's tiles)
   int xbytes, obytes;
+  int pool;           // pool1 in the epilogue (F32IN, segs == 1): `out` unused, pooled rows to pout
+  bf16* pout;
+  int pHb, pWb, pCb, ph_off, pw_off, pc_off;
 };
 
 template <int B, int E, class F>
@@ -274,32 +281,96 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
       __builtin_amdgcn_sched_barrier(0);
     });
 
-    // ---- epilogue: lane holds pixel m, filters 32 nb + 8 j + 4 h + (0..3) in acc[b][nb][4 j .. 4 j + 3].
-    // kSPW buffer stores per lane, always issued (a pixel outside the tile stores past the extent,
-    // which drops the write), so the vmcnt counts above hold on every wave.
-    const float* bs = reinterpret_cast<const float*>(lds + kBias);
+    // ---- pool1 epilogue (one workgroup per image, tiles in order): the tile's ReLU'd rows go to
+    // LDS as bf16, 48 filters at a time, into the ring slots of polyphase rows 4t .. 4t+3 (no wave
+    // reads those again: tile t+1 reads rows 4t+4 .. 4t+9, and this tile's store_units fills the
+    // slots of rows 4t-4 .. 4t-1). Pooled row 2t is rows 4t .. 4t+2; row 2t-1 is the carried max of
+    // rows 4t-2, 4t-1 with row 4t; rows 4t+2, 4t+3 are carried for row 2t+1. Max over ReLU outputs
+    // (>= 0) is the unsigned max of their bf16 bits.
+    if (F32IN && a.pool) {
+      __builtin_amdgcn_s_barrier();  // every wave is past its fragment reads of the scratch slots
+      asm volatile("" ::: "memory");
+      const float* bs = reinterpret_cast<const float*>(lds + kBias);
+      const int nrows = min(kRT, kHo - kRT * t);
+      const char* carry_old = lds + kLds + ((t & 1) ^ 1) * kCarryB;
+      char* carry_new = lds + kLds + (t & 1) * kCarryB;
+      sfor<0, 2>([&](auto P) {
+        constexpr int p = decltype(P)::value;
 #pragma unroll
-    for (int b = 0; b < kPB; ++b) {
-      const int m = 64 * wave + 32 * b + r, oy = kRT * t + mrow[b];
-      const bool ok = m < kRT * kWo && oy < kHo;
-      // the lane's filter half (4 h) rides in the VGPR offset: the SGPR offset must be wave-uniform,
-      // or the compiler runs each store as a two-pass waterfall loop (twice the store instructions,
-      // which also broke the vmcnt counts above)
-      [[maybe_unused]] const int obase =
-          ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox[b] + a.w_off) * a.Cb + a.c_off + 4 * h) * 2 : kOOB;
+        for (int b = 0; b < kPB; ++b) {
+          const int m = 64 * wave + 32 * b + r, oy = kRT * t + mrow[b];
+          if (m < kRT * kWo && oy < kHo) {
+            char* px = lds + ((kRT * t + mrow[b]) % kSlots) * kSlotB + ox[b] * (kCh * 2);
+            sfor<0, 12>([&](auto Q) {
+              constexpr int nb = decltype(Q)::value / 4, j = decltype(Q)::value % 4, f0 = 32 * nb + 8 * j;
+              if constexpr (f0 >= 48 * p && f0 < 48 * p + 48) {
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(bs + f0 + 4 * h);
+                bf16x4 v;
 #pragma unroll
-      for (int nb = 0; nb < 3; ++nb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int f0 = 32 * nb + 8 * j;  // wave-uniform
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(bs + f0 + 4 * h);
-          bf16x4 v;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
-#if __HIP_DEVICE_COMPILE__
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f0 * 2, 0);
-#endif
+                for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
+                *reinterpret_cast<bf16x4*>(px + (f0 - 48 * p + 4 * h) * 2) = v;
+              }
+            });
+          }
         }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (tid < kPw * 6) {  // (pooled column, 8-filter chunk of this half)
+          const int pc = tid / 6, c = tid - pc * 6;
+          u16x8 hr[kRT];
+#pragma unroll
+          for (int k = 0; k < kRT; ++k) {
+            hr[k] = u16x8{};
+            if (k < nrows) {
+              const char* q = lds + ((kRT * t + k) % kSlots) * kSlotB + 2 * pc * (kCh * 2) + c * 16;
+              hr[k] = __builtin_elementwise_max(__builtin_elementwise_max(*reinterpret_cast<const u16x8*>(q),
+                                                                          *reinterpret_cast<const u16x8*>(q + 96)),
+                                                *reinterpret_cast<const u16x8*>(q + 192));
+            }
+          }
+          const int cofs = pc * (kK * 2) + (48 * p + 8 * c) * 2;
+          const int ob = ((n * a.pHb + a.ph_off) * a.pWb + pc + a.pw_off) * a.pCb + a.pc_off + 48 * p + 8 * c;
+          const int rstride = a.pWb * a.pCb;
+          *reinterpret_cast<u16x8*>(a.pout + ob + 2 * t * rstride) =
+              __builtin_elementwise_max(__builtin_elementwise_max(hr[0], hr[1]), hr[2]);
+          if (t > t0)
+            *reinterpret_cast<u16x8*>(a.pout + ob + (2 * t - 1) * rstride) =
+                __builtin_elementwise_max(*reinterpret_cast<const u16x8*>(carry_old + cofs), hr[0]);
+          if (t + 1 < t1) *reinterpret_cast<u16x8*>(carry_new + cofs) = __builtin_elementwise_max(hr[2], hr[3]);
+        }
+        if constexpr (p == 0) {
+          __builtin_amdgcn_s_barrier();  // the second half overwrites the scratch rows
+          asm volatile("" ::: "memory");
+        }
+      });
+    } else {
+      // ---- epilogue: lane holds pixel m, filters 32 nb + 8 j + 4 h + (0..3) in acc[b][nb][4 j .. 4 j + 3].
+      // kSPW buffer stores per lane, always issued (a pixel outside the tile stores past the extent,
+      // which drops the write), so the vmcnt counts above hold on every wave.
+      const float* bs = reinterpret_cast<const float*>(lds + kBias);
+  #pragma unroll
+      for (int b = 0; b < kPB; ++b) {
+        const int m = 64 * wave + 32 * b + r, oy = kRT * t + mrow[b];
+        const bool ok = m < kRT * kWo && oy < kHo;
+        // the lane's filter half (4 h) rides in the VGPR offset: the SGPR offset must be wave-uniform,
+        // or the compiler runs each store as a two-pass waterfall loop (twice the store instructions,
+        // which also broke the vmcnt counts above)
+        [[maybe_unused]] const int obase =
+            ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox[b] + a.w_off) * a.Cb + a.c_off + 4 * h) * 2 : kOOB;
+  #pragma unroll
+        for (int nb = 0; nb < 3; ++nb)
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int f0 = 32 * nb + 8 * j;  // wave-uniform
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(bs + f0 + 4 * h);
+            bf16x4 v;
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
+  #if __HIP_DEVICE_COMPILE__
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f0 * 2, 0);
+  #endif
+          }
+      }
     }
     // F32IN: tile t+1's new rows (loaded at this tile's start) into tile t-1's slots, which no wave
     // reads in tile t; the next tile's barrier publishes them
@@ -324,7 +395,7 @@ void pack_conv1_ring_weights(const float* w_k48_33, std::vector<uint16_t>& out) 
 size_t conv1_ring_weight_bytes() { return kWBytes; }
 
 hipError_t conv1_bf16_ring(const void* xin, int N, const void* wpacked, const float* bias, OutViewB out, bool relu,
-                           hipStream_t s, int cus, bool f32_input) {
+                           hipStream_t s, int cus, bool f32_input, const OutViewB* pool_out) {
   if (N <= 0) return hipSuccess;
   if (!relu || !out.base || out.Cb % 4 || out.c_off % 4 || static_cast<long>(N) * kP * kRowB >= (1L << 31) ||
       static_cast<long>(N) * out.Hb * out.Wb * out.Cb * 2 >= (1L << 31) || out.Hb < kHo + out.h_off ||
@@ -359,10 +430,31 @@ hipError_t conv1_bf16_ring(const void* xin, int N, const void* wpacked, const fl
   if (xb >= (1L << 31)) return hipErrorInvalidValue;
   a.xbytes = static_cast<int>(xb);
   a.obytes = static_cast<int>(static_cast<long>(N) * out.Hb * out.Wb * out.Cb * 2);
+  if (pool_out) {
+    const OutViewB& q = *pool_out;
+    if (!q.base || q.Cb % 8 || q.c_off % 8 || q.Hb < kPw + q.h_off || q.Wb < kPw + q.w_off || q.Cb < kK + q.c_off ||
+        static_cast<long>(N) * q.Hb * q.Wb * q.Cb >= (1L << 31))
+      return hipErrorInvalidValue;
+    a.pool = f32_input && a.segs == 1;
+    a.pout = q.base;
+    a.pHb = q.Hb;
+    a.pWb = q.Wb;
+    a.pCb = q.Cb;
+    a.ph_off = q.h_off;
+    a.pw_off = q.w_off;
+    a.pc_off = q.c_off;
+    if (!a.pool && (out.Hb != kHo || out.Wb != kWo || out.Cb != kK || out.h_off || out.w_off || out.c_off))
+      return hipErrorInvalidValue;  // the separate pool below reads a dense 55x55x96 map
+  }
   if (f32_input)
-    conv1_bf16_ring_kernel<true><<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
+    conv1_bf16_ring_kernel<true><<<static_cast<unsigned>(N * a.segs), kNT, a.pool ? kLdsPool : kLds, s>>>(a);
   else
     conv1_bf16_ring_kernel<false><<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
+  if (pool_out && !a.pool) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return maxpool_bf16(out.base, N, kHo, kWo, kK, 3, 2, *pool_out, s);
+  }
   return hipGetLastError();
 }
 

@@ -294,12 +294,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
 //   hence 3 B stages), retires B_{t+1} at the end of L_t (vmcnt 8) and A_{t+1} at the end of M_t
 //   (vmcnt 4). Every L section ends with lgkmcnt(0) and every DMA lands in a stage whose last readers
 //   finished at least one barrier earlier (the refills never race a read).
-template <int BN>
+// BM = 192 (cfg 16): 96 rows per group, the same schedule with 3 A pieces per lane — 226 tiles for
+// conv5's 43264 x 256 output fill one round of 256 CUs where 256-row tiles leave 87 CUs idle.
+template <int BM, int BN>
 __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
-  constexpr int BM = 256, TM = 8, WN = BN / 4, TN = WN / 16;
-  constexpr int SZ = 256 * kBK;      // bf16 per A stage
+  constexpr int HM = BM / 2, TM = HM / 16, WN = BN / 4, TN = WN / 16;  // HM: a group's A rows
+  constexpr int SZ = BM * kBK;       // bf16 per A stage
   constexpr int SB = BN * kBK;       // bf16 per B stage
-  constexpr int NA = 4, NB = BN / 64;  // DMA pieces per lane per K tile: this group's A rows, B half
+  constexpr int NA = HM / 32, NB = BN / 64;  // DMA pieces per lane per K tile: this group's A rows, B half
+  static_assert(HM % 32 == 0, "a group's rows are whole 32-row DMA blocks");
   static_assert(TN >= 1 && NB >= 1, "tile split");
   constexpr int CH = BN / 8, EW = BN + 8;  // epilogue image rows padded by 16 B (conflict-free)
   extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
@@ -320,7 +323,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
   int aoff[NA], boff[NB];  // 32-bit element offsets from the (scalar) x / wg bases: fewer VGPRs
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    const int row = G * 128 + j * 32 + (tl >> 3);
+    const int row = G * HM + j * 32 + (tl >> 3);
     const int m = m0 + row;
     int o = 0;
     if (m < a.M) {
@@ -341,7 +344,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
     ufw = tap - ufh * a.F;
   }
   lds_b16* lds3 = (lds_b16*)(lds_b);
-  const int drow = (G * 128 + wl * 8) * kBK;  // this wave's first A DMA row (+ j*32 rows)
+  const int drow = (G * HM + wl * 8) * kBK;  // this wave's first A DMA row (+ j*32 rows)
   const int dbrow = (G * (BN / 2) + wl * 8) * kBK;  // ... and B row
   auto issueA = [&](int st) {  // the next K tile of this group's A rows (issued in K order)
     const int ko = ufh < a.F ? (ufh * a.Wp + ufw) * a.C + uc : 0;
@@ -367,7 +370,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int hq = lane >> 4, sw = (lane >> 1) & 7;
-  const int arow = (G * 128 + (lane & 15)) * kBK, brow = (wn * WN + (lane & 15)) * kBK;
+  const int arow = (G * HM + (lane & 15)) * kBK, brow = (wn * WN + (lane & 15)) * kBK;
 
   // prologue: tile 0 (both groups' halves), and G1's B_1
   issueA(0);
@@ -466,7 +469,7 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
     const f32x4 bv = (a.bias && f < a.Kg) ? *reinterpret_cast<const f32x4*>(a.bias + g * a.Kg + f) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int ml = G * 128 + i * 16 + mcol;
+      const int ml = G * HM + i * 16 + mcol;
       f32x4 v = acc[i][j] + bv;
       if (a.relu) v = f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
       *reinterpret_cast<bf16x4*>(E + ml * EW + nl) =
@@ -500,7 +503,8 @@ constexpr BigCfg kCfg[] = {{256, 256, 512, 2, 1, 1.0f},  {256, 128, 512, 2, 1, 0
                            {256, 256, 512, 0, 1, 1.04f},   // 12: ping-pong (A 2 + B 3 stages): 2-7 % over 0
                            {256, 128, 512, 0, 1, 0.8f},    // 13: ping-pong 256x128 (conv3/4: 90 / 125 us vs 77 / 109 for cfg 3)
                            {96, 96, 256, 2, 3, 0.8f},      // 14: 96x96, 3 workgroups/CU (short-K conv1p: 101 vs 109 us for cfg 4)
-                           {64, 96, 256, 2, 3, 0.6f}};     // 15: 64x96, 3 workgroups/CU
+                           {64, 96, 256, 2, 3, 0.6f},      // 15: 64x96, 3 workgroups/CU
+                           {192, 256, 512, 0, 1, 1.0f}};   // 16: ping-pong 192x256 (conv5: one round of 226 tiles)
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 // ---- FC layers (M = batch rows of K contiguous bf16, 1x1): activations straight to VGPRs ----
 // The 256x64 LDS-DMA config (cfg 8) ran FC7 at 23 us for 164 MB of operand traffic: one workgroup
@@ -622,7 +626,7 @@ constexpr int kFcDepth = 4;
 
 
 size_t lds_bytes(const BigCfg& c) {
-  if (c.nst == 0) return (static_cast<size_t>(2) * 256 + 3 * c.BN) * kBK * 2;  // ping-pong: A x 2 + B x 3 stages
+  if (c.nst == 0) return (static_cast<size_t>(2) * c.BM + 3 * c.BN) * kBK * 2;  // ping-pong: A x 2 + B x 3 stages
   return static_cast<size_t>(c.nst) * (c.BM + c.BN) * kBK * 2 + static_cast<size_t>(c.BM) * 4;
 }
 
@@ -670,7 +674,7 @@ BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus, int cfg) {
   const OutViewB probe{reinterpret_cast<__bf16*>(16), 1, 1, p.Kg, 0, 0, 0};
   // forced configs (knob bf16_fc_cfg, A/B): any slab-capable wide-tile config (not the ping-pong
   // kernels), K split at most kMaxFcSplit ways (the engine's slab workspace is sized for that)
-  r.cfg = cfg >= 0 && cfg != 12 && cfg != 13 ? cfg : 8;
+  r.cfg = cfg >= 0 && cfg != 12 && cfg != 13 && cfg != 16 ? cfg : 8;
   if (!conv_bf16_big_ok(p, r.cfg, probe)) return BigFc{-1, 1};
   const BigCfg& c = kCfg[r.cfg];
   const long tiles = (p.N + c.BM - 1) / c.BM * ((p.Kg + c.BN - 1) / c.BN);
@@ -685,7 +689,7 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
   if (!conv_bf16_big_ok(p, cfg, out)) return hipErrorInvalidValue;
   const int ksplit = std::max(1, split.ksplit);
   const bool slab = split.ws != nullptr;  // fp32 slabs (also at ksplit 1: an fp32 result via the reduce)
-  if ((cfg == 12 || cfg == 13) && slab) cfg = cfg == 12 ? 0 : 1;  // ping-pong: no split-K slab epilogue
+  if ((cfg == 12 || cfg == 13 || cfg == 16) && slab) cfg = cfg == 13 ? 1 : 0;  // ping-pong: no split-K slab epilogue
   if ((ksplit > 1 && !slab) || (slab && p.groups != 1)) return hipErrorInvalidValue;
   const long M = static_cast<long>(p.N) * p.Ho * p.Wo;
   if (M == 0) return hipSuccess;
@@ -749,10 +753,11 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
     return hipSuccess;
   }();
   if (attr != hipSuccess) return attr;
-  if (cfg == 12 || cfg == 13) {
+  if (cfg == 12 || cfg == 13 || cfg == 16) {
     static const hipError_t pattr = [] {
-      for (const void* k : {reinterpret_cast<const void*>(conv_bf16_pp_kernel<256>),
-                            reinterpret_cast<const void*>(conv_bf16_pp_kernel<128>)}) {
+      for (const void* k : {reinterpret_cast<const void*>(conv_bf16_pp_kernel<256, 256>),
+                            reinterpret_cast<const void*>(conv_bf16_pp_kernel<256, 128>),
+                            reinterpret_cast<const void*>(conv_bf16_pp_kernel<192, 256>)}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
       }
@@ -760,9 +765,11 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
     }();
     if (pattr != hipSuccess) return pattr;
     if (cfg == 12)
-      conv_bf16_pp_kernel<256><<<grid, 512, lds, s>>>(a);
+      conv_bf16_pp_kernel<256, 256><<<grid, 512, lds, s>>>(a);
+    else if (cfg == 13)
+      conv_bf16_pp_kernel<256, 128><<<grid, 512, lds, s>>>(a);
     else
-      conv_bf16_pp_kernel<128><<<grid, 512, lds, s>>>(a);
+      conv_bf16_pp_kernel<192, 256><<<grid, 512, lds, s>>>(a);
     return hipGetLastError();
   }
   switch (cfg) {

@@ -27,10 +27,11 @@ const Field kFields[] = {
     {"force_vec4", &Knobs::force_vec4, nullptr, -1, 255, nullptr},
     {"force_scalar", &Knobs::force_scalar, nullptr, -1, 255, nullptr},
     {"bf16_glds", &Knobs::bf16_glds, nullptr, 0, 3, "ANX_BF16_GLDS"},
-    {"bf16_big", &Knobs::bf16_big, nullptr, -2, 15, "ANX_BF16_BIG"},
+    {"bf16_big", &Knobs::bf16_big, nullptr, -2, 16, "ANX_BF16_BIG"},
     {"bf16_lrn_tile", &Knobs::bf16_lrn_tile, nullptr, 0, 1, nullptr},
     {"bf16_fc_cfg", &Knobs::bf16_fc_cfg, nullptr, -1, 11, "ANX_BF16_FC_CFG"},
     {"bf16_conv1", &Knobs::bf16_conv1, nullptr, 0, 2, "ANX_BF16_CONV1"},
+    {"bf16_pool1", &Knobs::bf16_pool1, nullptr, 0, 1, "ANX_BF16_POOL1"},
     {"bf16_fc", &Knobs::bf16_fc, nullptr, 0, 1, "ANX_BF16_FC"},
     {"conv1_occ", &Knobs::conv1_occ, nullptr, 0, 8, "ANX_CONV1_OCC"},
     {"conv2_occ", &Knobs::conv2_occ, nullptr, -1, 8, "ANX_CONV2_OCC"},

@@ -207,7 +207,9 @@ class AlexNetFull:
     def tap(self, i: int, N: int) -> torch.Tensor:
         """bf16 activation ``i`` of the last forward (see FullEngine::tap): conv1, pool1 window,
         conv2, pool2+LRN window, conv3/conv4 windows, conv5, pool5, fc6, fc7; 10: the bf16
-        polyphase (space-to-depth by 4) input of conv1."""
+        polyphase (space-to-depth by 4) input of conv1. Tap 0 holds conv1 only when the forward
+        wrote it: with pool1 fused into the Conv1 kernel (knob ``bf16_pool1``, one workgroup per
+        image) the 55x55 map never leaves the kernel."""
         y = torch.empty((N, *self.TAPS[i]), device=self.device, dtype=torch.bfloat16)
         n = C.c_size_t()
         nat.call("anx_full_tap", self._h, i, N, y.data_ptr(), C.byref(n), nat.stream_ptr(self.device))

@@ -81,7 +81,7 @@ def test_full_alexnet_per_layer_vs_bf16_oracle(cuda, groups2):
     layer in fp64 on bf16-rounded operands, rounded to bf16: only the fp32 summation order differs,
     so every layer agrees to <= 1e-2 of its max (|one bf16 ulp| = 0.4 %) and <= 4e-3 in L2."""
     N = 6
-    m = AlexNetFull(seed=9, device=cuda, max_batch=N, groups2=groups2)
+    m = AlexNetFull(seed=9, device=cuda, max_batch=N, groups2=groups2, knobs={"bf16_pool1": 0})  # conv1 map in tap 0
     x = (init_input(N, "rand", seed=9) * 10).to(cuda)
     logits = m(x).double()
     taps = [m.tap(i, N).double() for i in range(10)]
@@ -131,7 +131,7 @@ def test_bf16_lds_dma_kernel_matches_register_staged(cuda, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 12, 13, 14, 15])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 12, 13, 14, 15, 16])
 def test_bf16_wide_tile_kernel_matches_register_staged(cuda, cfg):
     """The wide-tile kernel (conv_bf16_big.hip; -1 = the cost model's per-layer pick, else that
     config forced wherever it fits) sums each output's products in the register-staged kernel's
@@ -201,7 +201,7 @@ def test_conv1_ring_kernel_matches_tile_kernels(cuda, N, mode):
     (N < CUs: an image's 14 row tiles over several workgroups) and the one-image-per-workgroup form
     are both covered."""
     x = (torch.randn(N, 227, 227, 3, generator=torch.Generator().manual_seed(N)) * 3).to(cuda)
-    m = AlexNetFull(seed=19, device=cuda, max_batch=N, knobs={"bf16_conv1": mode})
+    m = AlexNetFull(seed=19, device=cuda, max_batch=N, knobs={"bf16_conv1": mode, "bf16_pool1": 0})
     y = m(x).clone()
     c1 = m.tap(0, N).double()
     m.set_knob("bf16_conv1", 0)
@@ -211,6 +211,24 @@ def test_conv1_ring_kernel_matches_tile_kernels(cuda, N, mode):
     assert (c1 - r1).abs().max().item() <= 1.6e-2 * r1.abs().max().item()
     assert ((c1 - r1).norm() / r1.norm()).item() < 4e-3
     assert ((y - y0).norm() / y0.norm()).item() < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [256, 300, 40])
+def test_conv1_ring_fused_pool1_exact(cuda, N):
+    """pool1 in the ring kernel's epilogue (knob bf16_pool1=1; one workgroup per image from N = 256
+    CUs on; below that the kernel writes the 55x55 map and maxpool_bf16 follows): the pooled map
+    (tap 1, zero borders included) and the logits are bit-identical to Conv1 + the separate pool."""
+    x = (torch.randn(N, 227, 227, 3, generator=torch.Generator().manual_seed(N + 1)) * 3).to(cuda)
+    m = AlexNetFull(seed=31, device=cuda, max_batch=N, knobs={"bf16_pool1": 0})
+    y0 = m(x).clone()
+    q0 = m.tap(1, N).clone()
+    m.set_knob("bf16_pool1", 1)
+    y1 = m(x)
+    q1 = m.tap(1, N)
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q0)
+    assert torch.equal(y1, y0)
 
 
 @pytest.mark.gpu
