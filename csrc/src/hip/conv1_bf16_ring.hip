@@ -21,7 +21,8 @@
 //     28 % busy with 21 % of LDS cycles in bank conflicts);
 //   * a polyphase column's six 16-B channel units are stored in the order k ^ ((column >> 3) & 1)
 //     (applied on the DMA's source side), which halves the pixel reads' bank conflicts;
-//   * bias + ReLU + bf16 in the epilogue, straight into the NHWC output.
+//   * bias (registers) + ReLU + bf16 in the epilogue, straight into the NHWC output, or with pool1
+//     fused (one workgroup per image) through LDS into the pooled map.
 // Fragments are read two K steps ahead of their MFMAs (registers triple-buffered).
 //
 // Reference op: convKernel (final_project/v3_cuda_only/src/layers_cuda.cu:20-46); the full-network
@@ -29,6 +30,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -54,8 +57,7 @@ constexpr int kSlotB = kPieces * 1024 + 16;             // + one 16-B unit: a sl
 constexpr int kWRow = 440;                              // weight row stride (bf16): 880 B
 constexpr int kWBytes = 83 * 1024;                      // [96][440] bf16 = 84,480 B, padded to whole DMA pieces
 constexpr int kRing = kSlots * kSlotB;                  // 49,152 B
-constexpr int kBias = kRing + kWBytes;
-constexpr size_t kLds = kBias + kK * 4;                 // 146,976 B
+constexpr size_t kLds = kRing + kWBytes;                // 146,592 B
 constexpr int kPw = 27, kCarryB = kPw * kK * 2;         // pool1: a pooled row's running max, 5184 B
 constexpr size_t kLdsPool = kLds + 2 * kCarryB;         // + two carry rows: 157,344 B
 constexpr int kRT = 4;                                  // output rows per tile
@@ -82,6 +84,7 @@ struct Args {
   int pool;           // pool1 in the epilogue (F32IN, segs == 1): `out` unused, pooled rows to pout
   bf16* pout;
   int pHb, pWb, pCb, ph_off, pw_off, pc_off;
+  unsigned long long* dbg;  // ANX_RING_PHASES: per-workgroup phase clocks (wave 0), else null
 };
 
 template <int B, int E, class F>
@@ -185,7 +188,6 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(lds3 + (kRing + q * 1024) / 2), 16, q * 1024 + lane * 16, 0,
                                              0, 0);
 #endif
-  if (tid < kK) reinterpret_cast<float*>(lds + kBias)[tid] = a.bias[tid];
   if constexpr (F32IN) {
     load_units(kRT * t0);
     store_units(kRT * t0);
@@ -219,6 +221,19 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
 #if __HIP_DEVICE_COMPILE__
   const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.obytes, 0x00020000);
 #endif
+  // the lane's 48 bias values (filters 32 nb + 8 j + 4 h + 0..3) in registers for the kernel's
+  // lifetime: read from LDS per 4-filter group, each read's wait serialised the epilogue on LDS latency
+  f32x4 bias_r[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) bias_r[q] = *reinterpret_cast<const f32x4*>(a.bias + 32 * (q / 4) + 8 * (q % 4) + 4 * h);
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tc = __builtin_amdgcn_s_memtime();
+  auto lap = [&](int i) {
+    if (a.dbg) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      ph[i] += now - tc;
+      tc = now;
+    }
+  };
   for (int t = t0; t < t1; ++t) {
     // Rows 4t .. 4t+5 landed: this wave's DMAs by a counted vmcnt (vmcnt is in order; the last group,
     // rows 4t+2 .. 4t+5, was issued at tile t-1's start and only tile t-1's kSPW output stores per
@@ -232,6 +247,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kSPW) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    lap(0);
     if (t + 1 < t1) {  // tile t+1's new rows, into tile t-1's first slots
       if constexpr (F32IN)
         load_units(kRT * t + 6);
@@ -281,6 +297,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
       __builtin_amdgcn_sched_barrier(0);
     });
 
+    lap(1);
     // ---- pool1 epilogue (one workgroup per image, tiles in order): the tile's ReLU'd rows go to
     // LDS as bf16, 48 filters at a time, into the ring slots of polyphase rows 4t .. 4t+3 (no wave
     // reads those again: tile t+1 reads rows 4t+4 .. 4t+9, and this tile's store_units fills the
@@ -290,7 +307,6 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     if (F32IN && a.pool) {
       __builtin_amdgcn_s_barrier();  // every wave is past its fragment reads of the scratch slots
       asm volatile("" ::: "memory");
-      const float* bs = reinterpret_cast<const float*>(lds + kBias);
       const int nrows = min(kRT, kHo - kRT * t);
       const char* carry_old = lds + kLds + ((t & 1) ^ 1) * kCarryB;
       char* carry_new = lds + kLds + (t & 1) * kCarryB;
@@ -304,7 +320,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
             sfor<0, 12>([&](auto Q) {
               constexpr int nb = decltype(Q)::value / 4, j = decltype(Q)::value % 4, f0 = 32 * nb + 8 * j;
               if constexpr (f0 >= 48 * p && f0 < 48 * p + 48) {
-                const f32x4 bv = *reinterpret_cast<const f32x4*>(bs + f0 + 4 * h);
+                const f32x4 bv = bias_r[nb * 4 + j];
                 bf16x4 v;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
@@ -347,7 +363,6 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
       // ---- epilogue: lane holds pixel m, filters 32 nb + 8 j + 4 h + (0..3) in acc[b][nb][4 j .. 4 j + 3].
       // kSPW buffer stores per lane, always issued (a pixel outside the tile stores past the extent,
       // which drops the write), so the vmcnt counts above hold on every wave.
-      const float* bs = reinterpret_cast<const float*>(lds + kBias);
   #pragma unroll
       for (int b = 0; b < kPB; ++b) {
         const int m = 64 * wave + 32 * b + r, oy = kRT * t + mrow[b];
@@ -361,8 +376,8 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
         for (int nb = 0; nb < 3; ++nb)
   #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int f0 = 32 * nb + 8 * j;  // wave-uniform
-            const f32x4 bv = *reinterpret_cast<const f32x4*>(bs + f0 + 4 * h);
+            [[maybe_unused]] const int f0 = 32 * nb + 8 * j;  // wave-uniform
+            const f32x4 bv = bias_r[nb * 4 + j];
             bf16x4 v;
   #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
@@ -374,10 +389,14 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     }
     // F32IN: tile t+1's new rows (loaded at this tile's start) into tile t-1's slots, which no wave
     // reads in tile t; the next tile's barrier publishes them
+    lap(2);
     if constexpr (F32IN)
       if (t + 1 < t1) store_units(kRT * t + 6);
+    lap(3);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  if (a.dbg && tid == 0 && blockIdx.x < 64)
+    for (int i = 0; i < 4; ++i) a.dbg[blockIdx.x * 4 + i] = ph[i];
 }
 
 }  // namespace
@@ -446,10 +465,27 @@ hipError_t conv1_bf16_ring(const void* xin, int N, const void* wpacked, const fl
     if (!a.pool && (out.Hb != kHo || out.Wb != kWo || out.Cb != kK || out.h_off || out.w_off || out.c_off))
       return hipErrorInvalidValue;  // the separate pool below reads a dense 55x55x96 map
   }
+  static const bool phases = std::getenv("ANX_RING_PHASES") != nullptr;
+  if (phases) {
+    static unsigned long long* dbg = nullptr;
+    if (!dbg && hipMalloc(&dbg, 64 * 4 * 8) != hipSuccess) return hipErrorOutOfMemory;
+    a.dbg = dbg;
+  }
   if (f32_input)
     conv1_bf16_ring_kernel<true><<<static_cast<unsigned>(N * a.segs), kNT, a.pool ? kLdsPool : kLds, s>>>(a);
   else
     conv1_bf16_ring_kernel<false><<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
+  if (phases) {  // debug: per-phase s_memtime clocks summed over the tiles, workgroups 0..63 averaged
+    unsigned long long h[64 * 4];
+    if (hipStreamSynchronize(s) == hipSuccess && hipMemcpy(h, a.dbg, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+      double m[4] = {0, 0, 0, 0};
+      const int nb = std::min(64, N * a.segs);
+      for (int b = 0; b < nb; ++b)
+        for (int i = 0; i < 4; ++i) m[i] += static_cast<double>(h[b * 4 + i]) / nb;
+      std::fprintf(stderr, "ring phases (clk/workgroup): barrier-wait %.0f  loads+mfma %.0f  epilogue %.0f  store_units %.0f\n",
+                   m[0], m[1], m[2], m[3]);
+    }
+  }
   if (pool_out && !a.pool) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
