@@ -174,9 +174,8 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const int lb = wave * 24 + q * 8;  // logical byte in the column's 96 (rh = wave)
-        bf16x4 v;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) v[f] = static_cast<bf16>(u[4 * q + f]);
+        // one packed conversion per pair (element-wise casts became a cvt with a zero partner + a perm)
+        const bf16x4 v = __builtin_convertvector((f32x4{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]}), bf16x4);
         *reinterpret_cast<bf16x4*>(col + (((lb >> 4) ^ sw) << 4) + (lb & 15)) = v;
       }
     }
@@ -226,7 +225,11 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
   f32x4 bias_r[12];
 #pragma unroll
   for (int q = 0; q < 12; ++q) bias_r[q] = *reinterpret_cast<const f32x4*>(a.bias + 32 * (q / 4) + 8 * (q % 4) + 4 * h);
-  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tc = __builtin_amdgcn_s_memtime();
+  // consume them here: the compiler's wait for these loads otherwise lands in every tile's epilogue
+  // as vmcnt waits that also wait for the next tile's row loads issued before it
+#pragma unroll
+  for (int q = 0; q < 12; ++q) asm volatile("" : "+v"(bias_r[q]));
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tc = __builtin_amdgcn_s_memtime();
   auto lap = [&](int i) {
     if (a.dbg) {
       const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -307,7 +310,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     if (F32IN && a.pool) {
       __builtin_amdgcn_s_barrier();  // every wave is past its fragment reads of the scratch slots
       asm volatile("" ::: "memory");
-      const int nrows = min(kRT, kHo - kRT * t);
+      lap(4);
       const char* carry_old = lds + kLds + ((t & 1) ^ 1) * kCarryB;
       char* carry_new = lds + kLds + (t & 1) * kCarryB;
       sfor<0, 2>([&](auto P) {
@@ -321,39 +324,44 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
               constexpr int nb = decltype(Q)::value / 4, j = decltype(Q)::value % 4, f0 = 32 * nb + 8 * j;
               if constexpr (f0 >= 48 * p && f0 < 48 * p + 48) {
                 const f32x4 bv = bias_r[nb * 4 + j];
-                bf16x4 v;
+                f32x4 y;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
+                for (int i = 0; i < 4; ++i) y[i] = fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f);
+                const bf16x4 v = __builtin_convertvector(y, bf16x4);
                 *reinterpret_cast<bf16x4*>(px + (f0 - 48 * p + 4 * h) * 2) = v;
               }
             });
           }
         }
+        lap(5);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        lap(6);
         if (tid < kPw * 6) {  // (pooled column, 8-filter chunk of this half)
           const int pc = tid / 6, c = tid - pc * 6;
-          u16x8 hr[kRT];
+          const int cofs = pc * (kK * 2) + (48 * p + 8 * c) * 2;
+          // all 13 reads first, one wait (row 3 of the last tile and the carry at the first tile are
+          // read but unused)
+          u16x8 v[kRT][3];
 #pragma unroll
           for (int k = 0; k < kRT; ++k) {
-            hr[k] = u16x8{};
-            if (k < nrows) {
-              const char* q = lds + ((kRT * t + k) % kSlots) * kSlotB + 2 * pc * (kCh * 2) + c * 16;
-              hr[k] = __builtin_elementwise_max(__builtin_elementwise_max(*reinterpret_cast<const u16x8*>(q),
-                                                                          *reinterpret_cast<const u16x8*>(q + 96)),
-                                                *reinterpret_cast<const u16x8*>(q + 192));
-            }
+            const char* q = lds + ((kRT * t + k) % kSlots) * kSlotB + 2 * pc * (kCh * 2) + c * 16;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) v[k][d] = *reinterpret_cast<const u16x8*>(q + d * (kCh * 2));
           }
-          const int cofs = pc * (kK * 2) + (48 * p + 8 * c) * 2;
+          const u16x8 co = *reinterpret_cast<const u16x8*>(carry_old + cofs);
+          u16x8 hr[kRT];
+#pragma unroll
+          for (int k = 0; k < kRT; ++k) hr[k] = __builtin_elementwise_max(__builtin_elementwise_max(v[k][0], v[k][1]), v[k][2]);
           const int ob = ((n * a.pHb + a.ph_off) * a.pWb + pc + a.pw_off) * a.pCb + a.pc_off + 48 * p + 8 * c;
           const int rstride = a.pWb * a.pCb;
           *reinterpret_cast<u16x8*>(a.pout + ob + 2 * t * rstride) =
               __builtin_elementwise_max(__builtin_elementwise_max(hr[0], hr[1]), hr[2]);
           if (t > t0)
-            *reinterpret_cast<u16x8*>(a.pout + ob + (2 * t - 1) * rstride) =
-                __builtin_elementwise_max(*reinterpret_cast<const u16x8*>(carry_old + cofs), hr[0]);
+            *reinterpret_cast<u16x8*>(a.pout + ob + (2 * t - 1) * rstride) = __builtin_elementwise_max(co, hr[0]);
           if (t + 1 < t1) *reinterpret_cast<u16x8*>(carry_new + cofs) = __builtin_elementwise_max(hr[2], hr[3]);
         }
+        lap(7);
         if constexpr (p == 0) {
           __builtin_amdgcn_s_barrier();  // the second half overwrites the scratch rows
           asm volatile("" ::: "memory");
@@ -363,7 +371,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
       // ---- epilogue: lane holds pixel m, filters 32 nb + 8 j + 4 h + (0..3) in acc[b][nb][4 j .. 4 j + 3].
       // kSPW buffer stores per lane, always issued (a pixel outside the tile stores past the extent,
       // which drops the write), so the vmcnt counts above hold on every wave.
-  #pragma unroll
+#pragma unroll
       for (int b = 0; b < kPB; ++b) {
         const int m = 64 * wave + 32 * b + r, oy = kRT * t + mrow[b];
         const bool ok = m < kRT * kWo && oy < kHo;
@@ -372,18 +380,19 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
         // which also broke the vmcnt counts above)
         [[maybe_unused]] const int obase =
             ok ? (((n * a.Hb + oy + a.h_off) * a.Wb + ox[b] + a.w_off) * a.Cb + a.c_off + 4 * h) * 2 : kOOB;
-  #pragma unroll
+#pragma unroll
         for (int nb = 0; nb < 3; ++nb)
-  #pragma unroll
+#pragma unroll
           for (int j = 0; j < 4; ++j) {
             [[maybe_unused]] const int f0 = 32 * nb + 8 * j;  // wave-uniform
             const f32x4 bv = bias_r[nb * 4 + j];
-            bf16x4 v;
-  #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = static_cast<bf16>(fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f));
-  #if __HIP_DEVICE_COMPILE__
+            f32x4 y;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) y[i] = fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f);
+            [[maybe_unused]] const bf16x4 v = __builtin_convertvector(y, bf16x4);
+#if __HIP_DEVICE_COMPILE__
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f0 * 2, 0);
-  #endif
+#endif
           }
       }
     }
@@ -396,7 +405,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
   if (a.dbg && tid == 0 && blockIdx.x < 64)
-    for (int i = 0; i < 4; ++i) a.dbg[blockIdx.x * 4 + i] = ph[i];
+    for (int i = 0; i < 8; ++i) a.dbg[blockIdx.x * 8 + i] = ph[i];
 }
 
 }  // namespace
@@ -468,7 +477,7 @@ hipError_t conv1_bf16_ring(const void* xin, int N, const void* wpacked, const fl
   static const bool phases = std::getenv("ANX_RING_PHASES") != nullptr;
   if (phases) {
     static unsigned long long* dbg = nullptr;
-    if (!dbg && hipMalloc(&dbg, 64 * 4 * 8) != hipSuccess) return hipErrorOutOfMemory;
+    if (!dbg && hipMalloc(&dbg, 64 * 8 * 8) != hipSuccess) return hipErrorOutOfMemory;
     a.dbg = dbg;
   }
   if (f32_input)
@@ -476,14 +485,16 @@ hipError_t conv1_bf16_ring(const void* xin, int N, const void* wpacked, const fl
   else
     conv1_bf16_ring_kernel<false><<<static_cast<unsigned>(N * a.segs), kNT, kLds, s>>>(a);
   if (phases) {  // debug: per-phase s_memtime clocks summed over the tiles, workgroups 0..63 averaged
-    unsigned long long h[64 * 4];
+    unsigned long long h[64 * 8];
     if (hipStreamSynchronize(s) == hipSuccess && hipMemcpy(h, a.dbg, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
-      double m[4] = {0, 0, 0, 0};
+      double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       const int nb = std::min(64, N * a.segs);
       for (int b = 0; b < nb; ++b)
-        for (int i = 0; i < 4; ++i) m[i] += static_cast<double>(h[b * 4 + i]) / nb;
-      std::fprintf(stderr, "ring phases (clk/workgroup): barrier-wait %.0f  loads+mfma %.0f  epilogue %.0f  store_units %.0f\n",
-                   m[0], m[1], m[2], m[3]);
+        for (int i = 0; i < 8; ++i) m[i] += static_cast<double>(h[b * 8 + i]) / nb;
+      std::fprintf(stderr,
+                   "ring phases (clk/workgroup): barrier-wait %.0f  loads+mfma %.0f  epilogue %.0f  store_units %.0f"
+                   "  | pool1: drain+barrier %.0f  lds-write %.0f  barrier %.0f  pool %.0f\n",
+                   m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]);
     }
   }
   if (pool_out && !a.pool) {
