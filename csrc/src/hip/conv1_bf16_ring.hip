@@ -87,6 +87,18 @@ struct Args {
   unsigned long long* dbg;  // ANX_RING_PHASES: per-workgroup phase clocks (wave 0), else null
 };
 
+// bf16(relu(acc[4j .. 4j+3] + bias)): the add as two packed f32 adds, then one packed conversion, then
+// ReLU as a signed 16-bit max with 0 on the bf16 bits (a negative value, -0 included, has its sign bit
+// set) — bit-identical to fmaxf before the conversion, since the rounding is monotonic
+using i16x4 = __attribute__((ext_vector_type(4))) short;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+__device__ __forceinline__ bf16x4 bias_relu_bf16(const f32x16& acc, int j, f32x4 bv) {
+  const f32x2 lo = f32x2{acc[4 * j], acc[4 * j + 1]} + f32x2{bv[0], bv[1]};
+  const f32x2 hi = f32x2{acc[4 * j + 2], acc[4 * j + 3]} + f32x2{bv[2], bv[3]};
+  const bf16x4 v = __builtin_convertvector((f32x4{lo[0], lo[1], hi[0], hi[1]}), bf16x4);
+  return __builtin_bit_cast(bf16x4, __builtin_elementwise_max(__builtin_bit_cast(i16x4, v), i16x4{0, 0, 0, 0}));
+}
+
 template <int B, int E, class F>
 __device__ __forceinline__ void sfor(F&& f) {
   if constexpr (B < E) {
@@ -324,10 +336,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
               constexpr int nb = decltype(Q)::value / 4, j = decltype(Q)::value % 4, f0 = 32 * nb + 8 * j;
               if constexpr (f0 >= 48 * p && f0 < 48 * p + 48) {
                 const f32x4 bv = bias_r[nb * 4 + j];
-                f32x4 y;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) y[i] = fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f);
-                const bf16x4 v = __builtin_convertvector(y, bf16x4);
+                const bf16x4 v = bias_relu_bf16(acc[b][nb], j, bv);
                 *reinterpret_cast<bf16x4*>(px + (f0 - 48 * p + 4 * h) * 2) = v;
               }
             });
@@ -386,10 +395,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
           for (int j = 0; j < 4; ++j) {
             [[maybe_unused]] const int f0 = 32 * nb + 8 * j;  // wave-uniform
             const f32x4 bv = bias_r[nb * 4 + j];
-            f32x4 y;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) y[i] = fmaxf(acc[b][nb][4 * j + i] + bv[i], 0.f);
-            [[maybe_unused]] const bf16x4 v = __builtin_convertvector(y, bf16x4);
+            [[maybe_unused]] const bf16x4 v = bias_relu_bf16(acc[b][nb], j, bv);
 #if __HIP_DEVICE_COMPILE__
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), orr, obase, f0 * 2, 0);
 #endif
