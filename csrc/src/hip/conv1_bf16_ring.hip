@@ -67,7 +67,10 @@ constexpr int kKS = kKd / 16;                           // 27 K steps (3 per tap
 constexpr int kAhead = 2;                               // K steps of fragments in flight
 constexpr int kOOB = 0x7ffffff0;
 static_assert(kK * kWRow * 2 <= kWBytes && kRowB <= kPieces * 1024 && kRing % 16 == 0, "LDS layout");
-static_assert(kLdsPool <= 160 * 1024 && kWo * kCh * 2 <= kSlotB, "pool1: carry rows fit; a 48-filter output row fits a slot");
+// pool1 scratch rows: a pixel's 48 filters (96 B) at a 112-B stride, so the epilogue's 8-B writes of
+// 32 consecutive pixels hit 16 bank offsets (2-way) instead of 8 (4-way at 96 B)
+constexpr int kPix = 112;
+static_assert(kLdsPool <= 160 * 1024 && kWo * kPix <= kSlotB, "pool1: carry rows fit; a 48-filter output row fits a slot");
 static_assert(kWaves * kPB * 32 >= kRT * kWo, "a tile's pixels fit the waves' blocks");
 static_assert(kRT * kPieces % kWaves == 0, "a tile's row DMAs split evenly over the waves");
 [[maybe_unused]] constexpr int kDPW = kRT * kPieces / kWaves;            // row DMAs per wave per tile (6)
@@ -331,7 +334,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
         for (int b = 0; b < kPB; ++b) {
           const int m = 64 * wave + 32 * b + r, oy = kRT * t + mrow[b];
           if (m < kRT * kWo && oy < kHo) {
-            char* px = lds + ((kRT * t + mrow[b]) % kSlots) * kSlotB + ox[b] * (kCh * 2);
+            char* px = lds + ((kRT * t + mrow[b]) % kSlots) * kSlotB + ox[b] * kPix;
             sfor<0, 12>([&](auto Q) {
               constexpr int nb = decltype(Q)::value / 4, j = decltype(Q)::value % 4, f0 = 32 * nb + 8 * j;
               if constexpr (f0 >= 48 * p && f0 < 48 * p + 48) {
@@ -354,9 +357,9 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
           u16x8 v[kRT][3];
 #pragma unroll
           for (int k = 0; k < kRT; ++k) {
-            const char* q = lds + ((kRT * t + k) % kSlots) * kSlotB + 2 * pc * (kCh * 2) + c * 16;
+            const char* q = lds + ((kRT * t + k) % kSlots) * kSlotB + 2 * pc * kPix + c * 16;
 #pragma unroll
-            for (int d = 0; d < 3; ++d) v[k][d] = *reinterpret_cast<const u16x8*>(q + d * (kCh * 2));
+            for (int d = 0; d < 3; ++d) v[k][d] = *reinterpret_cast<const u16x8*>(q + d * kPix);
           }
           const u16x8 co = *reinterpret_cast<const u16x8*>(carry_old + cofs);
           u16x8 hr[kRT];
