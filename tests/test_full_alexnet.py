@@ -232,6 +232,26 @@ def test_conv1_ring_fused_pool1_exact(cuda, N):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N", [300, 512])
+def test_full_lanes_pool1_paths_match_one_lane(cuda, N):
+    """Two stream lanes (forward_async) split the batch: at 300 each lane's 150 images take the
+    unfused Conv1 + maxpool fallback, at 512 each lane's 256 take pool1 inside the ring kernel — lane
+    0's pooled map is bit-identical to the one-lane forward's first half either way, and the logits
+    agree to the FC layers' split-K summation order."""
+    x = (torch.randn(N, 227, 227, 3, generator=torch.Generator().manual_seed(N + 7)) * 3).to(cuda)
+    one = AlexNetFull(seed=37, device=cuda, max_batch=N)
+    ref = one(x).clone()
+    ref_q = one.tap(1, N)[: N // 2].clone()
+    m = AlexNetFull(seed=37, device=cuda, max_batch=N, lanes=2)
+    out = torch.empty_like(ref)
+    m.forward_async(x, out)
+    m.join()
+    torch.cuda.synchronize()
+    assert torch.equal(m.tap(1, N // 2), ref_q)
+    assert ((out.double() - ref.double()).norm() / ref.double().norm()).item() < 1e-2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("shift", [1, 2, 3])
 def test_conv1_ring_fp32_input_interior_pointer(cuda, shift):
     """The fused-input ring (bf16_conv1=2) reads the fp32 image with aligned 16-B window loads from the
