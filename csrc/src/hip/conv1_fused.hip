@@ -67,7 +67,8 @@ constexpr bool loads_at(int p) {
   const int av = p < 0 ? 0 : p / kN5, b = p < 0 ? kN5 - 1 : p % kN5;
   return b + 1 < kN5 ? needs_row(av + 1, b + 1) : needs_row(av + (p < 0 ? 1 : 2), 0);
 }
-static_assert(kTiles * kOS <= kLdsFloats, "epilogue scratch");
+static_assert(9 * kTiles * kOS <= kDummy && kTiles * kOS <= 2 * kVBuf,
+              "epilogue scratch: nine position images below the dummy DMA slot (UM 0), one in the V buffers (UM 1)");
 static_assert(kTiles * 24 == kNT, "V build: one (tile, channel pair) per thread");
 
 template <int B, int E, class F>
@@ -350,21 +351,45 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
     sti = pq % a.ty;
     sn = pq / a.ty;
   }
-  __syncthreads();  // every wave's last fragment reads are done: the LDS is scratch now
+  if constexpr (UM == 0) {
+    // all nine output positions' images at once (9 x 32 x 100 floats = 115 KB of the 128 KB): one
+    // barrier and nine back-to-back stores per thread instead of a write / barrier / store / barrier
+    // round per position. The images reach into the U ring's slots, so no DMA may still be landing.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's last fragment reads are done: the LDS is scratch now
 #pragma unroll
-  for (int q = 0; q < 9; ++q) {
+    for (int q = 0; q < 9; ++q)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float v = Y[q][i] + bv;
-      if (a.relu) v = fmaxf(v, 0.f);
-      tr[(wm * 16 + 4 * h4 + i) * kOS + f] = v;
+      for (int i = 0; i < 4; ++i) {
+        float v = Y[q][i] + bv;
+        if (a.relu) v = fmaxf(v, 0.f);
+        tr[(q * kTiles + wm * 16 + 4 * h4 + i) * kOS + f] = v;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const int oy = sti * 3 + q / 3, ox = stj * 3 + q % 3;
+      if (sp < a.P && oy < a.Ho && ox < a.Wo)
+        *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(sn * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
+                                  o.c_off + 4 * sq) = *reinterpret_cast<const f32x4*>(tr + (q * kTiles + st) * kOS + 4 * sq);
     }
-    __syncthreads();
-    const int oy = sti * 3 + q / 3, ox = stj * 3 + q % 3;
-    if (sp < a.P && oy < a.Ho && ox < a.Wo)
-      *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(sn * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
-                                o.c_off + 4 * sq) = *reinterpret_cast<const f32x4*>(tr + st * kOS + 4 * sq);
-    __syncthreads();
+  } else {  // UM 1 launches with 2 V buffers of LDS only: one position image (12.8 KB) at a time
+    __syncthreads();  // every wave's last fragment reads are done: the LDS is scratch now
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = Y[q][i] + bv;
+        if (a.relu) v = fmaxf(v, 0.f);
+        tr[(wm * 16 + 4 * h4 + i) * kOS + f] = v;
+      }
+      __syncthreads();
+      const int oy = sti * 3 + q / 3, ox = stj * 3 + q % 3;
+      if (sp < a.P && oy < a.Ho && ox < a.Wo)
+        *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(sn * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
+                                  o.c_off + 4 * sq) = *reinterpret_cast<const f32x4*>(tr + st * kOS + 4 * sq);
+      __syncthreads();
+    }
   }
 }
 
