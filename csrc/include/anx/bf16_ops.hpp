@@ -68,7 +68,8 @@ struct BigFc {
 };
 // cfg >= 0 forces that wide-tile config (knob bf16_fc_cfg; -1 = cfg 8, the measured default).
 constexpr int kMaxFcSplit = 16;
-BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus = 256, int cfg = -1);
+// min_kt: K tiles per split-K slice at least this many (knob bf16_fc_minkt)
+BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus = 256, int cfg = -1, int min_kt = 4);
 // Fully-connected layer on the activation-streaming kernel (activations global -> VGPR four K tiles
 // ahead, weights through an LDS-DMA ring): fp32 slabs [ksplit][N][Kg] into ws, then
 // splitk_reduce_bf16. Needs C % 64 == 0 and ksplit | K tiles with (K tiles / ksplit) % 4 == 0;

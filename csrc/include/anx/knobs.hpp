@@ -29,6 +29,8 @@ struct Knobs {
   int bf16_fc = 0;         // bf16 FC layers: 1 = activation-streaming kernel (fc_bf16; measured slower than the
                            // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
   int bf16_fc_cfg = -1;    // bf16 FC layers: force this wide-tile config (A/B; -1 = cfg 8, 256x64 3-stage)
+  int bf16_fc_minkt = 4;   // bf16 FC layers: K tiles per split-K slice at least this many (fewer slices, less
+                           // reduce; 8 / 16 measured no better: profiles/r04_bf16_fc_minkt_ab.jsonl)
   int bf16_lrn_tile = 0;   // bf16 pool2+LRN: 1 = the generic LDS-tile kernel instead of the C=256 wave kernel
   int bf16_conv1 = 2;      // bf16 Conv1 (polyphase): 2 = the persistent row-band kernel on the fp32 image
                            // (conv1_bf16_ring.hip: space-to-depth + bf16 inside, rows in an LDS ring, weights

@@ -117,7 +117,7 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
       const int ks = hip::fc_split_k(p);
       if (ks > 1) ws = std::max(ws, static_cast<size_t>(ks) * b * L_[i].K);
       for (int c = -1; c < hip::conv_bf16_big_cfgs(); ++c) {  // every config bf16_fc_cfg may force
-        const hip::BigFc f = hip::pick_bf16_big_fc(p, cus_, c);  // wide-tile FC slabs (ksplit 1 for fp32 logits)
+        const hip::BigFc f = hip::pick_bf16_big_fc(p, cus_, c, 1);  // wide-tile FC slabs (ksplit 1 for fp32 logits)
         if (f.cfg >= 0) ws = std::max(ws, static_cast<size_t>(f.ksplit) * b * L_[i].K);
       }
       if (hip::fc_bf16_ok(p)) ws = std::max(ws, static_cast<size_t>(std::max(1, hip::pick_fc_split(p, cus_))) * b * L_[i].K);
@@ -167,7 +167,7 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
     }
   }
   if (fc && k_.bf16_big != -2) {  // wide-tile FC: one 256-row tile of the batch, K split over the CUs
-    hip::BigFc f = hip::pick_bf16_big_fc(p, cus_, k_.bf16_fc_cfg);
+    hip::BigFc f = hip::pick_bf16_big_fc(p, cus_, k_.bf16_fc_cfg, k_.bf16_fc_minkt);
     if (f.cfg >= 0 && k_.bf16_big >= 0 && hip::conv_bf16_big_ok(p, k_.bf16_big, hip::OutViewB{B(ws_), 1, 1, p.Kg, 0, 0, 0}))
       f.cfg = k_.bf16_big;
     if (f.cfg >= 0 && (f.ksplit > 1 || out_f32)) {

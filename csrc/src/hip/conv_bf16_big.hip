@@ -668,7 +668,7 @@ int pick_bf16_big_cfg(const ConvPlanB& p, const OutViewB& out, int cus) {
 // slices ~ one workgroup per CU with >= 4 K tiles per slice. Measured at 256 images
 // (profiles/r02_bf16bench_b256.txt): FC6 36 us, FC7 23 us, FC8 18 us with the reduce, against 43 /
 // 28 / 24 us for the 128x128 split-K path.
-BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus, int cfg) {
+BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus, int cfg, int min_kt) {
   BigFc r{-1, 1};
   if (p.Ho != 1 || p.Wo != 1 || p.groups != 1 || p.Kg % 8) return r;
   const OutViewB probe{reinterpret_cast<__bf16*>(16), 1, 1, p.Kg, 0, 0, 0};
@@ -680,7 +680,8 @@ BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus, int cfg) {
   const long tiles = (p.N + c.BM - 1) / c.BM * ((p.Kg + c.BN - 1) / c.BN);
   const int ktiles = p.kpad / kBK;
   const long want = (static_cast<long>(cus) * c.wgs_per_cu + tiles - 1) / tiles;
-  r.ksplit = static_cast<int>(std::max<long>(1, std::min<long>({want, ktiles / 4, static_cast<long>(kMaxFcSplit)})));
+  r.ksplit = static_cast<int>(
+      std::max<long>(1, std::min<long>({want, ktiles / std::max(1, min_kt), static_cast<long>(kMaxFcSplit)})));
   return r;
 }
 

@@ -30,6 +30,7 @@ const Field kFields[] = {
     {"bf16_big", &Knobs::bf16_big, nullptr, -2, 16, "ANX_BF16_BIG"},
     {"bf16_lrn_tile", &Knobs::bf16_lrn_tile, nullptr, 0, 1, nullptr},
     {"bf16_fc_cfg", &Knobs::bf16_fc_cfg, nullptr, -1, 11, "ANX_BF16_FC_CFG"},
+    {"bf16_fc_minkt", &Knobs::bf16_fc_minkt, nullptr, 1, 64, nullptr},
     {"bf16_conv1", &Knobs::bf16_conv1, nullptr, 0, 2, "ANX_BF16_CONV1"},
     {"bf16_pool1", &Knobs::bf16_pool1, nullptr, 0, 1, "ANX_BF16_POOL1"},
     {"bf16_fc", &Knobs::bf16_fc, nullptr, 0, 1, "ANX_BF16_FC"},
