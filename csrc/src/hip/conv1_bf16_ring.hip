@@ -346,6 +346,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
           }
         }
         lap(5);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's rows written before the barrier
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         lap(6);
@@ -375,6 +376,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
         }
         lap(7);
         if constexpr (p == 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();  // the second half overwrites the scratch rows
           asm volatile("" ::: "memory");
         }
