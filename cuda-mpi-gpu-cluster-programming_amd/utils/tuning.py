@@ -11,8 +11,11 @@ Names and values:
   ``direct``.
 * integer knobs: ``chunk1``, ``chunk2`` (images per launch), ``conv1_occ``, ``conv2_occ`` (Winograd
   GEMM workgroups-per-CU caps), ``force_vec4``, ``force_scalar`` (direct GEMM tiles), and the bf16
-  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``, ``bf16_conv1`` (1, the default:
-  Conv1 as the persistent row-band kernel; 0: the implicit-GEMM tiles); ``conv1_band`` (2, the default: the
+  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``, ``bf16_fc_cfg``,
+  ``bf16_fc_minkt``, ``bf16_conv1`` (2, the default: Conv1 as the persistent row-band kernel reading
+  the fp32 image; 1: the same kernel on the s2d4 polyphase copy; 0: s2d4 + the implicit-GEMM tiles),
+  ``bf16_pool1`` (1, the default: pool1 in the row-band kernel's epilogue when each image has its own
+  workgroup; 0: Conv1 writes its map and maxpool_bf16 follows); ``conv1_band`` (2, the default: the
   Conv1 input transform stages a tile row's image rows in LDS, all 4 phase rows x half the tile
   columns per workgroup; 1: 2 phase rows x all columns; 0: per-tile global gathers);
   ``fuse_pool1`` (1, the
