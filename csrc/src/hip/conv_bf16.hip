@@ -475,27 +475,36 @@ __global__ void __launch_bounds__(256) pool_lrn256_bf16_kernel(const bf16* __res
   for (int base = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 * U; base < P; base += nw * 2 * U) {  // wave-uniform
     float m[U][8];
     int pix[U];
+    // every window load unconditional (clamped to a valid pixel, masked to -inf when outside): a
+    // load inside a branch made the compiler wait for it at the join, one load in flight per wave
+    bf16x8 wv[U][F * F];
+    bool wok[U][F * F];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int p = base + 2 * u + half;
       pix[u] = p;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) m[u][e] = -INFINITY;
-      if (p >= P) continue;
-      const int ox = p % Wo, q = p / Wo, oy = q % Ho, n = q / Ho;
+      const int pc = min(p, P - 1);
+      const int ox = pc % Wo, q = pc / Wo, oy = q % Ho, n = q / Ho;
 #pragma unroll
       for (int fh = 0; fh < F; ++fh) {
         const int iy = oy * S + fh;
 #pragma unroll
         for (int fw = 0; fw < F; ++fw) {
           const int ix = ox * S + fw;
-          if (iy < H && ix < W) {
-            const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((static_cast<size_t>(n) * H + iy) * W + ix) * C + cl * 8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) m[u][e] = fmaxf(m[u][e], static_cast<float>(v[e]));
-          }
+          wok[u][fh * F + fw] = iy < H && ix < W;
+          wv[u][fh * F + fw] = *reinterpret_cast<const bf16x8*>(
+              x + ((static_cast<size_t>(n) * H + min(iy, H - 1)) * W + min(ix, W - 1)) * C + cl * 8);
         }
       }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[u][e] = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < F * F; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[u][e] = fmaxf(m[u][e], wok[u][t] ? static_cast<float>(wv[u][t][e]) : -INFINITY);
     }
     const int left = ((lane + 63) & 63) * 4, right = ((lane + 1) & 63) * 4;
 #pragma unroll
