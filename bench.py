@@ -125,6 +125,16 @@ def parse():
                          "loaded clock (0 = off)")
     ap.add_argument("--model", default="blocks", choices=["blocks", "full"],
                     help="blocks = the headline AlexNet Blocks1-2 fp32; full = full AlexNet bf16 extension")
+    ap.add_argument("--calibrate-root", default="auto", choices=["auto", "on", "off"],
+                    help="dp, N>1 with root shedding: measure per-rank compute spans before the warmup and rescale "
+                         "rank 0's share to the peers' (auto = on when the share is the cost model's, not --root-batch)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="dp, N>1: skip the post-window gather checksum / oracle verification step")
+    ap.add_argument("--no-full", action="store_true",
+                    help="blocks dp on GPUs: skip the secondary full-AlexNet bf16 (BASELINE config 5) measurement")
+    ap.add_argument("--first-collective-s", type=float, default=float(os.environ.get("ANX_FIRST_COLLECTIVE_S", "240")),
+                    help="N>1: seconds the process-group setup and first collectives may take before the rank exits "
+                         "with a rank-tagged error (0 = no watchdog)")
     return ap.parse_args()
 
 
@@ -148,6 +158,9 @@ def process_cold_b1() -> dict:
         return {"b1_process_cold_ms": None, "b1_process_note": f"anx v3 failed rc={out.returncode}"}
     r = recs[0]
     return {"b1_process_cold_ms": round(r["cold_ms"], 3), "b1_process_wall_ms": round(wall, 1),
+            # where the cold time goes (init = HIP runtime / context, engine = weights + workspace, alloc,
+            # h2d / compute / d2h of the first image)
+            "b1_process_phases_ms": {k: round(v, 3) for k, v in (r.get("phases_cold") or {}).items()},
             "b1_process_warm_ms": round(float(r["warm_ms"]), 4),
             "b1_process_cold_vs_reference": round(BASELINE_V3_MS / r["cold_ms"], 2),
             "b1_process_note": "anx --version v3 --batch 1 child: cold_ms from main() entry incl. HIP context "
@@ -177,6 +190,65 @@ def batch1_latency(dev, reps: int = 20) -> dict:
             "b1_vs_reference_warm": round(BASELINE_V3_MS / warm, 1)}
 
 
+def full_bf16_secondary(dev, world: int, rank: int, steps: int = 10, warmup: int = 3, prewarm_s: float = 0.5) -> dict:
+    """BASELINE config 5 beside the headline: full AlexNet (Conv1-5 + FC6-8) bf16, 256 images per GPU,
+    weak scaling (each rank its own batch, no gather), timed like the headline over a short window."""
+    from anx.models.alexnet_full import FLOPS_PER_IMAGE, AlexNetFull
+    B = 256
+    m = AlexNetFull(seed=1234, device=dev, max_batch=B)
+    g = torch.Generator(device=dev)
+    g.manual_seed(77 + rank)
+    xs = [torch.rand((B, 227, 227, 3), device=dev, generator=g) for _ in range(2)]
+    y = torch.empty((B, 1000), device=dev)
+    k = 0
+    t0 = time.perf_counter()
+    while True:  # clock settle (also the first-call setup)
+        for _ in range(8):
+            m(xs[k % 2], y)
+            k += 1
+        torch.cuda.synchronize()
+        if time.perf_counter() - t0 > prewarm_s:
+            break
+    for _ in range(warmup):
+        m(xs[k % 2], y)
+        k += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m(xs[k % 2], y)
+        k += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    finite = bool(torch.isfinite(y).all().item())
+    m.close()
+    ips = B * world * steps / el
+    return {"metric": "images/sec full AlexNet (Conv1-5 + FC6-8) bf16 inference (BASELINE config 5, extension)",
+            "value": round(ips, 1), "unit": "images/s", "ms_per_step": round(el * 1e3 / steps, 4), "steps": steps,
+            "warmup": warmup, "batch_per_gpu": B, "global_batch": B * world, "n_gpus": world, "dtype": "bf16",
+            "scaling": "weak", "tflops": round(ips * FLOPS_PER_IMAGE / 1e12, 1), "outputs_finite": finite,
+            "data": "synthetic images, He-uniform random weights", "note": "secondary record; the headline is fp32"}
+
+
+def _oracle(model):
+    """fp64 PyTorch oracle of one image (max |y - ref| / max |ref|)."""
+    from anx.models.reference import blocks_forward
+
+    def check(x1, y1):
+        ref = blocks_forward(x1.detach().cpu(), model.weights, model.b1, model.b2)
+        return float((y1.detach().cpu().double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+    return check
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -186,15 +258,21 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     # before this process's first GPU call (a child of a GPU-initialised process would not be cold)
     b1p = process_cold_b1() if (rank == 0 and a.device == "cuda" and not a.no_b1 and a.model == "blocks") else {}
-    if a.device == "cuda":
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+    from anx.parallel import selfcheck
+    ident = None
+    with selfcheck.FirstCollectiveWatchdog(rank, a.first_collective_s if world > 1 else 0,
+                                           "process-group setup + first collective"):
+        if a.device == "cuda":
+            torch.cuda.set_device(local)
+            dev = torch.device("cuda", local)
+            if world > 1:
+                dist.init_process_group("nccl", device_id=dev, timeout=timedelta(seconds=300))  # a hung collective fails in 5 min, not 10
+        else:  # CPU rehearsal of the same program over gloo (tests; no GPU)
+            dev = torch.device("cpu")
+            if world > 1:
+                dist.init_process_group("gloo", timeout=timedelta(seconds=300))
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev, timeout=timedelta(seconds=300))  # a hung collective fails in 5 min, not 10
-    else:  # CPU rehearsal of the same program over gloo (tests; no GPU)
-        dev = torch.device("cpu")
-        if world > 1:
-            dist.init_process_group("gloo", timeout=timedelta(seconds=300))
+            ident = selfcheck.rank_identity(dev)  # the first collective: every rank's device, gathered
     cuda = dev.type == "cuda"
 
     d = anx.blocks_dims()
@@ -269,16 +347,16 @@ def main():
         if pipe.x_global is not None:
             pipe.x_global.copy_(torch.rand(pipe.x_global.shape, device=dev, generator=g) * 0.1)
         else:  # every input buffer of the (double-buffered) pipeline holds real images
-            for xb in pipe._xb:
+            for xb in pipe._xfull:
                 xb.copy_(torch.rand(xb.shape, device=dev, generator=g) * 0.1)
         step = pipe.step
         use_graph = bool(a.graph if a.graph >= 0 else world == 1) and world == 1 and cuda
         if pipe.x_global is None and not use_graph and cuda:
             # distinct batches round-robin: >= 4 and > 256 MB together, so the input is not resident in
             # the 256 MB Infinity Cache (a captured graph replays one input pointer: no rotation there)
-            nb = pipe._xb[0].numel() * 4
+            nb = pipe._xfull[0].numel() * 4
             n_rot = min(64, max(4, -(-(300 << 20) // nb)))
-            pipe.inputs = [torch.rand(pipe._xb[0].shape, device=dev, generator=g) * 0.1 for _ in range(n_rot)]
+            pipe.inputs = [torch.rand(pipe._xfull[0].shape, device=dev, generator=g) * 0.1 for _ in range(n_rot)]
         if use_graph:
             # The engine is stream-ordered (no allocation, copy or sync inside a forward), so one step
             # captures as a graph of its kernel launches; a replay then costs one host call per step.
@@ -299,6 +377,17 @@ def main():
     # profiles/r02_bench_warmup.txt). Untimed, bounded by --prewarm-s, reported in the JSON.
     # Every rank runs the same number of steps (step() holds collectives): 8 steps (first-call setup),
     # 8 timed probe steps, then as many more as the slowest rank's probe says fill the budget.
+    # rank 0's share, measured: per-rank lane compute spans while rank 0 receives (selfcheck)
+    calib = None
+    calibrate = a.calibrate_root == "on" or (a.calibrate_root == "auto" and a.root_batch < 0)
+    if wl is None and world > 1 and pipe.shed and pipe.async_lanes and calibrate:
+        from anx.models.alexnet_blocks import LANE_MIN
+        for _ in range(4):  # first-call setup outside the measured rounds
+            step()
+        lanes_b = len(model.lane_bounds(B)) - 1 if hasattr(model, "lane_bounds") else 1
+        calib = selfcheck.calibrate_root_batch(pipe, step, torch.cuda.synchronize if cuda else (lambda: None),
+                                               min_root=min(B, lanes_b * LANE_MIN if lanes_b > 1 else 1))
+        root_b = pipe.root_batch
     t_pw, n_pw = time.perf_counter(), 0
     if cuda and a.prewarm_s > 0:
         for _ in range(8):
@@ -348,6 +437,15 @@ def main():
     per_step = B if wl is not None else B * (world - 1) + root_b  # images per step over the whole job
     imgs = per_step * a.steps / el
     phases = wl.phase_ms() if wl is not None else None
+    # N > 1: one more (untimed) step, then prove the gather and the numerics (selfcheck.verify_gather)
+    verify = None
+    if wl is None and world > 1 and not a.no_verify and a.model == "blocks":
+        step()
+        pipe.drain()
+        sync()
+        corrupt = os.environ.get("ANX_BENCH_CORRUPT_RANK")
+        verify = selfcheck.verify_gather(pipe, oracle=_oracle(model),
+                                         corrupt_rank=int(corrupt) if corrupt not in (None, "") else None)
 
     if a.model == "full":
         if rank == 0:
@@ -370,6 +468,12 @@ def main():
         return
 
     b1 = batch1_latency(dev) if (rank == 0 and cuda and not a.no_b1) else {}
+    full = None
+    if cuda and wl is None and not a.no_full:
+        try:
+            full = full_bf16_secondary(dev, world, rank)
+        except Exception as e:  # the headline record must not depend on the extension
+            full = {"error": repr(e)[:300]}
     if rank == 0:
         mf = mfma_flops_per_image()
         if wl is None:
@@ -382,6 +486,7 @@ def main():
             rot = pipe.inputs or []
             extra = {"input_source": a.input_source, "lanes": a.lanes, "hip_graph": use_graph, "knobs": a.knob,
                      "batch_per_gpu": B, "root_batch": root_b,
+                     **({"root_batch_modelled": cfg.root_batch, **calib} if calib else {}),
                      "root_batch_note": ("rank 0 sheds the share its gather ingest costs it (cost model "
                                          "dp_root_batch; tools/probe_ingest.py)") if root_b != B else None,
                      "input_batches_rotated": len(rot) or 1,
@@ -468,6 +573,14 @@ def main():
                 **b1p,
             },
         }
+        if world > 1:  # who ran and whether the gathered outputs are right (selfcheck)
+            rec["rccl_world_size"] = ident["world_size"] if ident else world
+            rec["identity"] = ident
+            if verify is not None:
+                rec["gather_verified"] = verify["gather_verified"]
+                rec["verify"] = verify
+        if full is not None:
+            rec["full_bf16"] = full
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

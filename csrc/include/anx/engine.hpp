@@ -47,9 +47,12 @@ class BlocksEngine {
   const BlocksDims& dims() const { return d_; }
   int max_batch() const { return max_batch_; }
   Impl impl() const { return impl_; }
-  // Read at every launch: changing a knob between calls switches kernels (weights re-pack lazily).
-  Knobs& knobs() { return k_; }
+  // Read at every launch: changing a knob between calls switches kernels. Use set_knob (it prepares
+  // the weights / workspace the new setting needs outside any forward); a field written through
+  // knobs() directly re-packs direct-path weights lazily and runs a conv without its Winograd workspace
+  // on the direct path.
   const Knobs& knobs() const { return k_; }
+  int set_knob(const char* name, int value);  // 0, or -1 for a bad name / value (unchanged)
 
   // x: [N, H, W, C0] device; y: [N, Hp2, Wp2, C2] device.
   hipError_t forward(const float* x, int N, float* y, hipStream_t s);
@@ -72,6 +75,9 @@ class BlocksEngine {
   size_t q2_image_stride_floats(const TilePlan& t) const { return static_cast<size_t>(t.q.size()) * q2_row_floats(); }
 
  private:
+  void prepare();
+  hipError_t pack1(const hip::ConvPlan& p);  // direct-path packed weights for plan p (no-op when current)
+  hipError_t pack2(const hip::ConvPlan& p);
   hipError_t ensure_window(const TilePlan& t, int N, hipStream_t s);
   // conv1 (+ReLU) of n images into c1_ starting at image c1_img0
   hipError_t conv1_chunk(const float* xc, int n, const TilePlan& t, hipStream_t s, int c1_img0 = 0);
@@ -79,6 +85,9 @@ class BlocksEngine {
   hipError_t pool2_chunk(int n, const TilePlan& t, float* yc, hipStream_t s);  // c2_ -> y (+LRN)
   // Whether tile_forward of N images runs pool1 inside the Winograd input transform (Knobs::fuse_pool1)
   bool fused_pool1(int N, const TilePlan& t) const;
+  // ... and whether pool1 runs inside the one-kernel Conv1 instead (Knobs::conv1_pool; whole images only)
+  bool conv1_pools(int N, const TilePlan& t) const;
+  hipError_t tile_forward_conv1_pool(const float* x, int N, const TilePlan& t, float* y, hipStream_t s);
 
   BlockSpec b1_, b2_;
   BlocksDims d_;

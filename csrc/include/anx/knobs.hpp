@@ -49,6 +49,10 @@ struct Knobs {
   int conv1_fused = 1;     // Conv1 as one kernel (conv1_fused.hip: V built in LDS inside the GEMM, 32 tiles x 96
                            // filters per workgroup; bench step 277-278 k vs 252-254 k images/s,
                            // profiles/r04_conv1_fused_v3_bench_ab.jsonl), 2 = U fragments in registers (A/B), 0 = the band transform kernel + GEMM
+  int conv1_pool = 1;      // fused tile_forward of whole images: pool1 in the one-kernel Conv1's epilogue (conv1_fused 1;
+                           // the 55x55 map stays in LDS, pooled pixels go to the conv2 window, straddling windows'
+                           // partial maxima to a side buffer merged by the Conv2 input transform), 0 = Conv1 writes its
+                           // map and the input transform pools it
   int conv1_sub = 0;       // fused tile_forward: images per Conv1 (input transform + GEMM) launch pair inside a
                            // chunk (0 = the whole chunk); the V workspace is rewritten in place per sub-chunk, so
                            // a small one is written and re-read inside the 256 MB Infinity Cache
@@ -57,7 +61,7 @@ struct Knobs {
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
 // ANX_BF16_GLDS, ANX_BF16_BIG, ANX_BF16_FC, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1,
-// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED when set.
+// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

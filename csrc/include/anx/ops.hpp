@@ -108,6 +108,11 @@ hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s
 // (pool_F, pool_S; anything else returns hipErrorInvalidValue: the kernel's walk is written for 3/2).
 hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, int q_lo, int Hp, int Wp, int P,
                            int c1_lo, float* V, hipStream_t s, int pool_F = 3, int pool_S = 2);
+// Input transform of a conv2 window whose pool1 pixels were written by conv1_fused_pool: straddling
+// pixels take max(window, p1) (p1: [N][Hp][Wp][C], image 0 = tile-numbering image n_off of the Conv1
+// launch with ty1 x tx1 tiles per image). Window row R is pool1 row q_lo + R, column c pool1 column c - P.
+hipError_t wino_window_merge_input(const WinoPlan& w, const float* window, const float* p1, int n_off, int ty1, int tx1,
+                                   int q_lo, int Hp, int Wp, int P, float* V, hipStream_t s);
 // Fused batched GEMM + output transform + bias + optional ReLU into `out` (wino_gemm.hpp); Knobs:
 // conv2_occ (workgroups per CU cap).
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,
@@ -134,6 +139,21 @@ hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const fl
 bool conv1_fused_eligible(const Conv1WinoPlan& w, const OutView& out);
 hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out, bool relu,
                        hipStream_t s, int mode = 1);
+// The same kernel with pool1 (3x3 / 2 max) in its epilogue: the 55x55 conv1 map never leaves LDS. Pooled
+// pixel (py, px) of image n is written to `window` (pool1 image at h_off / w_off, e.g. the conv2 input
+// window) by the workgroup owning the window's top-left Conv1 tile; when the window's tiles straddle two
+// workgroups' 32-tile ranges (pool1_straddles), that value is the lower workgroup's partial max and the
+// upper one's is in p1 [N][Hp][Wp][K]: the consumer takes the max of both (wino_window_merge_input).
+// Exact (max in any order), so the merged pool1 map equals conv1_fused + maxpool.
+constexpr int kConv1FusedTiles = 32;  // Conv1 tiles per conv1_fused workgroup (raster order)
+__host__ __device__ inline bool pool1_straddles(int n, int py, int px, int ty1, int tx1) {
+  const int b = n * ty1 * tx1;
+  const int gm = b + (2 * py / 3) * tx1 + (2 * px) / 3, gM = b + ((2 * py + 2) / 3) * tx1 + (2 * px + 2) / 3;
+  return gm / kConv1FusedTiles != gM / kConv1FusedTiles;
+}
+bool conv1_fused_pool_eligible(const Conv1WinoPlan& w, const OutView& window, int Hp, int Wp);
+hipError_t conv1_fused_pool(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView window,
+                            float* p1, int Hp, int Wp, bool relu, hipStream_t s);
 
 // The fused Winograd GEMM + output transform (wino_gemm.hip). V [P][points][C], U [points][K][C/groups]
 // (row = filter), bias + optional ReLU, NHWC store through `out` (Cb, c_off multiples of 4). P tiles of
@@ -146,16 +166,6 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
                            int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
 
-// A/B build only (anx_wgemm; defined under ANX_WGEMM_ABLATIONS): the same GEMMs on the bf16 matrix
-// cores with fp32-exact operands (wino_gemm_sb.hpp): U as three bf16 planes Ub[point][plane h/m/l][row]
-// [C/groups] (wino_split_planes_host: x = h + m + l exactly), V fp32 split in registers; nprod = 9
-// (every part product) or 6 (drops the three below 2^-21 |x*y|). Measured no faster than f32 MFMA.
-void wino_split_planes_host(const std::vector<float>& u, int npt, int rows, int cols, std::vector<uint16_t>& ub);
-hipError_t wino_sb_gemm_conv2(const float* V, const uint16_t* Ub, const float* bias, OutView out, int P, int ty, int tx,
-                              int Ho, int Wo, int C, int K, int groups, bool relu, hipStream_t s, int nprod = 9,
-                              int occ = 0, int abl = 0);
-hipError_t wino_sb_gemm_conv1(const float* V, const uint16_t* Ub, const float* bias, OutView out, int P, int ty, int tx,
-                              int Ho, int Wo, int K, bool relu, hipStream_t s, int nprod = 9, int occ = 0, int abl = 0);
 
 // Dynamic LDS bytes that cap a kernel at `wgs` workgroups per CU (160 KiB LDS per CU): the larger of
 // `natural` and just over 160 KiB / (wgs + 1). wgs <= 0: `natural`.

@@ -96,6 +96,11 @@ class Transport {
   virtual void run_phase(Phase ph, const std::vector<Transfer>& xs, hipStream_t compute, int parity) = 0;
   // Collective teardown (unmap peers' buffers, free own ones).
   virtual void close() {}
+  // Fail-stop (not collective): release every device-side wait of this rank's streams on its peers so
+  // they drain (RCCL: ncclCommAbort; device flags: every flag word this rank waits on, and the ones its
+  // peers wait on, raised to the maximum). The transport is unusable afterwards; close() skips the
+  // collective part.
+  virtual void abort() {}
   // Record-only mode (no HIP / RCCL / socket call): every transfer is appended to log() — the
   // schedule the transport would execute, for tests and --dry-run.
   bool record_only = false;

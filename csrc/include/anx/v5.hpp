@@ -107,6 +107,10 @@ class V5Runtime {
   void step();
   // Wait for every enqueued step on every stream of this rank.
   void sync();
+  // Fail-stop after an error on this rank (not collective): the transport releases every device-side
+  // wait on a peer (ncclCommAbort / raised flag words), so the destructor's device sync returns; the
+  // collective teardown is skipped. Call before rethrowing; the runtime is unusable afterwards.
+  void abort();
   // Root: the output of the last step [batch, Hp2, Wp2, C2] into host memory (syncs first).
   void output(float* host_y);
   // Mean ms per step since the last reset, by phase, on the compute stream's critical path:

@@ -407,7 +407,7 @@ int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff
 }
 
 int anx_engine_set_knob(void* e, const char* name, int value) {
-  if (anx::set_knob(static_cast<anx::BlocksEngine*>(e)->knobs(), name, value) != 0)
+  if (static_cast<anx::BlocksEngine*>(e)->set_knob(name, value) != 0)
     return fail(std::string("bad knob or value: ") + (name ? name : "(null)"));
   return 0;
 }

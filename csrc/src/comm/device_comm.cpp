@@ -125,7 +125,7 @@ class LoopbackComm final : public DeviceComm {
   ~LoopbackComm() override {
     try {
       (void)hipStreamSynchronize(stream_);
-      hc_.barrier();  // no peer copies into our buffers or writes our flags any more
+      if (!aborted_) hc_.barrier();  // no peer copies into our buffers or writes our flags any more
     } catch (...) {
     }
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
@@ -135,6 +135,19 @@ class LoopbackComm final : public DeviceComm {
     if (stream_) (void)hipStreamDestroy(stream_);
   }
   const char* kind() const override { return "loopback"; }
+  // RCCL's ncclCommAbort equivalent: a stream parked in hipStreamWaitValue32 on a peer that died would
+  // never drain (and the destructor's stream sync would hang). Raise every flag word this rank waits
+  // on, and its words on every peer, to the maximum (a >= wait then returns) with synchronous host
+  // writes; skip the teardown barrier.
+  void abort() override {
+    aborted_ = true;
+    if (!flags_) return;
+    const std::vector<uint32_t> top(static_cast<size_t>(np_) * 2, 0xffffffffu);
+    (void)hipMemcpy(flags_, top.data(), top.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    for (int r = 0; r < np_; ++r)
+      if (r != rank_ && flags_of_[r]) (void)hipMemcpy(flags_of_[r] + rank_ * 2, top.data(), 2 * sizeof(uint32_t),
+                                                       hipMemcpyHostToDevice);
+  }
   hipStream_t stream() const override { return stream_; }
   void group_start() override {
     if (in_group_) throw std::runtime_error("loopback device comm: nested group");
@@ -259,6 +272,7 @@ class LoopbackComm final : public DeviceComm {
   std::map<int, uint32_t> landed_wait_;
   std::vector<Op> ops_;
   bool in_group_ = false;
+  bool aborted_ = false;
 };
 
 }  // namespace

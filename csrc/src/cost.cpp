@@ -121,7 +121,7 @@ int dp_root_batch(int np, int batch, const CostParams& p, int H, int W) {
   const BlocksDims d = blocks_dims(H, W);
   const double ingress = static_cast<double>(np - 1) * batch * d.Hp2 * d.Wp2 * d.C2 * 4;
   const int b0 = 2 * static_cast<int>(std::lround(batch / (1 + root_slowdown(p, ingress)) / 2));
-  return std::max(2, std::min(batch, b0));
+  return std::min(batch, std::max(2, b0));  // never above the batch (batch 1 stays 1)
 }
 
 StepCost model_step(Workload wl, int np, int batch, int row_ways, InputSource src, Decomp mode, const CostParams& p,

@@ -86,26 +86,81 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
   q2_cap_ = static_cast<size_t>(max_batch) * (d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1;
   q2_ = dev_alloc<float>(q2_cap_);
   c2_ = dev_alloc<float>(static_cast<size_t>(chunk_) * d_.H2 * d_.W2 * d_.C2);
-  const ConvSpec& k1 = b1.conv;
-  if (impl == Impl::Mfma && hip::conv1_wino_eligible(k1.C, k1.K, k1.F, k1.S, k1.P, k1.groups)) {
-    const hip::Conv1WinoPlan wp = hip::make_conv1_wino_plan(chunk_, H, W, k1.K, k1.F);
+  prepare();
+}
+
+// What the current knobs can launch, prepared outside any forward (no allocation, upload or host
+// packing inside one): the Winograd transformed weights and workspaces only if some launch of up to
+// max_batch images can run Winograd (a batch-1 engine under Auto never does: the V3 cold path skips
+// both transforms, 2.6 MB of U and the V buffers), and the direct path's packed weights for its
+// largest full-image launch (the one a batch-1 engine runs first), so the first forward packs nothing.
+void BlocksEngine::prepare() {
+  if (impl_ != Impl::Mfma) return;
+  const ConvSpec &k1 = b1_.conv, &k2 = b2_.conv;
+  if (u1w_ == nullptr && hip::conv1_wino_eligible(k1.C, k1.K, k1.F, k1.S, k1.P, k1.groups) &&
+      use_winograd(k_.conv1_algo, max_batch_, d_.H1, d_.H1)) {
+    const hip::Conv1WinoPlan wp = hip::make_conv1_wino_plan(chunk_, d_.H, d_.W, k1.K, k1.F);
     std::vector<float> u;
-    hip::conv1_wino_weights_host(k1.K, k1.F, w.w1.data(), u);
+    hip::conv1_wino_weights_host(k1.K, k1.F, w1h_.data(), u);
     u1w_ = dev_upload(u);
     wv1_cap_ = hip::conv1_wino_v_floats(wp);
     wv1_ = dev_alloc<float>(wv1_cap_);
   }
-  if (impl == Impl::Mfma && hip::wino_eligible(b2.conv.F, b2.conv.S, d_.C1, d_.C2, b2.conv.groups)) {
+  if (u2w_ == nullptr && hip::wino_eligible(k2.F, k2.S, d_.C1, d_.C2, k2.groups) &&
+      use_winograd(k_.conv2_algo, max_batch_, d_.H2, d_.H2)) {
     // Winograd workspace for a full-height window of chunk_ images (row tiles need less)
-    const hip::WinoPlan wp = hip::make_wino_plan(chunk_, d_.Hp1 + 2 * b2.conv.P, wq_, d_.C1, d_.C2, b2.conv.groups);
+    const hip::WinoPlan wp = hip::make_wino_plan(chunk_, d_.Hp1 + 2 * k2.P, wq_, d_.C1, d_.C2, k2.groups);
     if (hip::wino_v_floats(wp) < (1UL << 31)) {
       std::vector<float> u;
-      hip::wino_transform_weights_host(wp, w.w2.data(), u);
+      hip::wino_transform_weights_host(wp, w2h_.data(), u);
       u2w_ = dev_upload(u);
       wv_cap_ = hip::wino_v_floats(wp);
       wv_ = dev_alloc<float>(wv_cap_);
     }
   }
+  // direct path: the full-image launch of min(max_batch, the Auto crossover) images
+  const int n = std::max(1, std::min(max_batch_, chunk_));
+  const int nd = k_.conv1_algo == ConvAlgo::Direct ? n : std::min(n, 8);
+  if (!use_winograd(k_.conv1_algo, nd, d_.H1, d_.H1) || wv1_ == nullptr)
+    (void)pack1(hip::make_conv_plan(nd, d_.H, d_.W, d_.C0, k1.K, k1.F, k1.S, k1.groups, k_.force_vec4, k_.force_scalar));
+  const int nd2 = k_.conv2_algo == ConvAlgo::Direct ? n : std::min(n, 8);
+  if (!use_winograd(k_.conv2_algo, nd2, d_.H2, d_.H2) || wv_ == nullptr)
+    (void)pack2(hip::make_conv_plan(nd2, d_.Hp1 + 2 * k2.P, wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups, k_.force_vec4,
+                                    k_.force_scalar));
+}
+
+int BlocksEngine::set_knob(const char* name, int value) {
+  if (anx::set_knob(k_, name, value) != 0) return -1;
+  prepare();  // a knob may enable a path whose weights / workspace this engine has not built yet
+  return 0;
+}
+
+hipError_t BlocksEngine::pack1(const hip::ConvPlan& p) {
+  const int key = p.variant | (p.taps4 << 8);
+  if (key == plan_key1_) return hipSuccess;
+  std::vector<float> packed;
+  std::vector<int> koff;
+  hip::pack_conv_weights_host(p, w1h_.data(), packed, koff);
+  if (w1p_) ANX_TRY(hipFree(w1p_));
+  if (koff1_) ANX_TRY(hipFree(koff1_));
+  w1p_ = dev_upload(packed);
+  koff1_ = dev_upload(koff);
+  plan_key1_ = key;
+  return hipSuccess;
+}
+
+hipError_t BlocksEngine::pack2(const hip::ConvPlan& p) {
+  const int key = p.variant | (p.taps4 << 8);
+  if (key == plan_key2_) return hipSuccess;
+  std::vector<float> packed;
+  std::vector<int> koff;
+  hip::pack_conv_weights_host(p, w2h_.data(), packed, koff);
+  if (w2p_) ANX_TRY(hipFree(w2p_));
+  if (koff2_) ANX_TRY(hipFree(koff2_));
+  w2p_ = dev_upload(packed);
+  koff2_ = dev_upload(koff);
+  plan_key2_ = key;
+  return hipSuccess;
 }
 
 BlocksEngine::~BlocksEngine() {
@@ -145,17 +200,7 @@ hipError_t BlocksEngine::conv1_chunk(const float* xc, int n, const TilePlan& t, 
   if (impl_ == Impl::Mfma) {
     const hip::ConvPlan p =
         hip::make_conv_plan(n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, k1.groups, k_.force_vec4, k_.force_scalar);
-    const int key = p.variant | (p.taps4 << 8);
-    if (key != plan_key1_) {
-      std::vector<float> packed;
-      std::vector<int> koff;
-      hip::pack_conv_weights_host(p, w1h_.data(), packed, koff);
-      if (w1p_) ANX_TRY(hipFree(w1p_));
-      if (koff1_) ANX_TRY(hipFree(koff1_));
-      w1p_ = dev_upload(packed);
-      koff1_ = dev_upload(koff);
-      plan_key1_ = key;
-    }
+    ANX_TRY(pack1(p));  // prepared by prepare() for the usual launches: a no-op then
     return hip::conv2d_mfma(p, xc, w1p_, koff1_, b1d_, c1v, true, s);
   }
   return hip::conv2d_direct(xc, w1_, b1d_, c1_, n, t.in.size(), d_.W, d_.C0, k1.K, k1.F, k1.S, 0, k1.groups, true,
@@ -195,17 +240,7 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
   } else if (impl_ == Impl::Mfma) {
     const hip::ConvPlan p =
         hip::make_conv_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups, k_.force_vec4, k_.force_scalar);
-    const int key = p.variant | (p.taps4 << 8);
-    if (key != plan_key2_) {
-      std::vector<float> packed;
-      std::vector<int> koff;
-      hip::pack_conv_weights_host(p, w2h_.data(), packed, koff);
-      if (w2p_) ANX_TRY(hipFree(w2p_));
-      if (koff2_) ANX_TRY(hipFree(koff2_));
-      w2p_ = dev_upload(packed);
-      koff2_ = dev_upload(koff);
-      plan_key2_ = key;
-    }
+    ANX_TRY(pack2(p));
     ANX_TRY(hip::conv2d_mfma(p, qc, w2p_, koff2_, b2d_, c2v, true, s));
   } else {
     ANX_TRY(hip::conv2d_direct(qc, w2_, b2d_, c2_, n, t.q.size(), wq_, d_.C1, k2.K, k2.F, k2.S, 0, k2.groups, true,
@@ -261,6 +296,22 @@ bool BlocksEngine::fused_pool1(int N, const TilePlan& t) const {
   return true;
 }
 
+bool BlocksEngine::conv1_pools(int N, const TilePlan& t) const {
+  if (!k_.conv1_pool || k_.conv1_fused != 1 || k_.conv1_sub > 0 || wv1_ == nullptr || !fused_pool1(N, t)) return false;
+  // whole images: every conv1 row, every pool1 row
+  if (t.c1.lo != 0 || t.c1.hi != d_.H1 || t.p1.lo != 0 || t.p1.hi != d_.Hp1) return false;
+  const int chunk = std::min(chunk_, k_.chunk1 > 0 ? k_.chunk1 : chunk_);
+  const ConvSpec& k1 = b1_.conv;
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int n = std::min(chunk, N - n0);
+    if (!use_winograd(k_.conv1_algo, n, t.c1.size(), d_.H1)) return false;
+    const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
+    const hip::OutView win{q2_, t.q.size(), wq_, d_.C1, t.p1.lo - t.q.lo, b2_.conv.P, 0};
+    if (w.H1 != d_.H1 || !hip::conv1_fused_pool_eligible(w, win, d_.Hp1, d_.Wp1)) return false;
+  }
+  return true;
+}
+
 hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, float* y, hipStream_t s) {
   if (N > max_batch_) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
@@ -268,6 +319,7 @@ hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, 
     ANX_TRY(stage1(x, N, t, s));
     return stage2(N, t, y, s);
   }
+  if (conv1_pools(N, t)) return tile_forward_conv1_pool(x, N, t, y, s);
   // conv1 -> (pool1 + Winograd input transform) -> Winograd GEMM -> pool2 + LRN per chunk: the conv2
   // window is never materialised (bit-identical to stage1 + stage2)
   const ConvSpec& k2 = b2_.conv;
@@ -291,6 +343,43 @@ hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, 
       if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
       ANX_TRY(hip::wino_pool_input(w, c1_ + b0 * c1_img, t.c1.size(), d_.W1, t.q.lo, d_.Hp1, d_.Wp1, k2.P, t.c1.lo,
                                    wv_, s, b1_.pool.F, b1_.pool.S));
+      const hip::OutView c2v{c2_ + b0 * c2_img, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
+      ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
+    }
+    ANX_TRY(pool2_chunk(n, t, y + n0 * y_img, s));
+  }
+  return hipSuccess;
+}
+
+// Whole images with pool1 in the one-kernel Conv1: conv1 + pool1 -> the conv2 window (+ the straddling
+// windows' partial maxima in c1_) -> merged input transform -> Winograd GEMM -> pool2 + LRN, per chunk.
+// The conv1 map never reaches HBM; bit-identical to the path above (max is exact in any order).
+hipError_t BlocksEngine::tile_forward_conv1_pool(const float* x, int N, const TilePlan& t, float* y, hipStream_t s) {
+  const ConvSpec &k1 = b1_.conv, &k2 = b2_.conv;
+  ANX_TRY(ensure_window(t, N, s));  // zero border once; every interior pixel is rewritten per call
+  const size_t in_img = static_cast<size_t>(t.in.size()) * d_.W * d_.C0;
+  const size_t y_img = static_cast<size_t>(t.out.size()) * d_.Wp2 * d_.C2;
+  const size_t q_img = q2_image_stride_floats(t);
+  const size_t p1_img = static_cast<size_t>(d_.Hp1) * d_.Wp1 * d_.C1;
+  const size_t c2_img = static_cast<size_t>(t.c2.size()) * d_.W2 * d_.C2;
+  const int chunk = std::min(chunk_, k_.chunk1 > 0 ? k_.chunk1 : chunk_);
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int n = std::min(chunk, N - n0);
+    {
+      RoctxRange rx("anx conv1+pool1");
+      const hip::Conv1WinoPlan w1 = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
+      const hip::OutView win{q2_ + n0 * q_img, t.q.size(), wq_, d_.C1, t.p1.lo - t.q.lo, k2.P, 0};
+      ANX_TRY(hip::conv1_fused_pool(w1, x + n0 * in_img, u1w_, b1d_, win, c1_, d_.Hp1, d_.Wp1, true, s));
+    }
+    RoctxRange rx("anx conv2+pool2+lrn");
+    const hip::Conv1WinoPlan w1 = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
+    const int s2 = k_.conv2_sub > 0 ? std::min(n, k_.conv2_sub) : n;
+    for (int b0 = 0; b0 < n; b0 += s2) {
+      const int m = std::min(s2, n - b0);
+      const hip::WinoPlan w = hip::make_wino_plan(m, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
+      if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
+      ANX_TRY(hip::wino_window_merge_input(w, q2_ + (n0 + b0) * q_img, c1_ + b0 * p1_img, b0, w1.ty, w1.tx, t.q.lo,
+                                           d_.Hp1, d_.Wp1, k2.P, wv_, s));
       const hip::OutView c2v{c2_ + b0 * c2_img, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
       ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
     }

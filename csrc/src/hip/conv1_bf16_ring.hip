@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "anx/bf16_ops.hpp"
+#include "anx/hip_sync.hpp"
 
 namespace anx::hip {
 namespace {
@@ -258,12 +259,11 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     // wave followed it; the first tile waits for the prologue), every wave's by the barrier, which
     // also retires tile t-1's reads of the slots refilled below.
     if (t == t0)
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      lds_barrier<0>();
     else if constexpr (F32IN)  // the rows were written by ds_write at tile t-1's end
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_barrier<>();
     else
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kSPW) : "memory");
-    __builtin_amdgcn_s_barrier();
+      lds_barrier<kSPW>();
     asm volatile("" ::: "memory");
     lap(0);
     if (t + 1 < t1) {  // tile t+1's new rows, into tile t-1's first slots
@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
     // rows 4t-2, 4t-1 with row 4t; rows 4t+2, 4t+3 are carried for row 2t+1. Max over ReLU outputs
     // (>= 0) is the unsigned max of their bf16 bits.
     if (F32IN && a.pool) {
-      __builtin_amdgcn_s_barrier();  // every wave is past its fragment reads of the scratch slots
+      lds_barrier<>();  // every wave is past its fragment reads of the scratch slots
       asm volatile("" ::: "memory");
       lap(4);
       const char* carry_old = lds + kLds + ((t & 1) ^ 1) * kCarryB;
@@ -346,8 +346,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
           }
         }
         lap(5);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's rows written before the barrier
-        __builtin_amdgcn_s_barrier();
+        lds_barrier<>();  // this wave's rows written before the barrier
         asm volatile("" ::: "memory");
         lap(6);
         if (tid < kPw * 6) {  // (pooled column, 8-filter chunk of this half)
@@ -376,8 +375,7 @@ __global__ void __launch_bounds__(kNT, 1) conv1_bf16_ring_kernel(Args a) {
         }
         lap(7);
         if constexpr (p == 0) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();  // the second half overwrites the scratch rows
+          lds_barrier<>();  // the second half overwrites the scratch rows
           asm volatile("" ::: "memory");
         }
       });

@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "anx/ops.hpp"
+#include "anx/hip_sync.hpp"
 #include "anx/winograd_f33.hpp"
 
 namespace anx::hip {
@@ -69,6 +70,11 @@ constexpr bool loads_at(int p) {
 }
 static_assert(9 * kTiles * kOS <= kDummy && kTiles * kOS <= 2 * kVBuf,
               "epilogue scratch: nine position images below the dummy DMA slot (UM 0), one in the V buffers (UM 1)");
+// pool1 epilogue: candidate pooled pixels are those whose window starts in tiles p0 - kPoolBack .. p0 + 31
+// (a window's tiles span at most tx + 1 raster indices: kPoolBack >= tx + 1, checked by the launcher)
+constexpr int kPoolBack = 20, kPoolSlots = 4 * (kPoolBack + kTiles);
+constexpr int kPoolList = 9 * kTiles * kOS;  // the slot list after the nine position images
+static_assert(kPoolList + 1 + kPoolSlots <= kLdsFloats && kPoolSlots <= kNT, "pool1 slot list");
 static_assert(kTiles * 24 == kNT, "V build: one (tile, channel pair) per thread");
 
 template <int B, int E, class F>
@@ -93,11 +99,17 @@ struct Conv1FusedArgs {
   int xbytes, ubytes;                // buffer-resource extents (< 2^31)
   int n_ptiles, per_xcd;
   int relu;
+  // POOL: pool1 (3x3 / 2 max) in the epilogue. Pooled pixels whose window lies in this workgroup's
+  // 32 tiles are written to `out` (the conv2 input window); a window that straddles two workgroups'
+  // tile ranges gets the partial max of each: the lower workgroup's into `out`, the upper's into p1
+  // ([N][Hp][Wp][96]), merged by the consumer (pool1_straddles()).
+  float* p1;
+  int Hp, Wp;
 };
 
 // UM = 0: U through the 3-slot LDS ring (a barrier per point); UM = 1: each wave loads its own B
 // fragments of U straight into registers two points ahead (no LDS for U: one barrier per a-step).
-template <int UM>
+template <int UM, bool POOL>
 __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -271,10 +283,9 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
       if constexpr (UM == 0 || b == 0) {  // UM 1: only V_a needs publishing (and V_{a-1}'s readers done)
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (UM == 0)
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(inflight) : "memory");
+          lds_barrier<inflight>();
         else
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+          lds_barrier<>();
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("" ::: "memory");
       }
@@ -351,7 +362,70 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
     sti = pq % a.ty;
     sn = pq / a.ty;
   }
-  if constexpr (UM == 0) {
+  if constexpr (POOL) {
+    // pool1 from the same [9 positions][32 tiles][kOS] image. A pooled pixel (py, px) reads conv1 rows
+    // 2py .. 2py+2 x cols 2px .. 2px+2: tiles (2py/3 .. (2py+2)/3) x (2px/3 .. (2px+2)/3), raster
+    // indices gm .. gM with gM - gm <= tx + 1 < 32, so at most two workgroups' tile ranges meet in one
+    // window. The workgroup owning gm writes its partial max to `out`, the one owning gM (if another)
+    // to p1. Slots: the pooled pixels whose top-left tile is one of tiles p0 - 20 .. p0 + 31 (1-4 per
+    // tile), compacted into a list in LDS, then 24 threads (4 filters each) per listed pixel.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's last fragment reads are done: the LDS is scratch now
+    int* plist = reinterpret_cast<int*>(lds + kPoolList);  // [0] count, [1 ..] pixel descriptors
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = Y[q][i] + bv;
+        if (a.relu) v = fmaxf(v, 0.f);
+        tr[(q * kTiles + wm * 16 + 4 * h4 + i) * kOS + f] = v;
+      }
+    if (tid == 0) plist[0] = 0;
+    const int ipt = a.ty * a.tx;  // tiles per image
+    int desc = -1;
+    if (tid < kPoolSlots) {
+      const int gt = p0 - kPoolBack + (tid >> 2), dyi = (tid >> 1) & 1, dxi = tid & 1;
+      if (gt >= 0 && gt < a.P) {
+        const int n = gt / ipt, r = gt - n * ipt, tyy = r / a.tx, txx = r - tyy * a.tx;
+        // pooled rows whose window starts in tile row tyy: 2py in [3 tyy, 3 tyy + 2]
+        const int py = ((3 * tyy + 1) >> 1) + dyi, px = ((3 * txx + 1) >> 1) + dxi;
+        const bool ok = dyi < 2 - (tyy & 1) && dxi < 2 - (txx & 1) && py < a.Hp && px < a.Wp;
+        if (ok) {
+          const int gM = n * ipt + ((2 * py + 2) / 3) * a.tx + (2 * px + 2) / 3;
+          if (gt >= p0)
+            desc = ((n * 32 + py) * 32 + px) * 2;  // lower owner: `out`
+          else if (gM >= p0)
+            desc = ((n * 32 + py) * 32 + px) * 2 + 1;  // upper owner of a straddling window: p1
+        }
+      }
+    }
+    __syncthreads();  // position images and the zeroed count visible
+    if (desc >= 0) plist[1 + atomicAdd(&plist[0], 1)] = desc;
+    __syncthreads();
+    const int nlist = plist[0];
+    for (int it = tid; it < nlist * (kK / 4); it += kNT) {
+      const int d = plist[1 + it / (kK / 4)], fq = it % (kK / 4);
+      const int up = d & 1, px = (d >> 1) & 31, py = (d >> 6) & 31, n = d >> 11;
+      f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int y = 2 * py + i, tyy = y / 3, ry = y - 3 * tyy;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int x = 2 * px + j, txx = x / 3, rx = x - 3 * txx;
+          const int lt = n * ipt + tyy * a.tx + txx - p0;
+          if (static_cast<unsigned>(lt) < static_cast<unsigned>(kTiles)) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(tr + ((ry * 3 + rx) * kTiles + lt) * kOS + 4 * fq);
+            m = f32x4{fmaxf(m.x, v.x), fmaxf(m.y, v.y), fmaxf(m.z, v.z), fmaxf(m.w, v.w)};
+          }
+        }
+      }
+      float* dst = up ? a.p1 + (static_cast<size_t>(n * a.Hp + py) * a.Wp + px) * kK + 4 * fq
+                      : o.base + (static_cast<size_t>(n * o.Hb + py + o.h_off) * o.Wb + px + o.w_off) * o.Cb + o.c_off +
+                            4 * fq;
+      *reinterpret_cast<f32x4*>(dst) = m;
+    }
+  } else if constexpr (UM == 0) {
     // all nine output positions' images at once (9 x 32 x 100 floats = 115 KB of the 128 KB): one
     // barrier and nine back-to-back stores per thread instead of a write / barrier / store / barrier
     // round per position. The images reach into the U ring's slots, so no DMA may still be landing.
@@ -400,13 +474,13 @@ bool conv1_fused_eligible(const Conv1WinoPlan& w, const OutView& out) {
          static_cast<long>(w.N) * w.Hin * w.W * 3 * 4 < (1L << 31);
 }
 
-hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out, bool relu,
-                       hipStream_t s, int mode) {
-  if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
-  if (!conv1_fused_eligible(w, out)) return hipErrorInvalidValue;
+namespace {
+hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out,
+                              bool relu, hipStream_t s, int mode, float* p1, int Hp, int Wp) {
   static const hipError_t attr = [] {
-    for (const void* k : {reinterpret_cast<const void*>(conv1_fused_kernel<0>),
-                          reinterpret_cast<const void*>(conv1_fused_kernel<1>)}) {
+    for (const void* k : {reinterpret_cast<const void*>(conv1_fused_kernel<0, false>),
+                          reinterpret_cast<const void*>(conv1_fused_kernel<1, false>),
+                          reinterpret_cast<const void*>(conv1_fused_kernel<0, true>)}) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -430,11 +504,38 @@ hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, c
   a.n_ptiles = (w.P + kTiles - 1) / kTiles;
   a.per_xcd = (a.n_ptiles + 7) / 8;
   a.relu = relu ? 1 : 0;
-  if (mode == 2)
-    conv1_fused_kernel<1><<<static_cast<unsigned>(a.per_xcd * 8), kNT, 2 * kVBuf * sizeof(float), s>>>(a);
+  a.p1 = p1;
+  a.Hp = Hp;
+  a.Wp = Wp;
+  const unsigned grid = static_cast<unsigned>(a.per_xcd * 8);
+  if (p1 != nullptr)
+    conv1_fused_kernel<0, true><<<grid, kNT, kLds, s>>>(a);
+  else if (mode == 2)
+    conv1_fused_kernel<1, false><<<grid, kNT, 2 * kVBuf * sizeof(float), s>>>(a);
   else
-    conv1_fused_kernel<0><<<static_cast<unsigned>(a.per_xcd * 8), kNT, kLds, s>>>(a);
+    conv1_fused_kernel<0, false><<<grid, kNT, kLds, s>>>(a);
   return hipGetLastError();
+}
+}  // namespace
+
+hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out, bool relu,
+                       hipStream_t s, int mode) {
+  if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
+  if (!conv1_fused_eligible(w, out)) return hipErrorInvalidValue;
+  return conv1_fused_launch(w, x, U, bias, out, relu, s, mode, nullptr, 0, 0);
+}
+
+bool conv1_fused_pool_eligible(const Conv1WinoPlan& w, const OutView& window, int Hp, int Wp) {
+  // pooled pixels are decoded from 5 + 5 bits; a window's tiles within kPoolBack raster indices
+  return conv1_fused_eligible(w, window) && w.tx + 1 <= kPoolBack && Hp > 0 && Wp > 0 && Hp <= 32 && Wp <= 32 &&
+         2 * Hp + 1 <= w.H1 && 2 * Wp + 1 <= w.W1 && w.N < (1 << 20);
+}
+
+hipError_t conv1_fused_pool(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView window,
+                            float* p1, int Hp, int Wp, bool relu, hipStream_t s) {
+  if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
+  if (p1 == nullptr || !conv1_fused_pool_eligible(w, window, Hp, Wp)) return hipErrorInvalidValue;
+  return conv1_fused_launch(w, x, U, bias, window, relu, s, 1, p1, Hp, Wp);
 }
 
 }  // namespace anx::hip

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "anx/bf16_ops.hpp"
+#include "anx/hip_sync.hpp"
 #include "anx/lrn_math.hpp"
 
 namespace anx::hip {
@@ -270,10 +271,9 @@ __global__ void __launch_bounds__(128 * WMW) conv_bf16_glds_kernel(ArgsB a) {
     if (i < total) issue(i);
   for (int it = 0; it < total; ++it) {
     if (it + NST - 2 < total)
-      wait_vm<(NA + NB) * (NST - 2)>();
+      lds_barrier<(NA + NB) * (NST - 2)>();  // slice it landed for every wave; slot (it-1) % NST is free
     else
-      wait_vm<0>();
-    __builtin_amdgcn_s_barrier();  // slice it landed for every wave; slot (it-1) % NST is free
+      lds_barrier<0>();
     asm volatile("" ::: "memory");
     if (it + NST - 1 < total) issue(it + NST - 1);
     const bf16* base = lds_b + (it % NST) * STAGE;

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "anx/bf16_ops.hpp"
+#include "anx/hip_sync.hpp"
 
 namespace anx::hip {
 namespace {
@@ -179,10 +180,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
   int st = 0, st_free = NST - 1;  // stage of tile it; stage of tile it-1 (free once all waves pass)
   for (int it = 0; it < total; ++it) {
     if (it + NST - 2 < total)
-      wait_vm<NJ * (NST - 2)>();   // this lane's pieces of tile it landed (later tiles may fly)
-    else
-      wait_vm<0>();
-    __builtin_amdgcn_s_barrier();  // ... every lane's; and every wave is done reading tile it-1
+      lds_barrier<NJ * (NST - 2)>();  // this lane's pieces of tile it landed (later tiles may fly), every lane's
+    else                              // after the barrier; and every wave is done reading tile it-1
+      lds_barrier<0>();
     asm volatile("" ::: "memory");
     const bf16* base = lds_b + st * STAGE;
     st = st + 1 == NST ? 0 : st + 1;
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv_bf16_big_kernel(ArgsW a) 
     return;
   }
   // epilogue: the tile through LDS (all DMA retired above; wait for every wave's last reads)
-  __builtin_amdgcn_s_barrier();
+  lds_barrier<>();
   asm volatile("" ::: "memory");
   bf16* E = lds_b;
   using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
@@ -377,11 +377,10 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
   issueB(0, 0);
   if (G == 1 && T > 1) issueB(1, 1);
   if (G == 1 && T > 1)
-    wait_vm<NB>();
+    lds_barrier<NB>();  // #0
   else
-    wait_vm<0>();
-  __builtin_amdgcn_s_barrier();  // #0
-  if (G == 1) __builtin_amdgcn_s_barrier();  // the stagger
+    lds_barrier<0>();
+  if (G == 1) lds_barrier<>();  // the stagger
   asm volatile("" ::: "memory");
   int sb = 0;  // B stage of tile t (t % 3)
   for (int t = 0; t < T; ++t) {
@@ -415,9 +414,8 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
       else
         wait_vm<0>();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    lds_barrier<>();
     asm volatile("" ::: "memory");
     // ---- M_t ----
     __builtin_amdgcn_s_setprio(1);
@@ -433,18 +431,20 @@ __global__ void __launch_bounds__(512) conv_bf16_pp_kernel(ArgsW a) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     if (G == 0) {
-      if (t + 1 < T) wait_vm<0>();  // this group's A_{t+1}, B_{t+1}
+      if (t + 1 < T)
+        lds_barrier<0>();  // this group's A_{t+1}, B_{t+1}
+      else
+        lds_barrier<>();
     } else {
       if (t + 2 < T)  // A_{t+1} (B_{t+2} may fly)
-        wait_vm<NB>();
+        lds_barrier<NB>();
       else
-        wait_vm<0>();
+        lds_barrier<0>();
     }
-    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     sb = s1;
   }
-  if (G == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: every wave is past its last read
+  if (G == 0) lds_barrier<>();  // balance the stagger: every wave is past its last read
   asm volatile("" ::: "memory");
 
   // epilogue (as conv_bf16_big_kernel): the padded tile image (132 KiB) from the LDS base, ooff in
@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(512) fc_bf16_kernel(ArgsFc a) {
   for (int r = 0; r < D; ++r) issue(r, r, r);  // total >= D (host)
   const int brow = (lane & 15) * kBK;
   auto tile = [&](int s, int st) {  // MFMAs of the tile in register slot s / LDS stage st
-    __builtin_amdgcn_s_barrier();  // every lane's weight DMA of the tile; every wave past the previous one
+    lds_barrier<>();  // every lane's weight DMA of the tile (the caller's vmcnt); every wave past the previous one
     asm volatile("" ::: "memory");
     const bf16* base = lds_b + st * SB;
     bf16x8 b0[4], b1[4];

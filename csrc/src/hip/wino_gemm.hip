@@ -150,124 +150,6 @@ hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, Ou
 
 }  // namespace anx::hip
 
-// ---- split-bf16 GEMMs (wino_gemm_sb.hpp): A/B build only. Measured slower than or level with the f32
-// MFMA kernels (profiles/r03_sb_wgemm_ab.jsonl: Conv2 at 300 images x9 673 us, x6 580 us vs f32 627 us;
-// Conv1 x9 431 / x6 378 vs 382): the per-wave A split costs 44 VALU per 16-channel k-step, more issue
-// time than the 9 (or 6) bf16 MFMAs it feeds, and at 16x the MFMA rate the 64x64 tile (bounded by the
-// 144 fold registers per wave) needs ~3x the L2->LDS bandwidth of the f32 kernel.
-#ifdef ANX_WGEMM_ABLATIONS
-#include "wino_gemm_sb.hpp"
-namespace anx::hip {
-namespace {
-
-template <class G, int ABL>
-hipError_t launch_sb(const wg::Args& a0, hipStream_t s, int occ) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wsb::sb_gemm_kernel<G, ABL>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (attr != hipSuccess) return attr;
-  wg::Args a = a0;
-  a.n_ptiles = (a.P + G::BM - 1) / G::BM;
-  a.n_ntiles = a.kg / G::BN;
-  if (a.kg % G::BN || a.n_ntiles < 1 || a.u_rows < a.n_ntiles * G::BN) return hipErrorInvalidValue;
-  const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
-  wsb::sb_gemm_kernel<G, ABL><<<grid, G::NT, occupancy_lds(G::kLdsBytes, occ), s>>>(a);
-  return hipGetLastError();
-}
-
-// <points, channels, waves along tiles, waves along filters, ring slots, part products>
-using SB2x9 = wsb::Cfg<49, 96, 2, 2, 2, 9>;   // Conv2: 64 tiles x 64 filters, 60 KiB ring, 2 workgroups per CU
-using SB2x6 = wsb::Cfg<49, 96, 2, 2, 2, 6>;
-using SB2gx9 = wsb::Cfg<49, 48, 2, 2, 2, 9>;  // Conv2, 2 groups
-using SB2gx6 = wsb::Cfg<49, 48, 2, 2, 2, 6>;
-using SB1x9 = wsb::Cfg<25, 48, 2, 1, 2, 9>;   // Conv1: 64 tiles x 32 filters, 42 KiB ring
-using SB1x6 = wsb::Cfg<25, 48, 2, 1, 2, 6>;
-
-template <class G9, class G6>
-hipError_t launch_sb_prod(const wg::Args& a, hipStream_t s, int occ, int nprod, int abl) {
-  switch (nprod * 100 + abl) {
-    case 900: return launch_sb<G9, 0>(a, s, occ);
-    case 600: return launch_sb<G6, 0>(a, s, occ);
-    case 901: return launch_sb<G9, 1>(a, s, occ);
-    case 903: return launch_sb<G9, 3>(a, s, occ);
-    case 601: return launch_sb<G6, 1>(a, s, occ);
-    case 603: return launch_sb<G6, 3>(a, s, occ);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-}  // namespace
-
-void wino_split_planes_host(const std::vector<float>& u, int npt, int rows, int cols, std::vector<uint16_t>& ub) {
-  ub.assign(static_cast<size_t>(npt) * 3 * rows * cols, 0);
-  for (int ab = 0; ab < npt; ++ab)
-    for (int n = 0; n < rows; ++n)
-      for (int c = 0; c < cols; ++c) {
-        uint16_t h, m, l;
-        wsb::split_host(u[(static_cast<size_t>(ab) * rows + n) * cols + c], h, m, l);
-        const size_t o = (static_cast<size_t>(ab) * 3 * rows + n) * cols + c, ps = static_cast<size_t>(rows) * cols;
-        ub[o] = h;
-        ub[o + ps] = m;
-        ub[o + 2 * ps] = l;
-      }
-}
-
-hipError_t wino_sb_gemm_conv2(const float* V, const uint16_t* Ub, const float* bias, OutView out, int P, int ty, int tx,
-                              int Ho, int Wo, int C, int K, int groups, bool relu, hipStream_t s, int nprod, int occ,
-                              int abl) {
-  if (groups < 1 || C % groups || K % groups) return hipErrorInvalidValue;
-  const int Cg = C / groups, Kg = K / groups;
-  const long vb = static_cast<long>(P) * 49 * C * 4, ub = static_cast<long>(49) * 3 * K * Cg * 2;
-  if ((Cg != 96 && Cg != 48) || Kg % 64 || vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4)
-    return hipErrorInvalidValue;
-  if (P == 0) return hipSuccess;
-  for (int g = 0; g < groups; ++g) {
-    wg::Args a{};
-    a.V = V + g * Cg;
-    a.U = reinterpret_cast<const float*>(Ub + static_cast<size_t>(g) * Kg * Cg);  // bf16 planes (byte offsets)
-    a.bias = bias ? bias + g * Kg : nullptr;
-    a.out = out;
-    a.out.c_off += g * Kg;
-    a.P = P;
-    a.ty = ty;
-    a.tx = tx;
-    a.Ho = Ho;
-    a.Wo = Wo;
-    a.kg = Kg;
-    a.u_rows = K;
-    a.vct = C;
-    a.vbytes = static_cast<int>(vb - g * Cg * 4);
-    a.ubytes = static_cast<int>(ub - static_cast<long>(g) * Kg * Cg * 2);
-    a.relu = relu ? 1 : 0;
-    const hipError_t e = Cg == 48 ? launch_sb_prod<SB2gx9, SB2gx6>(a, s, occ, nprod, abl)
-                                  : launch_sb_prod<SB2x9, SB2x6>(a, s, occ, nprod, abl);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
-
-hipError_t wino_sb_gemm_conv1(const float* V, const uint16_t* Ub, const float* bias, OutView out, int P, int ty, int tx,
-                              int Ho, int Wo, int K, bool relu, hipStream_t s, int nprod, int occ, int abl) {
-  const long vb = static_cast<long>(P) * 25 * 48 * 4, ub = static_cast<long>(25) * 3 * K * 48 * 2;
-  if (vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
-  if (P == 0) return hipSuccess;
-  wg::Args a{};
-  a.V = V;
-  a.U = reinterpret_cast<const float*>(Ub);
-  a.bias = bias;
-  a.out = out;
-  a.P = P;
-  a.ty = ty;
-  a.tx = tx;
-  a.Ho = Ho;
-  a.Wo = Wo;
-  a.kg = K;
-  a.u_rows = K;
-  a.vct = 48;
-  a.vbytes = static_cast<int>(vb);
-  a.ubytes = static_cast<int>(ub);
-  a.relu = relu ? 1 : 0;
-  return launch_sb_prod<SB1x9, SB1x6>(a, s, occ, nprod, abl);
-}
-
-}  // namespace anx::hip
-#endif  // ANX_WGEMM_ABLATIONS
+// The split-bf16 GEMMs (every fp32 operand as three exact bf16 parts on the bf16 matrix cores) were
+// measured in round 3 and removed in round 5: slower than or level with these f32 MFMA kernels
+// (profiles/r03_sb_wgemm_ab.jsonl; docs/ARCHITECTURE.md, Round-3 A/B results).

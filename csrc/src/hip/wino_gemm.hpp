@@ -37,6 +37,7 @@
 
 #include <type_traits>
 
+#include "anx/hip_sync.hpp"
 #include "anx/ops.hpp"
 #include "anx/winograd_f33.hpp"
 #include "anx/winograd_f35.hpp"
@@ -245,11 +246,12 @@ __global__ void __launch_bounds__(G::NT, 2) gemm_kernel(Args a) {
     constexpr int ahead = abs_it ? ((G::TOTAL - 1 - lit) < NST - 2 ? (G::TOTAL - 1 - lit) : NST - 2) : NST - 2;
     const int ab = pb + lit / KS;
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (kDma)
-      wait_vm_lgkm<ahead * G::PW_MIN>();  // a wave that issues more pieces per slice waits a little early: safe
+    // a wave that issues more pieces per slice waits a little early: safe
+    constexpr int vm = kDma ? ahead * G::PW_MIN : 0;
+    if constexpr (kBar)
+      lds_barrier<vm>();
     else
-      wait_vm_lgkm<0>();
-    if constexpr (kBar) __builtin_amdgcn_s_barrier();
+      wait_vm_lgkm<vm>();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");  // keep the refill and the reads below the barrier
     if constexpr (refill) issue(pb + nlit / KS, nlit % KS, nlit % NST);

@@ -95,10 +95,16 @@ constexpr int kMaxWq = 31;  // window columns held in LDS
 // POOL = false: the same kernel on a materialised conv2 window (`c1` = window [N][Hq][Wq][C], q_lo, Hp,
 // Wp, P, c1_lo unused): the window rows of the tile row are copied to LDS with 16-B loads (each
 // window row read once per tile row instead of once per tile it touches, as wino_in2_kernel does).
-template <int kPG, int NT, bool POOL = true>  // channels, threads per workgroup
+// MERGE (with POOL = false): the window's pool1 pixels came from conv1_fused_pool, which leaves the
+// partial max of a window straddling two Conv1 workgroups in p1 ([N][Hp][Wp][C], images from n_off in
+// the Conv1 launch's tile numbering of ty1 x tx1 tiles per image; q_lo / P / Hp / Wp locate the pool1
+// image in the window): those pixels are max(window, p1), the rest the window's value.
+template <int kPG, int NT, bool POOL = true, bool MERGE = false>  // channels, threads per workgroup
 __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restrict__ c1, float* __restrict__ V, int groups,
                                                           int H1, int W1, int C, int Hq, int Wq, int q_lo, int Hp,
-                                                          int Wp, int P, int c1_lo, int ty, int tx) {
+                                                          int Wp, int P, int c1_lo, int ty, int tx,
+                                                          const float* __restrict__ p1 = nullptr, int n_off = 0,
+                                                          int ty1 = 0, int tx1 = 0) {
   __shared__ __attribute__((aligned(16))) float band[kN][kMaxWq][kPG];
   const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
   const int grp = (j / ty) * 8 + xcd, ti = j % ty;
@@ -116,6 +122,14 @@ __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restric
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (R < Hq)
         v = *reinterpret_cast<const f32x4*>(c1 + (static_cast<size_t>(n * Hq + R) * Wq + col) * C + cg * kPG + 4 * c4);
+      if constexpr (MERGE) {
+        const int pr = q_lo + R, pc = col - P;
+        if (R < Hq && pr >= 0 && pr < Hp && pc >= 0 && pc < Wp && pool1_straddles(n + n_off, pr, pc, ty1, tx1)) {
+          const f32x4 u =
+              *reinterpret_cast<const f32x4*>(p1 + (static_cast<size_t>(n * Hp + pr) * Wp + pc) * C + cg * kPG + 4 * c4);
+          v = f32x4{fmaxf(v.x, u.x), fmaxf(v.y, u.y), fmaxf(v.z, u.z), fmaxf(v.w, u.w)};
+        }
+      }
       *reinterpret_cast<f32x4*>(&band[r][col][4 * c4]) = v;
     }
   }
@@ -211,6 +225,18 @@ hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, i
   // 512 threads: 8 waves over the pooling walk and both transforms (bench step +2.7 % over 256 at 128
   // images per GPU; profiles/r03_transform_threads_*)
   pool_wino_in_kernel<pg, 512><<<grid, 512, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
+  return hipGetLastError();
+}
+
+hipError_t wino_window_merge_input(const WinoPlan& w, const float* window, const float* p1, int n_off, int ty1, int tx1,
+                                   int q_lo, int Hp, int Wp, int P, float* V, hipStream_t s) {
+  constexpr int pg = 32;
+  if (w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * kN * kN >= (1L << 31)) return hipErrorInvalidValue;
+  if (w.P == 0) return hipSuccess;
+  const int groups = w.N * (w.C / pg);
+  const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
+  pool_wino_in_kernel<pg, 512, false, true><<<grid, 512, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P,
+                                                                 0, w.ty, w.tx, p1, n_off, ty1, tx1);
   return hipGetLastError();
 }
 

@@ -161,14 +161,24 @@ int anx_v5_set_input(void* h, const float* host_x) {
 
 int anx_v5_step(void* h, int steps) {
   return guarded("anx_v5_step", [&] {
-    for (int i = 0; i < steps; ++i) H(h)->rt->step();
+    try {
+      for (int i = 0; i < steps; ++i) H(h)->rt->step();
+    } catch (...) {
+      H(h)->rt->abort();  // fail-stop: no stream of this rank stays parked on a peer
+      throw;
+    }
     return 0;
   });
 }
 
 int anx_v5_sync(void* h) {
   return guarded("anx_v5_sync", [&] {
-    H(h)->rt->sync();
+    try {
+      H(h)->rt->sync();
+    } catch (...) {
+      H(h)->rt->abort();
+      throw;
+    }
     return 0;
   });
 }

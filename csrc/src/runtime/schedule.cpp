@@ -223,6 +223,10 @@ struct RcclTransport : DeviceBase {
     dc_[1].reset();
     dc_[0].reset();
   }
+  void abort() override {
+    for (auto& d : dc_)
+      if (d) d->abort();
+  }
 };
 
 // ---------------------------------------------------------------------------------------- peer
@@ -429,6 +433,17 @@ struct PeerTransport : DeviceBase {
     opened_.clear();
     if (collective) c_->barrier();
     release();
+  }
+  void abort() override {
+    // flags mode: raise this rank's words (its own waits return) and its words on every peer (their
+    // waits on this rank return); a raised word satisfies every later >= wait too. Synchronous host
+    // writes, not on a stream that may itself be parked in a wait.
+    if (!flags_ || !flags_mine_) return;
+    const std::vector<uint32_t> top(static_cast<size_t>(np_) * kCh, 0xffffffffu);
+    (void)hipMemcpy(flags_mine_, top.data(), top.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    for (int r = 0; r < np_; ++r)
+      if (r != rank_ && r < static_cast<int>(flags_of_.size()) && flags_of_[r])
+        (void)hipMemcpy(flags_of_[r] + rank_ * kCh, top.data(), kCh * sizeof(uint32_t), hipMemcpyHostToDevice);
   }
   void release() {
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);

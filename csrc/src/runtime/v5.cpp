@@ -160,6 +160,7 @@ struct V5Runtime::Impl_ {
   bool alias_tile = false, alias_y = false;
   std::vector<float*> owned;  // device allocations to free
   hipStream_t st = nullptr, io = nullptr, hs = nullptr;
+  bool aborted = false;
   hipEvent_t e_sc[2] = {}, e_s2[2] = {}, e_hdone = nullptr;
   std::vector<hipEvent_t> e_s1, e_h;
   long k = 0;
@@ -425,10 +426,12 @@ V5Runtime::V5Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const
 V5Runtime::~V5Runtime() {
   if (!p_) return;
   Impl_& I = *p_;
-  (void)hipDeviceSynchronize();
+  (void)hipDeviceSynchronize();  // after abort() no stream waits on a peer any more
   try {
-    I.c.barrier();  // nobody pushes into a peer's buffers any more
-    I.x->close();   // collective: unmap, barrier, free own
+    if (!I.aborted) {
+      I.c.barrier();  // nobody pushes into a peer's buffers any more
+      I.x->close();   // collective: unmap, barrier, free own
+    }
   } catch (...) {
   }
   I.x.reset();
@@ -535,6 +538,12 @@ void V5Runtime::step() {
   }
   I.pending[slot] = true;
   ++I.k;
+}
+
+void V5Runtime::abort() {
+  if (!p_ || p_->aborted) return;
+  p_->aborted = true;
+  if (p_->x) p_->x->abort();
 }
 
 void V5Runtime::sync() {

@@ -357,17 +357,26 @@ int run_single(Setup& s) {
       warm.add("compute", now_ms() - a);
     }
   } else {
+    // cold phases (bench.py b1_process_phases_ms): input = host init of the image, init = HIP runtime +
+    // device context + stream, engine = weights (transformed / packed on the host) + workspace upload,
+    // alloc = the I/O buffers; then h2d / compute / d2h of the first call
+    double a0 = now_ms();
+    cold.add("input", a0 - t0);
     int ndev = 0;
     hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
     if (ndev < 1) throw std::runtime_error("v3 needs a GPU");
     hip_check(hipSetDevice(s.ri.local_rank % ndev), "hipSetDevice");
     hipStream_t st;
     hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+    cold.add("init", now_ms() - a0);
+    a0 = now_ms();
     BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
+    cold.add("engine", now_ms() - a0);
+    a0 = now_ms();
     float *dx, *dy;
     hip_check(hipMalloc(&dx, s.x.size() * 4), "hipMalloc");
     hip_check(hipMalloc(&dy, y.size() * 4), "hipMalloc");
-    cold.add("setup", now_ms() - t0);
+    cold.add("alloc", now_ms() - a0);
     auto step = [&](Phases& ph) {
       double a = now_ms();
       hip_check(hipMemcpyAsync(dx, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice, st), "H2D");
@@ -672,6 +681,8 @@ int run_rows_host(Setup& s, HostComm& c, bool gpu) {
 // Steady-state steps never synchronise a stream with the host. Phase times are the compute stream's
 // critical path (scatter / halo_p1 = time spent waiting for data). --dry-run prints the schedule each
 // rank's transport would execute (record-only, no GPU) as ANX_SCHEDULE lines.
+int run_v5_steps(Setup& s, HostComm& c, V5Runtime& rt, int N, double t0);
+
 int run_v5(Setup& s, HostComm& c, bool dry) {
   const int N = s.o.batch, rank = c.rank(), np = c.size();
   V5Options o;
@@ -702,13 +713,24 @@ int run_v5(Setup& s, HostComm& c, bool dry) {
     }
     return 0;
   }
-  Phases cold, warm;
   c.barrier();
   const double t0 = now_ms();
-  double a = now_ms();
   if (rank == 0) fill_input(s);
   V5Runtime rt(c, s.ri, s.b1, s.b2, s.d.H, s.d.W, s.w, o);
+  try {
+    return run_v5_steps(s, c, rt, N, t0);
+  } catch (...) {
+    rt.abort();  // before ~V5Runtime's device sync: release every wait on a peer (ncclCommAbort / flags)
+    throw;
+  }
+}
+
+// The timed part of run_v5 (t0: its start, before the runtime's construction).
+int run_v5_steps(Setup& s, HostComm& c, V5Runtime& rt, int N, double t0) {
+  const int rank = c.rank(), np = c.size();
+  Phases cold, warm;
   rt.set_input(rank == 0 ? s.x.data() : nullptr);
+  const double a = t0;
   cold.add("setup", now_ms() - a);
   std::vector<float> y_host(rank == 0 ? static_cast<size_t>(N) * s.d.Hp2 * s.out_row : 0);
   rt.step();

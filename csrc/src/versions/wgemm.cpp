@@ -128,29 +128,6 @@ int main(int argc, char** argv) {
                     "%.1f, \"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
                     images, cfg, abl, t, flop / t * 1e-6, d, rmax);
       }
-    {  // split-bf16 GEMMs (wino_gemm_sb.hpp)
-      std::vector<uint16_t> ubh;
-      hip::wino_split_planes_host(download(U, hip::wino_u_floats(w)), 49, 256, 96, ubh);
-      uint16_t* Ub = nullptr;
-      CHECK(hipMalloc(&Ub, ubh.size() * sizeof(uint16_t)));
-      CHECK(hipMemcpy(Ub, ubh.data(), ubh.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-      for (int np : {9, 6})
-        for (int abl : {0, 1, 3}) {
-          const hip::OutView ov{y1, 27, 27, 256, 0, 0, 0};
-          CHECK(hipMemset(y1, 0, ny * sizeof(float)));
-          auto run = [&] {
-            return hip::wino_sb_gemm_conv2(V, Ub, b, ov, w.P, w.ty, w.tx, 27, 27, 96, 256, 1, true, nullptr, np, occ, abl);
-          };
-          CHECK(run());
-          const double t = time_us(run, iters);
-          double rmax = 0;
-          const double d = max_abs_diff(download(y1, ny), ref, &rmax);
-          std::printf("{\"conv\": 2, \"images\": %d, \"arm\": \"split-bf16 x%d abl=%d\", \"us\": %.1f, \"f32_equiv_tflops\": "
-                      "%.1f, \"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
-                      images, np, abl, t, flop / t * 1e-6, d, rmax);
-        }
-      CHECK(hipFree(Ub));
-    }
     for (float* p : {V, U, b, y0, y1}) CHECK(hipFree(p));
   }
 
@@ -196,28 +173,6 @@ int main(int argc, char** argv) {
                     "\"tflops\": %.1f, \"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
                     images, cfg, abl, t, flop / t * 1e-6, dd, rmax);
       }
-    {  // split-bf16 GEMMs
-      std::vector<uint16_t> ubh;
-      hip::wino_split_planes_host(uh, 25, 96, 48, ubh);
-      uint16_t* Ub = nullptr;
-      CHECK(hipMalloc(&Ub, ubh.size() * sizeof(uint16_t)));
-      CHECK(hipMemcpy(Ub, ubh.data(), ubh.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-      for (int np : {9, 6})
-        for (int abl : {0, 1, 3}) {
-          CHECK(hipMemset(y1, 0, ny * sizeof(float)));
-          auto run = [&] {
-            return hip::wino_sb_gemm_conv1(V, Ub, b, o1, w.P, w.ty, w.tx, 55, 55, 96, true, nullptr, np, occ, abl);
-          };
-          CHECK(run());
-          const double t = time_us(run, iters);
-          double rmax = 0;
-          const double dd = max_abs_diff(download(y1, ny), ref, &rmax);
-          std::printf("{\"conv\": 1, \"images\": %d, \"arm\": \"split-bf16 x%d abl=%d (GEMM only)\", \"us\": %.1f, "
-                      "\"f32_equiv_tflops\": %.1f, \"max_abs_diff\": %.3g, \"ref_max\": %.3g}\n",
-                      images, np, abl, t, flop / t * 1e-6, dd, rmax);
-        }
-      CHECK(hipFree(Ub));
-    }
     for (float* p : {x, U, b, V, y0, y1}) CHECK(hipFree(p));
   }
   return 0;

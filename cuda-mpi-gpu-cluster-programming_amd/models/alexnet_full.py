@@ -175,7 +175,7 @@ class AlexNetFull:
             self._own_stream = torch.cuda.Stream(self.device)
         streams = [self._own_stream, *self._lane_streams]
         engines = [self, *self._lanes]
-        bounds = [N * i // L for i in range(L + 1)]
+        bounds = self.lane_bounds(N)
         fresh = all(st.query() for st in streams)
         cur = torch.cuda.current_stream(self.device)
         for i, (eng, st) in enumerate(zip(engines, streams)):
@@ -193,6 +193,14 @@ class AlexNetFull:
                 if on_lane is not None:
                     on_lane(i, lo, hi)
         return out
+
+    def lane_bounds(self, n: int) -> list[int]:
+        """Image boundaries [0, ..., n] of the lanes :meth:`forward_async` runs ``n`` images on (the
+        pipeline's per-lane gather segments; ScatterComputeGather's root shedding needs them)."""
+        L = 1 + len(self._lanes)
+        if L == 1 or n < L or self.device.type != "cuda":
+            return [0, n]
+        return [n * i // L for i in range(L + 1)]
 
     def join(self) -> None:
         if self.device.type != "cuda":

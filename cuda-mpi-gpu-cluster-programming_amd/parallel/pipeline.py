@@ -31,8 +31,14 @@ the root ``irecv``s every peer's segment in one batch into ``y_global[r, seg]`` 
 slice into ``y_global[0]`` (rows past ``root_batch`` of ``y_global[0]`` are unused).
 
 ``inputs`` (local input only): a list of input batches used round-robin, step k computing
-``inputs[k % len(inputs)]`` — a benchmark streams distinct data through the engine instead of one
-cache-resident batch.
+``inputs[k % len(inputs)]`` (its first rows: this rank's share) — a benchmark streams distinct data
+through the engine instead of one cache-resident batch. ``x_used`` is the batch the last step computed.
+
+``set_root_batch(n)`` changes the root's share between steps (after :meth:`drain`; the root's buffers
+are allocated for ``batch_per_rank`` rows and sliced), so a benchmark can calibrate it from measured
+per-rank compute (``timing = True``: every async step records each lane's compute span — from the end
+of its wait for the gather that last read its output slice to the end of its forward, before its own
+gather — as HIP events, or host time on CPU ranks; :meth:`lane_span_ms` is the mean span per step).
 
 Input semantics with prefetch: ``step()`` snapshots ``x_global`` as it is at the call (the scatter
 for the NEXT step is issued from it) and computes the batch snapshotted by the previous call (the
@@ -81,22 +87,17 @@ class ScatterComputeGather:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         B = cfg.batch_per_rank
-        rb = B if cfg.root_batch is None or self.world == 1 else cfg.root_batch
-        if rb != B and (cfg.scatter or not 0 < rb <= B):
-            raise ValueError(f"root_batch {rb} needs local input and 0 < root_batch <= batch_per_rank {B}")
-        self.root_batch, self.shed = rb, rb != B
         M = cfg.micro if self.world > 1 else 1
-        if self.shed and min(M, rb) != min(M, B):
-            raise ValueError(f"root_batch {rb} must give the root as many micro-batches ({M}) as its peers")
+        self._M = M
         self.peer_splits = micro_splits(B, M)  # a peer's micro-batches (the root receives these)
-        if self.rank == 0:
-            B = rb
-        self.splits = micro_splits(B, M)
+        self.root_batch, self.shed = B, False
         self.prefetch = cfg.prefetch and self.world > 1
         nbuf = 2 if self.prefetch else 1
-        self._xb = [torch.empty((B, *in_shape), device=self.device) for _ in range(nbuf)]
-        self._yb = [torch.empty((B, *out_shape), device=self.device) for _ in range(nbuf)]
-        self.x, self.y = self._xb[0], self._yb[0]
+        # full batch_per_rank rows on every rank: the root's share is a slice (set_root_batch)
+        self._xfull = [torch.empty((B, *in_shape), device=self.device) for _ in range(nbuf)]
+        self._yfull = [torch.empty((B, *out_shape), device=self.device) for _ in range(nbuf)]
+        self._n = B  # images this rank computes per step
+        self.set_root_batch(B if cfg.root_batch is None or self.world == 1 else cfg.root_batch, _init=True)
         self._k = 0
         self._scatter_pending = None          # works that fill the input of the next step
         self._gather_pending = [None] * nbuf  # works still reading y buffer i
@@ -107,10 +108,55 @@ class ScatterComputeGather:
                          if root and cfg.gather else None)
         self.async_lanes = cfg.async_lanes and not cfg.scatter and hasattr(model, "forward_async")
         if self.async_lanes and self.world > 1 and cfg.gather and nbuf < 2:  # a gather may still read y[k-1]
-            self._yb.append(torch.empty_like(self._yb[0]))
+            self._yfull.append(torch.empty_like(self._yfull[0]))
             self._gather_pending.append(None)
+        self._slice_bufs()
         self._lane_gathers = [dict() for _ in self._yb]  # per output buffer: lane -> gather work reading it
         self.inputs: list | None = None  # local input only: batches used round-robin (see module doc)
+        self.x_used = None  # the input batch the last step computed
+        self.timing = False  # record per-lane compute spans (lane_span_ms)
+        self._spans: list = []
+
+    def _slice_bufs(self) -> None:
+        n = self._n
+        self._xb = [t[:n] for t in self._xfull]
+        self._yb = [t[:n] for t in self._yfull]
+        self.x, self.y = self._xb[0], self._yb[0]
+
+    def set_root_batch(self, rb: int, _init: bool = False) -> None:
+        """Images rank 0 computes per step (local input, dp). Only between steps, after :meth:`drain`.
+        Every rank may call it (peers only validate): the root's lanes must split ``rb`` images into as
+        many lanes, and micro-batches, as a peer's ``batch_per_rank``."""
+        B, M = self.cfg.batch_per_rank, self._M
+        rb = B if self.world == 1 else int(rb)
+        if rb != B and (self.cfg.scatter or not 0 < rb <= B):
+            raise ValueError(f"root_batch {rb} needs local input and 0 < root_batch <= batch_per_rank {B}")
+        if rb != B and min(M, rb) != min(M, B):
+            raise ValueError(f"root_batch {rb} must give the root as many micro-batches ({M}) as its peers")
+        if rb != B and hasattr(self.model, "lane_bounds") and \
+                len(self.model.lane_bounds(rb)) != len(self.model.lane_bounds(B)):
+            raise ValueError(f"root_batch {rb} runs {len(self.model.lane_bounds(rb)) - 1} lanes, a peer's batch "
+                             f"{B} {len(self.model.lane_bounds(B)) - 1}")
+        self.root_batch, self.shed = rb, rb != B
+        self._n = rb if self.rank == 0 else B
+        self.splits = micro_splits(self._n, M)
+        if not _init:
+            self._slice_bufs()
+
+    def lane_span_ms(self, reset: bool = True) -> float:
+        """Mean compute span per step of this rank's lanes (ms) over the steps recorded with ``timing``
+        (async steps only; syncs the device first on GPUs)."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        per_step = {}
+        for k, lane, a, b in self._spans:
+            ms = a.elapsed_time(b) if hasattr(a, "elapsed_time") else (b - a) * 1e3
+            per_step.setdefault(k, []).append(ms)
+        if reset:
+            self._spans = []
+        if not per_step:
+            return 0.0
+        return sum(sum(v) / len(v) for v in per_step.values()) / len(per_step)
 
     def _gather(self, y, seg: int, lo: int, hi: int):
         """Collect micro-batch / lane segment ``seg`` (this rank's rows [lo, hi) of ``y``) at rank 0."""
@@ -131,8 +177,19 @@ class ScatterComputeGather:
 
     def _local_input(self, default):
         if self.inputs and not self.cfg.scatter:
-            return self.inputs[self._k % len(self.inputs)]
-        return default
+            x = self.inputs[self._k % len(self.inputs)][:self._n]
+        else:
+            x = default
+        self.x_used = x
+        return x
+
+    def _mark(self):
+        if self.device.type == "cuda":
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        import time
+        return time.perf_counter()
 
     def _scatter(self, x):
         root = self.rank == 0
@@ -176,12 +233,18 @@ class ScatterComputeGather:
         y, pend = self._yb[cur], self._lane_gathers[cur]
         gather = self.cfg.gather and self.world > 1
 
+        marks = {}
+
         def pre_lane(i, lo, hi):  # on lane i's stream: the gather of this slice two steps ago is done
             w = pend.pop(i, None)
             if w is not None:
                 w.wait()
+            if self.timing:
+                marks[i] = self._mark()
 
         def on_lane(i, lo, hi):  # on lane i's stream: gather its slice as soon as it is computed
+            if self.timing:
+                self._spans.append((self._k, i, marks.pop(i), self._mark()))
             if gather:
                 pend[i] = self._gather(y, i, lo, hi)
 

@@ -24,7 +24,8 @@ Names and values:
   (images per Conv1 / Conv2 transform + GEMM launch pair inside a fused forward; 0 = whole launch: a
   small sub-chunk rewrites the V workspace in place, inside the Infinity Cache); ``conv1_fused`` (1, the
   default: Conv1 as one kernel, the polyphase input transform built in LDS inside the Winograd GEMM;
-  0: the band transform kernel + GEMM).
+  0: the band transform kernel + GEMM); ``conv1_pool`` (1, the default: pool1 in that kernel's epilogue for
+  whole images, the conv1 map never reaches HBM; 0: Conv1 writes its map and the input transform pools it).
 """
 from __future__ import annotations
 
@@ -35,7 +36,7 @@ from .. import _native as nat
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
          "bf16_lrn_tile", "bf16_fc", "bf16_conv1", "bf16_pool1", "bf16_fc_cfg", "bf16_fc_minkt", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
-         "conv1_fused")
+         "conv1_fused", "conv1_pool")
 
 
 def knob_value(name: str, value) -> int:

@@ -345,3 +345,42 @@ def test_bench_root_batch_gloo():
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert rec["config"]["global_batch"] == 3 and rec["config"]["root_batch"] == 1
     assert rec["config"]["batch_per_gpu"] == 2
+
+
+def _bench3(extra_env=None, extra_args=()):
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "3",
+           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "4", "--root-batch", "2", "--device", "cpu",
+           *extra_args]
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(extra_env or {}))
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_selfcheck_gloo_n3():
+    """The N>1 record proves itself (gloo/CPU rehearsal at N=3): the communicator's world size and every
+    rank's identity; rank 0's share calibrated from measured per-rank compute spans (modelled / forced
+    value and the calibration rounds both reported); one post-window step whose gathered outputs match
+    every rank's own checksum, and two images per rank against the fp64 oracle."""
+    rec = _bench3(extra_args=("--calibrate-root", "on"))
+    assert rec["rccl_world_size"] == 3
+    ident = rec["identity"]
+    assert ident["world_size"] == 3 and [r["rank"] for r in ident["ranks"]] == [0, 1, 2]
+    assert ident["backend"] == "gloo"
+    cfg = rec["config"]
+    assert cfg["root_batch_modelled"] == 2 and "calibrated_root_batch" in cfg and cfg["calibration"]
+    assert 1 <= cfg["root_batch"] <= 4 and cfg["global_batch"] == 2 * 4 + cfg["root_batch"]
+    assert rec["gather_verified"] is True and rec["verify"]["mismatched_ranks"] == []
+    assert [r["images"] for r in rec["verify"]["per_rank"]] == [cfg["root_batch"], 4, 4]
+    assert rec["verify"]["oracle_max_rel_err"] < 1e-5
+
+
+def test_bench_selfcheck_detects_corrupt_rank_gloo():
+    """A rank whose gathered bytes do not match what it computed turns gather_verified false and is named."""
+    rec = _bench3({"ANX_BENCH_CORRUPT_RANK": "2"}, ("--calibrate-root", "off"))
+    assert rec["gather_verified"] is False and rec["verify"]["mismatched_ranks"] == [2]
+    assert "calibration" not in rec["config"] and rec["config"]["root_batch"] == 2

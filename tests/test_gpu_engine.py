@@ -495,3 +495,24 @@ def test_conv1_fused_row_tiles(cuda, np_, mode):
         xt = xd[:, t.inp.lo:t.inp.hi].contiguous()
         a, b = fused.tile_forward(xt, t), plain.tile_forward(xt, t)
         assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("N,kn", [(9, {}), (33, {}), (64, {}), (130, {}), (40, {"chunk1": 16}),
+                                  (64, {"conv2_sub": 24}), (20, {"chunk1": 9, "conv2_sub": 4})])
+def test_conv1_pool_epilogue_bitwise(cuda, N, kn):
+    """pool1 in the one-kernel Conv1's epilogue (knob conv1_pool: the conv1 map never reaches HBM; windows
+    straddling two workgroups' tile ranges merged from a side buffer by the Conv2 input transform) gives
+    the same bits as Conv1 writing its map and the input transform pooling it: partial workgroups (P
+    not a multiple of 32), chunked launches and Conv2 sub-chunks (their offset into the Conv1 launch's
+    tile numbering) included; the whole output is checked against the fp64 oracle too."""
+    x = init_input(N, "rand", seed=21).to(cuda)
+    base = {**WINO1, **WINO2, **kn}
+    on = AlexNetBlocks(device=cuda, init="rand", seed=21, max_batch=N, knobs={**base, "conv1_pool": 1})
+    off = AlexNetBlocks(device=cuda, init="rand", seed=21, max_batch=N, knobs={**base, "conv1_pool": 0})
+    y = on(x)
+    assert torch.equal(y, off(x))
+    y.fill_(float("nan"))  # every pooled pixel rewritten each call (the window border stays zero)
+    on(x, out=y)
+    assert torch.equal(y, off(x))
+    ref = blocks_forward(x.cpu(), on.weights, on.b1, on.b2)
+    torch.testing.assert_close(y.cpu().double(), ref, rtol=2e-5, atol=2e-6)

@@ -147,11 +147,11 @@ def _run_v5(world, kw, batch=6, steps=4, kind="v5", env=None, all_ranks=False):
     return res if all_ranks else res[0][:3]
 
 
-def _reference(knobs=None):
+def _reference(knobs=None, batch=6):
     from anx.models.alexnet_blocks import AlexNetBlocks
     from anx.utils.init import init_input
-    m = AlexNetBlocks(init="rand", seed=9, device="cuda", lrn_mode="raw", max_batch=6, knobs=knobs or {})
-    y = m(init_input(6, "rand", seed=9).cuda()).cpu()
+    m = AlexNetBlocks(init="rand", seed=9, device="cuda", lrn_mode="raw", max_batch=batch, knobs=knobs or {})
+    y = m(init_input(batch, "rand", seed=9).cuda()).cpu()
     m.close()
     return y
 
@@ -240,11 +240,17 @@ def test_rccl_transport_loopback_bitwise(v5_reference_direct, world, kw):
 
 
 @pytest.mark.gpu
-def test_v5_local_whole_images_run_lanes(v5_reference):
-    """One rank, 64 images: the whole-image tile runs as 2 free-running lanes of the fused forward."""
+def test_v5_local_whole_images_run_lanes(cuda):
+    """One rank, 64 images: the whole-image tile runs as 2 free-running lanes of the fused forward (each
+    its own engine, stream and tile / output offsets). Both lanes' slices (images 0-31 and 32-63) are
+    compared with a one-lane forward of all 64 images."""
+    ref = _reference(batch=64)
     y, desc, phases = _run_v5(1, {"pipeline": 1}, batch=64, steps=3)
     assert desc["lane_path"] is True and desc["lanes"] == 2
-    assert torch.from_numpy(y)[:6].sub(v5_reference).abs().max().item() / v5_reference.abs().max().item() < 1e-5
+    y = torch.from_numpy(y)
+    assert y.shape == ref.shape
+    for lo, hi in ((0, 32), (32, 64)):
+        assert y[lo:hi].sub(ref[lo:hi]).abs().max().item() / ref[lo:hi].abs().max().item() < 1e-5, (lo, hi)
 
 
 @pytest.mark.gpu
