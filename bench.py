@@ -130,6 +130,8 @@ def parse():
                          "rank 0's share to the peers' (auto = on when the share is the cost model's, not --root-batch)")
     ap.add_argument("--no-verify", action="store_true",
                     help="dp, N>1: skip the post-window gather checksum / oracle verification step")
+    ap.add_argument("--no-subrecords", action="store_true",
+                    help="v5: skip the forced 2-way-row (halo on) sub-records per device transport")
     ap.add_argument("--no-full", action="store_true",
                     help="blocks dp on GPUs: skip the secondary full-AlexNet bf16 (BASELINE config 5) measurement")
     ap.add_argument("--first-collective-s", type=float, default=float(os.environ.get("ANX_FIRST_COLLECTIVE_S", "240")),
@@ -237,6 +239,71 @@ def full_bf16_secondary(dev, world: int, rank: int, steps: int = 10, warmup: int
             "warmup": warmup, "batch_per_gpu": B, "global_batch": B * world, "n_gpus": world, "dtype": "bf16",
             "scaling": "weak", "tflops": round(ips * FLOPS_PER_IMAGE / 1e12, 1), "outputs_finite": finite,
             "data": "synthetic images, He-uniform random weights", "note": "secondary record; the headline is fp32"}
+
+
+def v5_halo_subrecords(a, world: int, rank: int, GB: int, dev, g) -> dict:
+    """BASELINE config 4 with the per-layer halo exchange forced on: 2-way row groups (the pool1 halo
+    between the two ranks of a group moves every step), once per device transport, so a run measures
+    RCCL against the peer (IPC copy + device flag) transport side by side with the halo bytes and the
+    halo_p1 wait. One GPU: two ranks sharing it as child processes (`anxrun -np 2 anx --version v5`;
+    peer, and the RCCL transport's code over the loopback device comm, since RCCL refuses a shared
+    device). N > 1 (even): in process, every rank."""
+    import subprocess
+    out = {}
+    if world == 1:
+        if rank != 0:
+            return out
+        root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cuda-mpi-gpu-cluster-programming_amd", "bin")
+        env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+        for tr in ("peer", "loopback"):
+            cmd = [os.path.join(root, "anxrun"), "-np", "2", "--timeout", "200", "--", os.path.join(root, "anx"),
+                   "--version", "v5", "--transport", tr, "--batch", str(GB), "--row-ways", "2", "--iters", "10",
+                   "--init", "rand", "--chunks", "1"]
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+                recs = [json.loads(l[len("ANX_JSON "):]) for l in r.stdout.splitlines() if l.startswith("ANX_JSON ")]
+                if r.returncode != 0 or not recs:
+                    out[f"v5_rows2_{tr}"] = {"error": f"rc={r.returncode}", "stderr": r.stderr[-300:]}
+                    continue
+                j = recs[0]
+                v5 = j.get("v5") or {}
+                out[f"v5_rows2_{tr}"] = {
+                    "ranks": 2, "shared_gpu": True, "row_ways": 2, "transport": v5.get("transport", tr),
+                    "images_per_s": float(j["images_per_s"]) if j.get("images_per_s") not in (None, "null") else None,
+                    "ms_per_step": float(j["warm_ms"]) if j.get("warm_ms") not in (None, "null") else None,
+                    "phases_ms": j.get("phases_warm"), "halo_exchange": v5.get("halo_exchange"),
+                    "halo_bytes_per_step": v5.get("halo_bytes_per_step"),
+                    "bytes_per_step": v5.get("bytes_per_step"), "checksum": j.get("checksum")}
+            except Exception as e:  # a sub-record never takes the headline down
+                out[f"v5_rows2_{tr}"] = {"error": repr(e)[:300]}
+        return out
+    if world % 2:
+        return out
+    from anx.parallel.workloads import NativeV5
+    from anx.utils.init import init_weights
+    b1, b2 = anx.config.blocks()
+    for tr in ("rccl", "peer"):
+        wl = NativeV5(GB, init_weights("rand", 1234, b1, b2) if rank == 0 else None, specs=(b1, b2), decomp="rows2",
+                      transport=tr, chunks=a.chunks, pipeline=a.pipeline, impl=a.impl, input_source="local",
+                      lanes=a.lanes)
+        wl.fill((torch.rand((GB, 227, 227, 3), device=dev, generator=g) * 0.1) if rank == 0 else None)
+        wl.step(steps=3)
+        wl.sync()
+        wl.reset_phases()
+        dist.barrier()
+        t0 = time.perf_counter()
+        wl.step(steps=10)
+        wl.sync()
+        dist.barrier()
+        el = time.perf_counter() - t0
+        d = wl.describe()
+        out[f"v5_rows2_{tr}"] = {"ranks": world, "row_ways": 2, "transport": d.get("transport"),
+                                 "images_per_s": round(GB * 10 / el, 1), "ms_per_step": round(el * 100, 4),
+                                 "phases_ms": wl.phase_ms(), "halo_exchange": d.get("halo_exchange"),
+                                 "halo_bytes_per_step": d.get("halo_bytes_per_step"),
+                                 "bytes_per_step": d.get("bytes_per_step")}
+        wl.close()
+    return out
 
 
 def _oracle(model):
@@ -467,6 +534,9 @@ def main():
             dist.destroy_process_group()
         return
 
+    subs = {}
+    if cuda and wl is not None and a.workload == "v5" and not a.no_subrecords:
+        subs = v5_halo_subrecords(a, world, rank, GB, dev, g)
     b1 = batch1_latency(dev) if (rank == 0 and cuda and not a.no_b1) else {}
     full = None
     if cuda and wl is None and not a.no_full:
@@ -581,6 +651,7 @@ def main():
                 rec["verify"] = verify
         if full is not None:
             rec["full_bf16"] = full
+        rec.update(subs)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

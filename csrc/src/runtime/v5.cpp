@@ -597,6 +597,17 @@ std::string V5Runtime::describe_json() const {
   // bytes per step by phase: per rank (arrays over ranks) and the root's / busiest rank's totals
   const std::vector<RankBytes> rb = lay_.rank_bytes();
   std::string j = b;
+  // whether this layout exchanges pool1 halos at all: the cost model's default may pick a pure batch
+  // split (whole images per rank), which is V5 without its per-layer halo exchange; say so explicitly
+  //  instead of leaving it to row_ways
+  const size_t nhalo = lay_.sched.phase[static_cast<int>(Phase::P1Halo)].size();
+  double halo_bytes = 0;
+  for (const RankBytes& x : rb) halo_bytes += x.halo_sent;
+  char h[160];
+  std::snprintf(h, sizeof h, "\"halo_exchange\": \"%s\", \"halo_transfers_per_step\": %zu, \"halo_bytes_per_step\": %.0f, ",
+                nhalo ? "pool1 rows between row-group neighbours" : "none (batch split: every rank whole images)", nhalo,
+                halo_bytes);
+  j += h;
   auto arr = [&](const char* name, double RankBytes::*f) {
     std::string a = "\"" + std::string(name) + "\": [";
     char t[32];

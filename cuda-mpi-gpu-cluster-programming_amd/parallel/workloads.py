@@ -43,7 +43,9 @@ from .comm import world
 from .plan import OVERLAP, PER_LAYER, HybridPlan, make_hybrid_plan
 
 DECOMPS = {"rows": None, "hybrid": 0, "batch": 1}  # row_ways (None = all ranks)
-V5_DECOMPS = {"auto": -1, "rows": None, "hybrid": 0, "batch": 1}  # -1: the cost model's pick (anx/cost.hpp)
+# -1: the cost model's pick (anx/cost.hpp); None: rows over every rank; rows2: 2-way row groups (the
+# halo exchange on at any even rank count: bench.py's v5 sub-records)
+V5_DECOMPS = {"auto": -1, "rows": None, "hybrid": 0, "batch": 1, "rows2": 2}
 PHASES = ("h2d", "scatter", "stage1", "halo_p1", "compute", "gather", "d2h")
 
 

@@ -19,6 +19,8 @@
 #   halo     V5 halo pipeline A/B on shared-GPU peer ranks, 2-way rows: np {2,4} x chunks {1, auto}
 #   tests_k  a subset of GPU tests: pytest -k "$TESTS_K" (one process)
 #   ingest   tools/probe_ingest.py: the bench step with a concurrent 155 MB/step receive-side copy
+#   libab    bench.py with the in-tree libanx vs an alternative build ($LIBAB/lib, e.g. ab_slp/: another
+#            CMake configuration of the same sources), alternated $BENCH_REPS times into libab.jsonl
 # Outputs land in gpurun_out/ (merged back by gpurun). This one script replaces the per-session
 # wrappers of rounds 1-3.
 set -o pipefail
@@ -43,7 +45,7 @@ pmc() {  # pmc NAME COUNTERS...: one counter pass over a short bench run
   shift
   echo "== pmc $name: $*"
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$O/$name" -o pmc -- \
-    python3 bench.py --steps 3 --warmup 1 $BARGS > "$O/$name.log" 2>&1 || { echo "== pmc $name FAILED"; exit 1; }
+    python3 bench.py --steps 3 --warmup 1 --no-full $BARGS > "$O/$name.log" 2>&1 || { echo "== pmc $name FAILED"; exit 1; }
 }
 
 for s in "$@"; do
@@ -55,7 +57,7 @@ for s in "$@"; do
              ${SWEEP_ARGS:-} ;;
     ab) run ab 900 python tools/ab_variants.py --arms "${AB_ARMS:-|conv1_occ=3}" --batch "${AB_BATCH:-300}" \
           --lanes "${AB_LANES:-1}" --rounds "${AB_ROUNDS:-5}" ;;
-    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 10 --warmup 3 $BARGS ;;
+    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 10 --warmup 3 --no-full $BARGS ;;
     pmc)
       pmc pmc1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_INSTS_MFMA
       pmc pmc2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INST_LEVEL_VMEM
@@ -90,13 +92,28 @@ for s in "$@"; do
           IFS=';' read -r -a kvs <<< "$arm"
           for kv in "${kvs[@]}"; do [ -n "$kv" ] && kargs+=(--knob "$kv"); done
           echo "== benchab rep $rep arm '$arm'"
-          timeout -k 10 200 python -u bench.py --steps "${BENCH_STEPS:-20}" --warmup 5 --no-b1 $BARGS "${kargs[@]}" \
+          timeout -k 10 200 python -u bench.py --steps "${BENCH_STEPS:-20}" --warmup 5 --no-b1 --no-full $BARGS "${kargs[@]}" \
             >> "$O/benchab.jsonl" 2>> "$O/benchab.err" || { echo "== benchab FAILED"; exit 1; }
           tail -1 "$O/benchab.jsonl" | cut -c1-160
         done
       done ;;
+    libab)
+      for rep in $(seq "${BENCH_REPS:-3}"); do
+        for arm in intree "${LIBAB:?LIBAB=dir}"; do
+          echo "== libab rep $rep arm $arm"
+          if [ "$arm" = intree ]; then
+            timeout -k 10 200 python -u bench.py --steps "${BENCH_STEPS:-20}" --warmup 5 --no-b1 --no-full $BARGS \
+              >> "$O/libab_intree.jsonl" 2>> "$O/libab.err" || { echo "== libab FAILED"; exit 1; }
+            tail -1 "$O/libab_intree.jsonl" | cut -c1-160
+          else
+            ANX_LIB="$arm/lib/libanx.so" timeout -k 10 200 python -u bench.py --steps "${BENCH_STEPS:-20}" --warmup 5 \
+              --no-b1 --no-full $BARGS >> "$O/libab_alt.jsonl" 2>> "$O/libab.err" || { echo "== libab FAILED"; exit 1; }
+            tail -1 "$O/libab_alt.jsonl" | cut -c1-160
+          fi
+        done
+      done ;;
     bytes)
-      BYARGS="--lanes 1 --steps 6 --warmup 2 --no-b1 --prewarm-s 0 $BARGS"
+      BYARGS="--lanes 1 --steps 6 --warmup 2 --no-b1 --no-full --prewarm-s 0 $BARGS"
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --kernel-trace \
         --output-format csv -d "$O/pmc_fetch" -o run -- python3 bench.py $BYARGS > "$O/pmc_fetch.log" 2>&1 &&
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --kernel-trace \

@@ -225,3 +225,24 @@ def test_v5_multinode_transport_choice():
     (rc0, _, err0), (rc1, _, err1) = _two_nodes(base + ["--transport", "peer"], timeout=60)
     assert rc0 != 0 and rc1 != 0
     assert "single-node" in err0 + err1
+
+
+@pytest.mark.gpu
+def test_v5_rows2_transports_bitwise(cuda):
+    """bench.py's V5 sub-records (2-way row groups, the pool1 halo on) per device transport: the peer
+    transport and the RCCL transport's code over the loopback device comm, on ranks sharing the GPU,
+    NaN-poisoned and pipelined, move the same halo bytes and give the same output bits (Winograd convs,
+    the bench's kernels), and match the single-rank run to fp32 rounding."""
+    args = ["--version", "v5", "--row-ways", "2", "--init", "rand", "--seed", "8", "--batch", "40", "--iters", "3",
+            "--chunks", "1", "--poison", "--pipeline", "on"]
+    peer, _ = native([*args, "--transport", "peer"], 2)
+    loop, _ = native([*args, "--transport", "loopback"], 2)
+    for r in (peer, loop):
+        assert r["v5"]["halo_transfers_per_step"] > 0 and r["v5"]["halo_bytes_per_step"] > 0
+        assert "none" not in r["v5"]["halo_exchange"]
+    assert peer["checksum"] == loop["checksum"]
+    assert peer["v5"]["halo_bytes_per_step"] == loop["v5"]["halo_bytes_per_step"]
+    assert peer["v5"]["transport"] == "peer" and loop["v5"]["transport"] == "rccl-loopback"
+    one, _ = native(["--version", "v5", "--init", "rand", "--seed", "8", "--batch", "40", "--check"], 1)
+    two, _ = native([*args, "--transport", "peer", "--check"], 2)
+    assert one["max_abs_err"] < 1e-3 and two["max_abs_err"] < 1e-3

@@ -188,6 +188,10 @@ def test_native_v5_shared_gpu(v5_reference, world, kw):
     y = torch.from_numpy(y)
     err = (y - v5_reference).abs().max().item() / v5_reference.abs().max().item()
     assert err < 1e-5, (err, desc)
+    # the layout says whether V5's per-layer halo exchange runs (a batch split has none)
+    assert ("none" in desc["halo_exchange"]) == (desc["halo_transfers_per_step"] == 0)
+    if world > 1 and kw.get("decomp") == "rows" and kw.get("layer") != "overlap":
+        assert desc["halo_transfers_per_step"] > 0 and desc["halo_bytes_per_step"] > 0
     assert desc["transport"] == kw.get("transport", "rccl" if world == 1 else "peer")
     assert desc["input_source"] == kw.get("input_source", "local")
     assert set(phases) == {"scatter", "stage1", "halo_p1", "stage2", "gather", "compute"}
