@@ -70,16 +70,6 @@ struct BigFc {
 constexpr int kMaxFcSplit = 16;
 // min_kt: K tiles per split-K slice at least this many (knob bf16_fc_minkt)
 BigFc pick_bf16_big_fc(const ConvPlanB& p, int cus = 256, int cfg = -1, int min_kt = 4);
-// Fully-connected layer on the activation-streaming kernel (activations global -> VGPR four K tiles
-// ahead, weights through an LDS-DMA ring): fp32 slabs [ksplit][N][Kg] into ws, then
-// splitk_reduce_bf16. Needs C % 64 == 0 and ksplit | K tiles with (K tiles / ksplit) % 4 == 0;
-// pick_fc_split returns such a ksplit (0: not applicable).
-bool fc_bf16_ok(const ConvPlanB& p);
-int pick_fc_split(const ConvPlanB& p, int cus = 256);
-// FC weights for fc_bf16: the packed [kpad_n][kpad] rows regrouped into 64x64 tiles, tile (n, k) at
-// ((n * K tiles + k) * 64 + row) * 64 (each workgroup's weight stream is contiguous).
-void pack_fc_blocked_bf16(const ConvPlanB& p, const std::vector<uint16_t>& pk, std::vector<uint16_t>& out);
-hipError_t fc_bf16(const ConvPlanB& p, const void* x, const void* wblocked, float* ws, int ksplit, hipStream_t s);
 hipError_t maxpool_bf16(const void* x, int N, int H, int W, int C, int F, int S, OutViewB out, hipStream_t s);
 // tile (Knobs::bf16_lrn_tile): 1 = the generic LDS-tile kernel even where the C = 256 wave kernel applies (A/B).
 hipError_t maxpool_lrn_bf16(const void* x, int N, int H, int W, int C, int F, int S, int size, float alpha,
@@ -140,7 +130,6 @@ class FullEngine {
   struct Layer {
     int C, K, F, S, groups;
     void* wp = nullptr;
-    void* wfc = nullptr;  // FC layers: tile-blocked copy of wp for fc_bf16
     int* koff = nullptr;
     float* bias = nullptr;
     int key = -1;

@@ -121,7 +121,7 @@ int anx_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups,
                   size_t* packed_floats, size_t* koff_ints);
 int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff);
 /* Per-engine kernel knobs (anx/knobs.hpp): names conv1_algo, conv2_algo, chunk1, chunk2, force_vec4,
-   force_scalar, bf16_glds, bf16_big, bf16_lrn_tile, bf16_fc, conv1_occ, conv2_occ.
+   force_scalar, bf16_glds, bf16_big, bf16_lrn_tile, conv1_occ, conv2_occ (anx/knobs.hpp).
    set returns non-zero for an unknown name or an out-of-range value. */
 int anx_engine_set_knob(void* engine, const char* name, int value);
 int anx_engine_get_knob(void* engine, const char* name, int* value);

@@ -16,6 +16,13 @@ namespace anx {
 // larger than 8 images' worth of output rows (use_winograd), the direct implicit GEMM below that.
 enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2 };
 
+// Three kinds of field (round 5: the measured-worse variants are gone from libanx; the split-bf16
+// GEMMs, the U-in-registers Conv1 and the activation-streaming FC kernel were deleted):
+//   production  the defaults every bench and driver run launches, and their shape fallbacks;
+//   oracle      a simpler kernel kept as the bitwise / tolerance reference of a fast one in the GPU tests:
+//               conv*_algo = direct, conv1_band = 0 (per-tile gathers), bf16_glds = 0 with bf16_big = -2
+//               (the register-staged 128x128 bf16 kernel), fuse_pool1 / conv1_pool / conv1_fused = 0;
+//   tuning      launch geometry (chunks, sub-chunks, occupancy caps, forced tile configs) for A/B runs.
 struct Knobs {
   ConvAlgo conv1_algo = ConvAlgo::Auto;  // Conv1: polyphase Winograd F(3x3,3x3) / direct implicit GEMM
   ConvAlgo conv2_algo = ConvAlgo::Auto;  // Conv2: Winograd F(3x3,5x5) / direct implicit GEMM
@@ -23,11 +30,9 @@ struct Knobs {
   int chunk2 = 0;          // images per stage-2 launch
   int force_vec4 = -1;     // conv_mfma tile variant override for Cg % 4 == 0 convs (-1 = heuristic)
   int force_scalar = -1;   // conv_mfma tile variant override for scalar-gather convs
-  int bf16_glds = 2;       // bf16 full model: 0 register-staged, 2 / 3 LDS-DMA ring slots
+  int bf16_glds = 2;       // bf16 128x128 kernel: 2 / 3 LDS-DMA ring slots; 0 register-staged (oracle)
   int bf16_big = -1;       // bf16 conv layers on the wide-tile kernel (conv_bf16_big.hip): -1 cost model
-                           // picks the config, -2 off (the 128x128 kernels above), 0.. force that config
-  int bf16_fc = 0;         // bf16 FC layers: 1 = activation-streaming kernel (fc_bf16; measured slower than the
-                           // wide-tile cfg 8 split, profiles/r02_bf16bench_fc_b256.txt), 0 = wide-tile / 128x128
+                           // picks the config, 0.. force that config; -2 off (the 128x128 kernels: oracle)
   int bf16_fc_cfg = -1;    // bf16 FC layers: force this wide-tile config (A/B; -1 = cfg 8, 256x64 3-stage)
   int bf16_fc_minkt = 4;   // bf16 FC layers: K tiles per split-K slice at least this many (fewer slices, less
                            // reduce; 8 / 16 measured no better: profiles/r04_bf16_fc_minkt_ab.jsonl)
@@ -48,7 +53,8 @@ struct Knobs {
                            // fused into the Winograd input transform (no window round trip), 0 = pool1 kernel
   int conv1_fused = 1;     // Conv1 as one kernel (conv1_fused.hip: V built in LDS inside the GEMM, 32 tiles x 96
                            // filters per workgroup; bench step 277-278 k vs 252-254 k images/s,
-                           // profiles/r04_conv1_fused_v3_bench_ab.jsonl), 2 = U fragments in registers (A/B), 0 = the band transform kernel + GEMM
+                           // profiles/r04_conv1_fused_v3_bench_ab.jsonl), 0 = the band transform kernel + GEMM (the
+                           // general path: also every conv1 with K != 96)
   int conv1_pool = 1;      // fused tile_forward of whole images: pool1 in the one-kernel Conv1's epilogue (conv1_fused 1;
                            // the 55x55 map stays in LDS, pooled pixels go to the conv2 window, straddling windows'
                            // partial maxima to a side buffer merged by the Conv2 input transform), 0 = Conv1 writes its
@@ -60,7 +66,7 @@ struct Knobs {
 };
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
-// ANX_BF16_GLDS, ANX_BF16_BIG, ANX_BF16_FC, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1,
+// ANX_BF16_GLDS, ANX_BF16_BIG, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1,
 // ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL when set.
 Knobs default_knobs();
 

@@ -134,11 +134,11 @@ void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<floa
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
                       bool relu, hipStream_t s, const Knobs& k);
 // The one-kernel form (conv1_fused.hip): the input transform generated in LDS inside the GEMM, each
-// workgroup 32 tiles x all 96 filters (V never reaches HBM). Eligible for K == 96. mode 1: U through
-// an LDS ring; mode 2: U fragments straight into registers (one barrier per a-step).
+// workgroup 32 tiles x all 96 filters (V never reaches HBM, U through an LDS-DMA ring). Eligible for
+// K == 96.
 bool conv1_fused_eligible(const Conv1WinoPlan& w, const OutView& out);
 hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out, bool relu,
-                       hipStream_t s, int mode = 1);
+                       hipStream_t s);
 // The same kernel with pool1 (3x3 / 2 max) in its epilogue: the 55x55 conv1 map never leaves LDS. Pooled
 // pixel (py, px) of image n is written to `window` (pool1 image at h_off / w_off, e.g. the conv2 input
 // window) by the workgroup owning the window's top-left Conv1 tile; when the window's tiles straddle two

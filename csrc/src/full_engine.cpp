@@ -120,7 +120,6 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
         const hip::BigFc f = hip::pick_bf16_big_fc(p, cus_, c, 1);  // wide-tile FC slabs (ksplit 1 for fp32 logits)
         if (f.cfg >= 0) ws = std::max(ws, static_cast<size_t>(f.ksplit) * b * L_[i].K);
       }
-      if (hip::fc_bf16_ok(p)) ws = std::max(ws, static_cast<size_t>(std::max(1, hip::pick_fc_split(p, cus_))) * b * L_[i].K);
     }
   if (ws) ws_ = static_cast<float*>(dalloc(ws * 4));
 }
@@ -128,7 +127,7 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
 FullEngine::~FullEngine() {
   if (mark_) (void)hipEventDestroy(mark_);
   for (Layer& L : L_)
-    for (void* p : {L.wp, L.wfc, static_cast<void*>(L.koff), static_cast<void*>(L.bias)})
+    for (void* p : {L.wp, static_cast<void*>(L.koff), static_cast<void*>(L.bias)})
       if (p) (void)hipFree(p);
   for (void* p : {xb_, c1_, q2_, c2_, q3_, q4_, q5_, c5_, f6_, f7_, f8_, static_cast<void*>(ws_), w1ring_})
     if (p) (void)hipFree(p);
@@ -148,24 +147,9 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
     ANX_TRY(hipMalloc(&L.koff, ko.size() * 4));
     ANX_TRY(hipMemcpy(L.wp, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
     ANX_TRY(hipMemcpy(L.koff, ko.data(), ko.size() * 4, hipMemcpyHostToDevice));
-    if (L.wfc) ANX_TRY(hipFree(L.wfc));
-    L.wfc = nullptr;
-    if (hip::fc_bf16_ok(p)) {
-      std::vector<uint16_t> bl;
-      hip::pack_fc_blocked_bf16(p, pk, bl);
-      ANX_TRY(hipMalloc(&L.wfc, bl.size() * 2));
-      ANX_TRY(hipMemcpy(L.wfc, bl.data(), bl.size() * 2, hipMemcpyHostToDevice));
-    }
     L.key = p.variant;
   }
   const bool fc = p.Hp == 1 && p.Wp == 1 && p.F == 1;
-  if (fc && k_.bf16_fc && L.wfc) {  // activation-streaming FC kernel, fp32 slabs + reduce
-    const int ks = hip::pick_fc_split(p, cus_);
-    if (ks > 0) {
-      ANX_TRY(hip::fc_bf16(p, x, L.wfc, ws_, ks, s));
-      return hip::splitk_reduce_bf16(ws_, ks, N, L.K, L.bias, relu, out, out_f32, s);
-    }
-  }
   if (fc && k_.bf16_big != -2) {  // wide-tile FC: one 256-row tile of the batch, K split over the CUs
     hip::BigFc f = hip::pick_bf16_big_fc(p, cus_, k_.bf16_fc_cfg, k_.bf16_fc_minkt);
     if (f.cfg >= 0 && k_.bf16_big >= 0 && hip::conv_bf16_big_ok(p, k_.bf16_big, hip::OutViewB{B(ws_), 1, 1, p.Kg, 0, 0, 0}))

@@ -27,6 +27,7 @@
 // Reference op: convKernel (v3_cuda_only/src/layers_cuda.cu:20-46), one thread per output.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "anx/ops.hpp"
@@ -60,21 +61,38 @@ constexpr size_t kLds = kLdsFloats * sizeof(float);
 static_assert(kLds <= 160 * 1024, "LDS");
 static_assert(kUSlot % 256 == 0 && kUPieces <= 2 * kWaves && kUPieces >= kWaves, "U ring pieces: 1 or 2 per wave");
 
-// V_a's X' row u is loaded (kN5 loads) iff B^T[a][u] != 0
+// V_a takes X' row u iff B^T[a][u] != 0
 constexpr bool needs_row(int av, int u) { return av < kN5 && w33::kBT[av][u] != 0.f; }
-// does point p = 5a + b load an X' row (the one consumed at the end of point p + 1: row b + 1 of V_{a+1},
-// or row 0 of V_{a+2} at b = 4; p = -1 is the prologue)?
-constexpr bool loads_at(int p) {
-  const int av = p < 0 ? 0 : p / kN5, b = p < 0 ? kN5 - 1 : p % kN5;
-  return b + 1 < kN5 ? needs_row(av + 1, b + 1) : needs_row(av + (p < 0 ? 1 : 2), 0);
+// Every X' row is loaded ONCE per thread and kept in registers while any later V needs it (round 4
+// re-loaded it for every V_a that takes it: 16 row loads per thread instead of 5, ~710 MB of L2 -> VGPR
+// traffic per 128 images; the no-load cost probe ran the kernel 37 us faster, profiles/r05_conv1_abl/).
+// The rows V_0 takes (0-3) load in the prologue; a row first taken by a later V_a (row 4: V_4) loads
+// four points before the point that adds it into t (point b = u of a-step a - 1).
+constexpr bool prologue_row(int u) { return needs_row(0, u); }
+constexpr int first_a(int u) {
+  for (int a = 1; a < kN5; ++a)
+    if (needs_row(a, u)) return a;
+  return kN5;
 }
-static_assert(9 * kTiles * kOS <= kDummy && kTiles * kOS <= 2 * kVBuf,
-              "epilogue scratch: nine position images below the dummy DMA slot (UM 0), one in the V buffers (UM 1)");
+constexpr int late_load_pt(int u) {
+  return prologue_row(u) || first_a(u) >= kN5 ? -1 : ((first_a(u) - 1) * kN5 + u >= 4 ? (first_a(u) - 1) * kN5 + u - 4 : 0);
+}
+// the X' row loaded at point p (-1: none)
+constexpr int loads_at(int p) {
+  for (int u = 0; u < kN5; ++u)
+    if (p >= 0 && late_load_pt(u) == p) return u;
+  return -1;
+}
+constexpr int x_ops(int p) { return p >= 0 && loads_at(p) >= 0 ? kN5 : 0; }
+static_assert(9 * kTiles * kOS <= kDummy, "epilogue scratch: nine position images below the dummy DMA slot");
 // pool1 epilogue: candidate pooled pixels are those whose window starts in tiles p0 - kPoolBack .. p0 + 31
 // (a window's tiles span at most tx + 1 raster indices: kPoolBack >= tx + 1, checked by the launcher)
 constexpr int kPoolBack = 20, kPoolSlots = 4 * (kPoolBack + kTiles);
 constexpr int kPoolList = 9 * kTiles * kOS;  // the slot list after the nine position images
-static_assert(kPoolList + 1 + kPoolSlots <= kLdsFloats && kPoolSlots <= kNT, "pool1 slot list");
+// then per listed pixel 12 ints: its 9 window pixels' LDS float offsets (-1: another workgroup's),
+// the destination's element offset, whether it goes to p1, padding (16-B aligned entries)
+constexpr int kPoolEnt = 12, kPoolOffs = (kPoolList + 1 + kPoolSlots + 3) / 4 * 4;
+static_assert(kPoolOffs + kPoolSlots * kPoolEnt <= kLdsFloats && kPoolSlots <= kNT, "pool1 slot list");
 static_assert(kTiles * 24 == kNT, "V build: one (tile, channel pair) per thread");
 
 template <int B, int E, class F>
@@ -107,9 +125,7 @@ struct Conv1FusedArgs {
   int Hp, Wp;
 };
 
-// UM = 0: U through the 3-slot LDS ring (a barrier per point); UM = 1: each wave loads its own B
-// fragments of U straight into registers two points ahead (no LDS for U: one barrier per a-step).
-template <int UM, bool POOL>
+template <bool POOL, int ABL = 0>
 __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -139,18 +155,10 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // second 1-KiB piece DMA zeros (out-of-range source) into a 1-KiB scratch row instead, so the compiler's (and the schedule's)
   // vmcnt values count the same ops on every wave (with a conditional second piece the compiler
   // assumed none and its waits for the X' rows also waited for the U DMA just issued).
-  [[maybe_unused]] f32x4 ureg[kUSlots][3];  // UM 1: B fragments of points p, p + 1, p + 2 (slot p % 3)
-  [[maybe_unused]] const int ureg_off = ((wave >> 1) * 16 + (lane & 15)) * kCh * 4 + 16 * (lane >> 4);
   auto issue_u = [&](auto AB) {
     [[maybe_unused]] constexpr int ab = decltype(AB)::value;
+    if constexpr ((ABL & 2) != 0) return;
 #if __HIP_DEVICE_COMPILE__
-    if constexpr (UM == 1) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g)
-        ureg[ab % kUSlots][g] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ur, ureg_off, (ab * kUSlot + 16 * g) * 4, 0));
-      return;
-    }
     lds_f32* st = uring + (ab % kUSlots) * kUSlot;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + wave * 256), 16, uoff[0], ab * kUSlot * 4, 0, 0);
     lds_f32* st2 = wave + kWaves < kUPieces ? st + (wave + kWaves) * 256 : lds3 + kDummy;  // scalar select
@@ -190,6 +198,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   }
   auto load_x = [&](int u, int v) -> f32x2 {
     f32x2 d = {0.f, 0.f};
+    if constexpr ((ABL & 1) != 0) return f32x2{static_cast<float>(offv[v] + u), static_cast<float>(v)};
 #if __HIP_DEVICE_COMPILE__
     const int so = (kPh * u * a.rowf + 12 * v) * 4;
     d = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, rok[u] ? offv[v] : kOOB, so, 0));
@@ -248,29 +257,26 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 
   // Schedule (points p = 5a + b in order). At point p a wave: waits for U_p (its own DMA: vmcnt; every
   // wave's: the barrier, which also publishes V_a), issues U_{p+2} (two points of MFMAs cover its
-  // latency) and the X' row consumed at the end of point p + 1, runs point p's MFMAs and fold, then
-  // adds the X' row loaded at point p - 1 into t (V_{a+1}, row b). V_{a+1} is stored at the end of
-  // a-step a. vmcnt is in order, so the wait at point p leaves exactly the ops issued at point p - 1
-  // in flight (2 U ops per wave, then kN5 X' loads when that point loads a row).
-  f32x2 dq[2][kN5];  // X' rows in flight, by the parity of the point that loaded them
-  // prologue: U_0, U_1 in flight, V_0 built and stored (its loads waited here), X' for point 0
+  // latency) and a late X' row if one loads at p, runs point p's MFMAs and fold, then adds X' row b
+  // (resident) into t (V_{a+1}). V_{a+1} is stored at the end of a-step a. vmcnt is in order: the wait
+  // at point p leaves in flight exactly the ops issued after U_p (inflight below).
+  f32x2 xrow[kN5][kN5];  // X' rows of this thread's (tile, channel pair), each loaded once (see late_load_pt)
+  // prologue: U_0, U_1 in flight; the rows V_0 takes loaded (kept), V_0 built and stored
   issue_u(std::integral_constant<int, 0>{});
   issue_u(std::integral_constant<int, 1>{});
   t_zero();
   sfor<0, kN5>([&](auto Uc) {
     constexpr int u = decltype(Uc)::value;
-    if constexpr (w33::kBT[0][u] != 0.f) {
-      f32x2 d[kN5];
+    if constexpr (prologue_row(u))
 #pragma unroll
-      for (int v = 0; v < kN5; ++v) d[v] = load_x(u, v);
-      t_add(std::integral_constant<int, 0>{}, Uc, d);
-    }
+      for (int v = 0; v < kN5; ++v) xrow[u][v] = load_x(u, v);
+  });
+  sfor<0, kN5>([&](auto Uc) {
+    constexpr int u = decltype(Uc)::value;
+    if constexpr (prologue_row(u)) t_add(std::integral_constant<int, 0>{}, Uc, xrow[u]);
   });
   v_store(0);
   t_zero();
-  if constexpr (loads_at(-1))
-#pragma unroll
-    for (int v = 0; v < kN5; ++v) dq[1][v] = load_x(0, v);
 
   sfor<0, kN5>([&](auto Ac) {
     constexpr int av = decltype(Ac)::value;
@@ -279,21 +285,21 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
     for (int j = 0; j < 3; ++j) T[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     sfor<0, kN5>([&](auto Bc) {
       constexpr int b = decltype(Bc)::value, p = av * kN5 + b;
-      constexpr int inflight = (p + 1 < kPts ? 2 : 0) + (loads_at(p - 1) ? kN5 : 0);
-      if constexpr (UM == 0 || b == 0) {  // UM 1: only V_a needs publishing (and V_{a-1}'s readers done)
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (UM == 0)
-          lds_barrier<inflight>();
-        else
-          lds_barrier<>();
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("" ::: "memory");
-      }
+      // in flight past this barrier: the ops issued after U_p (at point p - 2: its X' row, if any; at
+      // point p - 1: U_{p+1} and its X' row): this wave's U_p has landed, X' rows finish on their own
+      constexpr int inflight = (p + 1 < kPts ? 2 : 0) + x_ops(p - 1) + x_ops(p - 2);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((ABL & 4) != 0)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(inflight) : "memory");
+      else
+        lds_barrier<inflight>();
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
       if constexpr (p + 2 < kPts) issue_u(std::integral_constant<int, p + 2>{});  // slot of point p - 1: free
-      if constexpr (loads_at(p)) {
-        constexpr int r = b + 1 < kN5 ? b + 1 : 0;  // the X' row consumed at the end of point p + 1
+      if constexpr (loads_at(p) >= 0) {
+        constexpr int r = loads_at(p);
 #pragma unroll
-        for (int v = 0; v < kN5; ++v) dq[p & 1][v] = load_x(r, v);
+        for (int v = 0; v < kN5; ++v) xrow[r][v] = load_x(r, v);
       }
       __builtin_amdgcn_sched_barrier(0);  // loads issued before the MFMAs
       const float* vp = vb + b * kTiles * kVS + a_off;
@@ -302,26 +308,26 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
         const f32x4 af = *reinterpret_cast<const f32x4*>(vp + 16 * g);
-        f32x4 bf;
-        if constexpr (UM == 1)
-          bf = ureg[p % kUSlots][g];
-        else
-          bf = *reinterpret_cast<const f32x4*>(up + b_off[g]);
+        const f32x4 bf = *reinterpret_cast<const f32x4*>(up + b_off[g]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[i], acc, 0, 0, 0);
       }
       // fold, first half: T[j] += A^T[j][b] M_ab (compile-time coefficients; zero ones skipped)
+      if constexpr ((ABL & 16) != 0) asm volatile("" ::"v"(acc));
       sfor<0, 3>([&](auto Jc) {
         constexpr int j = decltype(Jc)::value;
         constexpr float c = w33::kAT[j][b];
-        if constexpr (c != 0.f)
+        if constexpr (c != 0.f && (ABL & 16) == 0)
 #pragma unroll
           for (int i = 0; i < 4; ++i) T[j][i] = __builtin_fmaf(c, acc[i], T[j][i]);  // scalar v_fma_f32
       });
       // pinned here (the empty asm takes t and T as operands: the DAG scheduler had sunk the adds to the
       // a-step's end, where their in-order vmcnt also waited for the U DMA just issued)
-      if constexpr (needs_row(av + 1, b)) {
-        t_add(std::integral_constant<int, av + 1>{}, Bc, dq[(p + 1) & 1]);
+      if constexpr (needs_row(av + 1, b) && (ABL & 8) != 0) {
+#pragma unroll
+        for (int v = 0; v < kN5; ++v) asm volatile("" ::"v"(xrow[b][v]));
+      } else if constexpr (needs_row(av + 1, b)) {
+        t_add(std::integral_constant<int, av + 1>{}, Bc, xrow[b]);
 #pragma unroll
         for (int v = 0; v < kN5; ++v) asm volatile("" : "+v"(t[v]));
       }
@@ -338,7 +344,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 #pragma unroll
         for (int q = 0; q < 9; ++q) asm volatile("" : "+v"(Y[q]));
       }
-      if constexpr (b == kN5 - 1 && av + 1 < kN5) {
+      if constexpr (b == kN5 - 1 && av + 1 < kN5 && (ABL & 8) == 0) {
         // V_{a+1} into the other buffer (last read in a-step a - 1, before this a-step's first barrier);
         // published by the barrier of point (a + 1, 0)
         v_store((av + 1) & 1);
@@ -403,10 +409,13 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
     if (desc >= 0) plist[1 + atomicAdd(&plist[0], 1)] = desc;
     __syncthreads();
     const int nlist = plist[0];
-    for (int it = tid; it < nlist * (kK / 4); it += kNT) {
-      const int d = plist[1 + it / (kK / 4)], fq = it % (kK / 4);
+    // per listed pixel, once: the LDS offsets of its window pixels this workgroup owns, its destination
+    using i32x4 = __attribute__((ext_vector_type(4))) int;
+    int* ent = reinterpret_cast<int*>(lds + kPoolOffs);
+    for (int k = tid; k < nlist; k += kNT) {
+      const int d = plist[1 + k];
       const int up = d & 1, px = (d >> 1) & 31, py = (d >> 6) & 31, n = d >> 11;
-      f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      int e[kPoolEnt];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int y = 2 * py + i, tyy = y / 3, ry = y - 3 * tyy;
@@ -414,18 +423,34 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         for (int j = 0; j < 3; ++j) {
           const int x = 2 * px + j, txx = x / 3, rx = x - 3 * txx;
           const int lt = n * ipt + tyy * a.tx + txx - p0;
-          if (static_cast<unsigned>(lt) < static_cast<unsigned>(kTiles)) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(tr + ((ry * 3 + rx) * kTiles + lt) * kOS + 4 * fq);
-            m = f32x4{fmaxf(m.x, v.x), fmaxf(m.y, v.y), fmaxf(m.z, v.z), fmaxf(m.w, v.w)};
-          }
+          e[i * 3 + j] = static_cast<unsigned>(lt) < static_cast<unsigned>(kTiles) ? ((ry * 3 + rx) * kTiles + lt) * kOS : -1;
         }
       }
-      float* dst = up ? a.p1 + (static_cast<size_t>(n * a.Hp + py) * a.Wp + px) * kK + 4 * fq
-                      : o.base + (static_cast<size_t>(n * o.Hb + py + o.h_off) * o.Wb + px + o.w_off) * o.Cb + o.c_off +
-                            4 * fq;
+      e[9] = up ? ((n * a.Hp + py) * a.Wp + px) * kK : ((n * o.Hb + py + o.h_off) * o.Wb + px + o.w_off) * o.Cb + o.c_off;
+      e[10] = up;
+      e[11] = 0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        *reinterpret_cast<i32x4*>(ent + k * kPoolEnt + 4 * q) = i32x4{e[4 * q], e[4 * q + 1], e[4 * q + 2], e[4 * q + 3]};
+    }
+    __syncthreads();
+    for (int it = tid; it < ((ABL & 32) != 0 ? 0 : nlist) * (kK / 4); it += kNT) {
+      const int k = it / (kK / 4), fq = it - k * (kK / 4);
+      const i32x4 e0 = *reinterpret_cast<const i32x4*>(ent + k * kPoolEnt);
+      const i32x4 e1 = *reinterpret_cast<const i32x4*>(ent + k * kPoolEnt + 4);
+      const i32x4 e2 = *reinterpret_cast<const i32x4*>(ent + k * kPoolEnt + 8);
+      const int off[9] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x};
+      f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+        if (off[i] >= 0) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(tr + off[i] + 4 * fq);
+          m = f32x4{fmaxf(m.x, v.x), fmaxf(m.y, v.y), fmaxf(m.z, v.z), fmaxf(m.w, v.w)};
+        }
+      float* dst = (e2.z ? a.p1 : o.base) + static_cast<size_t>(static_cast<unsigned>(e2.y)) + 4 * fq;
       *reinterpret_cast<f32x4*>(dst) = m;
     }
-  } else if constexpr (UM == 0) {
+  } else {
     // all nine output positions' images at once (9 x 32 x 100 floats = 115 KB of the 128 KB): one
     // barrier and nine back-to-back stores per thread instead of a write / barrier / store / barrier
     // round per position. The images reach into the U ring's slots, so no DMA may still be landing.
@@ -447,23 +472,6 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(sn * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
                                   o.c_off + 4 * sq) = *reinterpret_cast<const f32x4*>(tr + (q * kTiles + st) * kOS + 4 * sq);
     }
-  } else {  // UM 1 launches with 2 V buffers of LDS only: one position image (12.8 KB) at a time
-    __syncthreads();  // every wave's last fragment reads are done: the LDS is scratch now
-#pragma unroll
-    for (int q = 0; q < 9; ++q) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float v = Y[q][i] + bv;
-        if (a.relu) v = fmaxf(v, 0.f);
-        tr[(wm * 16 + 4 * h4 + i) * kOS + f] = v;
-      }
-      __syncthreads();
-      const int oy = sti * 3 + q / 3, ox = stj * 3 + q % 3;
-      if (sp < a.P && oy < a.Ho && ox < a.Wo)
-        *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(sn * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) * o.Cb +
-                                  o.c_off + 4 * sq) = *reinterpret_cast<const f32x4*>(tr + st * kOS + 4 * sq);
-      __syncthreads();
-    }
   }
 }
 
@@ -476,11 +484,10 @@ bool conv1_fused_eligible(const Conv1WinoPlan& w, const OutView& out) {
 
 namespace {
 hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out,
-                              bool relu, hipStream_t s, int mode, float* p1, int Hp, int Wp) {
+                              bool relu, hipStream_t s, float* p1, int Hp, int Wp) {
   static const hipError_t attr = [] {
-    for (const void* k : {reinterpret_cast<const void*>(conv1_fused_kernel<0, false>),
-                          reinterpret_cast<const void*>(conv1_fused_kernel<1, false>),
-                          reinterpret_cast<const void*>(conv1_fused_kernel<0, true>)}) {
+    for (const void* k : {reinterpret_cast<const void*>(conv1_fused_kernel<false>),
+                          reinterpret_cast<const void*>(conv1_fused_kernel<true>)}) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -508,34 +515,61 @@ hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const floa
   a.Hp = Hp;
   a.Wp = Wp;
   const unsigned grid = static_cast<unsigned>(a.per_xcd * 8);
+#ifdef ANX_CONV1_ABL  // cost-probe builds only (CMake ANX_CONV1_ABL=ON): ANX_CONV1_ABL=<bits> picks the probe
+  static const int abl = [] {
+    const char* e = std::getenv("ANX_CONV1_ABL");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (p1 != nullptr && abl != 0) {
+    auto go = [&](auto K) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(K), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      K<<<grid, kNT, kLds, s>>>(a);
+    };
+    switch (abl) {
+      case 1: go(conv1_fused_kernel<true, 1>); break;
+      case 2: go(conv1_fused_kernel<true, 2>); break;
+      case 3: go(conv1_fused_kernel<true, 3>); break;
+      case 4: go(conv1_fused_kernel<true, 4>); break;
+      case 8: go(conv1_fused_kernel<true, 8>); break;
+      case 16: go(conv1_fused_kernel<true, 16>); break;
+      case 24: go(conv1_fused_kernel<true, 24>); break;
+      case 32: go(conv1_fused_kernel<true, 32>); break;
+      case 7: go(conv1_fused_kernel<true, 7>); break;
+      case 63: go(conv1_fused_kernel<true, 63>); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+#endif
   if (p1 != nullptr)
-    conv1_fused_kernel<0, true><<<grid, kNT, kLds, s>>>(a);
-  else if (mode == 2)
-    conv1_fused_kernel<1, false><<<grid, kNT, 2 * kVBuf * sizeof(float), s>>>(a);
+    conv1_fused_kernel<true><<<grid, kNT, kLds, s>>>(a);
   else
-    conv1_fused_kernel<0, false><<<grid, kNT, kLds, s>>>(a);
+    conv1_fused_kernel<false><<<grid, kNT, kLds, s>>>(a);
   return hipGetLastError();
 }
 }  // namespace
 
 hipError_t conv1_fused(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out, bool relu,
-                       hipStream_t s, int mode) {
+                       hipStream_t s) {
   if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
   if (!conv1_fused_eligible(w, out)) return hipErrorInvalidValue;
-  return conv1_fused_launch(w, x, U, bias, out, relu, s, mode, nullptr, 0, 0);
+  return conv1_fused_launch(w, x, U, bias, out, relu, s, nullptr, 0, 0);
 }
 
 bool conv1_fused_pool_eligible(const Conv1WinoPlan& w, const OutView& window, int Hp, int Wp) {
   // pooled pixels are decoded from 5 + 5 bits; a window's tiles within kPoolBack raster indices
+  // element offsets of both destinations are 32-bit in the epilogue's per-pixel table
   return conv1_fused_eligible(w, window) && w.tx + 1 <= kPoolBack && Hp > 0 && Wp > 0 && Hp <= 32 && Wp <= 32 &&
-         2 * Hp + 1 <= w.H1 && 2 * Wp + 1 <= w.W1 && w.N < (1 << 20);
+         2 * Hp + 1 <= w.H1 && 2 * Wp + 1 <= w.W1 && w.N < (1 << 20) &&
+         static_cast<long>(w.N) * window.Hb * window.Wb * window.Cb < (1L << 31) &&
+         static_cast<long>(w.N) * Hp * Wp * kK < (1L << 31);
 }
 
 hipError_t conv1_fused_pool(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView window,
                             float* p1, int Hp, int Wp, bool relu, hipStream_t s) {
   if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
   if (p1 == nullptr || !conv1_fused_pool_eligible(w, window, Hp, Wp)) return hipErrorInvalidValue;
-  return conv1_fused_launch(w, x, U, bias, window, relu, s, 1, p1, Hp, Wp);
+  return conv1_fused_launch(w, x, U, bias, window, relu, s, p1, Hp, Wp);
 }
 
 }  // namespace anx::hip

@@ -248,7 +248,7 @@ void conv1_wino_weights_host(int K, int F, const float* w_kcff, std::vector<floa
 hipError_t conv1_wino(const Conv1WinoPlan& w, const float* x, float* V, const float* U, const float* bias, OutView out,
                       bool relu, hipStream_t s, const Knobs& kn) {
   if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
-  if (kn.conv1_fused && conv1_fused_eligible(w, out)) return conv1_fused(w, x, U, bias, out, relu, s, kn.conv1_fused);
+  if (kn.conv1_fused && conv1_fused_eligible(w, out)) return conv1_fused(w, x, U, bias, out, relu, s);
   if (w.K % kBN || static_cast<long>(w.P) * kPts * kCh >= (1L << 31) || static_cast<long>(w.P) * 12 >= (1L << 31) ||
       out.Cb % 4 || out.c_off % 4)  // 16-B epilogue stores
     return hipErrorInvalidValue;

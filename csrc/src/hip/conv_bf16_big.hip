@@ -506,123 +506,8 @@ constexpr BigCfg kCfg[] = {{256, 256, 512, 2, 1, 1.0f},  {256, 128, 512, 2, 1, 0
                            {64, 96, 256, 2, 3, 0.6f},      // 15: 64x96, 3 workgroups/CU
                            {192, 256, 512, 0, 1, 1.0f}};   // 16: ping-pong 192x256 (conv5: one round of 226 tiles)
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
-// ---- FC layers (M = batch rows of K contiguous bf16, 1x1): activations straight to VGPRs ----
-// The 256x64 LDS-DMA config (cfg 8) ran FC7 at 23 us for 164 MB of operand traffic: one workgroup
-// per CU with one or two 40 KiB stages in flight is latency-bound (Little's law: ~28 GB/s per CU).
-// Here each wave's 32 activation rows (used by that wave only) load global -> VGPR D K tiles ahead
-// (16 B per lane per 16-row block and k-step: the MFMA operand layout itself), and only the 64
-// weight rows every wave shares go through LDS, in a D+1-stage LDS-DMA ring of 8 KiB stages (same
-// source-side chunk swizzle as above). In flight per CU: 8 waves x 4 KiB x D + D x 8 KiB.
-// Output: fp32 split-K slabs [gridDim.y][M][N] (splitk_reduce_bf16 adds bias / ReLU).
-struct ArgsFc {
-  const bf16* x;  // [M][K] (row stride K = kpad)
-  const bf16* w;  // tile-blocked [n_tiles][ktiles][64][64] (pack_fc_blocked_bf16)
-  float* ws;
-  int M, N, kpad, ktiles, n_tiles, kt_per;
-};
-
-template <int D>
-__global__ void __launch_bounds__(512) fc_bf16_kernel(ArgsFc a) {
-  constexpr int BN = 64, NSB = D + 1, SB = BN * kBK;  // bf16 per weight stage
-  constexpr int VM = 5;                               // vm ops per lane per K tile: 4 A loads + 1 DMA
-  extern __shared__ __attribute__((aligned(16))) bf16 lds_b[];
-  lds_b16* lds3 = (lds_b16*)(lds_b);
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA M0 values stay scalar
-  // XCD-aware bijective remap over (K slice, tile), K-slice-major: each XCD walks a contiguous run,
-  // so it streams one or two K slices of the activations (L2-resident) instead of all of them.
-  int w;
-  {
-    const int nwg = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x, xcd = b & 7, q = nwg >> 3,
-              r = nwg & 7;
-    w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-  }
-  const int ksl = w / gridDim.x, tl = w - ksl * gridDim.x;
-  const int nt = tl % a.n_tiles, mt = tl / a.n_tiles;
-  const int m0 = mt * 256 + wave * 32, n0 = nt * BN;
-  const int kt0 = ksl * a.kt_per, total = a.kt_per;
-  const int u = (tid & 7) ^ ((tid >> 4) & 7);  // DMA unit tid: row tid >> 3, logical chunk u
-  // weight tile (nt, kt) is 8 KiB contiguous: one sequential stream per workgroup
-  const bf16* bsrc = a.w + (static_cast<size_t>(nt * a.ktiles + kt0) * BN + (tid >> 3)) * kBK + u * 8;
-  const int hq = lane >> 4, sw = (lane >> 1) & 7;
-  const bf16* asrc[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-    asrc[i] = a.x + static_cast<size_t>(min(m0 + i * 16 + (lane & 15), a.M - 1)) * a.kpad + kt0 * kBK + hq * 8;
-  bf16x8 av[D][2][2];
-  auto issue = [&](int r, int slot, int st) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) av[slot][i][h] = *reinterpret_cast<const bf16x8*>(asrc[i] + r * kBK + h * 32);
-    glds16(bsrc + r * SB, lds3 + st * SB + wave * 512);
-    __builtin_amdgcn_sched_barrier(0);  // issue order = program order on every path
-  };
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // Straight-line issue pattern (the compiler's own vmcnt for the register ring is then exact on
-  // every path: a conditional refill made it merge to vmcnt(0) once per ring turn): prologue tiles
-  // 0..D-1, the main loop refills every tile it retires, the last D tiles only drain.
-#pragma unroll
-  for (int r = 0; r < D; ++r) issue(r, r, r);  // total >= D (host)
-  const int brow = (lane & 15) * kBK;
-  auto tile = [&](int s, int st) {  // MFMAs of the tile in register slot s / LDS stage st
-    lds_barrier<>();  // every lane's weight DMA of the tile (the caller's vmcnt); every wave past the previous one
-    asm volatile("" ::: "memory");
-    const bf16* base = lds_b + st * SB;
-    bf16x8 b0[4], b1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      b0[j] = *reinterpret_cast<const bf16x8*>(base + brow + j * 16 * kBK + (hq ^ sw) * 8);
-      b1[j] = *reinterpret_cast<const bf16x8*>(base + brow + j * 16 * kBK + ((4 + hq) ^ sw) * 8);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], av[s][i][0], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], av[s][i][1], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  int st = 0;  // LDS stage of the tile being multiplied
-  for (int r0 = 0; r0 < total - D; r0 += D) {  // total % D == 0 (host)
-#pragma unroll
-    for (int s = 0; s < D; ++s) {
-      wait_vm<VM * (D - 1)>();  // this lane's tile r0+s landed (D-1 later tiles may fly)
-      tile(s, st);
-      // refill: tile r0+s+D into this register slot and the stage of tile r0+s-1 (all waves are past it)
-      issue(r0 + s + D, s, st == 0 ? NSB - 1 : st - 1);
-      st = st + 1 == NSB ? 0 : st + 1;
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < D; ++s) {
-    if (s == 0) wait_vm<VM * (D - 1)>();
-    if (s == 1) wait_vm<VM * (D - 2)>();
-    if (s == 2) wait_vm<VM * (D > 2 ? D - 3 : 0)>();
-    if (s >= 3) wait_vm<0>();
-    tile(s, st);
-    st = st + 1 == NSB ? 0 : st + 1;
-  }
-  // weights as the MFMA A operand: lane holds batch row m0 + 16 i + (lane & 15), 4 consecutive outputs
-  float* ws = a.ws + static_cast<size_t>(ksl) * a.M * a.N;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int f = n0 + j * 16 + hq * 4;
-    if (f >= a.N) continue;  // N % 4 == 0
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = m0 + i * 16 + (lane & 15);
-      if (m < a.M) *reinterpret_cast<f32x4*>(ws + static_cast<size_t>(m) * a.N + f) = acc[i][j];
-    }
-  }
-}
-constexpr int kFcDepth = 4;
+// (Round 5: the activation-streaming FC kernel, activations global -> VGPR four K tiles ahead, was
+// removed: slower than the wide-tile split-K FC at every layer, profiles/r02_bf16bench_fc_b256.txt.)
 
 
 size_t lds_bytes(const BigCfg& c) {
@@ -787,56 +672,6 @@ hipError_t conv2d_bf16_big(const ConvPlanB& p, int cfg, const void* x, const voi
       return hipErrorInvalidValue;
   }
 #undef ANX_BIG_CFGS
-  return hipGetLastError();
-}
-
-bool fc_bf16_ok(const ConvPlanB& p) {
-  return p.Hp == 1 && p.Wp == 1 && p.F == 1 && p.groups == 1 && p.C % kBK == 0 && p.kpad == p.C && p.Kg % 4 == 0 &&
-         p.kpad_n >= 1 && static_cast<long>(p.N) * p.C < (1L << 31);
-}
-
-// K split: the largest ks with tiles x ks <= one workgroup per CU, ks | K tiles and a multiple of
-// the register ring's depth D per slice (measured per layer: profiles/r02_bf16bench_fc_b256.txt).
-int pick_fc_split(const ConvPlanB& p, int cus) {  // slices of >= kFcDepth tiles
-  const long tiles = static_cast<long>((p.N + 255) / 256) * ((p.Kg + 63) / 64);
-  const int ktiles = p.kpad / kBK;
-  int best = 0;
-  for (int ks = 1; ks <= ktiles; ++ks)
-    if (ktiles % ks == 0 && (ktiles / ks) % kFcDepth == 0 && (best == 0 || tiles * ks <= cus)) best = ks;
-  return best;
-}
-
-void pack_fc_blocked_bf16(const ConvPlanB& p, const std::vector<uint16_t>& pk, std::vector<uint16_t>& out) {
-  const int nt = (p.Kg + 63) / 64, kt = p.kpad / kBK;
-  out.assign(static_cast<size_t>(nt) * kt * 64 * kBK, 0);
-  for (int t = 0; t < nt; ++t)
-    for (int k = 0; k < kt; ++k)
-      for (int r = 0; r < 64; ++r) {
-        const int n = t * 64 + r;
-        if (n >= p.kpad_n) continue;
-        std::copy_n(pk.begin() + static_cast<size_t>(n) * p.kpad + k * kBK, kBK,
-                    out.begin() + ((static_cast<size_t>(t) * kt + k) * 64 + r) * kBK);
-      }
-}
-
-hipError_t fc_bf16(const ConvPlanB& p, const void* x, const void* wblocked, float* ws, int ksplit, hipStream_t s) {
-  const int ktiles = p.kpad / kBK;
-  if (!fc_bf16_ok(p) || ksplit < 1 || ktiles % ksplit || (ktiles / ksplit) % kFcDepth || !ws)
-    return hipErrorInvalidValue;
-  if (p.N == 0) return hipSuccess;
-  ArgsFc a{};
-  a.x = static_cast<const bf16*>(x);
-  a.w = static_cast<const bf16*>(wblocked);
-  a.ws = ws;
-  a.M = p.N;
-  a.N = p.Kg;
-  a.kpad = p.kpad;
-  a.ktiles = ktiles;
-  a.n_tiles = (p.Kg + 63) / 64;
-  a.kt_per = ktiles / ksplit;
-  const dim3 grid(static_cast<unsigned>((p.N + 255) / 256 * a.n_tiles), ksplit);
-  constexpr size_t lds = static_cast<size_t>(kFcDepth + 1) * 64 * kBK * 2;
-  fc_bf16_kernel<kFcDepth><<<grid, 512, lds, s>>>(a);
   return hipGetLastError();
 }
 

@@ -91,18 +91,11 @@ int main(int argc, char** argv) {
     ck(hipMemcpy(dx, hx.data(), nx * 2, hipMemcpyHostToDevice), "H2D");
     ck(hipMemcpy(dw, pk.data(), pk.size() * 2, hipMemcpyHostToDevice), "H2D");
     ck(hipMemcpy(dko, ko.data(), ko.size() * 4, hipMemcpyHostToDevice), "H2D");
-    if (hip::fc_bf16_ok(p)) {
-      std::vector<uint16_t> bl;
-      hip::pack_fc_blocked_bf16(p, pk, bl);
-      ck(hipMalloc(&dwb, bl.size() * 2), "malloc");
-      ck(hipMemcpy(dwb, bl.data(), bl.size() * 2, hipMemcpyHostToDevice), "H2D");
-    }
     ck(hipMemcpy(db, hb.data(), L.K * 4, hipMemcpyHostToDevice), "H2D");
     const hip::OutViewB o0{static_cast<__bf16*>(dy0), p.Ho, p.Wo, L.K, 0, 0, 0};
     const hip::OutViewB o1{static_cast<__bf16*>(dy1), p.Ho, p.Wo, L.K, 0, 0, 0};
     // arms: -2 register-staged 128x128 (unsplit), -1 LDS-DMA ring 128x128 (the legacy FC split-K),
-    // c = wide-tile config c; FC layers: 100*ks + c = config c with K split ks ways (+ reduce),
-    // 10000 + ks = the activation-streaming FC kernel (fc_bf16) split ks ways (+ reduce)
+    // c = wide-tile config c; FC layers: 100*ks + c = config c with K split ks ways (+ reduce)
     const bool fc = L.Hp == 1;
     std::vector<int> arms = {-2, -1};
     for (int c = 0; c < hip::conv_bf16_big_cfgs(); ++c) {
@@ -114,9 +107,6 @@ int main(int argc, char** argv) {
       for (int ks : {1, 2, 4, 8, 16})
         if (ks * 4 <= p.kpad / 64 && ks > 1 && (c == 1 || c == 3 || c >= 5)) arms.push_back(100 * ks + c);
     }
-    if (fc && hip::fc_bf16_ok(p))
-      for (int ks : {1, 2, 3, 4, 6, 8, 16})
-        if ((p.kpad / 64) % ks == 0 && (p.kpad / 64 / ks) % 4 == 0) arms.push_back(10000 + ks);
     float* dws = nullptr;
     if (fc) ck(hipMalloc(&dws, static_cast<size_t>(16) * N * L.K * 4), "malloc ws");
     const int ks_legacy = hip::fc_split_k(p);
@@ -130,9 +120,6 @@ int main(int argc, char** argv) {
         } else {
           ck(hip::conv2d_bf16(p, dx, dw, dko, db, o1, nullptr, true, s, {}, 2), "conv2d_bf16 glds");
         }
-      } else if (arm >= 10000) {
-        ck(hip::fc_bf16(p, dx, dwb, dws, arm - 10000, s), "fc_bf16");
-        ck(hip::splitk_reduce_bf16(dws, arm - 10000, N, L.K, db, true, o1, nullptr, s), "reduce");
       } else if (arm >= 100) {
         const int ks = arm / 100, c = arm % 100;
         ck(hip::conv2d_bf16_big(p, c, dx, dw, dko, db, o1, true, s, hip::SplitK{ks, dws}), "big split");
@@ -143,8 +130,8 @@ int main(int argc, char** argv) {
     };
     if (fc) {
       const hip::BigFc f = hip::pick_bf16_big_fc(p);
-      std::printf("%s: legacy ksplit %d, picker cfg %d ksplit %d (arm %d), streaming FC arm %d\n", L.name, ks_legacy,
-                  f.cfg, f.ksplit, 100 * f.ksplit + f.cfg, 10000 + hip::pick_fc_split(p));
+      std::printf("%s: legacy ksplit %d, picker cfg %d ksplit %d (arm %d)\n", L.name, ks_legacy, f.cfg, f.ksplit,
+                  100 * f.ksplit + f.cfg);
     }
     std::vector<uint16_t> y0(ny), y1(ny);
     run(-2);

@@ -11,7 +11,7 @@ Names and values:
   ``direct``.
 * integer knobs: ``chunk1``, ``chunk2`` (images per launch), ``conv1_occ``, ``conv2_occ`` (Winograd
   GEMM workgroups-per-CU caps), ``force_vec4``, ``force_scalar`` (direct GEMM tiles), and the bf16
-  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc``, ``bf16_fc_cfg``,
+  full model's ``bf16_glds``, ``bf16_big``, ``bf16_lrn_tile``, ``bf16_fc_cfg``,
   ``bf16_fc_minkt``, ``bf16_conv1`` (2, the default: Conv1 as the persistent row-band kernel reading
   the fp32 image; 1: the same kernel on the s2d4 polyphase copy; 0: s2d4 + the implicit-GEMM tiles),
   ``bf16_pool1`` (1, the default: pool1 in the row-band kernel's epilogue when each image has its own
@@ -35,7 +35,7 @@ from .. import _native as nat
 
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
-         "bf16_lrn_tile", "bf16_fc", "bf16_conv1", "bf16_pool1", "bf16_fc_cfg", "bf16_fc_minkt", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
+         "bf16_lrn_tile", "bf16_conv1", "bf16_pool1", "bf16_fc_cfg", "bf16_fc_minkt", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
          "conv1_fused", "conv1_pool")
 
 

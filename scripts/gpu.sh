@@ -112,6 +112,15 @@ for s in "$@"; do
           fi
         done
       done ;;
+    c1abl)  # conv1_fused cost probes (build_abl: cmake -DANX_CONV1_ABL=ON -DANX_OUTPUT_ROOT=ab_abl), one lane
+      for abl in ${C1ABL:-0 1 2 4 8 16 24 32 7 63}; do
+        echo "== c1abl $abl"
+        ANX_LIB=ab_abl/lib/libanx.so ANX_CONV1_ABL=$abl timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv \
+          -d "$O/c1abl_$abl" -o run -- python3 bench.py --lanes 1 --steps 8 --warmup 2 --no-b1 --no-full --prewarm-s 0.5 \
+          > "$O/c1abl_$abl.log" 2>&1 || { echo "== c1abl FAILED"; exit 1; }
+        python3 tools/rocprof_summary.py "$(ls "$O"/c1abl_$abl/*kernel_trace.csv | head -1)" | grep -E "conv1_fused|gemm_kernel" \
+          | cut -c1-200 | tee -a "$O/c1abl.md"
+      done ;;
     bytes)
       BYARGS="--lanes 1 --steps 6 --warmup 2 --no-b1 --no-full --prewarm-s 0 $BARGS"
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --kernel-trace \
