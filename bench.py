@@ -370,28 +370,21 @@ def main():
                           decomp=a.decomp, chunks=a.chunks, impl=a.impl)
             wl.fill((torch.rand((GB, d.H, d.W, d.C0), generator=torch.Generator().manual_seed(1234)) * 0.1)
                     if rank == 0 else None)
-        elif a.workload == "v5" and cuda:
-            # the native V5 runtime: plan, buffers, streams and transport live in C++ (anx/v5.hpp)
+        else:
+            # the native V5 runtime: plan, buffers, streams and transport live in C++ (anx/v5.hpp). CPU
+            # ranks run the same runtime in host mode (host engine + host transport); V4 on CPU is its
+            # overlap-tile layer with the batch scattered from the root each step.
             from anx.parallel.workloads import NativeV5
             from anx.utils.init import init_weights
             b1, b2 = anx.config.blocks()
+            kw = dict(transport=a.transport, pipeline=a.pipeline, impl=a.impl, input_source=a.input_source,
+                      lanes=a.lanes)
+            if not cuda:
+                kw = dict(impl="host", input_source="root" if a.workload == "v4" else a.input_source,
+                          layer="overlap" if a.workload == "v4" else "per_layer")
             wl = NativeV5(GB, init_weights("rand", 1234, b1, b2) if rank == 0 else None, specs=(b1, b2),
-                          decomp=a.decomp, transport=a.transport, chunks=a.chunks, pipeline=a.pipeline, impl=a.impl,
-                          input_source=a.input_source, lanes=a.lanes)
+                          decomp=a.decomp, chunks=a.chunks, **kw)
             wl.fill((torch.rand((GB, d.H, d.W, d.C0), device=dev, generator=g) * 0.1) if rank == 0 else None)
-        else:
-            from anx.parallel.plan import make_hybrid_plan, pick_row_ways
-            from anx.parallel.workloads import RowsWorkload
-            if a.decomp == "auto":
-                a.decomp = {world: "rows", 1: "batch"}.get(pick_row_ways(world, GB, a.workload, "root"), "rows")
-            # every rank holds an engine sized for the largest share any rank gets
-            rw = {"rows": world, "hybrid": 0, "batch": 1}[a.decomp]
-            hp = make_hybrid_plan(227, 227, world, GB, rw)
-            cap = max(1, max(hp.images_of(q).size for q in range(world)))
-            model = AlexNetBlocks(init="rand", seed=1234, device=dev, impl=a.impl, max_batch=cap, lanes=a.lanes)
-            wl = RowsWorkload(model, GB, a.workload, a.decomp, device=dev)
-            if rank == 0:
-                wl.fill(torch.rand((GB, d.H, d.W, d.C0), device=dev, generator=g) * 0.1)
         step = wl.step
         B = GB  # images per step (whole job)
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
@@ -569,13 +562,16 @@ def main():
             pipeline = ("shared pinned host segment -> per-rank chunked H2D over its own link -> overlap tiles "
                         "-> per-rank D2H into the segment (host-staged, no device collectives)"
                         if a.workload == "v4" and cuda else
-                        "root host -> gloo scatter -> overlap tiles -> gloo gather (CPU rehearsal)"
-                        if a.workload == "v4" else
+                        ("native V5 runtime in host mode (CPU rehearsal: host engine, host transport over the "
+                         "runtime's own TCP channel): " + ("root scatter every step -> overlap tiles -> gather"
+                                                           if a.workload == "v4" else
+                                                           "stage1 -> pool1 halo chunks -> stage2 -> gather"))
+                        if not cuda else
                         ("device-resident input (placed once) -> " if a.input_source == "local" else
                          "root device -> scatter (every step) -> ") +
                         "stage1 (chunks) -> pool1 halo chunks -> stage2 (halo-free ranks: free-running lanes) -> "
                         "gather (native V5 runtime; gather on a second stream under the next step)")
-            extra = {**wl.describe(), "decomp": a.decomp, "phases_ms": phases}
+            extra = {**wl.describe(), "workload": a.workload, "decomp": a.decomp, "phases_ms": phases}
             if a.workload == "v4" and cuda:
                 gbps = wl.probe_h2d_gbps()
                 per_img = extra["h2d_bytes_per_step_rank"] / max(1, -(-GB // world))

@@ -122,6 +122,11 @@ class Transport {
 // `c` may be null for a record-only transport (no collective is issued then). loopback: over the
 // loopback DeviceComm (ranks sharing one GPU) instead of an RCCL communicator; name "rccl-loopback".
 std::unique_ptr<Transport> make_rccl_transport(HostComm* c, int device, int rank, bool loopback = false);
+// Host buffers on CPU ranks: the same transfer lists moved by HostComm's grouped point-to-point (TCP;
+// strided blocks packed / unpacked through staging), local blocks by memcpy. Blocking: run_phase
+// returns with the phase complete. Name "host". The V5 runtime's CPU mode (V5Options::host) runs on
+// it, which is how the CPU multi-rank tests rehearse the schedule the GPU transports execute.
+std::unique_ptr<Transport> make_host_transport(HostComm* c, int rank);
 // Peer ordering: "flags" (default where the device supports hipStreamWaitValue32) = the sender's
 // stream writes a sequence number into the receiver's IPC-mapped flag word after its pushes and the
 // receiver's stream waits for it on the device (no host involvement per phase); "notes" = IPC

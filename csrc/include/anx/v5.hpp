@@ -55,6 +55,10 @@ struct V5Options {
   std::string cost;                // cost-model overrides for the row-split pick ("name=value;...")
   Impl impl = Impl::Mfma;
   Knobs knobs = default_knobs();
+  // CPU ranks (no HIP call at all): the host engine (CpuBlocks) and the host transport (HostComm
+  // point-to-point) execute the same layout, schedule and phase order, serially per step; transport,
+  // lanes, pipeline and poison do not apply. What the CPU multi-rank tests and bench.py --device cpu run.
+  bool host = false;
 };
 
 // Decomposition quality of a plan: output rows per rank (max / mean, 1.0 = balanced) and the conv1
@@ -131,7 +135,9 @@ class V5Runtime {
 
  private:
   struct Impl_;
+  struct HostImpl_;
   std::unique_ptr<Impl_> p_;
+  std::unique_ptr<HostImpl_> h_;  // V5Options::host
   V5Layout lay_;
   bool pipeline_ = false;
 };

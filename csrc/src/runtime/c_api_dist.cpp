@@ -132,7 +132,8 @@ int anx_v5_create(void** out, int rank, int world, int local_rank, int local_wor
     o.keep_log = keep_log != 0;
     o.pipeline = pipeline;
     o.poison = poison != 0;
-    o.impl = impl ? anx::Impl::Direct : anx::Impl::Mfma;
+    o.impl = impl == 1 ? anx::Impl::Direct : anx::Impl::Mfma;
+    o.host = impl == 2;  // CPU ranks: the host engine and the host transport, no HIP call
     o.peer_sync = peer_sync ? peer_sync : "";
     const anx::BlockSpec s1 = spec(*b1), s2 = spec(*b2);
     const anx::HostWeights w = root_weights(rank, s1, s2, w1, bias1, w2, bias2);

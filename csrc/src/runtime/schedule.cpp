@@ -462,7 +462,58 @@ struct PeerTransport : DeviceBase {
   }
 };
 
+// ---------------------------------------------------------------------------------------- host
+struct HostTransport : Transport {
+  HostComm* hc_;
+  int rank_;
+  void* buf_[2][kB] = {};
+  std::map<std::pair<int, int>, std::vector<char>> stage_;  // (phase, transfer index) -> packed bytes
+  HostTransport(HostComm* c, int rank) : hc_(c), rank_(rank) {}
+  const char* name() const override { return "host"; }
+  const char* ordering() const override { return "blocking"; }
+  char* at(int par, const Region& r) const { return static_cast<char*>(buf_[par][static_cast<int>(r.buf)]) + r.off; }
+  static void copy2d(char* dst, size_t dpitch, const char* src, size_t spitch, size_t w, size_t h) {
+    for (size_t i = 0; i < h; ++i) std::memcpy(dst + i * dpitch, src + i * spitch, w);
+  }
+  void bind(const Schedule&, void* const bufs[2][kB], hipStream_t) override {
+    for (int p = 0; p < 2; ++p)
+      for (int b = 0; b < kB; ++b) buf_[p][b] = bufs[p][b];
+  }
+  void bcast(void* buf, size_t bytes, int root) override {
+    if (!record_only && hc_ && hc_->size() > 1) hc_->bcast(buf, bytes, root);
+  }
+  void run_phase(Phase ph, const std::vector<Transfer>& xs, hipStream_t, int par) override {
+    std::vector<std::pair<const Transfer*, std::vector<char>*>> unpack;
+    for (size_t i = 0; i < xs.size(); ++i) {
+      const Transfer& x = xs[i];
+      if (x.src != rank_ && x.dst != rank_) continue;
+      note(x);
+      if (record_only) continue;
+      if (x.src == x.dst) {
+        if (at(par, x.to) != at(par, x.from))
+          copy2d(at(par, x.to), x.to.pitch, at(par, x.from), x.from.pitch, x.width, x.height);
+        continue;
+      }
+      std::vector<char>& st = stage_[{static_cast<int>(ph), static_cast<int>(i)}];
+      st.resize(x.bytes());
+      if (x.src == rank_) {
+        copy2d(st.data(), x.width, at(par, x.from), x.from.pitch, x.width, x.height);
+        hc_->isend(st.data(), x.bytes(), x.dst);
+      } else {
+        hc_->irecv(st.data(), x.bytes(), x.src);
+        unpack.push_back({&x, &st});
+      }
+    }
+    if (record_only) return;
+    hc_->wait_all();
+    for (auto& u : unpack)
+      copy2d(at(par, u.first->to), u.first->to.pitch, u.second->data(), u.first->width, u.first->width, u.first->height);
+  }
+};
+
 }  // namespace
+
+std::unique_ptr<Transport> make_host_transport(HostComm* c, int rank) { return std::make_unique<HostTransport>(c, rank); }
 
 std::unique_ptr<Transport> make_rccl_transport(HostComm* c, int device, int rank, bool loopback) {
   return std::make_unique<RcclTransport>(c, device, rank, loopback);

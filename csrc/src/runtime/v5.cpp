@@ -2,12 +2,14 @@
 #include "anx/v5.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
 
+#include "anx/cpu_engine.hpp"
 #include "anx/trace.hpp"
 
 namespace anx {
@@ -299,9 +301,111 @@ struct V5Runtime::Impl_ {
   }
 };
 
+// ------------------------------------------------------------------------------------------ host
+// V5Options::host: CPU ranks run the same layout (plan, schedule, halo chunks) through the host
+// transport, one phase after another: scatter (root input), stage1, every halo chunk, stage2 (or the
+// whole-tile forward where no halo touches the rank), gather. Phase times are host wall clock.
+struct V5Runtime::HostImpl_ {
+  HostComm& c;
+  V5Options o;
+  const V5Layout& L;
+  BlocksDims d;
+  int rank = 0, np = 1;
+  std::unique_ptr<Transport> x;
+  std::unique_ptr<CpuBlocks> eng;
+  TilePlan t;
+  int n = 0;
+  bool lane_path = false, local = true;
+  std::vector<float> X, tile[2], y[2], yfull[2];
+  long k = 0, timed = 0;
+  double sums[5] = {0, 0, 0, 0, 0};
+  HostImpl_(HostComm& cc, const V5Options& oo, const V5Layout& l) : c(cc), o(oo), L(l) {}
+
+  void init(const BlockSpec& b1, const BlockSpec& b2, int H, int W, const HostWeights& w) {
+    rank = c.rank();
+    np = c.size();
+    d = blocks_dims(H, W, b1, b2);
+    x = make_host_transport(&c, rank);
+    x->keep_log = o.keep_log;
+    local = L.local_input;
+    HostWeights hw;  // the root's weights, broadcast over the transport (the reference's MPI_Bcast, M4/M5)
+    init_const(hw, b1, b2);
+    if (rank == 0) {
+      if (w.w1.size() != hw.w1.size() || w.b1.size() != hw.b1.size() || w.w2.size() != hw.w2.size() ||
+          w.b2.size() != hw.b2.size())
+        throw std::runtime_error("v5: weight sizes do not match the block specs");
+      hw = w;
+    }
+    for (std::vector<float>* v : {&hw.w1, &hw.b1, &hw.w2, &hw.b2}) x->bcast(v->data(), v->size() * 4, 0);
+    const HybridPlan& hp = L.plan;
+    t = hp.tile(rank);
+    const RowRange im = hp.images[hp.group_of[rank]];
+    n = t.out.empty() ? 0 : im.size();
+    lane_path = o.mode == Decomp::Overlap || hp.group_size[hp.group_of[rank]] == 1;
+    eng = std::make_unique<CpuBlocks>(b1, b2, H, W, hw);
+    const size_t in_img = static_cast<size_t>(H) * W * d.C0, out_img = static_cast<size_t>(d.Hp2) * d.Wp2 * d.C2;
+    if (rank == 0) {
+      X.assign(static_cast<size_t>(o.batch) * in_img, 0.f);
+      for (auto& v : yfull) v.assign(static_cast<size_t>(o.batch) * out_img, 0.f);
+    }
+    for (int p = 0; p < 2; ++p) {
+      tile[p].assign(std::max<size_t>(1, static_cast<size_t>(n) * t.in.size() * W * d.C0), 0.f);
+      y[p].assign(std::max<size_t>(1, static_cast<size_t>(n) * t.out.size() * d.Wp2 * d.C2), 0.f);
+    }
+    float* win = nullptr;  // the conv2 window exists (and keeps its address) once stage1 has run
+    if (n && !lane_path) {
+      eng->stage1(tile[0].data(), n, t);
+      win = eng->window_row(t, 0, t.q.lo);
+    }
+    void* bufs[2][kB];
+    for (int p = 0; p < 2; ++p) {
+      bufs[p][static_cast<int>(BufId::X)] = X.empty() ? nullptr : X.data();
+      bufs[p][static_cast<int>(BufId::Tile)] = tile[p].data();
+      bufs[p][static_cast<int>(BufId::Win)] = win;
+      bufs[p][static_cast<int>(BufId::Y)] = y[p].data();
+      bufs[p][static_cast<int>(BufId::YFull)] = yfull[p].empty() ? nullptr : yfull[p].data();
+    }
+    x->bind(L.sched, bufs, nullptr);
+    c.barrier();
+  }
+  static double now() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  void step() {
+    const int par = static_cast<int>(k & 1);
+    double t0 = now();
+    if (!local) x->run_phase(Phase::Scatter, L.sched.phase[0], nullptr, par);
+    const double t1 = now();
+    if (n && !lane_path) eng->stage1(tile[par].data(), n, t);
+    const double t2 = now();
+    if (!lane_path)
+      for (const auto& ch : L.halo_chunks) x->run_phase(Phase::P1Halo, ch, nullptr, par);
+    const double t3 = now();
+    if (n) {
+      if (lane_path)
+        eng->tile_forward(tile[par].data(), n, t, y[par].data());
+      else
+        eng->stage2(n, t, y[par].data());
+    }
+    const double t4 = now();
+    x->run_phase(Phase::Gather, L.sched.phase[2], nullptr, par);
+    const double t5 = now();
+    const double v[5] = {t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4};
+    for (int i = 0; i < 5; ++i) sums[i] += v[i];
+    ++timed;
+    ++k;
+  }
+};
+
 V5Runtime::V5Runtime(HostComm& c, const RankInfo& ri, const BlockSpec& b1, const BlockSpec& b2, int H, int W,
                      const HostWeights& w, const V5Options& o)
     : lay_(make_v5_layout(c.size(), b1, b2, H, W, o)) {
+  if (o.host) {  // CPU ranks: no HIP call anywhere on this path
+    h_ = std::make_unique<HostImpl_>(c, o, lay_);
+    h_->init(b1, b2, H, W, w);
+    pipeline_ = false;
+    return;
+  }
   p_ = std::make_unique<Impl_>(c, ri, o, lay_);
   Impl_& I = *p_;
   I.rank = c.rank();
@@ -455,10 +559,23 @@ V5Runtime::~V5Runtime() {
     if (s) (void)hipStreamDestroy(s);
 }
 
-const char* V5Runtime::transport() const { return p_->x->name(); }
-long V5Runtime::steps() const { return p_->k; }
+const char* V5Runtime::transport() const { return h_ ? h_->x->name() : p_->x->name(); }
+long V5Runtime::steps() const { return h_ ? h_->k : p_->k; }
 
 void V5Runtime::set_input(const float* host_x) {
+  if (h_) {
+    HostImpl_& I = *h_;
+    if (I.rank == 0) {
+      if (!host_x) throw std::runtime_error("v5 set_input: the root needs the batch");
+      std::memcpy(I.X.data(), host_x, I.X.size() * 4);
+    }
+    if (I.local) {  // every rank's images x input rows placed once, in both step parities
+      I.c.barrier();
+      for (int par = 0; par < 2; ++par) I.x->run_phase(Phase::Scatter, lay_.sched.phase[0], nullptr, par);
+    }
+    I.c.barrier();
+    return;
+  }
   Impl_& I = *p_;
   sync();
   if (I.rank == 0) {
@@ -480,6 +597,7 @@ void V5Runtime::set_input(const float* host_x) {
 }
 
 void V5Runtime::step() {
+  if (h_) return h_->step();
   Impl_& I = *p_;
   const long k = I.k;
   const int par = static_cast<int>(k & 1);
@@ -541,20 +659,28 @@ void V5Runtime::step() {
 }
 
 void V5Runtime::abort() {
-  if (!p_ || p_->aborted) return;
+  if (!p_ || p_->aborted) return;  // host mode: every phase is complete on return, nothing is parked
   p_->aborted = true;
   if (p_->x) p_->x->abort();
 }
 
 void V5Runtime::sync() {
+  if (h_) return;  // host mode: blocking phases
   Impl_& I = *p_;
   for (hipStream_t s : {I.st, I.io, I.hs}) hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize");
   for (size_t i = 1; i < I.ls.size(); ++i) hip_ok(hipStreamSynchronize(I.ls[i]), "hipStreamSynchronize");
 }
 
-std::vector<std::string> V5Runtime::transfer_log() const { return p_->x->log(); }
+std::vector<std::string> V5Runtime::transfer_log() const { return h_ ? h_->x->log() : p_->x->log(); }
 
 void V5Runtime::output(float* host_y) {
+  if (h_) {
+    if (h_->rank != 0) return;
+    if (h_->k == 0) throw std::runtime_error("v5 output: no step has run");
+    const std::vector<float>& v = h_->yfull[(h_->k - 1) & 1];
+    std::memcpy(host_y, v.data(), v.size() * 4);
+    return;
+  }
   Impl_& I = *p_;
   sync();
   if (I.rank != 0) return;
@@ -563,16 +689,28 @@ void V5Runtime::output(float* host_y) {
 }
 
 std::vector<std::pair<std::string, double>> V5Runtime::phase_ms() {
-  Impl_& I = *p_;
-  sync();
-  for (int i = 0; i < kRing; ++i) I.fold(i);
+  const double* sums;
+  long timed;
+  if (h_) {
+    sums = h_->sums, timed = h_->timed;
+  } else {
+    Impl_& I = *p_;
+    sync();
+    for (int i = 0; i < kRing; ++i) I.fold(i);
+    sums = I.sums, timed = I.timed;
+  }
   std::vector<std::pair<std::string, double>> v;
-  for (int i = 0; i < 5; ++i) v.push_back({kPhase[i], I.timed ? I.sums[i] / I.timed : 0.0});
+  for (int i = 0; i < 5; ++i) v.push_back({kPhase[i], timed ? sums[i] / timed : 0.0});
   v.push_back({"compute", v[1].second + v[2].second + v[3].second});
   return v;
 }
 
 void V5Runtime::reset_phases() {
+  if (h_) {
+    std::fill(std::begin(h_->sums), std::end(h_->sums), 0.0);
+    h_->timed = 0;
+    return;
+  }
   Impl_& I = *p_;
   sync();
   std::fill(I.pending.begin(), I.pending.end(), false);
@@ -581,7 +719,10 @@ void V5Runtime::reset_phases() {
 }
 
 std::string V5Runtime::describe_json() const {
-  const Impl_& I = *p_;
+  const Transport& X = h_ ? *h_->x : *p_->x;
+  const Decomp mode = h_ ? h_->o.mode : p_->o.mode;
+  const int dev = h_ ? -1 : p_->dev, nl = h_ ? 1 : p_->nl;
+  const bool local = h_ ? h_->local : p_->local, lane = h_ ? h_->lane_path : p_->lane_path;
   const PlanStats s = stats();
   char b[1024];
   std::snprintf(b, sizeof b,
@@ -590,10 +731,10 @@ std::string V5Runtime::describe_json() const {
                 "\"conv1_redundancy\": %.4f, \"images_per_rank_max\": %g, \"transfers_per_step\": %zu, "
                 "\"decomp\": \"%s\", \"device\": %d, \"input_source\": \"%s\", \"lanes\": %d, "
                 "\"lane_path\": %s, \"input_placement_bytes\": %.0f, ",
-                I.x->name(), I.x->ordering(), pipeline_ ? "true" : "false", lay_.chunks, s.groups, s.row_ways, s.rows_max,
+                X.name(), X.ordering(), pipeline_ ? "true" : "false", lay_.chunks, s.groups, s.row_ways, s.rows_max,
                 s.rows_mean, s.imbalance, s.conv1_redundancy, s.images_max, lay_.step_transfers().size(),
-                I.o.mode == Decomp::PerLayer ? "per_layer" : "overlap", I.dev, I.local ? "local" : "root", I.nl,
-                I.lane_path ? "true" : "false", lay_.input_placement_bytes());
+                mode == Decomp::PerLayer ? "per_layer" : "overlap", dev, local ? "local" : "root", nl,
+                lane ? "true" : "false", lay_.input_placement_bytes());
   // bytes per step by phase: per rank (arrays over ranks) and the root's / busiest rank's totals
   const std::vector<RankBytes> rb = lay_.rank_bytes();
   std::string j = b;

@@ -31,7 +31,7 @@ import torch.distributed as dist
 from .config import blocks_dims, flops_per_image
 from .parallel import comm
 from .parallel.plan import OVERLAP, PER_LAYER
-from .parallel.strategies import batch_forward, replicate_forward, rows_forward
+from .parallel.strategies import replicate_forward
 from .parallel.tensor import filter_parallel_forward
 from .utils.init import init_input, init_weights
 from .utils.timer import PhaseTimer
@@ -105,6 +105,26 @@ def _checksum(y: torch.Tensor) -> int:
     return zlib.crc32(y.detach().float().cpu().contiguous().numpy().tobytes()) & 0xFFFFFFFF
 
 
+def _native_runtime(cfg: RunConfig, w: dict | None, b1, b2, gpu: bool):
+    """Multi-rank row / image splits run on the native runtimes (libanx_dist), CPU and GPU alike:
+    V4 on GPUs = the host-staged runtime (anx/v4.hpp; a per_layer V4 runs V5's schedule with the
+    batch on the root), V5 = the device-resident runtime (anx/v5.hpp), V2.2 and the CPU rehearsals = the
+    V5 runtime in host mode (host engine + host transport). Every step starts from the root's batch,
+    as the reference's programs did."""
+    from .parallel.workloads import NativeV4, NativeV5
+    decomp = "batch" if cfg.strategy == "batch" else "rows"
+    if not gpu:
+        return NativeV5(cfg.batch, w, specs=(b1, b2), decomp=decomp, layer=cfg.decomp, impl="host",
+                        input_source="root")
+    for k, v in (("ANX_CONV1_ALGO", cfg.conv1_algo), ("ANX_CONV2_ALGO", cfg.conv2_algo)):
+        if v != "auto":  # knob seeds of the runtimes' engines
+            os.environ[k] = v
+    if cfg.version == "v4" and (cfg.decomp == OVERLAP or decomp == "batch"):
+        return NativeV4(cfg.batch, w, specs=(b1, b2), decomp=decomp, impl=cfg.impl)
+    return NativeV5(cfg.batch, w, specs=(b1, b2), decomp=decomp, layer=cfg.decomp, impl=cfg.impl,
+                    input_source="root")
+
+
 def run(cfg: RunConfig) -> RunResult | None:
     """Run one version; returns the result on rank 0 (None on other ranks)."""
     from .models.alexnet_blocks import AlexNetBlocks
@@ -119,7 +139,9 @@ def run(cfg: RunConfig) -> RunResult | None:
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")
-    backend = "nccl" if (cfg.version == "v5" and gpu) else "gloo"
+    # the native runtimes carry their own transports; torch.distributed only broadcasts their port and
+    # runs the Python strategies (broadcast-all, filter split)
+    backend = "nccl" if (cfg.version == "v5" and gpu and cfg.strategy == "filter") else "gloo"
     t_start = time.perf_counter()
     rank, ws = _init_dist(backend)
     if cfg.version in ("v1", "v3") and ws > 1:
@@ -130,13 +152,19 @@ def run(cfg: RunConfig) -> RunResult | None:
     from .config import blocks
     b1, b2 = blocks(cfg.lrn_mode, cfg.groups2)
     d = blocks_dims(b1=b1, b2=b2)
+    native = model = None
+    use_native = cfg.version in ("v2.2", "v4", "v5") and cfg.strategy in ("rows", "batch")
     with timer.phase("setup"):
         w = init_weights(cfg.init, cfg.seed, b1, b2) if rank == 0 else \
             {k: torch.empty_like(v) for k, v in init_weights("const", 0, b1, b2).items()}
-        w = comm.bcast_weights(w, device=comm_dev)
-        model = AlexNetBlocks(w, specs=(b1, b2), device=device, impl=cfg.impl, max_batch=cfg.batch,
-                              knobs={"conv1_algo": cfg.conv1_algo, "conv2_algo": cfg.conv2_algo} if gpu else None)
         x = init_input(cfg.batch, cfg.init, cfg.seed) if rank == 0 else None
+        if use_native:
+            native = _native_runtime(cfg, w if rank == 0 else None, b1, b2, gpu)
+            native.fill(x)
+        else:
+            w = comm.bcast_weights(w, device=comm_dev)
+            model = AlexNetBlocks(w, specs=(b1, b2), device=device, impl=cfg.impl, max_batch=cfg.batch,
+                                  knobs={"conv1_algo": cfg.conv1_algo, "conv2_algo": cfg.conv2_algo} if gpu else None)
         if cfg.version == "v2.1" or (cfg.strategy == "filter" and cfg.version in ("v2.2", "v4", "v5")):
             # broadcast-all: every rank receives the whole input (M3, main.cpp:71); the filter
             # (tensor-parallel) strategy also replicates Block 1 and needs the whole input
@@ -145,7 +173,7 @@ def run(cfg: RunConfig) -> RunResult | None:
                 xb = xb.to(device) if backend == "nccl" else xb  # RCCL broadcasts device memory
                 dist.broadcast(xb, 0)
             x = xb
-        if x is not None:
+        if x is not None and native is None:
             x = x.to(comm_dev if cfg.version in ("v4", "v5") else device)
 
     def once(tm: PhaseTimer):
@@ -159,19 +187,24 @@ def run(cfg: RunConfig) -> RunResult | None:
                 with tm.phase("d2h"):
                     y = y.cpu()
             return y if rank == 0 else None
-        if cfg.strategy == "batch":
-            return batch_forward(model, x, cfg.batch, comm_device=comm_dev, timer=tm)
+        if native is not None:
+            with tm.phase("step"):
+                native.step()
+                native.sync()
+            return native.output()
         if cfg.strategy == "filter":
             with tm.phase("compute"):
                 return filter_parallel_forward(x.to(device), model.weights, b1, b2, gather="root",
                                                comm_device=comm_dev)
-        return rows_forward(model, x, cfg.batch, decomp=cfg.decomp, comm_device=comm_dev, timer=tm)
+        raise ValueError(f"{cfg.version} with strategy {cfg.strategy!r} at np={ws}")
 
     if ws > 1:
         dist.barrier()
     with timer.phase("total"):
         y = once(timer)
     phases_cold = dict(timer.ms)
+    if native is not None:  # the runtime's own per-phase split of the step
+        phases_cold.update({f"step.{k}": v for k, v in native.phase_ms(reset=True).items()})
     cold_ms = phases_cold.pop("total") + phases_cold.get("setup", 0.0)
     phases_cold["wall_since_start"] = (time.perf_counter() - t_start) * 1e3
 
@@ -190,6 +223,8 @@ def run(cfg: RunConfig) -> RunResult | None:
             dist.barrier()
         warm_ms = (time.perf_counter() - t0) * 1e3 / cfg.iters
         phases_warm = wt.scaled(1.0 / cfg.iters)
+        if native is not None:
+            phases_warm.update({f"step.{k}": v for k, v in native.phase_ms().items()})
 
     res = None
     if rank == 0:
@@ -197,7 +232,7 @@ def run(cfg: RunConfig) -> RunResult | None:
         err = None
         if cfg.check:
             from .models.reference import blocks_forward
-            ref = blocks_forward(init_input(cfg.batch, cfg.init, cfg.seed), model.weights, b1, b2)
+            ref = blocks_forward(init_input(cfg.batch, cfg.init, cfg.seed), w if native else model.weights, b1, b2)
             err = float((y.double() - ref).abs().max())
         ips = cfg.batch / (warm_ms / 1e3) if warm_ms else None
         res = RunResult(cfg.version, ws, cfg.batch, list(y.shape[1:]), [round(float(v), 4) for v in y.flatten()[:10]],
@@ -208,6 +243,8 @@ def run(cfg: RunConfig) -> RunResult | None:
                         None if ips is None else round(ips * flops_per_image(b1=b1, b2=b2) / 1e12, 3))
         if not cfg.quiet:
             print_contract(res)
+    if native is not None:
+        native.close()
     if ws > 1:
         dist.barrier()
     return res

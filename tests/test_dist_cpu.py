@@ -257,29 +257,35 @@ def test_prefetch_pipeline_input_semantics():
 def _workload_worker(rank, world, port, q, version, decomp, batch):
     sys.path.insert(0, ROOT)
     import anx  # noqa: F401
-    from anx.models.alexnet_blocks import AlexNetBlocks
-    from anx.parallel.workloads import RowsWorkload
-    from anx.utils.init import init_input
+    from anx.parallel.workloads import NativeV5
+    from anx.utils.init import init_input, init_weights
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
-    m = AlexNetBlocks(init="rand", seed=4, device="cpu")
-    wl = RowsWorkload(m, batch, version, decomp, device="cpu")
-    wl.fill(init_input(batch, "rand", seed=4))
+    kw = dict(layer="overlap", input_source="root") if version == "v4" else dict(layer="per_layer")
+    wl = NativeV5(batch, init_weights("rand", 4) if rank == 0 else None, decomp=decomp, impl="host",
+                  timeout_s=120, keep_log=True, **kw)
+    wl.fill(init_input(batch, "rand", seed=4) if rank == 0 else None)
     wl.step()
-    wl.step()  # steady state: buffers reused
+    wl.step()  # steady state: the other parity's buffers
+    d = wl.describe()
+    assert d["transport"] == "host" and d["device"] == -1
+    log = wl.transfer_log()
     if rank == 0:
-        q.put(wl.output().clone())
+        q.put((wl.output().clone(), d, len(log)))
+    wl.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("version,decomp,world,batch", [
     ("v5", "rows", 2, 2), ("v5", "rows", 3, 1), ("v5", "hybrid", 4, 3), ("v4", "rows", 2, 2),
-    ("v4", "hybrid", 3, 2), ("v5", "batch", 2, 3)])
-def test_rows_workload_gloo(version, decomp, world, batch):
-    """bench.py's V4/V5 workloads (scatter -> tiles [-> pool1 halos] -> gather) on CPU ranks
-    reproduce the single-process output bit for bit (host engine: direct convolutions)."""
+    ("v4", "hybrid", 3, 2), ("v5", "batch", 2, 3), ("v5", "rows2", 4, 2)])
+def test_native_v5_host_gloo(version, decomp, world, batch):
+    """The native V5 runtime in host mode (CPU ranks: host engine, host transport; the same layout,
+    schedule and halo chunks as on GPUs, libanx_dist) reproduces the single-process output bit for
+    bit: V5 per_layer tiles with the pool1 halo exchange, and V4's overlap tiles scattered from the root
+    every step."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
@@ -287,7 +293,7 @@ def test_rows_workload_gloo(version, decomp, world, batch):
              for r in range(world)]
     for p in procs:
         p.start()
-    y = q.get(timeout=300)
+    y, d, nlog = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -295,7 +301,10 @@ def test_rows_workload_gloo(version, decomp, world, batch):
     from anx.models.alexnet_blocks import AlexNetBlocks
     from anx.utils.init import init_input
     ref = AlexNetBlocks(init="rand", seed=4, device="cpu")(init_input(batch, "rand", seed=4))
-    torch.testing.assert_close(y, ref, rtol=0, atol=0)
+    torch.testing.assert_close(y.view_as(ref), ref, rtol=0, atol=0)
+    assert d["decomp"] == ("overlap" if version == "v4" else "per_layer")
+    assert d["input_source"] == ("root" if version == "v4" else "local")
+    assert nlog > 0
 
 
 @pytest.mark.parametrize("workload", ["v4", "v5"])
