@@ -27,7 +27,6 @@
 // Reference op: convKernel (v3_cuda_only/src/layers_cuda.cu:20-46), one thread per output.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -55,7 +54,6 @@ constexpr int kUSlot = kK * kCh;           // floats per U ring slot (one point)
 constexpr int kUPieces = kUSlot / 256;     // 1-KiB DMA pieces per slot
 constexpr int kUSlots = 3;                 // U ring slots: U_{p+2} is in flight while point p computes
 constexpr int kOOB = 0x7ffffff0;           // a buffer offset past any extent: the load returns 0
-constexpr int kWgPerXcd = 32;              // persistent grid: 8 x 32 workgroups = one per CU
 constexpr int kOS = kK + 4;                // epilogue transpose row stride (floats)
 constexpr int kDummy = 2 * kVBuf + kUSlots * kUSlot;  // 1-KiB scratch for the dummy DMAs
 constexpr int kLdsFloats = kDummy + 256;
@@ -85,18 +83,7 @@ constexpr int loads_at(int p) {
     if (p >= 0 && late_load_pt(u) == p) return u;
   return -1;
 }
-// the point at which the next tile block's prologue rows load (persistent loop): the first point of
-// the last a-step, after every row of this block has been added into t
-constexpr int kPrefetchPt = (kN5 - 1) * kN5;
-constexpr int n_prologue_rows() {
-  int n = 0;
-  for (int u = 0; u < kN5; ++u) n += prologue_row(u) ? 1 : 0;
-  return n;
-}
-constexpr int x_ops(int p) {
-  return (p >= 0 && loads_at(p) >= 0 ? kN5 : 0) + (p == kPrefetchPt ? kN5 * n_prologue_rows() : 0);
-}
-static_assert(late_load_pt(kN5 - 1) < kPrefetchPt, "every late row loads before the prefetch point");
+constexpr int x_ops(int p) { return p >= 0 && loads_at(p) >= 0 ? kN5 : 0; }
 static_assert(9 * kTiles * kOS <= kDummy, "epilogue scratch: nine position images below the dummy DMA slot");
 // pool1 epilogue: candidate pooled pixels are those whose window starts in tiles p0 - kPoolBack .. p0 + 31
 // (a window's tiles span at most tx + 1 raster indices: kPoolBack >= tx + 1, checked by the launcher)
@@ -144,16 +131,10 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: the DMA M0 values stay scalar
   const int wm = wave & 1, wn = wave >> 1;
-  // Persistent: workgroup (xcd label, w) of gridDim.x / 8 per label runs tile blocks j = w, w + nw, ...
-  // of its label's contiguous range (consecutive blocks share image rows: same XCD under round-robin
-  // dispatch, L2 reuse; speed only). Each block's X' rows are loaded during the previous block's last
-  // a-step, so only a workgroup's first block waits for its image rows.
-  const int xlab = blockIdx.x & 7, nw = static_cast<int>(gridDim.x >> 3);
-  int jb = static_cast<int>(blockIdx.x >> 3);
-  auto block_of = [&](int j) { return j < a.per_xcd ? xlab * a.per_xcd + j : a.n_ptiles; };
-  int pt = block_of(jb);
+  // consecutive tile blocks on one XCD (they read overlapping image rows: L2 reuse; speed only)
+  const int pt = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
   if (pt >= a.n_ptiles) return;  // whole workgroup, before any barrier
-  int p0 = pt * kTiles;
+  const int p0 = pt * kTiles;
 #if __HIP_DEVICE_COMPILE__
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), 0, a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
@@ -188,6 +169,18 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // ---- the V build slot of this thread: tile bt, channels 2 bc, 2 bc + 1 (phase row rh, floats 2 bc % 12
   // .. +1 of the 12-float (rw, c) run)
   const int bt = tid / 24, bc = tid - bt * 24, rh = (2 * bc) / 12, bf2 = 2 * bc - rh * 12;
+  const int bp = p0 + bt;
+  const bool bval = bp < a.P;
+  int btj = 0, bti = 0, bn = 0;
+  if (bval) {
+    btj = bp % a.tx;
+    const int pq = bp / a.tx;
+    bti = pq % a.ty;
+    bn = pq / a.ty;
+  }
+  const int row0 = bti * kPitch + rh;               // image row of u = 0 (this slot's phase row)
+  const int col0 = btj * kPitch * 3 + bf2;          // float of v = 0 inside the row
+  [[maybe_unused]] const int xoff = ((bn * a.Hin + row0) * a.rowf + col0) * 4;
   // X'[u][v] (2 channels): image row 12 ti + 4u + rh, floats (12 tj + 4v) * 3 + bf2 .. +1 (zero outside).
   // Every load is issued by every lane (a lane outside the image reads past the buffer's extent, which
   // returns 0), so each X' row is exactly kN5 vector-memory ops per wave and the schedule's vmcnt
@@ -196,29 +189,13 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // zeroed once per a-step before V is formed (vpart), instead of a select per load.
   bool rok[kN5], cpart[kN5];
   int offv[kN5];  // per column v: this lane's byte offset, or past the extent (zeros)
-  // this thread's X' addressing for the block starting at tile q0 (q0 >= P: every load returns zeros)
-  auto setup = [&](int q0) {
-    const int bp = q0 + bt;
-    const bool bval = bp < a.P;
-    int btj = 0, bti = 0, bn = 0;
-    if (bval) {
-      btj = bp % a.tx;
-      const int pq = bp / a.tx;
-      bti = pq % a.ty;
-      bn = pq / a.ty;
-    }
-    const int row0 = bti * kPitch + rh;       // image row of u = 0 (this slot's phase row)
-    const int col0 = btj * kPitch * 3 + bf2;  // float of v = 0 inside the row
-    const int xoff = ((bn * a.Hin + row0) * a.rowf + col0) * 4;
 #pragma unroll
-    for (int i = 0; i < kN5; ++i) {
-      const int o = col0 + 12 * i;
-      rok[i] = bval && row0 + kPh * i < a.Hin;
-      offv[i] = o < a.rowf ? xoff : kOOB;
-      cpart[i] = o + 1 == a.rowf;
-    }
-  };
-  setup(p0);
+  for (int i = 0; i < kN5; ++i) {
+    const int o = col0 + 12 * i;
+    rok[i] = bval && row0 + kPh * i < a.Hin;
+    offv[i] = o < a.rowf ? xoff : kOOB;
+    cpart[i] = o + 1 == a.rowf;
+  }
   auto load_x = [&](int u, int v) -> f32x2 {
     f32x2 d = {0.f, 0.f};
     if constexpr ((ABL & 1) != 0) return f32x2{static_cast<float>(offv[v] + u), static_cast<float>(v)};
@@ -284,35 +261,22 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // (resident) into t (V_{a+1}). V_{a+1} is stored at the end of a-step a. vmcnt is in order: the wait
   // at point p leaves in flight exactly the ops issued after U_p (inflight below).
   f32x2 xrow[kN5][kN5];  // X' rows of this thread's (tile, channel pair), each loaded once (see late_load_pt)
-  auto load_prologue_rows = [&]() {  // the rows V_0 takes (kept for the later V_a)
-    sfor<0, kN5>([&](auto Uc) {
-      constexpr int u = decltype(Uc)::value;
-      if constexpr (prologue_row(u))
-#pragma unroll
-        for (int v = 0; v < kN5; ++v) xrow[u][v] = load_x(u, v);
-    });
-  };
-  auto build_v0 = [&]() {
-    t_zero();
-    sfor<0, kN5>([&](auto Uc) {
-      constexpr int u = decltype(Uc)::value;
-      if constexpr (prologue_row(u)) t_add(std::integral_constant<int, 0>{}, Uc, xrow[u]);
-    });
-  };
-  // prologue of the first block: U_0, U_1 in flight, its rows loaded, V_0 built and stored
+  // prologue: U_0, U_1 in flight; the rows V_0 takes loaded (kept), V_0 built and stored
   issue_u(std::integral_constant<int, 0>{});
   issue_u(std::integral_constant<int, 1>{});
-  load_prologue_rows();
-  build_v0();
+  t_zero();
+  sfor<0, kN5>([&](auto Uc) {
+    constexpr int u = decltype(Uc)::value;
+    if constexpr (prologue_row(u))
+#pragma unroll
+      for (int v = 0; v < kN5; ++v) xrow[u][v] = load_x(u, v);
+  });
+  sfor<0, kN5>([&](auto Uc) {
+    constexpr int u = decltype(Uc)::value;
+    if constexpr (prologue_row(u)) t_add(std::integral_constant<int, 0>{}, Uc, xrow[u]);
+  });
   v_store(0);
   t_zero();
-  const int f = wn * 16 + r16;
-  const float bv = a.bias ? a.bias[f] : 0.f;
-  const OutView o = a.out;
-  float* tr = lds;
-
-  for (;;) {  // tile blocks of this workgroup
-  const int pn = block_of(jb + nw) < a.n_ptiles ? block_of(jb + nw) * kTiles : a.P;  // next block (or none: a.P)
 
   sfor<0, kN5>([&](auto Ac) {
     constexpr int av = decltype(Ac)::value;
@@ -324,7 +288,6 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
       // in flight past this barrier: the ops issued after U_p (at point p - 2: its X' row, if any; at
       // point p - 1: U_{p+1} and its X' row): this wave's U_p has landed, X' rows finish on their own
       constexpr int inflight = (p + 1 < kPts ? 2 : 0) + x_ops(p - 1) + x_ops(p - 2);
-      static_assert(inflight < 64, "vmcnt");
       __builtin_amdgcn_sched_barrier(0);
       if constexpr ((ABL & 4) != 0)
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(inflight) : "memory");
@@ -337,10 +300,6 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         constexpr int r = loads_at(p);
 #pragma unroll
         for (int v = 0; v < kN5; ++v) xrow[r][v] = load_x(r, v);
-      }
-      if constexpr (p == kPrefetchPt) {  // every row of this block consumed: the next block's rows (zeros
-        setup(pn);                       // past the last block, so every wave issues the same ops)
-        load_prologue_rows();
       }
       __builtin_amdgcn_sched_barrier(0);  // loads issued before the MFMAs
       const float* vp = vb + b * kTiles * kVS + a_off;
@@ -396,7 +355,10 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 
   // ---- epilogue: per output position q, bias + ReLU into an LDS image [32 tiles][96 filters], then
   // 16-B row-contiguous stores. D layout: lane holds col = lane & 15 (filter), rows 4 (lane >> 4) + i.
-  build_v0();  // the next block's t for V_0 (its rows landed at the last point's wait), stored below
+  const int f = wn * 16 + r16;
+  const float bv = a.bias ? a.bias[f] : 0.f;
+  const OutView o = a.out;
+  float* tr = lds;
   const int st = tid / (kK / 4), sq = tid - st * (kK / 4);  // this thread's store: tile st, filters 4 sq .. +3
   const int sp = p0 + st;
   int sn = 0, sti = 0, stj = 0;
@@ -511,20 +473,6 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
                                   o.c_off + 4 * sq) = *reinterpret_cast<const f32x4*>(tr + (q * kTiles + st) * kOS + 4 * sq);
     }
   }
-  // ---- next block (uniform over the workgroup): once every wave's epilogue LDS reads are done, its
-  // first two U points go into the ring and V_0 into buffer 0; its point 0 barrier publishes both
-  jb += nw;
-  if (pn >= a.P) break;
-  pt = pn / kTiles;
-  p0 = pn;
-  lds_barrier<>();
-  issue_u(std::integral_constant<int, 0>{});
-  issue_u(std::integral_constant<int, 1>{});
-  v_store(0);
-  t_zero();
-#pragma unroll
-  for (int q = 0; q < 9; ++q) Y[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }  // tile blocks
 }
 
 }  // namespace
@@ -566,9 +514,7 @@ hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const floa
   a.p1 = p1;
   a.Hp = Hp;
   a.Wp = Wp;
-  // persistent: one workgroup per CU (128 KB of LDS each), 32 per XCD label, each walking its label's
-  // contiguous tile blocks; smaller launches keep one block per workgroup
-  const unsigned grid = static_cast<unsigned>(std::min(a.per_xcd, kWgPerXcd) * 8);
+  const unsigned grid = static_cast<unsigned>(a.per_xcd * 8);
 #ifdef ANX_CONV1_ABL  // cost-probe builds only (CMake ANX_CONV1_ABL=ON): ANX_CONV1_ABL=<bits> picks the probe
   static const int abl = [] {
     const char* e = std::getenv("ANX_CONV1_ABL");
