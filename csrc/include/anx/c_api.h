@@ -139,6 +139,9 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
    x [N,Hq,Wq,C] (padding already in the window), KCFF weights on the HOST, y [N,Hq-4,Wq-4,K]. */
 int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
                    const float* bias, float* y, int relu, void* stream);
+// The same with the Winograd output tile m = 3 (F(3x3,5x5)) or 4 (F(4x4,5x5), one group of 96 channels).
+int anx_conv2_wino_tile(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
+                        const float* bias, float* y, int relu, void* stream, int m);
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,
                     float* out, int Hb, int Wb, int Cb, int h_off, int w_off, int c_off, int relu, void* stream);
 

@@ -108,6 +108,8 @@ class BlocksEngine {
   // Winograd conv2: transformed weights [49][K][C/groups] + V workspace
   float *u2w_ = nullptr, *wv_ = nullptr;
   size_t wv_cap_ = 0;
+  int u2_m_ = 3;       // Winograd output tile of u2w_ / wv_ (Knobs::conv2_tile when eligible)
+  int tile2() const;   // the tile the knobs ask for and Conv2's shape allows
   // Winograd conv1: transformed polyphase weights + V workspace (full-height tiles of chunk_ images)
   float *u1w_ = nullptr, *wv1_ = nullptr;
   size_t wv1_cap_ = 0;

@@ -63,11 +63,15 @@ struct Knobs {
                            // chunk (0 = the whole chunk); the V workspace is rewritten in place per sub-chunk, so
                            // a small one is written and re-read inside the 256 MB Infinity Cache
   int conv2_sub = 0;       // ... and per (pool1 + Conv2 input transform, Conv2 GEMM) pair
+  int conv2_tile = 4;      // Conv2 Winograd output tile: 4 = F(4x4,5x5) (64 points per 16 outputs: 21 % fewer
+                           // multiplies, 16x16x4 MFMAs, wino_gemm16.hpp; one group of 96 channels only, else 3;
+                           // bench step 305-309 k vs 293 k images/s, profiles/r05_f45/), 3 = F(3x3,5x5) (49
+                           // points, 32x32x2 MFMAs: grouped Conv2 and the A/B arm)
 };
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
 // ANX_BF16_GLDS, ANX_BF16_BIG, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1,
-// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL when set.
+// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL, ANX_CONV2_TILE when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

@@ -88,16 +88,19 @@ void pack_conv_weights_host(const ConvPlan& p, const float* w_kcff, std::vector<
 hipError_t conv2d_mfma(const ConvPlan& p, const float* x, const float* wpacked, const int* koff,
                        const float* bias, OutView out, bool relu, hipStream_t s);
 
-// Winograd F(3x3,5x5) for stride-1 5x5 convolutions over a pre-padded input window (winograd.hip).
+// Winograd F(m x m, 5x5) for stride-1 5x5 convolutions over a pre-padded input window (winograd.hip):
+// m = 3 (7x7 input tiles, 49 points) or m = 4 (8x8, 64 points; Knobs::conv2_tile).
 struct WinoPlan {
   int N, Hq, Wq, C, K, groups;
-  int Ho, Wo, ty, tx, P;  // output dims, 3x3 tiles per column/row, total tiles
+  int Ho, Wo, ty, tx, P;  // output dims, m x m tiles per column/row, total tiles
+  int m;                  // output tile side
 };
-// 96 or 48 channels per group and a multiple of 64 filters per group (the fused GEMM's shapes)
-bool wino_eligible(int F, int S, int C, int K, int groups);
-WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups);
-size_t wino_v_floats(const WinoPlan& w);  // V workspace [P][49][C]
-size_t wino_u_floats(const WinoPlan& w);  // transformed weights [49][K][C/groups]
+// m = 3: 96 or 48 channels per group and a multiple of 64 filters per group; m = 4: one group, 96
+// channels, a multiple of 32 filters (the fused GEMMs' shapes)
+bool wino_eligible(int F, int S, int C, int K, int groups, int m = 3);
+WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups, int m = 3);
+size_t wino_v_floats(const WinoPlan& w);  // V workspace [P][(m+4)^2][C]
+size_t wino_u_floats(const WinoPlan& w);  // transformed weights [(m+4)^2][K][C/groups]
 // U[(ab*groups + g)*Kg + k][c] = (G g G^T)[a][b] in fp64, rounded once.
 void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff);
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s);
@@ -165,6 +168,9 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
                            int cfg = -1);
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
                            int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
+// The F(4x4,5x5) form (wino_gemm16.hpp): V [P][64][96], U [64][K][96], P tiles of 4x4 outputs, K % 32 == 0.
+hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
+                               int Ho, int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
 
 
 // Dynamic LDS bytes that cap a kernel at `wgs` workgroups per CU (160 KiB LDS per CU): the larger of

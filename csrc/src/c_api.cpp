@@ -461,11 +461,12 @@ int anx_conv1_wino(const float* x, int N, int Hin, int W, const float* w_kcff, i
   });
 }
 
-int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
-                   const float* bias, float* y, int relu, void* stream) {
+int anx_conv2_wino_tile(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
+                        const float* bias, float* y, int relu, void* stream, int m) {
   return guarded("anx_conv2_wino", [&] {
-    if (!anx::hip::wino_eligible(5, 1, C, K, groups)) return fail("anx_conv2_wino: shape not eligible");
-    const auto w = anx::hip::make_wino_plan(N, Hq, Wq, C, K, groups);
+    if ((m != 3 && m != 4) || !anx::hip::wino_eligible(5, 1, C, K, groups, m))
+      return fail("anx_conv2_wino: shape not eligible");
+    const auto w = anx::hip::make_wino_plan(N, Hq, Wq, C, K, groups, m);
     std::vector<float> u;
     anx::hip::wino_transform_weights_host(w, w_kcff, u);
     float *dv = nullptr, *du = nullptr;
@@ -485,6 +486,11 @@ int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_
     (void)hipFree(du);
     return hip_status(e, "conv2_wino");
   });
+}
+
+int anx_conv2_wino(const float* x, int N, int Hq, int Wq, int C, const float* w_kcff, int K, int groups,
+                   const float* bias, float* y, int relu, void* stream) {
+  return anx_conv2_wino_tile(x, N, Hq, Wq, C, w_kcff, K, groups, bias, y, relu, stream, 3);
 }
 
 int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const int* koff, const float* bias,

@@ -106,10 +106,16 @@ void BlocksEngine::prepare() {
     wv1_cap_ = hip::conv1_wino_v_floats(wp);
     wv1_ = dev_alloc<float>(wv1_cap_);
   }
+  if (u2w_ != nullptr && u2_m_ != tile2()) {  // the tile knob changed: other transformed weights / workspace
+    for (float** q : {&u2w_, &wv_})
+      if (*q) (void)hipFree(*q), *q = nullptr;
+    wv_cap_ = 0;
+  }
   if (u2w_ == nullptr && hip::wino_eligible(k2.F, k2.S, d_.C1, d_.C2, k2.groups) &&
       use_winograd(k_.conv2_algo, max_batch_, d_.H2, d_.H2)) {
     // Winograd workspace for a full-height window of chunk_ images (row tiles need less)
-    const hip::WinoPlan wp = hip::make_wino_plan(chunk_, d_.Hp1 + 2 * k2.P, wq_, d_.C1, d_.C2, k2.groups);
+    const hip::WinoPlan wp = hip::make_wino_plan(chunk_, d_.Hp1 + 2 * k2.P, wq_, d_.C1, d_.C2, k2.groups, tile2());
+    u2_m_ = wp.m;
     if (hip::wino_v_floats(wp) < (1UL << 31)) {
       std::vector<float> u;
       hip::wino_transform_weights_host(wp, w2h_.data(), u);
@@ -127,6 +133,11 @@ void BlocksEngine::prepare() {
   if (!use_winograd(k_.conv2_algo, nd2, d_.H2, d_.H2) || wv_ == nullptr)
     (void)pack2(hip::make_conv_plan(nd2, d_.Hp1 + 2 * k2.P, wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups, k_.force_vec4,
                                     k_.force_scalar));
+}
+
+int BlocksEngine::tile2() const {
+  const ConvSpec& k2 = b2_.conv;
+  return k_.conv2_tile == 4 && hip::wino_eligible(k2.F, k2.S, d_.C1, d_.C2, k2.groups, 4) ? 4 : 3;
 }
 
 int BlocksEngine::set_knob(const char* name, int value) {
@@ -233,7 +244,7 @@ hipError_t BlocksEngine::conv2_chunk(int n, const TilePlan& t, const float* qc, 
   const ConvSpec& k2 = b2_.conv;
   const hip::OutView c2v{c2_, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
   if (impl_ == Impl::Mfma && wv_ != nullptr && use_winograd(k_.conv2_algo, n, t.c2.size(), d_.H2)) {
-    const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
+    const hip::WinoPlan w = hip::make_wino_plan(n, t.q.size(), wq_, d_.C1, k2.K, k2.groups, u2_m_);
     if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
     ANX_TRY(hip::wino_input(w, qc, wv_, s));
     ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
@@ -339,7 +350,7 @@ hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, 
     const int s2 = k_.conv2_sub > 0 ? std::min(n, k_.conv2_sub) : n;
     for (int b0 = 0; b0 < n; b0 += s2) {
       const int m = std::min(s2, n - b0);
-      const hip::WinoPlan w = hip::make_wino_plan(m, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
+      const hip::WinoPlan w = hip::make_wino_plan(m, t.q.size(), wq_, d_.C1, k2.K, k2.groups, u2_m_);
       if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
       ANX_TRY(hip::wino_pool_input(w, c1_ + b0 * c1_img, t.c1.size(), d_.W1, t.q.lo, d_.Hp1, d_.Wp1, k2.P, t.c1.lo,
                                    wv_, s, b1_.pool.F, b1_.pool.S));
@@ -376,7 +387,7 @@ hipError_t BlocksEngine::tile_forward_conv1_pool(const float* x, int N, const Ti
     const int s2 = k_.conv2_sub > 0 ? std::min(n, k_.conv2_sub) : n;
     for (int b0 = 0; b0 < n; b0 += s2) {
       const int m = std::min(s2, n - b0);
-      const hip::WinoPlan w = hip::make_wino_plan(m, t.q.size(), wq_, d_.C1, k2.K, k2.groups);
+      const hip::WinoPlan w = hip::make_wino_plan(m, t.q.size(), wq_, d_.C1, k2.K, k2.groups, u2_m_);
       if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
       ANX_TRY(hip::wino_window_merge_input(w, q2_ + (n0 + b0) * q_img, c1_ + b0 * p1_img, b0, w1.ty, w1.tx, t.q.lo,
                                            d_.Hp1, d_.Wp1, k2.P, wv_, s));

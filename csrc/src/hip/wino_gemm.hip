@@ -6,6 +6,7 @@
 // ring beat BK 32 x 4 slots and BK 16 x 6 slots (the deeper rings raised MFMA-busy but the chip then
 // held a lower clock); Conv2 623 us (old fused kernel 649, bit-identical output), Conv1 380 us.
 #include "wino_gemm.hpp"
+#include "wino_gemm16.hpp"
 
 namespace anx::hip {
 namespace {
@@ -55,6 +56,47 @@ using C1_64x96 = wg::Cfg<25, 48, 2, 3, 48, 2>;   // 64 x 96 (every filter: V rea
 using C1_32x96 = wg::Cfg<25, 48, 1, 3, 48, 2>;   // 32 x 96, 3 waves, 48 KiB ring
 using C1_48x2w4 = wg::Cfg<25, 48, 4, 1, 48, 2>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
 #endif
+
+// The F(4x4,5x5) kernel (wino_gemm16.hpp): same Args, its own tile shape
+template <class G, int ABL>
+hipError_t launch16(const wg::Args& a0, hipStream_t s, int occ) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wg16::gemm16_kernel<G, ABL>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return attr;
+  wg::Args a = a0;
+  a.n_ptiles = (a.P + G::BM - 1) / G::BM;
+  a.n_ntiles = a.kg / G::BN;
+  if (a.kg % G::BN || a.n_ntiles < 1 || a.u_rows < a.n_ntiles * G::BN) return hipErrorInvalidValue;
+  if (occ < 0) occ = a.n_ptiles * a.n_ntiles <= device_cus() ? 1 : 0;
+  const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
+  wg16::gemm16_kernel<G, ABL><<<grid, G::NT, occupancy_lds(G::kLdsBytes, occ), s>>>(a);
+  return hipGetLastError();
+}
+// <waves along tiles, waves along filters, K slice, ring slots>: 32 tiles x 16 filters per wave
+// 32 tiles x 64 filters, 4 waves, 36 KiB ring: V read by 4 filter blocks instead of 8 (128 images alone:
+// 289.7 us vs 299.3 for 64 x 32 and 310.2 for the F(3x3,5x5) kernel; profiles/r05_f45/wg45_128.log)
+using F45 = wg16::Cfg<1, 4, 48, 2>;
+#ifdef ANX_WGEMM_ABLATIONS
+using F45_64x64 = wg16::Cfg<2, 4, 48, 2>;   // 8 waves, 48 KiB ring, one workgroup per CU's VGPR budget
+using F45_128x32 = wg16::Cfg<4, 2, 48, 2>;  // 8 waves, 60 KiB ring
+using F45_s3 = wg16::Cfg<2, 2, 48, 3>;      // 64 x 32, 3-slot ring (55 KiB)
+using F45_32x4 = wg16::Cfg<2, 2, 32, 4>;    // 64 x 32, K slice 32 x 4 slots (48 KiB)
+using F45_64x32 = wg16::Cfg<2, 2, 48, 2>;   // 64 tiles x 32 filters, 4 waves
+using F45_32x64_32x4 = wg16::Cfg<1, 4, 32, 4>;  // 32 x 64, K slice 32 x 4 slots
+using F45_32x64_s3 = wg16::Cfg<1, 4, 48, 3>;    // 32 x 64, 3-slot ring
+using F45_32x128 = wg16::Cfg<1, 8, 48, 2>;      // 32 x 128, 8 waves (V read by 2 filter blocks)
+#endif
+template <class G>
+hipError_t launch16_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
+  switch (abl) {
+    case 0: return launch16<G, 0>(a, s, occ);
+#ifdef ANX_WGEMM_ABLATIONS
+    case 3: return launch16<G, 3>(a, s, occ);
+    case 32: return launch16<G, 32>(a, s, occ);
+#endif
+    default: return hipErrorInvalidValue;
+  }
+}
 
 template <class G>
 hipError_t launch_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
@@ -114,6 +156,43 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
+                               int Ho, int Wo, int K, bool relu, hipStream_t s, int occ, int abl, int cfg) {
+  const long vb = static_cast<long>(P) * 64 * 96 * 4, ub = static_cast<long>(64) * K * 96 * 4;
+  if (K % 32 || vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
+  if (P == 0) return hipSuccess;
+  wg::Args a{};
+  a.V = V;
+  a.U = U;
+  a.bias = bias;
+  a.out = out;
+  a.P = P;
+  a.ty = ty;
+  a.tx = tx;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.kg = K;
+  a.u_rows = K;
+  a.vct = 96;
+  a.vbytes = static_cast<int>(vb);
+  a.ubytes = static_cast<int>(ub);
+  a.relu = relu ? 1 : 0;
+  switch (cfg < 0 ? 0 : cfg) {
+    case 0: return launch16_abl<F45>(a, s, occ, abl);
+#ifdef ANX_WGEMM_ABLATIONS
+    case 1: return launch16_abl<F45_64x64>(a, s, occ, abl);
+    case 2: return launch16_abl<F45_128x32>(a, s, occ, abl);
+    case 3: return launch16_abl<F45_s3>(a, s, occ, abl);
+    case 4: return launch16_abl<F45_32x4>(a, s, occ, abl);
+    case 5: return launch16_abl<F45_64x32>(a, s, occ, abl);
+    case 6: return launch16_abl<F45_32x64_32x4>(a, s, occ, abl);
+    case 7: return launch16_abl<F45_32x64_s3>(a, s, occ, abl);
+    case 8: return launch16_abl<F45_32x128>(a, s, occ, abl);
+#endif
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,

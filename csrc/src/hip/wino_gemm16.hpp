@@ -1,0 +1,280 @@
+// Fused Winograd F(4x4,5x5) batched GEMM + output transform for Conv2, fp32 on v_mfma_f32_16x16x4_f32
+// (included by wino_gemm.hip and by the anx_wgemm A/B tool).
+//
+// Why a second tile size: F(3x3,5x5) spends 49 transform points on 9 outputs (5.44 multiplies per
+// output), F(4x4,5x5) 64 on 16 (4.0): Conv2's 27x27 map is 81 tiles of 3x3 but 49 tiles of 4x4 (one
+// wasted row and column), so the MFMA work per image drops from 195 to 154 MFLOP (-21 %) and V from
+// 1.52 to 1.20 MB per image. Its fp32 error is 6.8e-7 of sum|x*w| against 5.2e-7 for F(3,5)
+// (tools/winograd_numerics.py; points {0, +-1, +-2, +-1/2, inf}).
+//
+// The price is the output fold: 16 outputs per tile. The 3x3 kernel's wave tile (32 tiles x 32 filters
+// on 32x32x2 MFMAs) would need 16 x 16 = 256 fold registers per lane, so this kernel runs 32 tiles x 16
+// filters per wave on 16x16x4 MFMAs (same f32 rate: 64 FLOP per cycle per SIMD): two 16x16 blocks share
+// each B fragment, the fold holds Y[16 outputs][8 values] = 128 registers, and every point folds
+// 128 FMAs (2.7 per MFMA) behind the next point's MFMAs.
+//
+// Everything else is wino_gemm.hpp's schedule: an NST-slot LDS ring of BK-channel slices filled by
+// buffer_load ... lds (1 KiB per wave instruction, swizzled source offsets), one barrier per slice,
+// compile-time slot / offset / wait counts in a UP-point loop body with a peeled tail, fold pinned
+// behind the MFMAs with sched_group_barrier, bias + ReLU + NHWC store once at the end through an LDS
+// transpose (16-B stores).
+//
+// Fragment reads: 16x16x4 takes one A and one B value per lane, lane l = (row l % 16, k-group l / 16).
+// A lane's ds_read_b128 of unit 4s + l/16 of its row yields 4 channels, one per k-step: k-step j of
+// channel group s multiplies channel 16s + 4(l/16) + j (the same permutation on A and B, so the sum is
+// unchanged). The 16 lanes of a read group hit rows r0..r0+15 at one unit: with 48-float rows and the
+// (row >> 2) & 3 swizzle they land on 16 distinct 16-B slots (conflict-free).
+//
+// Reference op: convKernel (v3_cuda_only/src/layers_cuda.cu:20-46), one thread per output.
+#pragma once
+#include "wino_gemm.hpp"
+
+#include "anx/winograd_f45.hpp"
+
+namespace anx::hip::wg16 {
+
+using wg::f32x4;
+using wg::lds_f32;
+using wg::lds_void;
+using wg::static_for;
+
+struct Coef64 {
+  float v[64][16];
+};
+constexpr Coef64 make_coef64() {
+  Coef64 t{};
+  for (int ab = 0; ab < 64; ++ab)
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) t.v[ab][i * 4 + j] = wino45::kAT[i][ab / 8] * wino45::kAT[j][ab % 8];
+  return t;
+}
+static __constant__ Coef64 c_coef64 = make_coef64();
+
+// WM x WN waves of 32 tiles x 16 filters; BK-channel slices through an NST-slot ring.
+template <int WM_, int WN_, int BK_, int NST_>
+struct Cfg {
+  static constexpr int NPT = 64, C = 96, NQ = 16, NE = 8;  // points, channels, outputs, values per lane
+  static constexpr int WM = WM_, WN = WN_, BK = BK_, NST = NST_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int BM = 32 * WM, BN = 16 * WN, U4 = BK / 4;
+  static constexpr int KS = C / BK, TOTAL = NPT * KS;
+  static constexpr int A_INS = BM * U4 / 64, B_INS = BN * U4 / 64;
+  static constexpr int A_MAX = (A_INS + NW - 1) / NW, B_MAX = (B_INS + NW - 1) / NW;
+  static constexpr int PW_MIN = A_INS / NW + B_INS / NW;
+  static constexpr int A_FL = BM * BK, STAGE = (BM + BN) * BK;
+  static constexpr size_t kLdsBytes = static_cast<size_t>(NST) * STAGE * sizeof(float);
+  static constexpr int UP = wg::even_up(KS, NST);
+  static constexpr int NI = (TOTAL + 1 - NST) / (UP * KS);
+  static constexpr int TAIL = NPT - NI * UP;
+  static constexpr int G4 = BK / 16;     // 16-channel groups per slice (one ds_read_b128 per operand row each)
+  static constexpr int MF = BK / 4 * 2;  // MFMAs per slice (k-steps x 2 row blocks)
+  static constexpr int NF = NQ * NE;     // fold FMAs per point
+  static constexpr int MINB = NW >= 8 ? 1 : 8 / NW;  // workgroups per CU the VGPR budget is sized for (8 waves)
+  static_assert(C % BK == 0 && BK % 16 == 0 && A_INS * 64 == BM * U4 && B_INS * 64 == BN * U4, "tile shape");
+  static_assert(U4 == 4 || U4 == 8 || U4 == 12, "swizzle defined for 4, 8, 12 units per row");
+  static_assert(NST >= 2 && NI >= 1 && TAIL >= 1, "ring / loop shape");
+};
+
+// ABL (A/B tool only; production instantiates 0): bit0 no fold, bit1 no DMA refills, bit2 no barrier,
+// bit4 no sched_group_barrier pinning, bit5 no epilogue stores.
+template <class G, int ABL>
+__global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
+  constexpr int KS = G::KS, BK = G::BK, NW = G::NW, NST = G::NST, U4 = G::U4, MF = G::MF, G4 = G::G4, NF = G::NF;
+  constexpr bool kFold = !(ABL & 1), kDma = !(ABL & 2), kBar = !(ABL & 4), kPin = !(ABL & 16), kStore = !(ABL & 32);
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % G::WM, wn = wave / G::WM;
+  // XCD-aware order (as wino_gemm.hpp): the n_ntiles workgroups reading one V slab share blockIdx.x % 8
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int nt = jb % a.n_ntiles, pt = (jb / a.n_ntiles) * 8 + xcd;
+  if (pt >= a.n_ptiles) return;  // whole workgroup, before any DMA or barrier
+  const int p0 = pt * G::BM, n0 = nt * G::BN;
+
+  int voff[G::A_MAX], uoff[G::B_MAX];
+#pragma unroll
+  for (int i = 0; i < G::A_MAX; ++i) {
+    const int q = wave + NW * i;
+    const int U = (q < G::A_INS ? q : 0) * 64 + lane;
+    const int row = U / U4, u = (U - row * U4) ^ wg::swz<U4>(row);
+    const int p = p0 + row;
+    voff[i] = ((p < a.P ? p : 0) * G::NPT * a.vct + 4 * u) * 4;  // rows past P read tile 0, never stored
+  }
+#pragma unroll
+  for (int i = 0; i < G::B_MAX; ++i) {
+    const int q = wave + NW * i;
+    const int U = (q < G::B_INS ? q : 0) * 64 + lane;
+    const int row = U / U4, u = (U - row * U4) ^ wg::swz<U4>(row);
+    uoff[i] = ((n0 + row) * G::C + 4 * u) * 4;
+  }
+#if __HIP_DEVICE_COMPILE__
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.V), 0, a.vbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
+#endif
+  [[maybe_unused]] lds_f32* lds3 = (lds_f32*)(lds);
+  auto issue = [&](int ab, int ks, int slot) {
+    if constexpr (kDma) {
+#if __HIP_DEVICE_COMPILE__
+      lds_f32* st = lds3 + slot * G::STAGE;
+      const int vso = (ab * a.vct + ks * BK) * 4;
+      const int uso = (ab * a.u_rows * G::C + ks * BK) * 4;
+#pragma unroll
+      for (int i = 0; i < G::A_MAX; ++i)
+        if ((G::A_INS % NW == 0) || wave + NW * i < G::A_INS)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (lds_void*)(st + (wave + NW * i) * 256), 16, voff[i], vso, 0, 0);
+#pragma unroll
+      for (int i = 0; i < G::B_MAX; ++i)
+        if ((G::B_INS % NW == 0) || wave + NW * i < G::B_INS)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + G::A_FL + (wave + NW * i) * 256), 16, uoff[i],
+                                                   uso, 0, 0);
+#endif
+    }
+  };
+
+  const int r16 = lane & 15, kg = lane >> 4;
+  // byte addresses (slot 0) of my rows' fragment units: A rows wm*32 + r16 (+16), B row wn*16 + r16
+  int ra0[G4], ra1[G4], rb[G4];
+#pragma unroll
+  for (int s = 0; s < G4; ++s) {
+    const int u = 4 * s + kg, x0 = wm * 32 + r16, x1 = x0 + 16, y = wn * 16 + r16;
+    ra0[s] = (x0 * BK + 4 * (u ^ wg::swz<U4>(x0))) * 4;
+    ra1[s] = (x1 * BK + 4 * (u ^ wg::swz<U4>(x1))) * 4;
+    rb[s] = (G::A_FL + y * BK + 4 * (u ^ wg::swz<U4>(y))) * 4;
+  }
+
+  float Y[G::NQ][G::NE];  // Y[q][e]: output q of accumulator value e (block e >> 2, register e & 3)
+#pragma unroll
+  for (int q = 0; q < G::NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < G::NE; ++e) Y[q][e] = 0.f;
+  f32x4 acc[2][2] = {};  // [point parity][row block]
+  float cq[2][G::NQ];
+
+  auto frag = [&](int addr) { return *reinterpret_cast<const f32x4*>(reinterpret_cast<const char*>(lds) + addr); };
+  auto fold_one = [&](auto J, auto FI) {
+    constexpr int j = decltype(J)::value, fi = decltype(FI)::value, q = j >> 3, e = j & 7;
+    Y[q][e] = __builtin_fmaf(cq[fi][q], acc[fi][e >> 2][e & 3], Y[q][e]);
+  };
+
+  auto slice = [&](int pb, auto LIT, auto ABS, auto FOLD) {
+    constexpr int lit = decltype(LIT)::value;
+    constexpr bool abs_it = decltype(ABS)::value, fold = decltype(FOLD)::value && kFold;
+    constexpr int ks = lit % KS, ai = (lit / KS) & 1, slot = lit % NST, nlit = lit + NST - 1;
+    constexpr bool refill = !abs_it || nlit < G::TOTAL;
+    constexpr int ahead = abs_it ? ((G::TOTAL - 1 - lit) < NST - 2 ? (G::TOTAL - 1 - lit) : NST - 2) : NST - 2;
+    const int ab = pb + lit / KS;
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int vm = kDma ? ahead * G::PW_MIN : 0;
+    if constexpr (kBar)
+      lds_barrier<vm>();
+    else
+      wg::wait_vm_lgkm<vm>();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    if constexpr (refill) issue(pb + nlit / KS, nlit % KS, nlit % NST);
+    if constexpr (ks == 0) {
+      const float* cr = c_coef64.v[ab];
+#pragma unroll
+      for (int q = 0; q < G::NQ; ++q) cq[ai][q] = cr[q];
+    }
+    constexpr int so = slot * G::STAGE * 4;
+    constexpr int j0 = NF * ks / KS, nj = NF * (ks + 1) / KS - j0;
+    f32x4 fa0[2], fa1[2], fb[2];
+    fa0[0] = frag(ra0[0] + so);
+    fa1[0] = frag(ra1[0] + so);
+    fb[0] = frag(rb[0] + so);
+    static_for<0, G4>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      if constexpr (s + 1 < G4) {
+        fa0[(s + 1) & 1] = frag(ra0[s + 1] + so);
+        fa1[(s + 1) & 1] = frag(ra1[s + 1] + so);
+        fb[(s + 1) & 1] = frag(rb[s + 1] + so);
+      }
+      static_for<0, 4>([&](auto K) {
+        constexpr int k = decltype(K)::value, m = s * 8 + 2 * k;
+        constexpr bool first = ks == 0 && s == 0 && k == 0;
+        acc[ai][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa0[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][0], 0,
+                                                          0, 0);
+        if constexpr (fold)
+          static_for<j0 + nj * m / MF, j0 + nj * (m + 1) / MF>(
+              [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
+        acc[ai][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa1[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][1], 0,
+                                                          0, 0);
+        if constexpr (fold)
+          static_for<j0 + nj * (m + 1) / MF, j0 + nj * (m + 2) / MF>(
+              [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
+      });
+      if constexpr (kPin) {
+        if constexpr (s + 1 < G4) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // the next group's reads
+        static_for<0, 8>([&](auto M) {
+          constexpr int m = s * 8 + decltype(M)::value;
+          constexpr int np = nj * (m + 1) / MF - nj * m / MF;  // fold FMAs behind this MFMA
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if constexpr (fold && np > 0) __builtin_amdgcn_sched_group_barrier(0x002, np, 0);
+        });
+      }
+    });
+    if constexpr (decltype(FOLD)::value && !kFold && ks == 0)
+      Y[0][0] += acc[ai ^ 1][0][0] + acc[ai ^ 1][1][0];  // probe: keep both blocks' MFMAs live
+  };
+  using std::integral_constant;
+  using T_ = integral_constant<bool, true>;
+  using F_ = integral_constant<bool, false>;
+
+  static_for<0, NST - 1>([&](auto IT) {
+    constexpr int it = decltype(IT)::value;
+    issue(it / KS, it % KS, it);
+  });
+  static_for<0, G::UP * KS>([&](auto IT) {
+    constexpr int it = decltype(IT)::value;
+    slice(0, IT, T_{}, integral_constant<bool, (it >= KS)>{});
+  });
+  for (int pb = G::UP; pb < G::NI * G::UP; pb += G::UP) {
+    static_for<0, G::UP * KS>([&](auto LIT) { slice(pb, LIT, F_{}, T_{}); });
+  }
+  static_for<G::NI * G::UP * KS, G::TOTAL>([&](auto IT) { slice(0, IT, T_{}, T_{}); });
+  static_for<0, NF>([&](auto J) { fold_one(J, integral_constant<int, (G::NPT - 1) & 1>{}); });
+
+  // Epilogue: bias + ReLU, then per output q one LDS transpose of the wave's 32 tiles x 16 filters so each
+  // lane stores a 16-B filter group. D layout (16x16x4): lane (r16, kg) holds filter n0 + wn*16 + r16 of
+  // tiles wm*32 + 16*(e >> 2) + 4*kg + (e & 3).
+  __syncthreads();  // the ring is idle (the last slice waited vmcnt(0)): reuse it as scratch
+  constexpr int kTS = 16 + 4;
+  static_assert(G::kLdsBytes >= static_cast<size_t>(NW) * 32 * kTS * 4, "epilogue scratch");
+  float* tr = lds + wave * 32 * kTS;
+  const int fb = n0 + wn * 16;
+  const float bv = a.bias ? a.bias[fb + r16] : 0.f;
+  const OutView o = a.out;
+  int oy0[2], ox0[2], img[2], trd[2];
+  const int grp = 4 * (lane & 3);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int t = (k * 64 + lane) >> 2, p = p0 + wm * 32 + t;
+    const int tj = p % a.tx, pq = p / a.tx;
+    oy0[k] = p < a.P ? (pq % a.ty) * 4 : (1 << 28);  // out of range: never stored
+    ox0[k] = tj * 4;
+    img[k] = pq / a.ty;
+    trd[k] = t * kTS + grp;
+  }
+#pragma unroll
+  for (int q = 0; q < G::NQ; ++q) {
+#pragma unroll
+    for (int e = 0; e < G::NE; ++e) {
+      float v = Y[q][e] + bv;
+      if (a.relu) v = fmaxf(v, 0.f);
+      tr[(16 * (e >> 2) + 4 * kg + (e & 3)) * kTS + r16] = v;
+    }
+    // same-wave LDS accesses complete in order: the reads see the writes above, and the next q's
+    // writes cannot overtake these reads
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(tr + trd[k]);
+      const int oy = oy0[k] + q / 4, ox = ox0[k] + q % 4;
+      if (oy < a.Ho && ox < a.Wo && (kStore || v4.x == -1.f))  // ABL 32: ReLU outputs are never -1
+        *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(img[k] * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) *
+                                               o.Cb + o.c_off + fb + grp) = v4;
+    }
+  }
+}
+
+}  // namespace anx::hip::wg16

@@ -1,4 +1,5 @@
-// Winograd F(3x3, 5x5) convolution for stride-1 5x5 layers (AlexNet Conv2), fp32 end to end.
+// Winograd F(3x3, 5x5) and F(4x4, 5x5) convolution for stride-1 5x5 layers (AlexNet Conv2), fp32 end
+// to end (WinoPlan::m = 3 or 4; the 4x4 tiles: 64 points per 16 outputs, wino_gemm16.hpp).
 //
 //   Y = A^T [ U (.) V ] A,  U = G g G^T (49 x C x K, once per weight set, host fp64 -> fp32),
 //                           V = B^T d B (per 7x7 input tile and channel), 3x3 outputs per tile.
@@ -17,6 +18,7 @@
 
 #include "anx/ops.hpp"
 #include "anx/winograd_f35.hpp"
+#include "anx/winograd_f45.hpp"
 
 namespace anx::hip {
 namespace {
@@ -24,13 +26,32 @@ namespace {
 using f32x2 = __attribute__((ext_vector_type(2))) float;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 constexpr int kT = 256;
-constexpr int kN = wino::kN, kM = wino::kM;
+
+// The two tile sizes (WinoPlan::m): F(3x3,5x5) -> 3x3 outputs from 7x7 inputs, F(4x4,5x5) -> 4x4 from 8x8.
+template <int M>
+struct WT;
+template <>
+struct WT<3> {
+  static constexpr int kM = 3, kN = 7;
+  static constexpr float bt(int a, int u) { return wino::kBT[a][u]; }
+  static constexpr double g(int a, int u) { return wino::kG[a][u]; }
+};
+template <>
+struct WT<4> {
+  static constexpr int kM = 4, kN = 8;
+  static constexpr float bt(int a, int u) { return wino45::kBT[a][u]; }
+  static constexpr double g(int a, int u) { return wino45::kG[a][u]; }
+};
+constexpr int npt(int m) { return (m + 4) * (m + 4); }
 
 // Thread = (tile, 2 channels): consecutive threads read consecutive channel pairs (coalesced NHWC
 // 8-B loads and stores); the 7x7 patch streams through t = B^T d one input row at a time. 98
 // transform registers keep 3+ waves per SIMD. C even.
+template <int M>
 __global__ void __launch_bounds__(kT) wino_in2_kernel(const float* __restrict__ x, float* __restrict__ V, int N, int Hq,
                                                       int Wq, int C, int ty, int tx) {
+  using T = WT<M>;
+  constexpr int kN = T::kN, kM = T::kM;
   const int C2 = C >> 1;
   // 32-bit index math (total < 2^31, checked by the launcher): 64-bit divisions cost more than the loads
   const int total = N * ty * tx * C2;
@@ -59,11 +80,11 @@ __global__ void __launch_bounds__(kT) wino_in2_kernel(const float* __restrict__ 
       }
 #pragma unroll
       for (int a = 0; a < kN; ++a)
-        if (wino::kBT[a][u] != 0.f)
+        if (T::bt(a, u) != 0.f)
 #pragma unroll
           for (int v = 0; v < kN; ++v) {  // per-component fmaf (no packed FMA): the transform's rounding
-            t[a][v].x = fmaf(wino::kBT[a][u], row[v].x, t[a][v].x);
-            t[a][v].y = fmaf(wino::kBT[a][u], row[v].y, t[a][v].y);
+            t[a][v].x = fmaf(T::bt(a, u), row[v].x, t[a][v].x);
+            t[a][v].y = fmaf(T::bt(a, u), row[v].y, t[a][v].y);
           }
     }
     float* out = V + static_cast<size_t>(p) * (kN * kN) * C + c;
@@ -74,9 +95,9 @@ __global__ void __launch_bounds__(kT) wino_in2_kernel(const float* __restrict__ 
         f32x2 s2 = {0.f, 0.f};
 #pragma unroll
         for (int v = 0; v < kN; ++v)
-          if (wino::kBT[b][v] != 0.f) {
-            s2.x = fmaf(wino::kBT[b][v], t[a][v].x, s2.x);
-            s2.y = fmaf(wino::kBT[b][v], t[a][v].y, s2.y);
+          if (T::bt(b, v) != 0.f) {
+            s2.x = fmaf(T::bt(b, v), t[a][v].x, s2.x);
+            s2.y = fmaf(T::bt(b, v), t[a][v].y, s2.y);
           }
         *reinterpret_cast<f32x2*>(out + static_cast<size_t>(a * kN + b) * C) = s2;
       }
@@ -99,12 +120,14 @@ constexpr int kMaxWq = 31;  // window columns held in LDS
 // partial max of a window straddling two Conv1 workgroups in p1 ([N][Hp][Wp][C], images from n_off in
 // the Conv1 launch's tile numbering of ty1 x tx1 tiles per image; q_lo / P / Hp / Wp locate the pool1
 // image in the window): those pixels are max(window, p1), the rest the window's value.
-template <int kPG, int NT, bool POOL = true, bool MERGE = false>  // channels, threads per workgroup
+template <int M, int kPG, int NT, bool POOL = true, bool MERGE = false>  // tile, channels, threads per workgroup
 __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restrict__ c1, float* __restrict__ V, int groups,
                                                           int H1, int W1, int C, int Hq, int Wq, int q_lo, int Hp,
                                                           int Wp, int P, int c1_lo, int ty, int tx,
                                                           const float* __restrict__ p1 = nullptr, int n_off = 0,
                                                           int ty1 = 0, int tx1 = 0) {
+  using T = WT<M>;
+  constexpr int kN = T::kN, kM = T::kM;
   __shared__ __attribute__((aligned(16))) float band[kN][kMaxWq][kPG];
   const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
   const int grp = (j / ty) * 8 + xcd, ti = j % ty;
@@ -182,9 +205,9 @@ __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restric
       t[a] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < kN; ++u)
-        if (wino::kBT[a][u] != 0.f)
+        if (T::bt(a, u) != 0.f)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) t[a][e] = fmaf(wino::kBT[a][u], d[u][e], t[a][e]);
+          for (int e = 0; e < 4; ++e) t[a][e] = fmaf(T::bt(a, u), d[u][e], t[a][e]);
     }
 #pragma unroll
     for (int a = 0; a < kN; ++a) *reinterpret_cast<f32x4*>(&band[a][col][4 * c4]) = t[a];
@@ -204,9 +227,9 @@ __global__ void __launch_bounds__(NT) pool_wino_in_kernel(const float* __restric
       f32x4 s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int v = 0; v < kN; ++v)
-        if (wino::kBT[bb][v] != 0.f)
+        if (T::bt(bb, v) != 0.f)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) s1[e] = fmaf(wino::kBT[bb][v], t[v][e], s1[e]);
+          for (int e = 0; e < 4; ++e) s1[e] = fmaf(T::bt(bb, v), t[v][e], s1[e]);
       *reinterpret_cast<f32x4*>(out + static_cast<size_t>(bb) * C) = s1;
     }
   }
@@ -218,30 +241,41 @@ hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, i
                            int c1_lo, float* V, hipStream_t s, int pool_F, int pool_S) {
   constexpr int pg = 32;
   if (pool_F != 3 || pool_S != 2) return hipErrorInvalidValue;  // the walk below is 3x3 / stride 2 only  // 16 channels (14 KiB of LDS) ran slower under lanes: profiles/r03_transform_lds_*
-  if (w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * kN * kN >= (1L << 31)) return hipErrorInvalidValue;
+  if (w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * npt(w.m) >= (1L << 31)) return hipErrorInvalidValue;
   if (w.P == 0) return hipSuccess;
   const int groups = w.N * (w.C / pg);
   const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
   // 512 threads: 8 waves over the pooling walk and both transforms (bench step +2.7 % over 256 at 128
   // images per GPU; profiles/r03_transform_threads_*)
-  pool_wino_in_kernel<pg, 512><<<grid, 512, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
+  if (w.m == 4)
+    pool_wino_in_kernel<4, pg, 512>
+        <<<grid, 512, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
+  else
+    pool_wino_in_kernel<3, pg, 512>
+        <<<grid, 512, 0, s>>>(c1, V, groups, H1, W1, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P, c1_lo, w.ty, w.tx);
   return hipGetLastError();
 }
 
 hipError_t wino_window_merge_input(const WinoPlan& w, const float* window, const float* p1, int n_off, int ty1, int tx1,
                                    int q_lo, int Hp, int Wp, int P, float* V, hipStream_t s) {
   constexpr int pg = 32;
-  if (w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * kN * kN >= (1L << 31)) return hipErrorInvalidValue;
+  if (w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * npt(w.m) >= (1L << 31)) return hipErrorInvalidValue;
   if (w.P == 0) return hipSuccess;
   const int groups = w.N * (w.C / pg);
   const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
-  pool_wino_in_kernel<pg, 512, false, true><<<grid, 512, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp, Wp, P,
-                                                                 0, w.ty, w.tx, p1, n_off, ty1, tx1);
+  if (w.m == 4)
+    pool_wino_in_kernel<4, pg, 512, false, true><<<grid, 512, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp,
+                                                                      Wp, P, 0, w.ty, w.tx, p1, n_off, ty1, tx1);
+  else
+    pool_wino_in_kernel<3, pg, 512, false, true><<<grid, 512, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp,
+                                                                      Wp, P, 0, w.ty, w.tx, p1, n_off, ty1, tx1);
   return hipGetLastError();
 }
 
-WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups) {
+WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups, int m) {
+  if (m != 3 && m != 4) m = 3;
   WinoPlan w{};
+  w.m = m;
   w.N = N;
   w.Hq = Hq;
   w.Wq = Wq;
@@ -250,24 +284,28 @@ WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups) {
   w.groups = groups;
   w.Ho = Hq - (wino::kR - 1);
   w.Wo = Wq - (wino::kR - 1);
-  w.ty = (w.Ho + kM - 1) / kM;
-  w.tx = (w.Wo + kM - 1) / kM;
+  w.ty = (w.Ho + m - 1) / m;
+  w.tx = (w.Wo + m - 1) / m;
   w.P = N * w.ty * w.tx;
   return w;
 }
 
-bool wino_eligible(int F, int S, int C, int K, int groups) {
-  // the fused GEMM's configurations: 96 or 48 channels per group, filters per group a multiple of 64
+bool wino_eligible(int F, int S, int C, int K, int groups, int m) {
+  // the fused GEMMs' configurations: F(3,5) 96 or 48 channels per group and filters per group a multiple
+  // of 64; F(4,5) one group of 96 channels and a multiple of 32 filters
   if (F != wino::kR || S != 1 || groups < 1 || C % groups || K % groups) return false;
   const int Cg = C / groups, Kg = K / groups;
+  if (m == 4) return groups == 1 && C == 96 && K % 32 == 0;
   return (Cg == 96 || Cg == 48) && Kg % 64 == 0;
 }
 
-size_t wino_v_floats(const WinoPlan& w) { return static_cast<size_t>(w.P) * kN * kN * w.C; }
-size_t wino_u_floats(const WinoPlan& w) { return static_cast<size_t>(kN * kN) * w.K * (w.C / w.groups); }
+size_t wino_v_floats(const WinoPlan& w) { return static_cast<size_t>(w.P) * npt(w.m) * w.C; }
+size_t wino_u_floats(const WinoPlan& w) { return static_cast<size_t>(npt(w.m)) * w.K * (w.C / w.groups); }
 
-void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff) {
-  // U[(ab*groups + g)*Kg + k][c] = (G g_{k,c} G^T)[a][b], computed in fp64 then rounded once.
+template <int M>
+static void transform_weights(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff) {
+  using T = WT<M>;
+  constexpr int kN = T::kN;
   const int Cg = w.C / w.groups, Kg = w.K / w.groups, R = wino::kR;
   u_kcff.assign(wino_u_floats(w), 0.f);
   for (int g = 0; g < w.groups; ++g)
@@ -278,38 +316,54 @@ void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::ve
         for (int a = 0; a < kN; ++a)
           for (int v = 0; v < R; ++v) {
             double s = 0;
-            for (int u = 0; u < R; ++u) s += wino::kG[a][u] * f[u * R + v];
+            for (int u = 0; u < R; ++u) s += T::g(a, u) * f[u * R + v];
             tmp[a][v] = s;
           }
         for (int a = 0; a < kN; ++a)
           for (int b = 0; b < kN; ++b) {
             double s = 0;
-            for (int v = 0; v < R; ++v) s += tmp[a][v] * wino::kG[b][v];
+            for (int v = 0; v < R; ++v) s += tmp[a][v] * T::g(b, v);
             const int ab = a * kN + b;
             u_kcff[(static_cast<size_t>(ab * w.groups + g) * Kg + k) * Cg + c] = static_cast<float>(s);
           }
       }
 }
 
+void wino_transform_weights_host(const WinoPlan& w, const float* w_kcff, std::vector<float>& u_kcff) {
+  // U[(ab*groups + g)*Kg + k][c] = (G g_{k,c} G^T)[a][b], computed in fp64 then rounded once.
+  if (w.m == 4)
+    transform_weights<4>(w, w_kcff, u_kcff);
+  else
+    transform_weights<3>(w, w_kcff, u_kcff);
+}
+
 hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s) {
   const long n = static_cast<long>(w.P) * w.C;
   if (n >= (1L << 31) || w.C % 2) return hipErrorInvalidValue;
-  if (w.C % 32 == 0 && w.Wq <= kMaxWq && n * kN * kN < (1L << 31)) {  // band form (bit-identical V)
+  if (w.C % 32 == 0 && w.Wq <= kMaxWq && n * npt(w.m) < (1L << 31)) {  // band form (bit-identical V)
     if (w.P == 0) return hipSuccess;
     const int groups = w.N * (w.C / 32);
     const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
-    pool_wino_in_kernel<32, 512, false>
-        <<<grid, 512, 0, s>>>(x, V, groups, 0, 0, w.C, w.Hq, w.Wq, 0, 0, 0, 0, 0, w.ty, w.tx);
+    if (w.m == 4)
+      pool_wino_in_kernel<4, 32, 512, false>
+          <<<grid, 512, 0, s>>>(x, V, groups, 0, 0, w.C, w.Hq, w.Wq, 0, 0, 0, 0, 0, w.ty, w.tx);
+    else
+      pool_wino_in_kernel<3, 32, 512, false>
+          <<<grid, 512, 0, s>>>(x, V, groups, 0, 0, w.C, w.Hq, w.Wq, 0, 0, 0, 0, 0, w.ty, w.tx);
     return hipGetLastError();
   }
   const long g = (n / 2 + kT - 1) / kT;
   const unsigned gg = static_cast<unsigned>(g < (1 << 20) ? g : (1 << 20));
-  wino_in2_kernel<<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
+  if (w.m == 4)
+    wino_in2_kernel<4><<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
+  else
+    wino_in2_kernel<3><<<gg, kT, 0, s>>>(x, V, w.N, w.Hq, w.Wq, w.C, w.ty, w.tx);
   return hipGetLastError();
 }
 
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,
                       hipStream_t s, const Knobs& k) {
+  if (w.m == 4) return wino_gemm_conv2_f45(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.K, relu, s, k.conv2_occ);
   return wino_gemm_conv2(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.C, w.K, w.groups, relu, s, k.conv2_occ);
 }
 

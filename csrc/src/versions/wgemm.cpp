@@ -82,7 +82,7 @@ int main(int argc, char** argv) {
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!std::strcmp(argv[i], "--images")) images = std::atoi(argv[i + 1]);
     else if (!std::strcmp(argv[i], "--iters")) iters = std::atoi(argv[i + 1]);
-    else if (!std::strcmp(argv[i], "--conv")) only = std::atoi(argv[i + 1]);  // 1 or 2: that conv only
+    else if (!std::strcmp(argv[i], "--conv")) only = std::atoi(argv[i + 1]);  // 1 or 2: that conv only; 4: Conv2 F(4x4,5x5)
     else if (!std::strcmp(argv[i], "--cfg")) only_cfg = std::atoi(argv[i + 1]);
     else if (!std::strcmp(argv[i], "--occ")) occ = std::atoi(argv[i + 1]);  // workgroups-per-CU cap
   }
@@ -94,7 +94,7 @@ int main(int argc, char** argv) {
   const Knobs kn = default_knobs();
 
   // ---- Conv2: 31x31x96 window -> 27x27x256
-  if (only != 1) {
+  if (only != 1 && only != 4) {
     const hip::WinoPlan w = hip::make_wino_plan(images, 31, 31, 96, 256, 1);
     float* V = upload_random(hip::wino_v_floats(w), 1, -1.f, 1.f);
     float* U = upload_random(hip::wino_u_floats(w), 2, -0.05f, 0.05f);
@@ -131,8 +131,70 @@ int main(int argc, char** argv) {
     for (float* p : {V, U, b, y0, y1}) CHECK(hipFree(p));
   }
 
+  // ---- Conv2 as F(4x4,5x5) (--conv 4): a real window and weights through both tile sizes; the 3x3-tile
+  // output is the reference of the 4x4-tile arms (both ~1e-6 of the direct sum)
+  if (only == 4 || only == 0) {
+    const hip::WinoPlan w3 = hip::make_wino_plan(images, 31, 31, 96, 256, 1, 3);
+    const hip::WinoPlan w4 = hip::make_wino_plan(images, 31, 31, 96, 256, 1, 4);
+    std::vector<float> xh(static_cast<size_t>(images) * 31 * 31 * 96, 0.f);
+    std::mt19937 g(7);
+    std::uniform_real_distribution<float> dx(0.f, 1.f), dw(-0.02f, 0.02f);
+    for (int n = 0; n < images; ++n)
+      for (int y = 2; y < 29; ++y)
+        for (int x = 2; x < 29; ++x)
+          for (int c = 0; c < 96; ++c) xh[((static_cast<size_t>(n) * 31 + y) * 31 + x) * 96 + c] = dx(g);
+    std::vector<float> wh(static_cast<size_t>(256) * 96 * 25);
+    for (auto& v : wh) v = dw(g);
+    std::vector<float> u3, u4;
+    hip::wino_transform_weights_host(w3, wh.data(), u3);
+    hip::wino_transform_weights_host(w4, wh.data(), u4);
+    float *x = nullptr, *U3 = nullptr, *U4 = nullptr, *V3 = nullptr, *V4 = nullptr, *y0 = nullptr, *y1 = nullptr;
+    const size_t ny = static_cast<size_t>(images) * 27 * 27 * 256;
+    CHECK(hipMalloc(&x, xh.size() * 4));
+    CHECK(hipMemcpy(x, xh.data(), xh.size() * 4, hipMemcpyHostToDevice));
+    CHECK(hipMalloc(&U3, u3.size() * 4));
+    CHECK(hipMemcpy(U3, u3.data(), u3.size() * 4, hipMemcpyHostToDevice));
+    CHECK(hipMalloc(&U4, u4.size() * 4));
+    CHECK(hipMemcpy(U4, u4.data(), u4.size() * 4, hipMemcpyHostToDevice));
+    CHECK(hipMalloc(&V3, hip::wino_v_floats(w3) * 4));
+    CHECK(hipMalloc(&V4, hip::wino_v_floats(w4) * 4));
+    CHECK(hipMalloc(&y0, ny * 4));
+    CHECK(hipMalloc(&y1, ny * 4));
+    float* b = upload_random(256, 3, 0.f, 0.1f);
+    const hip::OutView o0{y0, 27, 27, 256, 0, 0, 0}, o1{y1, 27, 27, 256, 0, 0, 0};
+    const double ti3 = time_us([&] { return hip::wino_input(w3, x, V3, nullptr); }, iters);
+    const double ti4 = time_us([&] { return hip::wino_input(w4, x, V4, nullptr); }, iters);
+    const double t3 = time_us([&] { return hip::wino_conv2(w3, V3, U3, b, o0, true, nullptr, kn); }, iters);
+    const auto ref = download(y0, ny);
+    const double f3 = 2.0 * w3.P * 49 * 96 * 256, f4 = 2.0 * w4.P * 64 * 96 * 256;
+    std::printf("{\"conv\": 4, \"images\": %d, \"arm\": \"F(3,5) input transform\", \"us\": %.1f}\n", images, ti3);
+    std::printf("{\"conv\": 4, \"images\": %d, \"arm\": \"F(4,5) input transform\", \"us\": %.1f}\n", images, ti4);
+    std::printf("{\"conv\": 4, \"images\": %d, \"arm\": \"F(3,5) GEMM (production)\", \"us\": %.1f, \"tflops\": %.1f, "
+                "\"direct_equiv_tflops\": %.1f}\n",
+                images, t3, f3 / t3 * 1e-6, 2.0 * images * 27 * 27 * 256 * 96 * 25 / t3 * 1e-6);
+    for (int cfg = 0; cfg < 9; ++cfg)
+      for (int abl : kAbl) {
+        if (only_cfg >= 0 && cfg != only_cfg) continue;
+        CHECK(hipMemset(y1, 0, ny * 4));
+        if (hip::wino_gemm_conv2_f45(V4, U4, b, o1, w4.P, w4.ty, w4.tx, 27, 27, 256, true, nullptr, occ, abl, cfg) ==
+            hipErrorInvalidValue)
+          continue;
+        const double t = time_us(
+            [&] {
+              return hip::wino_gemm_conv2_f45(V4, U4, b, o1, w4.P, w4.ty, w4.tx, 27, 27, 256, true, nullptr, occ, abl, cfg);
+            },
+            iters);
+        double rmax = 0;
+        const double d = max_abs_diff(download(y1, ny), ref, &rmax);
+        std::printf("{\"conv\": 4, \"images\": %d, \"arm\": \"F(4,5) GEMM cfg=%d abl=%d\", \"us\": %.1f, \"tflops\": %.1f, "
+                    "\"direct_equiv_tflops\": %.1f, \"max_abs_diff_vs_f35\": %.3g, \"ref_max\": %.3g}\n",
+                    images, cfg, abl, t, f4 / t * 1e-6, 2.0 * images * 27 * 27 * 256 * 96 * 25 / t * 1e-6, d, rmax);
+      }
+    for (float* p : {x, U3, U4, V3, V4, y0, y1, b}) CHECK(hipFree(p));
+  }
+
   // ---- Conv1: 227x227x3 image -> 55x55x96 (polyphase F(3x3,3x3))
-  if (only != 2) {
+  if (only != 2 && only != 4) {
     const hip::Conv1WinoPlan w = hip::make_conv1_wino_plan(images, 227, 227, 96, 11);
     float* x = upload_random(static_cast<size_t>(images) * 227 * 227 * 3, 4, 0.f, 0.1f);
     std::vector<float> wh(static_cast<size_t>(96) * 3 * 11 * 11);

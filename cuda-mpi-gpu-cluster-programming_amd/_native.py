@@ -97,6 +97,7 @@ _SIGS = {
     "anx_conv_pack": (_I, [C.POINTER(_I), _P, _P, _P]),
     "anx_conv1_wino": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P]),
     "anx_conv2_wino": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P]),
+    "anx_conv2_wino_tile": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P, _I]),
     "anx_engine_set_knob": (_I, [_P, C.c_char_p, _I]),
     "anx_engine_get_knob": (_I, [_P, C.c_char_p, C.POINTER(_I)]),
     "anx_full_set_knob": (_I, [_P, C.c_char_p, _I]),

@@ -132,6 +132,13 @@ for s in "$@"; do
     wgemm)
       run wg300 120 $B/anx_wgemm --images 300 --iters 20
       run wg64 120 $B/anx_wgemm --images 64 --iters 20 ;;
+    wg45)  # Conv2 F(4x4,5x5) GEMM configurations vs the F(3x3,5x5) production GEMM (anx_wgemm --conv 4)
+      run wg45_128 120 $B/anx_wgemm --conv 4 --images 128 --iters 20
+      run wg45_300 120 $B/anx_wgemm --conv 4 --images 300 --iters 20 ;;
+    wg45pmc)
+      timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+        --kernel-trace --output-format csv -d "$O/wg45pmc" -o run -- $B/anx_wgemm --conv 4 --images 128 --iters 3 \
+        > "$O/wg45pmc.log" 2>&1 && python3 tools/pmc_clock.py "$O/wg45pmc" | tee "$O/wg45pmc.md" || { echo "== wg45pmc FAILED"; exit 1; } ;;
     wgpmc)
       timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
         --kernel-trace --output-format csv -d "$O/wgpmc" -o run -- $B/anx_wgemm --images 300 --iters 3 \

@@ -16,6 +16,7 @@ pytestmark = pytest.mark.gpu
 # Bounds relative to Σ|x·w| per output. F(3x3,5x5) (Conv2) interpolates at 7 points (0, ±1, ±2, ±1/2)
 # and F(3x3,3x3) (Conv1 polyphase) at 5, so the transforms cancel more for Conv2. MI355X run: Conv2
 # max 1.8-2.6e-6 (mean 8e-8), Conv1 max 1.0-1.3e-6 (mean 4.4e-8). A broken transform or fold is >=1e-3.
+# F(4x4,5x5) (8 points, {0, +-1, +-2, +-1/2, inf}) sits ~1.3x above F(3,5) in tools/winograd_numerics.py.
 BOUND_CONV2 = 1e-5
 BOUND_CONV1 = 4e-6
 
@@ -28,9 +29,11 @@ def _rel_to_terms(y, x, w, b, S, P, groups=1):
     return rel.max().item()
 
 
-@pytest.mark.parametrize("N,groups", [(12, 1), (12, 2), (9, 1), (128, 1), (140, 2)])
-def test_conv2_winograd_randn_he(cuda, N, groups):
-    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights."""
+@pytest.mark.parametrize("N,groups,tile", [(12, 1, 3), (12, 2, 3), (9, 1, 3), (128, 1, 3), (140, 2, 3), (12, 1, 4),
+                                          (9, 1, 4), (128, 1, 4), (141, 1, 4)])
+def test_conv2_winograd_randn_he(cuda, N, groups, tile):
+    """Conv2 (31x31 padded window, 96 -> 256, 5x5): randn inputs, He-normal weights; Winograd F(3x3,5x5)
+    and F(4x4,5x5) (wino_gemm16.hpp: 16x16x4 MFMAs, 4x4 output tiles with a clipped last row/column)."""
     torch.manual_seed(21 + N)
     C, K = 96, 256
     x = torch.randn(N, 31, 31, C, device=cuda)
@@ -41,8 +44,8 @@ def test_conv2_winograd_randn_he(cuda, N, groups):
     w = torch.randn(K, C // groups, 5, 5) * math.sqrt(2.0 / (C // groups * 25))
     b = torch.randn(K, device=cuda) * 0.1
     y = torch.full((N, 27, 27, K), float("nan"), device=cuda)
-    nat.call("anx_conv2_wino", x.data_ptr(), N, 31, 31, C, w.contiguous().data_ptr(), K, groups, b.data_ptr(),
-             y.data_ptr(), 0, nat.stream_ptr(cuda))
+    nat.call("anx_conv2_wino_tile", x.data_ptr(), N, 31, 31, C, w.contiguous().data_ptr(), K, groups, b.data_ptr(),
+             y.data_ptr(), 0, nat.stream_ptr(cuda), tile)
     assert torch.isfinite(y).all()
     assert _rel_to_terms(y, x, w.to(cuda), b, 1, 0, groups) < BOUND_CONV2
 
@@ -61,13 +64,16 @@ def test_conv1_polyphase_winograd_randn_he(cuda, N):
     assert _rel_to_terms(y, x, w.to(cuda), b, 4, 0) < BOUND_CONV1
 
 
-def test_full_blocks_randn_he_vs_oracle(cuda):
-    """The whole Blocks 1-2 engine (both Winograd convs, pools, LRN) at randn/He scale."""
+@pytest.mark.parametrize("tile", [3, 4])
+def test_full_blocks_randn_he_vs_oracle(cuda, tile):
+    """The whole Blocks 1-2 engine (both Winograd convs, pools, LRN) at randn/He scale, Conv2 on either
+    Winograd tile (Knobs::conv2_tile)."""
     torch.manual_seed(5)
     w1 = torch.randn(96, 3, 11, 11) * math.sqrt(2.0 / 363)
     w2 = torch.randn(256, 96, 5, 5) * math.sqrt(2.0 / 2400)
     ws = {"w1": w1, "b1": torch.randn(96) * 0.1, "w2": w2, "b2": torch.randn(256) * 0.1}
-    m = AlexNetBlocks(ws, device=cuda, max_batch=24)
+    m = AlexNetBlocks(ws, device=cuda, max_batch=24, knobs={"conv2_tile": tile})
+    assert m.get_knob("conv2_tile") == tile
     x = torch.randn(24, 227, 227, 3)
     y = m(x.to(cuda)).cpu().double()
     ref = blocks_forward(x, m.weights, m.b1, m.b2)
