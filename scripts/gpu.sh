@@ -57,7 +57,7 @@ for s in "$@"; do
              ${SWEEP_ARGS:-} ;;
     ab) run ab 900 python tools/ab_variants.py --arms "${AB_ARMS:-|conv1_occ=3}" --batch "${AB_BATCH:-300}" \
           --lanes "${AB_LANES:-1}" --rounds "${AB_ROUNDS:-5}" ;;
-    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 10 --warmup 3 --no-full $BARGS ;;
+    prof) run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 bench.py --steps 10 --warmup 3 --no-full $BARGS ;;
     pmc)
       pmc pmc1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_INSTS_MFMA
       pmc pmc2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INST_LEVEL_VMEM
