@@ -44,7 +44,7 @@ before this process touches the GPU; ``b1_engine_cold_ms`` = a fresh engine on t
 initialised device; ``b1_warm_ms`` = the median of further calls. ``vs_baseline`` is the
 like-for-like cold ratio 610.661 ms / ``b1_process_cold_ms`` (``vs_baseline_kind`` says which ratio
 it is); the warm ratio is ``b1_vs_reference_warm``. ``mfma_tflops`` counts the matrix-core FLOPs the Winograd
-kernels execute (0.278 GFLOP/image); ``direct_equiv_tflops`` counts direct-convolution FLOPs
+kernels execute (0.237 GFLOP/image with 4x4-tile Conv2); ``direct_equiv_tflops`` counts direct-convolution FLOPs
 (1.107 GFLOP/image) and can exceed the chip's fp32 peak because Winograd does 4x fewer multiplies.
 """
 from __future__ import annotations
@@ -173,10 +173,12 @@ def batch1_latency(dev, reps: int = 20) -> dict:
     """The reference's V3 configuration (v3_cuda_only/src/main_cuda.cpp:30-35): one image, timed
     around H2D + forward + D2H. cold = a fresh engine (allocation, weight upload, first launch) on
     an already-initialised device; warm = median of `reps` further calls."""
+    from anx.utils.init import init_weights
     x = (torch.rand(1, 227, 227, 3) * 0.1).pin_memory()
-    torch.cuda.synchronize()
+    w = init_weights("rand", 7)  # host weights exist before the clock starts (the reference's V3 fills them
+    torch.cuda.synchronize()      # on the host before its timed region too)
     t0 = time.perf_counter()
-    m = AlexNetBlocks(init="rand", seed=7, device=dev, max_batch=1)
+    m = AlexNetBlocks(w, device=dev, max_batch=1)
     y = m(x.to(dev, non_blocking=True)).cpu()
     cold = (time.perf_counter() - t0) * 1e3
     ts = []
@@ -276,9 +278,11 @@ def v5_halo_subrecords(a, world: int, rank: int, GB: int, dev, g) -> dict:
                     "bytes_per_step": v5.get("bytes_per_step"), "checksum": j.get("checksum")}
             except Exception as e:  # a sub-record never takes the headline down
                 out[f"v5_rows2_{tr}"] = {"error": repr(e)[:300]}
+        _match_arms(out, "loopback", "peer", "checksum")
         return out
     if world % 2:
         return out
+    from anx.parallel import selfcheck
     from anx.parallel.workloads import NativeV5
     from anx.utils.init import init_weights
     b1, b2 = anx.config.blocks()
@@ -297,13 +301,25 @@ def v5_halo_subrecords(a, world: int, rank: int, GB: int, dev, g) -> dict:
         dist.barrier()
         el = time.perf_counter() - t0
         d = wl.describe()
+        y = wl.output()  # rank 0: the gathered output of the last step (both transports: identical math)
         out[f"v5_rows2_{tr}"] = {"ranks": world, "row_ways": 2, "transport": d.get("transport"),
                                  "images_per_s": round(GB * 10 / el, 1), "ms_per_step": round(el * 100, 4),
                                  "phases_ms": wl.phase_ms(), "halo_exchange": d.get("halo_exchange"),
                                  "halo_bytes_per_step": d.get("halo_bytes_per_step"),
-                                 "bytes_per_step": d.get("bytes_per_step")}
+                                 "bytes_per_step": d.get("bytes_per_step"),
+                                 "output_crc": selfcheck.tensor_crc(y) if y is not None else None}
         wl.close()
+    _match_arms(out, "rccl", "peer", "output_crc")
     return out
+
+
+def _match_arms(out: dict, a: str, b: str, key: str) -> None:
+    """The peer transport's cross-device ordering (flag write after the copy into the receiver's memory)
+    checked on the node that runs it: both arms compute the same tiles with the same kernels, so their
+    outputs must agree bit for bit; ``outputs_match`` goes into the second arm's record."""
+    ra, rb = out.get(f"v5_rows2_{a}") or {}, out.get(f"v5_rows2_{b}") or {}
+    if ra.get(key) is not None and rb.get(key) is not None:
+        rb["outputs_match_" + a] = ra[key] == rb[key]
 
 
 def _oracle(model):
@@ -538,7 +554,8 @@ def main():
         except Exception as e:  # the headline record must not depend on the extension
             full = {"error": repr(e)[:300]}
     if rank == 0:
-        mf = mfma_flops_per_image()
+        from anx.utils.tuning import default_knob
+        mf = mfma_flops_per_image(conv2_tile=int(knobs.get("conv2_tile", default_knob("conv2_tile"))))
         if wl is None:
             par, scaling = f"dp{world}", "weak"
             pipeline = (("root scatter -> compute -> gather (RCCL), %d micro-batches%s"

@@ -102,14 +102,17 @@ def flops_per_image(H: int = IN_H, W: int = IN_W, b1: BlockSpec = BLOCK1, b2: Bl
     return 2.0 * (c1 + c2)
 
 
-def mfma_flops_per_image(H: int = IN_H, W: int = IN_W, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2) -> float:
+def mfma_flops_per_image(H: int = IN_H, W: int = IN_W, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2,
+                         conv2_tile: int = 4) -> float:
     """FLOPs the matrix cores actually execute per image on the default fp32 path (2 per MAC):
     Conv1 as polyphase Winograd F(3x3,3x3) = ceil(H1/3) x ceil(W1/3) tiles x 25 points x 48
-    channels x C1 filters, Conv2 as Winograd F(3x3,5x5) = ceil(H2/3) x ceil(W2/3) tiles x 49 points x
-    C1 x C2 / groups. 0.278 GFLOP for the default, against 1.107 of direct convolution
-    (flops_per_image): the ratio is what the fast algorithms save, and this count (not the direct
-    one) is what a matrix-core roofline compares against (157 TF/s fp32 peak)."""
+    channels x C1 filters, Conv2 as Winograd F(m x m,5x5) = ceil(H2/m) x ceil(W2/m) tiles x (m+4)^2
+    points x C1 x C2 / groups, m = the engine's ``conv2_tile`` (4, the default, for one group of 96
+    channels; 3 otherwise). 0.237 GFLOP for the default (0.278 with 3x3 tiles), against 1.107 of direct
+    convolution (flops_per_image): the ratio is what the fast algorithms save, and this count (not the
+    direct one) is what a matrix-core roofline compares against (157 TF/s fp32 peak)."""
     d = blocks_dims(H, W, b1, b2)
+    m = 4 if conv2_tile == 4 and b2.conv.groups == 1 and b2.conv.C == 96 else 3
     c1 = -(-d.H1 // 3) * -(-d.W1 // 3) * 25 * 48 * d.C1
-    c2 = -(-d.H2 // 3) * -(-d.W2 // 3) * 49 * (b2.conv.C // b2.conv.groups) * d.C2
+    c2 = -(-d.H2 // m) * -(-d.W2 // m) * (m + 4) ** 2 * (b2.conv.C // b2.conv.groups) * d.C2
     return 2.0 * (c1 + c2)

@@ -58,6 +58,10 @@ def test_bench_workloads_one_gpu(workload):
         assert "RCCL" not in c["pipeline"] and "per-rank chunked H2D" in c["pipeline"]
     else:  # the native runtime: critical-path phases, balanced layout, transport
         assert c["phases_ms"]["stage2"] > 0 and c["transport"] == "rccl" and c["imbalance"] == 1.0
+        # the halo-on sub-records: both device transports, the same output bit for bit
+        peer, loop = rec["v5_rows2_peer"], rec["v5_rows2_loopback"]
+        assert peer["halo_bytes_per_step"] > 0 and loop["checksum"] is not None
+        assert peer["outputs_match_loopback"] is True
 
 
 @pytest.mark.gpu

@@ -14,6 +14,13 @@ from collections import defaultdict
 
 
 def load(path):
+    import os
+    if os.path.isdir(path):  # a rocprofv3 -d DIR: its kernel_trace csv or results db
+        import glob
+        hits = glob.glob(os.path.join(path, "*kernel_trace.csv")) or glob.glob(os.path.join(path, "*.db"))
+        if not hits:
+            raise SystemExit(f"no kernel trace under {path}")
+        path = hits[0]
     rows = []
     if path.endswith(".db"):
         c = sqlite3.connect(path)
