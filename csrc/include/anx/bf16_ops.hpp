@@ -54,6 +54,7 @@ hipError_t conv2d_bf16(const ConvPlanB& p, const void* x, const void* wpacked, c
 // those three without it (A/B); 12 / 13 = 256x256 / 256x128 ping-pong (two staggered 4-wave
 // groups; A 2 / B 3 stages; conv only).
 int conv_bf16_big_cfgs();
+constexpr int kConvBf16BigCfgs = 17;  // == conv_bf16_big_cfgs() (static_assert in conv_bf16_big.hip); knob range
 bool conv_bf16_big_ok(const ConvPlanB& p, int cfg, const OutViewB& out);
 // The config a cost model of wave quantization picks for this launch (-1: none applies).
 int pick_bf16_big_cfg(const ConvPlanB& p, const OutViewB& out, int cus = 256);

@@ -9,7 +9,6 @@
 #include <vector>
 #include <algorithm>
 
-#include "anx/bf16_ops.hpp"
 #include "anx/cost.hpp"
 #include "anx/cpu_engine.hpp"
 #include "anx/engine.hpp"
@@ -240,48 +239,6 @@ int anx_engine_window(void* e, const anx_tile_c* t, int n, int r, float** ptr, s
   return 0;
 }
 
-int anx_full_weight_sizes(int classes, int groups2, size_t* wn, size_t* bn) {
-  anx::full_weight_shapes(classes, groups2, wn, bn);
-  return 0;
-}
-
-int anx_full_create(void** out, const float* const* weights, const float* const* biases, int classes,
-                    int max_batch, int groups2, int lrn_mode) {
-  return guarded("anx_full_create", [&] {
-    size_t wn[8], bn[8];
-    anx::full_weight_shapes(classes, groups2, wn, bn);
-    anx::FullWeights w;
-    for (int i = 0; i < 8; ++i) {
-      w.w[i].assign(weights[i], weights[i] + wn[i]);
-      w.b[i].assign(biases[i], biases[i] + bn[i]);
-    }
-    *out = new anx::FullEngine(w, classes, max_batch, groups2, static_cast<anx::LrnMode>(lrn_mode));
-    return 0;
-  });
-}
-
-int anx_full_destroy(void* e) {
-  delete static_cast<anx::FullEngine*>(e);
-  return 0;
-}
-
-int anx_full_forward(void* e, const float* x, int N, float* logits, void* stream) {
-  return guarded("anx_full_forward", [&] {
-    return hip_status(static_cast<anx::FullEngine*>(e)->forward(x, N, logits, S(stream)), "full forward");
-  });
-}
-
-int anx_full_forward_mark(void* e, const float* x, int N, float* logits, void* stream) {
-  return guarded("anx_full_forward_mark", [&] {
-    return hip_status(static_cast<anx::FullEngine*>(e)->forward(x, N, logits, S(stream), true), "full forward");
-  });
-}
-
-int anx_full_wait_mark(void* e, void* stream) {
-  return guarded("anx_full_wait_mark", [&] {
-    return hip_status(static_cast<anx::FullEngine*>(e)->wait_mark(S(stream)), "full wait mark");
-  });
-}
 
 int anx_cpu_engine_create(void** out, const anx_block_c* b1, const anx_block_c* b2, int H, int W, const float* w1,
                           const float* bias1, const float* w2, const float* bias2) {
@@ -413,20 +370,6 @@ int anx_engine_set_knob(void* e, const char* name, int value) {
 }
 int anx_engine_get_knob(void* e, const char* name, int* value) {
   if (anx::get_knob(static_cast<anx::BlocksEngine*>(e)->knobs(), name, value) != 0)
-    return fail(std::string("unknown knob: ") + (name ? name : "(null)"));
-  return 0;
-}
-int anx_full_tap(void* e, int i, int N, void* dst, size_t* elems, void* stream) {
-  *elems = static_cast<anx::FullEngine*>(e)->tap(i, N, dst, S(stream));
-  return *elems ? 0 : fail("anx_full_tap: bad tap index or batch");
-}
-int anx_full_set_knob(void* e, const char* name, int value) {
-  if (anx::set_knob(static_cast<anx::FullEngine*>(e)->knobs(), name, value) != 0)
-    return fail(std::string("bad knob or value: ") + (name ? name : "(null)"));
-  return 0;
-}
-int anx_full_get_knob(void* e, const char* name, int* value) {
-  if (anx::get_knob(static_cast<anx::FullEngine*>(e)->knobs(), name, value) != 0)
     return fail(std::string("unknown knob: ") + (name ? name : "(null)"));
   return 0;
 }

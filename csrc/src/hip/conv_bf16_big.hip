@@ -517,6 +517,7 @@ size_t lds_bytes(const BigCfg& c) {
 
 }  // namespace
 
+static_assert(kNumCfg == kConvBf16BigCfgs, "bf16_ops.hpp: kConvBf16BigCfgs");
 int conv_bf16_big_cfgs() { return kNumCfg; }
 
 bool conv_bf16_big_ok(const ConvPlanB& p, int cfg, const OutViewB& out) {

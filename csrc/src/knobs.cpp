@@ -54,7 +54,7 @@ const Field* find(const char* name) {
 bool valid(const Field& f, int v) {
   if (v < f.lo || v > f.hi) return false;
   if (std::strcmp(f.name, "bf16_glds") == 0) return v == 0 || v == 2 || v == 3;
-  if (std::strcmp(f.name, "bf16_big") == 0) return v < hip::conv_bf16_big_cfgs();
+  if (std::strcmp(f.name, "bf16_big") == 0) return v < hip::kConvBf16BigCfgs;
   if (std::strcmp(f.name, "force_vec4") == 0) return hip::conv_variant_valid(0, v);
   if (std::strcmp(f.name, "force_scalar") == 0) return hip::conv_variant_valid(1, v);
   return true;

@@ -21,6 +21,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before libanx)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ANX_LIB", os.path.join(_HERE, "lib", "libanx.so"))
 DIST_PATH = os.path.join(os.path.dirname(LIB_PATH), "libanx_dist.so")
+BF16_PATH = os.path.join(os.path.dirname(LIB_PATH), "libanx_bf16.so")
 
 _lock = threading.Lock()
 _lib = None
@@ -80,12 +81,6 @@ _SIGS = {
     "anx_cpu_engine_stage2": (_I, [_P, _I, C.POINTER(TileC), _P]),
     "anx_cpu_engine_window": (_I, [_P, C.POINTER(TileC), _I, _I, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_SZ)]),
     "anx_memcpy2d_host": (_I, [_P, _SZ, _P, _SZ, _SZ, _SZ]),
-    "anx_full_weight_sizes": (_I, [_I, _I, C.POINTER(_SZ), C.POINTER(_SZ)]),
-    "anx_full_create": (_I, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), _I, _I, _I, _I]),
-    "anx_full_destroy": (_I, [_P]),
-    "anx_full_forward": (_I, [_P, _P, _I, _P, _P]),
-    "anx_full_forward_mark": (_I, [_P, _P, _I, _P, _P]),
-    "anx_full_wait_mark": (_I, [_P, _P]),
     "anx_memcpy2d_async": (_I, [_P, _SZ, _P, _SZ, _SZ, _SZ, _P]),
     "anx_conv2d_direct": (_I, [_P, _P, _P, _P] + [_I] * 10 + [_P]),
     "anx_relu": (_I, [_P, _SZ, _P]),
@@ -100,9 +95,6 @@ _SIGS = {
     "anx_conv2_wino_tile": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _I, _P, _I]),
     "anx_engine_set_knob": (_I, [_P, C.c_char_p, _I]),
     "anx_engine_get_knob": (_I, [_P, C.c_char_p, C.POINTER(_I)]),
-    "anx_full_set_knob": (_I, [_P, C.c_char_p, _I]),
-    "anx_full_tap": (_I, [_P, _I, _I, _P, C.POINTER(_SZ), _P]),
-    "anx_full_get_knob": (_I, [_P, C.c_char_p, C.POINTER(_I)]),
     "anx_default_knob": (_I, [C.c_char_p, C.POINTER(_I)]),
     "anx_conv2d_mfma": (_I, [C.POINTER(_I), _P, _P, _P, _P, _P] + [_I] * 6 + [_I, _P]),
     "anx_cpu_conv2d": (_I, [_P, _P, _P, _P] + [_I] * 10),
@@ -150,6 +142,21 @@ def available() -> bool:
         return True
     except NativeError:
         return False
+
+
+# libanx_bf16: the full-AlexNet bf16 engine (its own library, loaded on first use)
+_BF16_SIGS = {
+    "anx_full_weight_sizes": (_I, [_I, _I, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "anx_full_create": (_I, [C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), _I, _I, _I, _I]),
+    "anx_full_destroy": (_I, [_P]),
+    "anx_full_forward": (_I, [_P, _P, _I, _P, _P]),
+    "anx_full_forward_mark": (_I, [_P, _P, _I, _P, _P]),
+    "anx_full_wait_mark": (_I, [_P, _P]),
+    "anx_full_set_knob": (_I, [_P, C.c_char_p, _I]),
+    "anx_full_tap": (_I, [_P, _I, _I, _P, C.POINTER(_SZ), _P]),
+    "anx_full_get_knob": (_I, [_P, C.c_char_p, C.POINTER(_I)]),
+}
+_bf16 = None
 
 
 def lib():
@@ -201,6 +208,29 @@ def dist_call(name: str, *args) -> None:
     check(getattr(dist(), name)(*args), name)
 
 
+def bf16():
+    """libanx_bf16 (the bf16 full-AlexNet engine; loaded only when a full model is built)."""
+    global _bf16
+    if _bf16 is not None:
+        return _bf16
+    lib()  # libanx first: libanx_bf16 links against it and reports errors through anx_last_error
+    with _lock:
+        if _bf16 is not None:
+            return _bf16
+        if not os.path.exists(BF16_PATH):
+            raise NativeError(f"libanx_bf16 not built: {BF16_PATH} missing (run `python __graft_entry__.py build`)")
+        try:
+            h = C.CDLL(BF16_PATH, mode=C.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - depends on the machine
+            raise NativeError(f"cannot load {BF16_PATH}: {e}") from e
+        for name, (res, args) in _BF16_SIGS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _bf16 = h
+        return _bf16
+
+
 def check(status: int, what: str = "") -> None:
     if status != 0:
         msg = lib().anx_last_error().decode(errors="replace")
@@ -208,7 +238,7 @@ def check(status: int, what: str = "") -> None:
 
 
 def call(name: str, *args) -> None:
-    check(getattr(lib(), name)(*args), name)
+    check(getattr(bf16() if name in _BF16_SIGS else lib(), name)(*args), name)
 
 
 def ptr(t) -> int:

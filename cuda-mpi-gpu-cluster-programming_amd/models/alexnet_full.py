@@ -81,7 +81,7 @@ class AlexNetFull:
             return
         if self._h is not None:
             torch.cuda.synchronize(self.device)
-            nat.lib().anx_full_destroy(self._h)
+            nat.bf16().anx_full_destroy(self._h)
             self._h = None
         ws = (C.c_void_p * 8)(*[self.weights["w_" + k].data_ptr() for k in LAYERS])
         bs = (C.c_void_p * 8)(*[self.weights["b_" + k].data_ptr() for k in LAYERS])
@@ -92,7 +92,7 @@ class AlexNetFull:
         try:
             apply_knobs(h, self.knobs, full=True)
         except Exception:
-            nat.lib().anx_full_destroy(h)
+            nat.bf16().anx_full_destroy(h)
             raise
         self._h, self._cap = h, max(1, n)
 
@@ -108,7 +108,7 @@ class AlexNetFull:
             m.close()
         if self._h is not None:
             torch.cuda.synchronize(self.device)
-            nat.lib().anx_full_destroy(self._h)
+            nat.bf16().anx_full_destroy(self._h)
             self._h = None
 
     def __del__(self):  # pragma: no cover
