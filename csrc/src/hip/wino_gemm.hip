@@ -85,10 +85,6 @@ using F45_64x32 = wg16::Cfg<2, 2, 48, 2>;   // 64 tiles x 32 filters, 4 waves
 using F45_32x64_32x4 = wg16::Cfg<1, 4, 32, 4>;  // 32 x 64, K slice 32 x 4 slots
 using F45_32x64_s3 = wg16::Cfg<1, 4, 48, 3>;    // 32 x 64, 3-slot ring
 using F45_32x128 = wg16::Cfg<1, 8, 48, 2>;      // 32 x 128, 8 waves (V read by 2 filter blocks)
-using F45_r = wg16::Cfg<1, 4, 48, 2, true>;      // 32 x 64, U fragments straight to registers
-using F45_r3 = wg16::Cfg<1, 4, 48, 3, true>;     // ... 3 slots / U buffers
-using F45_r128 = wg16::Cfg<1, 8, 48, 2, true>;   // 32 x 128, 8 waves, U in registers
-using F45_r32 = wg16::Cfg<1, 4, 32, 3, true>;    // 32 x 64, K slice 32 x 3 slots, U in registers
 #endif
 template <class G>
 hipError_t launch16_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
@@ -194,10 +190,6 @@ hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias
     case 6: return launch16_abl<F45_32x64_32x4>(a, s, occ, abl);
     case 7: return launch16_abl<F45_32x64_s3>(a, s, occ, abl);
     case 8: return launch16_abl<F45_32x128>(a, s, occ, abl);
-    case 9: return launch16_abl<F45_r>(a, s, occ, abl);
-    case 10: return launch16_abl<F45_r3>(a, s, occ, abl);
-    case 11: return launch16_abl<F45_r128>(a, s, occ, abl);
-    case 12: return launch16_abl<F45_r32>(a, s, occ, abl);
 #endif
     default: return hipErrorInvalidValue;
   }

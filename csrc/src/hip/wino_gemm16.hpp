@@ -50,32 +50,27 @@ constexpr Coef64 make_coef64() {
 }
 static __constant__ Coef64 c_coef64 = make_coef64();
 
-// WM x WN waves of 32 tiles x 16 filters; BK-channel slices through an NST-slot ring. BREG: the U (B)
-// fragments skip LDS — each wave loads its own 16 filters' slice straight into registers (NST buffers,
-// NST - 1 slices ahead) — which pays when WM = 1: no other wave reads them, and LDS then carries only V.
-template <int WM_, int WN_, int BK_, int NST_, bool BREG_ = false>
+// WM x WN waves of 32 tiles x 16 filters; BK-channel slices through an NST-slot ring.
+template <int WM_, int WN_, int BK_, int NST_>
 struct Cfg {
   static constexpr int NPT = 64, C = 96, NQ = 16, NE = 8;  // points, channels, outputs, values per lane
   static constexpr int WM = WM_, WN = WN_, BK = BK_, NST = NST_;
-  static constexpr bool BREG = BREG_;
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int BM = 32 * WM, BN = 16 * WN, U4 = BK / 4;
   static constexpr int KS = C / BK, TOTAL = NPT * KS;
-  static constexpr int G4 = BK / 16;     // 16-channel groups per slice (one 16-B fragment per operand row each)
-  static constexpr int A_INS = BM * U4 / 64, B_INS = BREG ? 0 : BN * U4 / 64;
+  static constexpr int A_INS = BM * U4 / 64, B_INS = BN * U4 / 64;
   static constexpr int A_MAX = (A_INS + NW - 1) / NW, B_MAX = (B_INS + NW - 1) / NW;
-  static constexpr int PW_MIN = A_INS / NW + (BREG ? G4 : B_INS / NW);  // vector-memory ops per wave per slice
-  static constexpr int A_FL = BM * BK, STAGE = (BM + (BREG ? 0 : BN)) * BK;
-  static constexpr size_t kRingBytes = static_cast<size_t>(NST) * STAGE * sizeof(float);
-  static constexpr size_t kEpiBytes = static_cast<size_t>(NW) * 32 * (16 + 4) * sizeof(float);  // epilogue transpose
-  static constexpr size_t kLdsBytes = kRingBytes > kEpiBytes ? kRingBytes : kEpiBytes;
+  static constexpr int PW_MIN = A_INS / NW + B_INS / NW;
+  static constexpr int A_FL = BM * BK, STAGE = (BM + BN) * BK;
+  static constexpr size_t kLdsBytes = static_cast<size_t>(NST) * STAGE * sizeof(float);
   static constexpr int UP = wg::even_up(KS, NST);
   static constexpr int NI = (TOTAL + 1 - NST) / (UP * KS);
   static constexpr int TAIL = NPT - NI * UP;
+  static constexpr int G4 = BK / 16;     // 16-channel groups per slice (one ds_read_b128 per operand row each)
   static constexpr int MF = BK / 4 * 2;  // MFMAs per slice (k-steps x 2 row blocks)
   static constexpr int NF = NQ * NE;     // fold FMAs per point
   static constexpr int MINB = NW >= 8 ? 1 : 8 / NW;  // workgroups per CU the VGPR budget is sized for (8 waves)
-  static_assert(C % BK == 0 && BK % 16 == 0 && A_INS * 64 == BM * U4 && (BREG || B_INS * 64 == BN * U4), "tile shape");
+  static_assert(C % BK == 0 && BK % 16 == 0 && A_INS * 64 == BM * U4 && B_INS * 64 == BN * U4, "tile shape");
   static_assert(U4 == 4 || U4 == 8 || U4 == 12, "swizzle defined for 4, 8, 12 units per row");
   static_assert(NST >= 2 && NI >= 1 && TAIL >= 1, "ring / loop shape");
 };
@@ -96,7 +91,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
   if (pt >= a.n_ptiles) return;  // whole workgroup, before any DMA or barrier
   const int p0 = pt * G::BM, n0 = nt * G::BN;
 
-  int voff[G::A_MAX], uoff[G::B_MAX > 0 ? G::B_MAX : 1];
+  int voff[G::A_MAX], uoff[G::B_MAX];
 #pragma unroll
   for (int i = 0; i < G::A_MAX; ++i) {
     const int q = wave + NW * i;
@@ -117,19 +112,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
   const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
 #endif
   [[maybe_unused]] lds_f32* lds3 = (lds_f32*)(lds);
-  const int r16 = lane & 15, kg = lane >> 4;
-  // BREG: this lane's U fragment offsets (floats) within a point's [K][C] block, per 16-channel group
-  [[maybe_unused]] int boff[G4];
-#pragma unroll
-  for (int s = 0; s < G4; ++s) boff[s] = (n0 + wn * 16 + r16) * G::C + 16 * s + 4 * kg;
-  [[maybe_unused]] f32x4 fbr[NST][G4];  // BREG: U fragments of the slices in flight, by ring slot
-  auto issue = [&](int ab, int ks, auto SLOT) {
-    constexpr int slot = decltype(SLOT)::value;
-    if constexpr (G::BREG && kDma) {
-      const float* ub = a.U + (static_cast<size_t>(ab) * a.u_rows * G::C + ks * BK);
-#pragma unroll
-      for (int s = 0; s < G4; ++s) fbr[slot][s] = *reinterpret_cast<const f32x4*>(ub + boff[s]);
-    }
+  auto issue = [&](int ab, int ks, int slot) {
     if constexpr (kDma) {
 #if __HIP_DEVICE_COMPILE__
       lds_f32* st = lds3 + slot * G::STAGE;
@@ -148,6 +131,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     }
   };
 
+  const int r16 = lane & 15, kg = lane >> 4;
   // byte addresses (slot 0) of my rows' fragment units: A rows wm*32 + r16 (+16), B row wn*16 + r16
   int ra0[G4], ra1[G4], rb[G4];
 #pragma unroll
@@ -187,8 +171,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
       wg::wait_vm_lgkm<vm>();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
-    if constexpr (refill) issue(pb + nlit / KS, nlit % KS, std::integral_constant<int, nlit % NST>{});
-    if constexpr (G::BREG) __builtin_amdgcn_sched_barrier(0);  // the U loads go out here, a slice ahead
+    if constexpr (refill) issue(pb + nlit / KS, nlit % KS, nlit % NST);
     if constexpr (ks == 0) {
       const float* cr = c_coef64.v[ab];
 #pragma unroll
@@ -199,34 +182,30 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     f32x4 fa0[2], fa1[2], fb[2];
     fa0[0] = frag(ra0[0] + so);
     fa1[0] = frag(ra1[0] + so);
-    if constexpr (!G::BREG) fb[0] = frag(rb[0] + so);
+    fb[0] = frag(rb[0] + so);
     static_for<0, G4>([&](auto S) {
       constexpr int s = decltype(S)::value;
       if constexpr (s + 1 < G4) {
         fa0[(s + 1) & 1] = frag(ra0[s + 1] + so);
         fa1[(s + 1) & 1] = frag(ra1[s + 1] + so);
-        if constexpr (!G::BREG) fb[(s + 1) & 1] = frag(rb[s + 1] + so);
+        fb[(s + 1) & 1] = frag(rb[s + 1] + so);
       }
       static_for<0, 4>([&](auto K) {
         constexpr int k = decltype(K)::value, m = s * 8 + 2 * k;
         constexpr bool first = ks == 0 && s == 0 && k == 0;
-        float bk;
-        if constexpr (G::BREG)
-          bk = fbr[slot][s][k];
-        else
-          bk = fb[s & 1][k];
-        acc[ai][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa0[s & 1][k], bk, first ? f32x4{} : acc[ai][0], 0, 0, 0);
+        acc[ai][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa0[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][0], 0,
+                                                          0, 0);
         if constexpr (fold)
           static_for<j0 + nj * m / MF, j0 + nj * (m + 1) / MF>(
               [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
-        acc[ai][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa1[s & 1][k], bk, first ? f32x4{} : acc[ai][1], 0, 0, 0);
+        acc[ai][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa1[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][1], 0,
+                                                          0, 0);
         if constexpr (fold)
           static_for<j0 + nj * (m + 1) / MF, j0 + nj * (m + 2) / MF>(
               [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
       });
       if constexpr (kPin) {
-        if constexpr (s + 1 < G4)  // the next group's reads
-          __builtin_amdgcn_sched_group_barrier(0x100, G::BREG ? 2 : 3, 0);
+        if constexpr (s + 1 < G4) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // the next group's reads
         static_for<0, 8>([&](auto M) {
           constexpr int m = s * 8 + decltype(M)::value;
           constexpr int np = nj * (m + 1) / MF - nj * m / MF;  // fold FMAs behind this MFMA
@@ -244,7 +223,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
 
   static_for<0, NST - 1>([&](auto IT) {
     constexpr int it = decltype(IT)::value;
-    issue(it / KS, it % KS, IT);
+    issue(it / KS, it % KS, it);
   });
   static_for<0, G::UP * KS>([&](auto IT) {
     constexpr int it = decltype(IT)::value;
@@ -263,8 +242,8 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
   constexpr int kTS = 16 + 4;
   static_assert(G::kLdsBytes >= static_cast<size_t>(NW) * 32 * kTS * 4, "epilogue scratch");
   float* tr = lds + wave * 32 * kTS;
-  const int fb0 = n0 + wn * 16;
-  const float bv = a.bias ? a.bias[fb0 + r16] : 0.f;
+  const int fb = n0 + wn * 16;
+  const float bv = a.bias ? a.bias[fb + r16] : 0.f;
   const OutView o = a.out;
   int oy0[2], ox0[2], img[2], trd[2];
   const int grp = 4 * (lane & 3);
@@ -293,7 +272,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
       const int oy = oy0[k] + q / 4, ox = ox0[k] + q % 4;
       if (oy < a.Ho && ox < a.Wo && (kStore || v4.x == -1.f))  // ABL 32: ReLU outputs are never -1
         *reinterpret_cast<f32x4*>(o.base + (static_cast<size_t>(img[k] * o.Hb + oy + o.h_off) * o.Wb + ox + o.w_off) *
-                                               o.Cb + o.c_off + fb0 + grp) = v4;
+                                               o.Cb + o.c_off + fb + grp) = v4;
     }
   }
 }
