@@ -73,10 +73,12 @@ hipError_t launch16(const wg::Args& a0, hipStream_t s, int occ) {
   return hipGetLastError();
 }
 // <waves along tiles, waves along filters, K slice, ring slots>: 32 tiles x 16 filters per wave
-// 32 tiles x 64 filters, 4 waves, 36 KiB ring: V read by 4 filter blocks instead of 8 (128 images alone:
-// 289.7 us vs 299.3 for 64 x 32 and 310.2 for the F(3x3,5x5) kernel; profiles/r05_f45/wg45_128.log)
-using F45 = wg16::Cfg<1, 4, 48, 2>;
+// 32 tiles x 64 filters, 4 waves, one point (all 96 channels) per K slice, 72 KiB ring: V read by 4 filter
+// blocks instead of 8, one barrier and one refill wait per point (128 images alone: 273.2 us vs 291.8 with
+// 48-channel slices, 298.0 for the F(3x3,5x5) kernel; profiles/r05_f45/wg45k_128.log)
+using F45 = wg16::Cfg<1, 4, 96, 2>;
 #ifdef ANX_WGEMM_ABLATIONS
+using F45_b48 = wg16::Cfg<1, 4, 48, 2>;      // the first production shape: 48-channel slices, 2 per point
 using F45_64x64 = wg16::Cfg<2, 4, 48, 2>;   // 8 waves, 48 KiB ring, one workgroup per CU's VGPR budget
 using F45_128x32 = wg16::Cfg<4, 2, 48, 2>;  // 8 waves, 60 KiB ring
 using F45_s3 = wg16::Cfg<2, 2, 48, 3>;      // 64 x 32, 3-slot ring (55 KiB)
@@ -85,6 +87,7 @@ using F45_64x32 = wg16::Cfg<2, 2, 48, 2>;   // 64 tiles x 32 filters, 4 waves
 using F45_32x64_32x4 = wg16::Cfg<1, 4, 32, 4>;  // 32 x 64, K slice 32 x 4 slots
 using F45_32x64_s3 = wg16::Cfg<1, 4, 48, 3>;    // 32 x 64, 3-slot ring
 using F45_32x128 = wg16::Cfg<1, 8, 48, 2>;      // 32 x 128, 8 waves (V read by 2 filter blocks)
+using F45_k96x64 = wg16::Cfg<2, 2, 96, 2>;      // 64 x 32, K slice 96
 #endif
 template <class G>
 hipError_t launch16_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
@@ -190,6 +193,8 @@ hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias
     case 6: return launch16_abl<F45_32x64_32x4>(a, s, occ, abl);
     case 7: return launch16_abl<F45_32x64_s3>(a, s, occ, abl);
     case 8: return launch16_abl<F45_32x128>(a, s, occ, abl);
+    case 9: return launch16_abl<F45_b48>(a, s, occ, abl);
+    case 10: return launch16_abl<F45_k96x64>(a, s, occ, abl);
 #endif
     default: return hipErrorInvalidValue;
   }

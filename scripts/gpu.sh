@@ -90,7 +90,9 @@ for s in "$@"; do
         for arm in "${arms[@]}"; do
           kargs=()
           IFS=';' read -r -a kvs <<< "$arm"
-          for kv in "${kvs[@]}"; do [ -n "$kv" ] && kargs+=(--knob "$kv"); done
+          for kv in "${kvs[@]}"; do  # k=v: an engine knob; --flag=v: a bench.py argument
+            if [[ $kv == --* ]]; then kargs+=("$kv"); elif [ -n "$kv" ]; then kargs+=(--knob "$kv"); fi
+          done
           echo "== benchab rep $rep arm '$arm'"
           timeout -k 10 200 python -u bench.py --steps "${BENCH_STEPS:-20}" --warmup 5 --no-b1 --no-full $BARGS "${kargs[@]}" \
             >> "$O/benchab.jsonl" 2>> "$O/benchab.err" || { echo "== benchab FAILED"; exit 1; }
