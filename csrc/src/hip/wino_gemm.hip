@@ -5,6 +5,8 @@
 // Measured at 300 images, each kernel alone (profiles/r03_wgemm_ab.md): 64x64 tiles, BK 48 and a 2-slot
 // ring beat BK 32 x 4 slots and BK 16 x 6 slots (the deeper rings raised MFMA-busy but the chip then
 // held a lower clock); Conv2 623 us (old fused kernel 649, bit-identical output), Conv1 380 us.
+#include <type_traits>
+
 #include "wino_gemm.hpp"
 #include "wino_gemm16.hpp"
 
@@ -44,18 +46,8 @@ hipError_t launch(const wg::Args& a0, hipStream_t s, int occ) {
 using C2 = wg::Cfg<49, 96, 2, 2, 48, 2>;    // Conv2: 64 tiles x 64 filters, 48 KiB ring, 2 workgroups per CU
 using C2g = wg::Cfg<49, 48, 2, 2, 48, 2>;   // Conv2 with 2 groups (48 channels per group)
 using C1 = wg::Cfg<25, 48, 2, 1, 48, 2>;    // Conv1: 64 tiles x 32 filters, 2 waves, 4 workgroups per CU
-#ifdef ANX_WGEMM_ABLATIONS
-using C2_32x4 = wg::Cfg<49, 96, 2, 2, 32, 4>;    // 64 KiB ring: 2 slices in flight behind the current one
-// 64 tiles x 128 filters, 8 waves, 72 KiB ring: a quarter less operand traffic per FLOP, but 636 vs 623 us
-// alone at 300 images and 246-247 k vs 255 k images/s in the bench step (profiles/r03_conv2_wide_*)
-using C2_64x128 = wg::Cfg<49, 96, 2, 4, 48, 2>;
-using C2_64x64s3 = wg::Cfg<49, 96, 2, 2, 48, 3>;  // 64 x 64, 3-slot ring (72 KiB: still 2 workgroups per CU)
-using C2_64x128s3 = wg::Cfg<49, 96, 2, 4, 48, 3>; // 64 x 128, 8 waves, 3-slot ring (108 KiB)
-using C2_128x64 = wg::Cfg<49, 96, 4, 2, 48, 2>;   // 128 tiles x 64 filters, 8 waves (V read by 4 workgroups, U by half as many)
-using C1_64x96 = wg::Cfg<25, 48, 2, 3, 48, 2>;   // 64 x 96 (every filter: V read once), 6 waves, 60 KiB ring
-using C1_32x96 = wg::Cfg<25, 48, 1, 3, 48, 2>;   // 32 x 96, 3 waves, 48 KiB ring
-using C1_48x2w4 = wg::Cfg<25, 48, 4, 1, 48, 2>;  // 128 x 32, 4 waves, 60 KiB ring, 2 per CU
-#endif
+// Round 3-4 alternatives (BK 32 x 4 slots, 64x128, 3-slot rings, 128x64; Conv1 64x96, 32x96, 128x32) were
+// measured slower and removed from the A/B build: profiles/r03_wgemm_ab.md, profiles/r04_wgemm_ab/.
 
 // The F(4x4,5x5) kernel (wino_gemm16.hpp): same Args, its own tile shape
 template <class G, int ABL>
@@ -78,27 +70,22 @@ hipError_t launch16(const wg::Args& a0, hipStream_t s, int occ) {
 // 48-channel slices, 298.0 for the F(3x3,5x5) kernel; profiles/r05_f45/wg45k_128.log)
 using F45 = wg16::Cfg<1, 4, 96, 2>;
 #ifdef ANX_WGEMM_ABLATIONS
+// measured alone at 128 images (profiles/r05_f45/wg45_128_v2.log, wg45k_128.log): 64 x 64 on 8 waves
+// 323 us, 128 x 32 317, 3-slot rings 303-315, 32 x 128 302: not kept as configurations
 using F45_b48 = wg16::Cfg<1, 4, 48, 2>;      // the first production shape: 48-channel slices, 2 per point
-using F45_64x64 = wg16::Cfg<2, 4, 48, 2>;   // 8 waves, 48 KiB ring, one workgroup per CU's VGPR budget
-using F45_128x32 = wg16::Cfg<4, 2, 48, 2>;  // 8 waves, 60 KiB ring
-using F45_s3 = wg16::Cfg<2, 2, 48, 3>;      // 64 x 32, 3-slot ring (55 KiB)
-using F45_32x4 = wg16::Cfg<2, 2, 32, 4>;    // 64 x 32, K slice 32 x 4 slots (48 KiB)
-using F45_64x32 = wg16::Cfg<2, 2, 48, 2>;   // 64 tiles x 32 filters, 4 waves
-using F45_32x64_32x4 = wg16::Cfg<1, 4, 32, 4>;  // 32 x 64, K slice 32 x 4 slots
-using F45_32x64_s3 = wg16::Cfg<1, 4, 48, 3>;    // 32 x 64, 3-slot ring
-using F45_32x128 = wg16::Cfg<1, 8, 48, 2>;      // 32 x 128, 8 waves (V read by 2 filter blocks)
-using F45_k96x64 = wg16::Cfg<2, 2, 96, 2>;      // 64 x 32, K slice 96
+using F45_k96x32 = wg16::Cfg<2, 2, 96, 2>;   // 64 x 32, one point per slice (275.8 us)
+using F45_b48x32 = wg16::Cfg<2, 2, 48, 2>;   // 64 x 32, 48-channel slices
 #endif
 template <class G>
 hipError_t launch16_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
-  switch (abl) {
-    case 0: return launch16<G, 0>(a, s, occ);
+  if (abl == 0) return launch16<G, 0>(a, s, occ);
 #ifdef ANX_WGEMM_ABLATIONS
-    case 3: return launch16<G, 3>(a, s, occ);
-    case 32: return launch16<G, 32>(a, s, occ);
-#endif
-    default: return hipErrorInvalidValue;
+  if constexpr (std::is_same_v<G, F45>) {  // cost probes of the production shape only (compile time)
+    if (abl == 3) return launch16<G, 3>(a, s, occ);
+    if (abl == 32) return launch16<G, 32>(a, s, occ);
   }
+#endif
+  return hipErrorInvalidValue;
 }
 
 template <class G>
@@ -147,13 +134,6 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
     else
       switch (cfg < 0 ? 0 : cfg) {
         case 0: e = launch_abl<C2>(a, s, occ, abl); break;
-#ifdef ANX_WGEMM_ABLATIONS
-        case 1: e = launch_abl<C2_32x4>(a, s, occ, abl); break;
-        case 2: e = launch_abl<C2_64x128>(a, s, occ, abl); break;
-        case 3: e = launch_abl<C2_64x64s3>(a, s, occ, abl); break;
-        case 4: e = launch_abl<C2_64x128s3>(a, s, occ, abl); break;
-        case 5: e = launch_abl<C2_128x64>(a, s, occ, abl); break;
-#endif
         default: break;
       }
     if (e != hipSuccess) return e;
@@ -185,16 +165,9 @@ hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias
   switch (cfg < 0 ? 0 : cfg) {
     case 0: return launch16_abl<F45>(a, s, occ, abl);
 #ifdef ANX_WGEMM_ABLATIONS
-    case 1: return launch16_abl<F45_64x64>(a, s, occ, abl);
-    case 2: return launch16_abl<F45_128x32>(a, s, occ, abl);
-    case 3: return launch16_abl<F45_s3>(a, s, occ, abl);
-    case 4: return launch16_abl<F45_32x4>(a, s, occ, abl);
-    case 5: return launch16_abl<F45_64x32>(a, s, occ, abl);
-    case 6: return launch16_abl<F45_32x64_32x4>(a, s, occ, abl);
-    case 7: return launch16_abl<F45_32x64_s3>(a, s, occ, abl);
-    case 8: return launch16_abl<F45_32x128>(a, s, occ, abl);
-    case 9: return launch16_abl<F45_b48>(a, s, occ, abl);
-    case 10: return launch16_abl<F45_k96x64>(a, s, occ, abl);
+    case 1: return launch16_abl<F45_b48>(a, s, occ, abl);
+    case 2: return launch16_abl<F45_k96x32>(a, s, occ, abl);
+    case 3: return launch16_abl<F45_b48x32>(a, s, occ, abl);
 #endif
     default: return hipErrorInvalidValue;
   }
@@ -223,11 +196,6 @@ hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, Ou
   a.relu = relu ? 1 : 0;
   switch (cfg < 0 ? 0 : cfg) {
     case 0: return launch_abl<C1>(a, s, occ, abl);
-#ifdef ANX_WGEMM_ABLATIONS
-    case 1: return launch_abl<C1_64x96>(a, s, occ, abl);
-    case 2: return launch_abl<C1_32x96>(a, s, occ, abl);
-    case 3: return launch_abl<C1_48x2w4>(a, s, occ, abl);
-#endif
     default: return hipErrorInvalidValue;
   }
 }
