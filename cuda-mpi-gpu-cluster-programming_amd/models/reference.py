@@ -41,3 +41,12 @@ def blocks_forward(x, weights, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2, d
     if b2.has_lrn:
         h = lrn_nhwc(h, b2.lrn.N, b2.lrn.alpha, b2.lrn.beta, b2.lrn.k, b2.lrn.mode)
     return h
+
+
+def blocks_forward_all(x, weights, b1: BlockSpec = BLOCK1, b2: BlockSpec = BLOCK2, device=None, chunk: int = 64):
+    """The fp64 oracle of EVERY image of a batch, ``chunk`` images at a time on ``device`` (the GPU in
+    the GPU tests: fp64 convolutions run there as im2col + DGEMM in seconds where the CPU takes
+    minutes), returned on the CPU. The tests check whole batches with it, not samples."""
+    dev = torch.device(device) if device is not None else x.device
+    outs = [blocks_forward(x[i:i + chunk].to(dev), weights, b1, b2).cpu() for i in range(0, x.shape[0], chunk)]
+    return torch.cat(outs)

@@ -7,7 +7,7 @@ import torch
 
 from anx import _native as nat
 from anx.models.alexnet_blocks import AlexNetBlocks
-from anx.models.reference import blocks_forward, conv2d_nhwc, lrn_nhwc, maxpool_nhwc
+from anx.models.reference import blocks_forward, blocks_forward_all, conv2d_nhwc, lrn_nhwc, maxpool_nhwc
 from anx.parallel.plan import OVERLAP, PER_LAYER, make_plan
 from anx.utils.init import init_input
 
@@ -59,9 +59,8 @@ def test_engine_large_batch_variant(cuda):
     m = AlexNetBlocks(device=cuda, init="rand", seed=8, max_batch=N)
     x = init_input(N, "rand", seed=8)
     y = m(x.to(cuda)).cpu()
-    idx = torch.tensor([0, 1, 127, 128, 200, 255])
-    ref = blocks_forward(x[idx], m.weights, m.b1, m.b2)
-    torch.testing.assert_close(y[idx].double(), ref, rtol=2e-5, atol=2e-6)
+    ref = blocks_forward_all(x, m.weights, m.b1, m.b2, device=cuda)  # every image, fp64
+    torch.testing.assert_close(y.double(), ref, rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.parametrize("np_", [2, 4, 8])
@@ -274,9 +273,7 @@ def test_conv1_winograd_engine_vs_oracle(cuda, N):
     m = AlexNetBlocks(device=cuda, init="rand", seed=50 + N, max_batch=N, knobs=WINO1)
     x = init_input(N, "rand", seed=50 + N)
     y = m(x.to(cuda)).cpu().double()
-    idx = torch.arange(N) if N <= 8 else torch.tensor([0, 1, 63, 64, 126, 127])
-    ref = blocks_forward(x[idx], m.weights, m.b1, m.b2)
-    torch.testing.assert_close(y[idx], ref, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(y, blocks_forward_all(x, m.weights, m.b1, m.b2, device=cuda), rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.parametrize("np_", [2, 3, 4, 8])
@@ -317,8 +314,7 @@ def test_winograd_conv2_gemm_sizes(cuda, N, groups2):
     m = AlexNetBlocks(device=cuda, init="rand", seed=80 + N, max_batch=N, groups2=groups2, knobs=WINO2)
     x = init_input(N, "rand", seed=80 + N)
     y = m(x.to(cuda)).cpu().double()
-    idx = torch.arange(N) if N <= 9 else torch.tensor([0, 1, 63, 64, N // 2, N - 1])
-    torch.testing.assert_close(y[idx], blocks_forward(x[idx], m.weights, m.b1, m.b2), rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(y, blocks_forward_all(x, m.weights, m.b1, m.b2, device=cuda), rtol=2e-5, atol=2e-6)
 
 
 def test_engine_batch_above_launch_chunk(cuda):
@@ -328,9 +324,8 @@ def test_engine_batch_above_launch_chunk(cuda):
     m = AlexNetBlocks(device=cuda, init="rand", seed=44, max_batch=N)
     x = init_input(N, "rand", seed=44)
     y = m(x.to(cuda))
-    idx = torch.tensor([0, 1238, 1239, N - 1])
-    ref = blocks_forward(x[idx], m.weights, m.b1, m.b2)
-    torch.testing.assert_close(y[idx.to(cuda)].cpu().double(), ref, rtol=2e-5, atol=2e-6)
+    ref = blocks_forward_all(x, m.weights, m.b1, m.b2, device=cuda)  # every image, both launches, fp64
+    torch.testing.assert_close(y.cpu().double(), ref, rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.parametrize("lanes,N", [(2, 150), (3, 200), (2, 100)])
@@ -401,9 +396,8 @@ def test_fused_pool1_bitwise(cuda, N, chunk):
     plain = AlexNetBlocks(device=cuda, init="rand", seed=11, max_batch=N, knobs={**kn, "fuse_pool1": 0})
     y = fused(x)
     assert torch.equal(y, plain(x))
-    idx = [0, N - 1]
-    ref = blocks_forward(x[idx].cpu(), fused.weights, fused.b1, fused.b2)
-    torch.testing.assert_close(y[idx].cpu().double(), ref, rtol=2e-5, atol=2e-6)
+    ref = blocks_forward_all(x, fused.weights, fused.b1, fused.b2, device=cuda)
+    torch.testing.assert_close(y.cpu().double(), ref, rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.parametrize("N,sub1,sub2", [(64, 16, 0), (64, 0, 24), (40, 16, 16), (20, 9, 12)])
@@ -475,9 +469,8 @@ def test_conv1_fused_kernel(cuda, N, mode):
     plain = AlexNetBlocks(device=cuda, init="rand", seed=16, max_batch=N, knobs={**WINO1, **WINO2, "conv1_fused": 0})
     y, y0 = fused(x.to(cuda)), plain(x.to(cuda))
     assert (y - y0).abs().max().item() <= 1e-5 * y0.abs().max().item()
-    idx = [0, N - 1]
-    ref = blocks_forward(x[idx], fused.weights, fused.b1, fused.b2)
-    torch.testing.assert_close(y[idx].cpu().double(), ref, rtol=2e-5, atol=2e-6)
+    ref = blocks_forward_all(x, fused.weights, fused.b1, fused.b2, device=cuda)
+    torch.testing.assert_close(y.cpu().double(), ref, rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.parametrize("mode", [1])
