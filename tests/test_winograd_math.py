@@ -1,7 +1,10 @@
 """CPU checks of the fast-convolution algebra the HIP kernels implement (numpy, fp64).
 
-* The F(3x3,3x3) and F(3x3,5x5) tables in csrc/include/anx/winograd_f*.hpp (parsed from the
-  headers the kernels compile against) reproduce direct correlation exactly in fp64.
+* The F(3x3,3x3), F(3x3,5x5) and F(4x4,5x5) tables in csrc/include/anx/winograd_f*.hpp (parsed from
+  the headers the kernels compile against) reproduce direct correlation exactly in fp64.
+* Conv2's tilings of its 31x31 window: 9x9 tiles of 3x3 outputs, and 7x7 tiles of 4x4 outputs whose
+  last tile row / column reads window row / column 31 (outside the window: zero) for the output row
+  27 that is dropped — the kernels' bounds logic (winograd.hip, wino_gemm16.hpp).
 * Conv1's polyphase rewrite (stride 4 -> 48 channels of a stride-1 3x3 conv) followed by F(3x3,3x3)
   tiles equals the direct 11x11/4 convolution, including ragged right/bottom tiles — the exact data
   flow of hip/conv1_wino.hip (channel order ch = (rh*4 + rw)*3 + c, 12-pixel tile pitch).
@@ -33,7 +36,8 @@ def _wino2d(d, g, AT, BT, G):
     return AT @ (U * V) @ AT.T
 
 
-@pytest.mark.parametrize("header,m,r", [("winograd_f33.hpp", 3, 3), ("winograd_f35.hpp", 3, 5)])
+@pytest.mark.parametrize("header,m,r", [("winograd_f33.hpp", 3, 3), ("winograd_f35.hpp", 3, 5),
+                                        ("winograd_f45.hpp", 4, 5)])
 def test_tables_exact(header, m, r):
     AT, BT, G = _load(header)
     n = m + r - 1
@@ -99,3 +103,29 @@ def test_conv1_polyphase_winograd(H, W):
     x = rng.uniform(0, 0.1, (H, W, 3))
     w = rng.uniform(-0.01, 0.01, (8, 3, 11, 11))
     np.testing.assert_allclose(_conv1_polyphase_wino(x, w), _conv1_direct(x, w), rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("header,m", [("winograd_f35.hpp", 3), ("winograd_f45.hpp", 4)])
+def test_conv2_window_tiling(header, m):
+    AT, BT, G = _load(header)
+    r, n, Hq, Ho = 5, m + 4, 31, 27
+    rng = np.random.default_rng(1)
+    C, K = 3, 2
+    x = np.zeros((Hq, Hq, C))
+    x[2:29, 2:29] = rng.standard_normal((27, 27, C))  # the zero border of the conv2 window
+    w = rng.standard_normal((K, C, r, r))
+    ty = -(-Ho // m)
+    y = np.zeros((ty * m, ty * m, K))
+    for ti in range(ty):
+        for tj in range(ty):
+            d = np.zeros((n, n, C))  # window rows / columns past 30 read as zero (the kernels' bounds checks)
+            rr, cc = min(n, Hq - ti * m), min(n, Hq - tj * m)
+            d[:rr, :cc] = x[ti * m:ti * m + rr, tj * m:tj * m + cc]
+            for k in range(K):
+                y[ti * m:(ti + 1) * m, tj * m:(tj + 1) * m, k] = sum(
+                    _wino2d(d[:, :, c], w[k, c], AT, BT, G) for c in range(C))
+    ref = np.zeros((Ho, Ho, K))
+    for oy in range(Ho):
+        for ox in range(Ho):
+            ref[oy, ox] = np.einsum("hwc,kchw->k", x[oy:oy + r, ox:ox + r], w)
+    np.testing.assert_allclose(y[:Ho, :Ho], ref, rtol=1e-9, atol=1e-9)
