@@ -62,3 +62,16 @@ def test_out_tensor_is_checked():
     m.forward_async(x, y)
     m.join()
     assert torch.equal(y, good)
+
+
+def test_oracle_all_images_chunked():
+    """blocks_forward_all (the whole-batch fp64 oracle of the GPU tests and smoke) equals the one-call
+    oracle image for image, across chunk boundaries (to fp64 rounding)."""
+    from anx.models.reference import blocks_forward_all
+    from anx.utils.init import init_weights
+    w = init_weights("rand", 3)
+    x = torch.rand(5, 67, 67, 3) * 0.1  # small images: conv1 15x15 -> pool 7 -> conv2 7 -> pool 3
+    ref = blocks_forward(x, w)
+    got = blocks_forward_all(x, w, chunk=2)
+    assert got.dtype == torch.float64 and got.shape == ref.shape
+    torch.testing.assert_close(got, ref, rtol=1e-12, atol=1e-14)  # fp64: the batch split may reorder sums
