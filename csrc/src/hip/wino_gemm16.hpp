@@ -48,29 +48,6 @@ constexpr Coef64 make_coef64() {
   return t;
 }
 static __constant__ Coef64 c_coef64 = make_coef64();
-// separable fold (Cfg::SEP): A^T[i][a] by a-row, i.e. [a][i]
-struct CoefA {
-  float v[8][4];
-};
-constexpr CoefA make_coefa() {
-  CoefA t{};
-  for (int a = 0; a < 8; ++a)
-    for (int i = 0; i < 4; ++i) t.v[a][i] = wino45::kAT[i][a];
-  return t;
-}
-static __constant__ CoefA c_coefa = make_coefa();
-// nonzero A^T[j][b] of column b: their count and the k-th one's j
-constexpr int nzj(int b) {
-  int n = 0;
-  for (int j = 0; j < 4; ++j) n += wino45::kAT[j][b] != 0.f;
-  return n;
-}
-constexpr int sep_units(int bp) { return (bp == 0 ? 32 : 8 * nzj(bp)) + (bp == 7 ? 128 : 0); }
-constexpr int kth_j(int b, int k) {
-  for (int j = 0; j < 4; ++j)
-    if (wino45::kAT[j][b] != 0.f && k-- == 0) return j;
-  return -1;
-}
 
 // LDS swizzle of the 16-B unit u of row r: u ^ swz16(r). ds_read_b128 is served in four 16-lane groups,
 // {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32 (MI355X_MICROARCH.md, LDS): with 48-float rows
@@ -87,14 +64,11 @@ __device__ __forceinline__ int swz16(int row) {
     return wg::swz<U4>(row);
 }
 
-// WM x WN waves of 32 tiles x 16 filters; BK-channel slices through an NST-slot ring. SEP: separable
-// output fold — T[j] += A^T[j][b] M_ab over an a-row's 8 points, then Y[i][j] += A^T[i][a] T[j] once per
-// a-row (~42 instead of 128 FMAs per point; the loop body then covers a whole a-row: b compile-time).
-template <int WM_, int WN_, int BK_, int NST_, bool SEP_ = false>
+// WM x WN waves of 32 tiles x 16 filters; BK-channel slices through an NST-slot ring.
+template <int WM_, int WN_, int BK_, int NST_>
 struct Cfg {
   static constexpr int NPT = 64, C = 96, NQ = 16, NE = 8;  // points, channels, outputs, values per lane
   static constexpr int WM = WM_, WN = WN_, BK = BK_, NST = NST_;
-  static constexpr bool SEP = SEP_;
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int BM = 32 * WM, BN = 16 * WN, U4 = BK / 4;
   static constexpr int KS = C / BK, TOTAL = NPT * KS;
@@ -103,7 +77,7 @@ struct Cfg {
   static constexpr int PW_MIN = A_INS / NW + B_INS / NW;
   static constexpr int A_FL = BM * BK, STAGE = (BM + BN) * BK;
   static constexpr size_t kLdsBytes = static_cast<size_t>(NST) * STAGE * sizeof(float);
-  static constexpr int UP = SEP ? 8 : wg::even_up(KS, NST);
+  static constexpr int UP = wg::even_up(KS, NST);
   static constexpr int NI = (TOTAL + 1 - NST) / (UP * KS);
   static constexpr int TAIL = NPT - NI * UP;
   static constexpr int G4 = BK / 16;     // 16-channel groups per slice (one ds_read_b128 per operand row each)
@@ -113,7 +87,6 @@ struct Cfg {
   static_assert(C % BK == 0 && BK % 16 == 0 && A_INS * 64 == BM * U4 && B_INS * 64 == BN * U4, "tile shape");
   static_assert(U4 == 4 || U4 == 8 || U4 == 12 || U4 == 24, "swizzle defined for 4, 8, 12, 24 units per row");
   static_assert(NST >= 2 && NI >= 1 && TAIL >= 1, "ring / loop shape");
-  static_assert(!SEP || (UP * KS) % NST == 0, "SEP: a body of 8 points must repeat the ring slots");
 };
 
 // ABL (A/B tool only; production instantiates 0): bit0 no fold, bit1 no DMA refills, bit2 no barrier,
@@ -196,26 +169,6 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     constexpr int j = decltype(J)::value, fi = decltype(FI)::value, q = j >> 3, e = j & 7;
     Y[q][e] = __builtin_fmaf(cq[fi][q], acc[fi][e >> 2][e & 3], Y[q][e]);
   };
-  // SEP: T[j][e] (the a-row's partial output transform) and A^T[i][a] of the row being closed
-  [[maybe_unused]] float T[4][G::NE];
-  [[maybe_unused]] float ca[4];
-  // fold unit J of point (b = BP) held in acc[FI]: T units first (an assignment when BP = 0), then, when the
-  // point closes its a-row (BP = 7), the 128 Y units Y[i][j] += A^T[i][a] T[j]
-  auto sep_one = [&](auto J, auto FI, auto BP) {
-    constexpr int u = decltype(J)::value, fi = decltype(FI)::value, bp = decltype(BP)::value;
-    constexpr int nT = bp == 0 ? 32 : 8 * nzj(bp);
-    if constexpr (u < nT) {
-      constexpr int e = u & 7, j = bp == 0 ? (u >> 3) : kth_j(bp, u >> 3);
-      constexpr float c = wino45::kAT[j][bp];
-      if constexpr (bp == 0)
-        T[j][e] = c * acc[fi][e >> 2][e & 3];
-      else
-        T[j][e] = __builtin_fmaf(c, acc[fi][e >> 2][e & 3], T[j][e]);
-    } else {
-      constexpr int k = u - nT, q = k >> 3, e = k & 7;
-      Y[q][e] = __builtin_fmaf(ca[q >> 2], T[q & 3][e], Y[q][e]);
-    }
-  };
 
   auto slice = [&](int pb, auto LIT, auto ABS, auto FOLD) {
     constexpr int lit = decltype(LIT)::value;
@@ -233,20 +186,13 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     if constexpr (refill) issue(pb + nlit / KS, nlit % KS, nlit % NST);
-    constexpr int bpt = (lit / KS) % 8, bprev = (bpt + 7) % 8;  // SEP: this point's b and the folded one's
-    if constexpr (ks == 0 && !G::SEP) {
+    if constexpr (ks == 0) {
       const float* cr = c_coef64.v[ab];
 #pragma unroll
       for (int q = 0; q < G::NQ; ++q) cq[ai][q] = cr[q];
     }
-    if constexpr (ks == 0 && G::SEP && bpt == 0 && decltype(FOLD)::value) {  // this point closes the previous a-row
-      const float* cr = c_coefa.v[ab / 8 - 1];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ca[i] = cr[i];
-    }
     constexpr int so = slot * G::STAGE * 4;
-    constexpr int NFP = G::SEP ? sep_units(bprev) : NF;  // fold units of the previous point
-    constexpr int j0 = NFP * ks / KS, nj = NFP * (ks + 1) / KS - j0;
+    constexpr int j0 = NF * ks / KS, nj = NF * (ks + 1) / KS - j0;
     f32x4 fa0[2], fa1[2], fb[2];
     fa0[0] = frag(ra0[0] + so);
     fa1[0] = frag(ra1[0] + so);
@@ -264,21 +210,13 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
         acc[ai][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa0[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][0], 0,
                                                           0, 0);
         if constexpr (fold)
-          static_for<j0 + nj * m / MF, j0 + nj * (m + 1) / MF>([&](auto J) {
-            if constexpr (G::SEP)
-              sep_one(J, std::integral_constant<int, ai ^ 1>{}, std::integral_constant<int, bprev>{});
-            else
-              fold_one(J, std::integral_constant<int, ai ^ 1>{});
-          });
+          static_for<j0 + nj * m / MF, j0 + nj * (m + 1) / MF>(
+              [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
         acc[ai][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa1[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][1], 0,
                                                           0, 0);
         if constexpr (fold)
-          static_for<j0 + nj * (m + 1) / MF, j0 + nj * (m + 2) / MF>([&](auto J) {
-            if constexpr (G::SEP)
-              sep_one(J, std::integral_constant<int, ai ^ 1>{}, std::integral_constant<int, bprev>{});
-            else
-              fold_one(J, std::integral_constant<int, ai ^ 1>{});
-          });
+          static_for<j0 + nj * (m + 1) / MF, j0 + nj * (m + 2) / MF>(
+              [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
       });
       if constexpr (kPin) {
         if constexpr (s + 1 < G4) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // the next group's reads
@@ -309,14 +247,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     static_for<0, G::UP * KS>([&](auto LIT) { slice(pb, LIT, F_{}, T_{}); });
   }
   static_for<G::NI * G::UP * KS, G::TOTAL>([&](auto IT) { slice(0, IT, T_{}, T_{}); });
-  if constexpr (G::SEP) {  // the last point (a = 7, b = 7) closes the last a-row
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ca[i] = c_coefa.v[7][i];
-    static_for<0, sep_units(7)>(
-        [&](auto J) { sep_one(J, integral_constant<int, (G::NPT - 1) & 1>{}, integral_constant<int, 7>{}); });
-  } else {
-    static_for<0, NF>([&](auto J) { fold_one(J, integral_constant<int, (G::NPT - 1) & 1>{}); });
-  }
+  static_for<0, NF>([&](auto J) { fold_one(J, integral_constant<int, (G::NPT - 1) & 1>{}); });
 
   // Epilogue: bias + ReLU, then per output q one LDS transpose of the wave's 32 tiles x 16 filters so each
   // lane stores a 16-B filter group. D layout (16x16x4): lane (r16, kg) holds filter n0 + wn*16 + r16 of
