@@ -1,8 +1,10 @@
-// Launchers of the fused Winograd GEMM (wino_gemm.hpp) for Conv2 (F(3x3,5x5)) and Conv1 (polyphase
-// F(3x3,3x3)). The production build instantiates one configuration per channel count; the anx_wgemm
-// A/B tool (ANX_WGEMM_ABLATIONS) also instantiates the alternative ring / tile shapes and ablations.
+// Launchers of the fused Winograd GEMMs: Conv2 on F(4x4,5x5) (wino_gemm16.hpp, the default since round 5)
+// or F(3x3,5x5) (wino_gemm.hpp: grouped Conv2 and the conv2_tile=3 arm), and the two-kernel Conv1's
+// polyphase F(3x3,3x3) GEMM (wino_gemm.hpp). The production build instantiates one configuration per
+// shape; the anx_wgemm A/B tool (ANX_WGEMM_ABLATIONS) also instantiates a few alternatives and the cost
+// probes of the production F(4,5) kernel.
 //
-// Measured at 300 images, each kernel alone (profiles/r03_wgemm_ab.md): 64x64 tiles, BK 48 and a 2-slot
+// F(3x3,5x5), measured at 300 images alone (profiles/r03_wgemm_ab.md): 64x64 tiles, BK 48 and a 2-slot
 // ring beat BK 32 x 4 slots and BK 16 x 6 slots (the deeper rings raised MFMA-busy but the chip then
 // held a lower clock); Conv2 623 us (old fused kernel 649, bit-identical output), Conv1 380 us.
 #include <type_traits>
