@@ -87,6 +87,7 @@ class BlocksEngine {
   bool fused_pool1(int N, const TilePlan& t) const;
   // ... and whether pool1 runs inside the one-kernel Conv1 instead (Knobs::conv1_pool; whole images only)
   bool conv1_pools(int N, const TilePlan& t) const;
+  bool conv2_pools(const TilePlan& t) const;  // pool2 in the F(4x4,5x5) GEMM's epilogue (Knobs::conv2_pool)
   hipError_t tile_forward_conv1_pool(const float* x, int N, const TilePlan& t, float* y, hipStream_t s);
 
   BlockSpec b1_, b2_;

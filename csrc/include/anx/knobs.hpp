@@ -21,7 +21,7 @@ enum class ConvAlgo : int { Auto = 0, Direct = 1, Winograd = 2 };
 //   production  the defaults every bench and driver run launches, and their shape fallbacks;
 //   oracle      a simpler kernel kept as the bitwise / tolerance reference of a fast one in the GPU tests:
 //               conv*_algo = direct, conv1_band = 0 (per-tile gathers), bf16_glds = 0 with bf16_big = -2
-//               (the register-staged 128x128 bf16 kernel), fuse_pool1 / conv1_pool / conv1_fused = 0;
+//               (the register-staged 128x128 bf16 kernel), fuse_pool1 / conv1_pool / conv2_pool / conv1_fused = 0;
 //   tuning      launch geometry (chunks, sub-chunks, occupancy caps, forced tile configs) for A/B runs.
 struct Knobs {
   ConvAlgo conv1_algo = ConvAlgo::Auto;  // Conv1: polyphase Winograd F(3x3,3x3) / direct implicit GEMM
@@ -63,6 +63,12 @@ struct Knobs {
                            // chunk (0 = the whole chunk); the V workspace is rewritten in place per sub-chunk, so
                            // a small one is written and re-read inside the 256 MB Infinity Cache
   int conv2_sub = 0;       // ... and per (pool1 + Conv2 input transform, Conv2 GEMM) pair
+  int conv2_pool = 0;      // tuning: 1 = for whole images on F(4x4,5x5) with LRN over 256 channels, pool2 in the Conv2
+                           // GEMM's epilogue (the 27x27 map never reaches HBM: -125 MB per 128 images; straddling
+                           // windows' partial maxima to a side buffer merged by the LRN kernel). Measured level with
+                           // 0 on the bench step (320.8-322.1 k vs 322.1-323.0 k: the GEMM runs 278 instead of 266 us,
+                           // the LRN 9.7 instead of 25.8; profiles/r05_conv2_pool/), so 0 = the GEMM writes its map
+                           // and maxpool_lrn pools it
   int conv2_tile = 4;      // Conv2 Winograd output tile: 4 = F(4x4,5x5) (64 points per 16 outputs: 21 % fewer
                            // multiplies, 16x16x4 MFMAs, wino_gemm16.hpp; one group of 96 channels only, else 3;
                            // bench step 305-309 k vs 293 k images/s, profiles/r05_f45/), 3 = F(3x3,5x5) (49
@@ -71,7 +77,7 @@ struct Knobs {
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
 // ANX_BF16_GLDS, ANX_BF16_BIG, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1,
-// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL, ANX_CONV2_TILE when set.
+// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL, ANX_CONV2_POOL, ANX_CONV2_TILE when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

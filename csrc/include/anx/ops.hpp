@@ -171,6 +171,20 @@ hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, Ou
 // The F(4x4,5x5) form (wino_gemm16.hpp): V [P][64][96], U [64][K][96], P tiles of 4x4 outputs, K % 32 == 0.
 hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
                                int Ho, int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
+// The same GEMM with pool2 (3x3 / 2 max) in its epilogue: the 27x27 conv2 map never reaches HBM. Pooled
+// pixel (py, px) of image n goes to pooled [n][Hp][Wp][K] from the workgroup owning the window's top-left
+// 4x4 tile (tile (py / 2, px / 2)); when the window's tiles straddle two workgroups' 32-tile ranges
+// (pool2_straddles), that value is the lower workgroup's partial max and the upper one's is in p2 (same
+// layout): the consumer takes the max of both (lrn_pooled_merge). Exact (max in any order).
+constexpr int kConv2PoolTiles = 32;  // Conv2 4x4 tiles per F(4x4,5x5) GEMM workgroup (raster order)
+__host__ __device__ inline bool pool2_straddles(int n, int py, int px, int ty2, int tx2) {
+  const int gm = n * ty2 * tx2 + (py >> 1) * tx2 + (px >> 1);
+  const int gM = gm + ((py & 1) ? tx2 : 0) + (px & 1);
+  return gm / kConv2PoolTiles != gM / kConv2PoolTiles;
+}
+hipError_t wino_gemm_conv2_f45_pool(const float* V, const float* U, const float* bias, float* pooled, float* p2, int P,
+                                    int ty, int tx, int Ho, int Wo, int Hp, int Wp, int K, bool relu, hipStream_t s,
+                                    int occ = 0);
 
 
 // Dynamic LDS bytes that cap a kernel at `wgs` workgroups per CU (160 KiB LDS per CU): the larger of
@@ -182,6 +196,11 @@ hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, Out
 // Fused max-pool + cross-channel LRN (block 2 tail).
 hipError_t maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int F, int S, int size,
                        float alpha, float beta, float k, LrnMode mode, hipStream_t s);
+// LRN of a pooled map written by wino_gemm_conv2_f45_pool (C == 256, size 5): pixel (n, py, px) is
+// max(pooled, p2) where pool2_straddles(n % sub, ...) (sub: images per GEMM launch, ty2 x tx2 tiles per
+// image), pooled alone elsewhere. Bit-identical to maxpool_lrn of the unpooled map.
+hipError_t lrn_pooled_merge(const float* pooled, const float* p2, float* y, int N, int Hp, int Wp, int C, int ty2,
+                            int tx2, int sub, int size, float alpha, float beta, float k, LrnMode mode, hipStream_t s);
 
 // Zero the rows of an NHWC buffer outside [row_lo, row_hi) and the W border (halo buffers).
 hipError_t fill(float* x, size_t n, float v, hipStream_t s);

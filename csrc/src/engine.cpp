@@ -323,6 +323,12 @@ bool BlocksEngine::conv1_pools(int N, const TilePlan& t) const {
   return true;
 }
 
+bool BlocksEngine::conv2_pools(const TilePlan& t) const {
+  const LrnSpec& l = b2_.lrn;
+  return k_.conv2_pool && u2_m_ == 4 && b2_.has_lrn && l.N == 5 && d_.C2 == 256 && b2_.pool.F == 3 &&
+         b2_.pool.S == 2 && t.c2.lo == 0 && t.c2.size() == d_.H2 && t.out.lo == 0 && t.out.size() == d_.Hp2;
+}
+
 hipError_t BlocksEngine::tile_forward(const float* x, int N, const TilePlan& t, float* y, hipStream_t s) {
   if (N > max_batch_) return hipErrorInvalidValue;
   if (t.out.empty()) return hipSuccess;
@@ -385,16 +391,35 @@ hipError_t BlocksEngine::tile_forward_conv1_pool(const float* x, int N, const Ti
     RoctxRange rx("anx conv2+pool2+lrn");
     const hip::Conv1WinoPlan w1 = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
     const int s2 = k_.conv2_sub > 0 ? std::min(n, k_.conv2_sub) : n;
+    // pool2 in the GEMM: the pooled map [n][Hp2][Wp2][C2] at c2_, the straddling windows' upper parts
+    // behind it (2 x 13 x 13 < 27 x 27 pixels per image: inside the conv2 map's workspace)
+    const bool pool2 = conv2_pools(t);
+    const size_t pimg = static_cast<size_t>(d_.Hp2) * d_.Wp2 * d_.C2;
+    float* const p2 = c2_ + static_cast<size_t>(n) * pimg;
+    int ty2 = 0, tx2 = 0;
     for (int b0 = 0; b0 < n; b0 += s2) {
       const int m = std::min(s2, n - b0);
       const hip::WinoPlan w = hip::make_wino_plan(m, t.q.size(), wq_, d_.C1, k2.K, k2.groups, u2_m_);
       if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
       ANX_TRY(hip::wino_window_merge_input(w, q2_ + (n0 + b0) * q_img, c1_ + b0 * p1_img, b0, w1.ty, w1.tx, t.q.lo,
                                            d_.Hp1, d_.Wp1, k2.P, wv_, s));
-      const hip::OutView c2v{c2_ + b0 * c2_img, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
-      ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
+      if (pool2) {
+        ty2 = w.ty;
+        tx2 = w.tx;
+        ANX_TRY(hip::wino_gemm_conv2_f45_pool(wv_, u2w_, b2d_, c2_ + b0 * pimg, p2 + b0 * pimg, w.P, w.ty, w.tx, w.Ho,
+                                              w.Wo, d_.Hp2, d_.Wp2, w.K, true, s, k_.conv2_occ));
+      } else {
+        const hip::OutView c2v{c2_ + b0 * c2_img, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
+        ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));
+      }
     }
-    ANX_TRY(pool2_chunk(n, t, y + n0 * y_img, s));
+    if (pool2) {
+      const LrnSpec& l = b2_.lrn;
+      ANX_TRY(hip::lrn_pooled_merge(c2_, p2, y + n0 * y_img, n, d_.Hp2, d_.Wp2, d_.C2, ty2, tx2, s2, l.N, l.alpha, l.beta,
+                                    l.k, l.mode, s));
+    } else {
+      ANX_TRY(pool2_chunk(n, t, y + n0 * y_img, s));
+    }
   }
   return hipSuccess;
 }

@@ -175,10 +175,14 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn_kernel(const float* __re
 // 1-KiB pixel rows; the LRN neighbours (channels 4i-2, 4i-1, 4i+4, 4i+5) come from lanes i-1 / i+1
 // by ds_bpermute, so there is no LDS tile, no barrier, and no bank conflicts. The squared-sum order
 // is that of maxpool_lrn_kernel (left to right), so both kernels give bitwise equal results.
-template <int F, int U>
+// MERGE: x is a pooled map [N][Ho][Wo][256] from the pool2 GEMM epilogue (wino_gemm_conv2_f45_pool), p2 the
+// upper workgroups' partial maxima of the straddling windows (pool2_straddles of image n % sub, ty2 x tx2
+// tiles per image): the pooled pixel is max(x, p2) there, x elsewhere.
+template <int F, int U, bool MERGE = false>
 __global__ void __launch_bounds__(kThreads) maxpool_lrn256_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                                   int P, int H, int W, int S, int Ho, int Wo, float a,
-                                                                  float beta, float k) {
+                                                                  float beta, float k, const float* __restrict__ p2 = nullptr,
+                                                                  int ty2 = 0, int tx2 = 0, int sub = 1) {
   constexpr int C = 256;
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * (kThreads / 64);
@@ -189,7 +193,16 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn256_kernel(const float* _
       const int p = base + u;
       if (p < P) {
         const int ox = p % Wo, r = p / Wo, oy = r % Ho, n = r / Ho;
-        own[u] = window_max<F>(x + nhwc(n, oy * S, ox * S, lane * 4, H, W, C), W, C);
+        if constexpr (MERGE) {
+          own[u] = *reinterpret_cast<const f32x4*>(x + static_cast<size_t>(p) * C + lane * 4);
+          if (pool2_straddles(n % sub, oy, ox, ty2, tx2)) {
+            const f32x4 q = *reinterpret_cast<const f32x4*>(p2 + static_cast<size_t>(p) * C + lane * 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) own[u][i] = fmaxf(own[u][i], q[i]);
+          }
+        } else {
+          own[u] = window_max<F>(x + nhwc(n, oy * S, ox * S, lane * 4, H, W, C), W, C);
+        }
       } else {
         own[u] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -221,6 +234,20 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn256_kernel(const float* _
 }
 
 }  // namespace
+
+hipError_t lrn_pooled_merge(const float* pooled, const float* p2, float* y, int N, int Hp, int Wp, int C, int ty2,
+                            int tx2, int sub, int size, float alpha, float beta, float k, LrnMode mode, hipStream_t s) {
+  const long P = static_cast<long>(N) * Hp * Wp;
+  if (P == 0) return hipSuccess;
+  if (C != 256 || size != 5 || sub < 1 || P * C >= (1L << 31)) return hipErrorInvalidValue;
+  const float a = mode == LrnMode::DivN ? alpha / static_cast<float>(size) : alpha;
+  constexpr int U = 2;  // pixels per wave step (as maxpool_lrn)
+  const long waves = (P + U - 1) / U;
+  const unsigned g = static_cast<unsigned>((waves + kThreads / 64 - 1) / (kThreads / 64));
+  maxpool_lrn256_kernel<3, U, true><<<g, kThreads, 0, s>>>(pooled, y, static_cast<int>(P), Hp, Wp, 1, Hp, Wp, a, beta,
+                                                           k, p2, ty2, tx2, sub);
+  return hipGetLastError();
+}
 
 hipError_t maxpool(const float* x, int N, int H, int W, int C, int F, int S, OutView out, hipStream_t s) {
   const int Ho = pool_out_dim(H, F, S), Wo = pool_out_dim(W, F, S);

@@ -52,9 +52,9 @@ using C1 = wg::Cfg<25, 48, 2, 1, 48, 2>;    // Conv1: 64 tiles x 32 filters, 2 w
 // measured slower and removed from the A/B build: profiles/r03_wgemm_ab.md, profiles/r04_wgemm_ab/.
 
 // The F(4x4,5x5) kernel (wino_gemm16.hpp): same Args, its own tile shape
-template <class G, int ABL>
+template <class G, int ABL, bool POOL = false>
 hipError_t launch16(const wg::Args& a0, hipStream_t s, int occ) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wg16::gemm16_kernel<G, ABL>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(wg16::gemm16_kernel<G, ABL, POOL>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return attr;
   wg::Args a = a0;
@@ -63,7 +63,7 @@ hipError_t launch16(const wg::Args& a0, hipStream_t s, int occ) {
   if (a.kg % G::BN || a.n_ntiles < 1 || a.u_rows < a.n_ntiles * G::BN) return hipErrorInvalidValue;
   if (occ < 0) occ = a.n_ptiles * a.n_ntiles <= device_cus() ? 1 : 0;
   const dim3 grid((a.n_ptiles + 7) / 8 * 8 * a.n_ntiles);
-  wg16::gemm16_kernel<G, ABL><<<grid, G::NT, occupancy_lds(G::kLdsBytes, occ), s>>>(a);
+  wg16::gemm16_kernel<G, ABL, POOL><<<grid, G::NT, occupancy_lds(G::kLdsBytes, occ), s>>>(a);
   return hipGetLastError();
 }
 // <waves along tiles, waves along filters, K slice, ring slots>: 32 tiles x 16 filters per wave
@@ -178,6 +178,39 @@ hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias
 #endif
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t wino_gemm_conv2_f45_pool(const float* V, const float* U, const float* bias, float* pooled, float* p2, int P,
+                                    int ty, int tx, int Ho, int Wo, int Hp, int Wp, int K, bool relu, hipStream_t s,
+                                    int occ) {
+  const long vb = static_cast<long>(P) * 64 * 96 * 4, ub = static_cast<long>(64) * K * 96 * 4;
+  // the epilogue's window walk: 4x4 tiles covering the map, a window's tiles within tx + 1 raster steps
+  // of its first (< one workgroup's 32), pooled dims of a 3x3 / 2 pool
+  if (K % 64 || vb >= (1L << 31) || ub >= (1L << 31) || ty * 4 < Ho || tx * 4 < Wo || tx + 1 > kConv2PoolTiles ||
+      Hp != (Ho - 3) / 2 + 1 || Wp != (Wo - 3) / 2 + 1 || Ho < 3 || Wo < 3 || P % (ty * tx) ||
+      static_cast<long>(P / (ty * tx)) * Hp * Wp * K >= (1L << 31))
+    return hipErrorInvalidValue;
+  if (P == 0) return hipSuccess;
+  wg::Args a{};
+  a.V = V;
+  a.U = U;
+  a.bias = bias;
+  a.out = OutView{pooled, Hp, Wp, K, 0, 0, 0};
+  a.P = P;
+  a.ty = ty;
+  a.tx = tx;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.kg = K;
+  a.u_rows = K;
+  a.vct = 96;
+  a.vbytes = static_cast<int>(vb);
+  a.ubytes = static_cast<int>(ub);
+  a.relu = relu ? 1 : 0;
+  a.p2 = p2;
+  a.Hp = Hp;
+  a.Wp = Wp;
+  return launch16<F45, 0, true>(a, s, occ);
 }
 
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,

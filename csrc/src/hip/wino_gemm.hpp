@@ -62,6 +62,8 @@ struct Args {
   int vct;             // V floats per (tile, point): C, or groups * C
   int vbytes, ubytes;  // buffer sizes (< 2^31)
   int relu;
+  float* p2;   // pool2 epilogue (gemm16_kernel<..., POOL>): straddling windows' partial maxima; out.base = pooled map
+  int Hp, Wp;  // pooled map dims
 };
 
 // Fold coefficients per point, coef[ab][i*3 + j] = A^T[i][a] * A^T[j][b].

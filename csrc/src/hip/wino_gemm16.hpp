@@ -91,7 +91,7 @@ struct Cfg {
 
 // ABL (A/B tool only; production instantiates 0): bit0 no fold, bit1 no DMA refills, bit2 no barrier,
 // bit4 no sched_group_barrier pinning, bit5 no epilogue stores.
-template <class G, int ABL>
+template <class G, int ABL, bool POOL = false>
 __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
   constexpr int KS = G::KS, BK = G::BK, NW = G::NW, NST = G::NST, U4 = G::U4, MF = G::MF, G4 = G::G4, NF = G::NF;
   constexpr bool kFold = !(ABL & 1), kDma = !(ABL & 2), kBar = !(ABL & 4), kPin = !(ABL & 16), kStore = !(ABL & 32);
@@ -253,11 +253,127 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
   // lane stores a 16-B filter group. D layout (16x16x4): lane (r16, kg) holds filter n0 + wn*16 + r16 of
   // tiles wm*32 + 16*(e >> 2) + 4*kg + (e & 3).
   __syncthreads();  // the ring is idle (the last slice waited vmcnt(0)): reuse it as scratch
+  const int fb = n0 + wn * 16;
+  const float bv = a.bias ? a.bias[fb + r16] : 0.f;
+  if constexpr (POOL) {
+    // Pool2 (3x3 / 2 max) on 4x4 tiles: pooled pixel (2 ty + dy, 2 tx + dx) of tile t = (ty, tx) covers
+    // rows 2 dy .. 2 dy + 2 and columns 2 dx .. 2 dx + 2 of the tile, i.e. its own rows 0-2 / 2-3 x columns
+    // 0-2 / 2-3, plus column 0 of tile t + 1 (dx = 1), row 0 of tile t + tx (dy = 1) and position (0, 0) of
+    // tile t + tx + 1 (both). A lane (filter r16) folds its 8 tiles' own parts in registers and posts the
+    // five values its tiles give to their left / upper neighbours into a per-wave LDS image; the lane
+    // owning a pixel's tile merges them. Neighbours past this workgroup's 32 tiles: the pixel is written
+    // as a partial max, and the next workgroup writes its part to p2 (pool2_straddles; lrn_pooled_merge).
+    constexpr int kCS = 5 * 16 + 4;  // floats per tile; + 4 puts the four kg lane groups on distinct banks
+    static_assert(G::WM == 1 && G::BM == kConv2PoolTiles, "pool2 epilogue: one row of 32 tiles per workgroup");
+    static_assert(G::kLdsBytes >= static_cast<size_t>(NW) * 32 * kCS * 4, "pool2 scratch");
+    // LDS / global address spaces spelled out: with generic pointers every global store may alias the LDS
+    // image, and the compiler serialises each pixel's LDS reads behind the previous pixel's store
+    using gbl_f32 = __attribute__((address_space(1))) float;
+    lds_f32* cb = lds3 + wave * 32 * kCS;
+    float own[G::NE][4];
+#pragma unroll
+    for (int e = 0; e < G::NE; ++e) {
+      float v[G::NQ];
+#pragma unroll
+      for (int q = 0; q < G::NQ; ++q) {
+        v[q] = Y[q][e] + bv;
+        if (a.relu) v[q] = fmaxf(v[q], 0.f);
+      }
+      float h0[4], h1[4];  // per row: columns 0-2, 2-3
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        h0[r] = fmaxf(fmaxf(v[4 * r], v[4 * r + 1]), v[4 * r + 2]);
+        h1[r] = fmaxf(v[4 * r + 2], v[4 * r + 3]);
+      }
+      own[e][0] = fmaxf(fmaxf(h0[0], h0[1]), h0[2]);
+      own[e][1] = fmaxf(fmaxf(h1[0], h1[1]), h1[2]);
+      own[e][2] = fmaxf(h0[2], h0[3]);
+      own[e][3] = fmaxf(h1[2], h1[3]);
+      lds_f32* c = cb + (16 * (e >> 2) + 4 * kg + (e & 3)) * kCS + r16;
+      c[0] = fmaxf(fmaxf(v[0], v[4]), v[8]);  // column 0, rows 0-2: pixel (0, 1) of tile t - 1
+      c[16] = fmaxf(v[8], v[12]);             // column 0, rows 2-3: pixel (1, 1) of tile t - 1
+      c[32] = h0[0];                          // row 0, columns 0-2: pixel (1, 0) of tile t - tx
+      c[48] = h1[0];                          // row 0, columns 2-3: pixel (1, 1) of tile t - tx
+      c[64] = v[0];                           // (0, 0): pixel (1, 1) of tile t - tx - 1
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave, LDS in order: every lane's posts are visible
+    const int ipt = a.ty * a.tx;
+    gbl_f32* const pooled = (gbl_f32*)(a.out.base);
+    gbl_f32* const p2 = (gbl_f32*)(a.p2);
+    const int pc = a.out.Cb;  // channels per pooled pixel
+    // tile t -> (image, tile row, tile column): one division per run of 4 consecutive tiles, then steps
+    // (integer division is ~30 VALU instructions; 8 per lane cost the epilogue several us per launch)
+    struct Pos {
+      int n, y, x;
+    };
+    auto pos_of = [&](int t) {
+      const int n = t / ipt, r = t - n * ipt, y = r / a.tx;
+      return Pos{n, y, r - y * a.tx};
+    };
+    auto step = [&](Pos q) {  // the next tile in raster order
+      if (++q.x == a.tx) {
+        q.x = 0;
+        if (++q.y == a.ty) q.y = 0, ++q.n;
+      }
+      return q;
+    };
+    Pos run[2] = {pos_of(p0 + 4 * kg), pos_of(p0 + 16 + 4 * kg)};
+    float pix[G::NE][4];
+#pragma unroll
+    for (int e = 0; e < G::NE; ++e) {
+      const int lt = 16 * (e >> 2) + 4 * kg + (e & 3), t = p0 + lt;
+      const Pos ps = run[e >> 2];
+      run[e >> 2] = step(ps);
+      // the neighbours' posts, loaded unconditionally (tile index clamped into this wave's image) so the
+      // 40 reads of a lane go out together behind one wait; -inf where the tile is another workgroup's
+      const int j1 = lt + 1, j7 = lt + a.tx, j8 = j7 + 1;
+      const lds_f32* c1 = cb + (j1 < 32 ? j1 : 31) * kCS + r16;
+      const lds_f32* c7 = cb + (j7 < 32 ? j7 : 31) * kCS + r16;
+      const lds_f32* c8 = cb + (j8 < 32 ? j8 : 31) * kCS + r16;
+      const float ninf = -__builtin_inff();
+      const float l0 = c1[0], l1 = c1[16], u0 = c7[32], u1 = c7[48], dg = c8[64];
+      pix[e][0] = own[e][0];
+      pix[e][1] = fmaxf(own[e][1], j1 < 32 ? l0 : ninf);
+      pix[e][2] = fmaxf(own[e][2], j7 < 32 ? u0 : ninf);
+      pix[e][3] = fmaxf(fmaxf(own[e][3], j1 < 32 ? l1 : ninf), fmaxf(j7 < 32 ? u1 : ninf, j8 < 32 ? dg : ninf));
+      if (t >= a.P) continue;
+      const int n = ps.n, tyy = ps.y, txx = ps.x;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int dy = d >> 1, dx = d & 1, py = 2 * tyy + dy, px = 2 * txx + dx;
+        if (py >= a.Hp || px >= a.Wp) continue;  // a valid pixel's neighbour tiles are in its image
+        pooled[(static_cast<size_t>(n * a.Hp + py) * a.Wp + px) * pc + fb + r16] = pix[e][d];
+      }
+    }
+    // the upper part of straddling windows: pixels of tiles p0 - tx - 1 .. p0 - 1 (another workgroup's)
+    // with a neighbour tile here; 3 pixels x 16 filters per tile
+    const int back = a.tx + 1;
+    const Pos pb = pos_of(p0 >= back ? p0 - back : 0);  // wave-uniform
+    for (int it = lane; it < back * 3 * 16; it += 64) {
+      const int f16 = it & 15, pix = it >> 4, ob = pix / 3, d = pix - ob * 3 + 1;
+      const int ot = p0 - back + ob;
+      if (ot < 0) continue;
+      // tile ot = pb + ob (p0 >= back here): ob <= tx, at most one row (and image) wrap
+      int n = pb.n, tyy = pb.y, txx = pb.x + ob;
+      if (txx >= a.tx) {
+        txx -= a.tx;
+        if (++tyy == a.ty) tyy = 0, ++n;
+      }
+      const int dy = d >> 1, dx = d & 1, py = 2 * tyy + dy, px = 2 * txx + dx;
+      if (py >= a.Hp || px >= a.Wp) continue;
+      const int lo = ot - p0;  // < 0: neighbour lo + j is here iff >= 0 (and < 32: j <= tx + 1 <= 32 + lo)
+      float m = -__builtin_inff();
+      bool any = false;
+      if (dx && lo + 1 >= 0) m = fmaxf(m, cb[(lo + 1) * kCS + 16 * dy + f16]), any = true;
+      if (dy && lo + a.tx >= 0) m = fmaxf(m, cb[(lo + a.tx) * kCS + 32 + 16 * dx + f16]), any = true;
+      if (dy && dx && lo + a.tx + 1 >= 0) m = fmaxf(m, cb[(lo + a.tx + 1) * kCS + 64 + f16]), any = true;
+      if (any) p2[(static_cast<size_t>(n * a.Hp + py) * a.Wp + px) * pc + fb + f16] = m;
+    }
+    return;
+  }
   constexpr int kTS = 16;  // reads conflict-free in the b128 lane groups; writes 2-way, free for ds_write_b32
   static_assert(G::kLdsBytes >= static_cast<size_t>(NW) * 32 * kTS * 4, "epilogue scratch");
   float* tr = lds + wave * 32 * kTS;
-  const int fb = n0 + wn * 16;
-  const float bv = a.bias ? a.bias[fb + r16] : 0.f;
   const OutView o = a.out;
   int oy0[2], ox0[2], img[2], trd[2];
   const int grp = 4 * (lane & 3);

@@ -41,6 +41,7 @@ const Field kFields[] = {
     {"conv1_pool", &Knobs::conv1_pool, nullptr, 0, 1, "ANX_CONV1_POOL"},
     {"conv1_sub", &Knobs::conv1_sub, nullptr, 0, 1 << 30, "ANX_CONV1_SUB"},
     {"conv2_sub", &Knobs::conv2_sub, nullptr, 0, 1 << 30, "ANX_CONV2_SUB"},
+    {"conv2_pool", &Knobs::conv2_pool, nullptr, 0, 1, "ANX_CONV2_POOL"},
     {"conv2_tile", &Knobs::conv2_tile, nullptr, 3, 4, "ANX_CONV2_TILE"},
 };
 

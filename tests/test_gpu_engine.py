@@ -508,3 +508,30 @@ def test_conv1_pool_epilogue_bitwise(cuda, N, kn):
     assert torch.equal(y, off(x))
     ref = blocks_forward(x.cpu(), on.weights, on.b1, on.b2)
     torch.testing.assert_close(y.cpu().double(), ref, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("N,kn,hw,mode", [(1, {}, None, "div_n"), (9, {}, None, "div_n"), (33, {}, None, "raw"),
+                                          (64, {}, None, "div_n"), (130, {}, None, "div_n"),
+                                          (40, {"chunk1": 16}, None, "div_n"), (64, {"conv2_sub": 24}, None, "div_n"),
+                                          (20, {"chunk1": 9, "conv2_sub": 4}, None, "raw"),
+                                          (5, {}, (195, 259), "div_n")])
+def test_conv2_pool_epilogue_bitwise(cuda, N, kn, hw, mode):
+    """pool2 in the F(4x4,5x5) Conv2 GEMM's epilogue (tuning knob conv2_pool: the conv2 map never reaches HBM;
+    windows straddling two workgroups' 32-tile ranges merged from a side buffer by the LRN kernel) gives
+    the same bits as the GEMM writing its map and maxpool_lrn pooling it: partial workgroups, chunks,
+    Conv2 sub-chunks (the merge's image index inside a GEMM launch), both LRN modes and a non-square
+    image; the whole output against the fp64 oracle too."""
+    H, W = hw if hw else (227, 227)
+    x = init_input(N, "rand", seed=23, H=H, W=W).to(cuda)
+    base = {**WINO1, **WINO2, **kn}
+    mk = lambda p: AlexNetBlocks(device=cuda, init="rand", seed=23, max_batch=N, H=H, W=W, lrn_mode=mode,
+                                 knobs={**base, "conv2_pool": p})
+    on, off = mk(1), mk(0)
+    assert on.get_knob("conv2_pool") == 1 and off.get_knob("conv2_pool") == 0
+    y = on(x)
+    assert torch.equal(y, off(x))
+    y.fill_(float("nan"))  # every pooled pixel rewritten each call
+    on(x, out=y)
+    assert torch.equal(y, off(x))
+    ref = blocks_forward_all(x, on.weights, on.b1, on.b2, device=cuda)
+    torch.testing.assert_close(y.double(), ref.to(cuda), rtol=2e-5, atol=2e-6)
