@@ -350,7 +350,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     const int back = a.tx + 1;
     const Pos pb = pos_of(p0 >= back ? p0 - back : 0);  // wave-uniform
     for (int it = lane; it < back * 3 * 16; it += 64) {
-      const int f16 = it & 15, pix = it >> 4, ob = pix / 3, d = pix - ob * 3 + 1;
+      const int f16 = it & 15, px3 = it >> 4, ob = px3 / 3, d = px3 - ob * 3 + 1;
       const int ot = p0 - back + ob;
       if (ot < 0) continue;
       // tile ot = pb + ob (p0 >= back here): ob <= tx, at most one row (and image) wrap
