@@ -77,6 +77,8 @@ using F45 = wg16::Cfg<1, 4, 96, 2>;
 using F45_b48 = wg16::Cfg<1, 4, 48, 2>;      // the first production shape: 48-channel slices, 2 per point
 using F45_k96x32 = wg16::Cfg<2, 2, 96, 2>;   // 64 x 32, one point per slice (275.8 us)
 using F45_b48x32 = wg16::Cfg<2, 2, 48, 2>;   // 64 x 32, 48-channel slices
+using F45_n1 = wg16::Cfg<2, 4, 96, 2, 1>;    // 32 x 64 on 8 waves of 16 x 16 (one MFMA block each: Y 64 registers,
+                                             // 4 waves per SIMD instead of 2)
 // Also measured at 128 / 64 images and not kept (profiles/r05_f45/wg45r*.log; within 1-2 %, the box
 // noise): 48-channel slices x 4 slots, 32 x 6 slots, a separable output fold (T over an a-row's 8
 // points, then Y once per row: 42 instead of 128 FMAs per point), filter blocks spread by XCD so each
@@ -175,6 +177,7 @@ hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias
     case 1: return launch16_abl<F45_b48>(a, s, occ, abl);
     case 2: return launch16_abl<F45_k96x32>(a, s, occ, abl);
     case 3: return launch16_abl<F45_b48x32>(a, s, occ, abl);
+    case 4: return launch16_abl<F45_n1>(a, s, occ, abl);
 #endif
     default: return hipErrorInvalidValue;
   }

@@ -64,13 +64,15 @@ __device__ __forceinline__ int swz16(int row) {
     return wg::swz<U4>(row);
 }
 
-// WM x WN waves of 32 tiles x 16 filters; BK-channel slices through an NST-slot ring.
-template <int WM_, int WN_, int BK_, int NST_>
+// WM x WN waves of 16 NB tiles x 16 filters (NB 16x16 MFMA blocks sharing each B fragment); BK-channel
+// slices through an NST-slot ring.
+template <int WM_, int WN_, int BK_, int NST_, int NB_ = 2>
 struct Cfg {
-  static constexpr int NPT = 64, C = 96, NQ = 16, NE = 8;  // points, channels, outputs, values per lane
+  static constexpr int NB = NB_;
+  static constexpr int NPT = 64, C = 96, NQ = 16, NE = 4 * NB;  // points, channels, outputs, values per lane
   static constexpr int WM = WM_, WN = WN_, BK = BK_, NST = NST_;
   static constexpr int NW = WM * WN, NT = 64 * NW;
-  static constexpr int BM = 32 * WM, BN = 16 * WN, U4 = BK / 4;
+  static constexpr int BM = 16 * NB * WM, BN = 16 * WN, U4 = BK / 4;
   static constexpr int KS = C / BK, TOTAL = NPT * KS;
   static constexpr int A_INS = BM * U4 / 64, B_INS = BN * U4 / 64;
   static constexpr int A_MAX = (A_INS + NW - 1) / NW, B_MAX = (B_INS + NW - 1) / NW;
@@ -81,12 +83,15 @@ struct Cfg {
   static constexpr int NI = (TOTAL + 1 - NST) / (UP * KS);
   static constexpr int TAIL = NPT - NI * UP;
   static constexpr int G4 = BK / 16;     // 16-channel groups per slice (one ds_read_b128 per operand row each)
-  static constexpr int MF = BK / 4 * 2;  // MFMAs per slice (k-steps x 2 row blocks)
+  static constexpr int MF = BK / 4 * NB;  // MFMAs per slice (k-steps x row blocks)
   static constexpr int NF = NQ * NE;     // fold FMAs per point
-  static constexpr int MINB = NW >= 8 ? 1 : 8 / NW;  // workgroups per CU the VGPR budget is sized for (8 waves)
+  // workgroups per CU the VGPR budget is sized for: 8 waves per CU with 2 blocks per wave (Y = 128
+  // registers), 16 with one (Y = 64: 4 waves per SIMD)
+  static constexpr int MINB = (NB == 2 ? 8 : 16) / NW >= 1 ? (NB == 2 ? 8 : 16) / NW : 1;
   static_assert(C % BK == 0 && BK % 16 == 0 && A_INS * 64 == BM * U4 && B_INS * 64 == BN * U4, "tile shape");
   static_assert(U4 == 4 || U4 == 8 || U4 == 12 || U4 == 24, "swizzle defined for 4, 8, 12, 24 units per row");
   static_assert(NST >= 2 && NI >= 1 && TAIL >= 1, "ring / loop shape");
+  static_assert(NB == 1 || NB == 2, "one or two 16-tile blocks per wave");
 };
 
 // ABL (A/B tool only; production instantiates 0): bit0 no fold, bit1 no DMA refills, bit2 no barrier,
@@ -150,7 +155,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
   int ra0[G4], ra1[G4], rb[G4];
 #pragma unroll
   for (int s = 0; s < G4; ++s) {
-    const int u = 4 * s + kg, x0 = wm * 32 + r16, x1 = x0 + 16, y = wn * 16 + r16;
+    const int u = 4 * s + kg, x0 = wm * 16 * G::NB + r16, x1 = x0 + 16, y = wn * 16 + r16;
     ra0[s] = (x0 * BK + 4 * (u ^ swz16<U4>(x0))) * 4;
     ra1[s] = (x1 * BK + 4 * (u ^ swz16<U4>(x1))) * 4;
     rb[s] = (G::A_FL + y * BK + 4 * (u ^ swz16<U4>(y))) * 4;
@@ -166,7 +171,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
 
   auto frag = [&](int addr) { return *reinterpret_cast<const f32x4*>(reinterpret_cast<const char*>(lds) + addr); };
   auto fold_one = [&](auto J, auto FI) {
-    constexpr int j = decltype(J)::value, fi = decltype(FI)::value, q = j >> 3, e = j & 7;
+    constexpr int j = decltype(J)::value, fi = decltype(FI)::value, q = j / G::NE, e = j % G::NE;
     Y[q][e] = __builtin_fmaf(cq[fi][q], acc[fi][e >> 2][e & 3], Y[q][e]);
   };
 
@@ -193,35 +198,38 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     }
     constexpr int so = slot * G::STAGE * 4;
     constexpr int j0 = NF * ks / KS, nj = NF * (ks + 1) / KS - j0;
+    constexpr int NB = G::NB;
     f32x4 fa0[2], fa1[2], fb[2];
     fa0[0] = frag(ra0[0] + so);
-    fa1[0] = frag(ra1[0] + so);
+    if constexpr (NB == 2) fa1[0] = frag(ra1[0] + so);
     fb[0] = frag(rb[0] + so);
     static_for<0, G4>([&](auto S) {
       constexpr int s = decltype(S)::value;
       if constexpr (s + 1 < G4) {
         fa0[(s + 1) & 1] = frag(ra0[s + 1] + so);
-        fa1[(s + 1) & 1] = frag(ra1[s + 1] + so);
+        if constexpr (NB == 2) fa1[(s + 1) & 1] = frag(ra1[s + 1] + so);
         fb[(s + 1) & 1] = frag(rb[s + 1] + so);
       }
       static_for<0, 4>([&](auto K) {
-        constexpr int k = decltype(K)::value, m = s * 8 + 2 * k;
+        constexpr int k = decltype(K)::value, m = (s * 4 + k) * NB;
         constexpr bool first = ks == 0 && s == 0 && k == 0;
         acc[ai][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa0[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][0], 0,
                                                           0, 0);
         if constexpr (fold)
           static_for<j0 + nj * m / MF, j0 + nj * (m + 1) / MF>(
               [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
-        acc[ai][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa1[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][1], 0,
-                                                          0, 0);
-        if constexpr (fold)
-          static_for<j0 + nj * (m + 1) / MF, j0 + nj * (m + 2) / MF>(
-              [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
+        if constexpr (NB == 2) {
+          acc[ai][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa1[s & 1][k], fb[s & 1][k], first ? f32x4{} : acc[ai][1],
+                                                            0, 0, 0);
+          if constexpr (fold)
+            static_for<j0 + nj * (m + 1) / MF, j0 + nj * (m + 2) / MF>(
+                [&](auto J) { fold_one(J, std::integral_constant<int, ai ^ 1>{}); });
+        }
       });
       if constexpr (kPin) {
-        if constexpr (s + 1 < G4) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // the next group's reads
-        static_for<0, 8>([&](auto M) {
-          constexpr int m = s * 8 + decltype(M)::value;
+        if constexpr (s + 1 < G4) __builtin_amdgcn_sched_group_barrier(0x100, 1 + NB, 0);  // the next group's reads
+        static_for<0, 4 * NB>([&](auto M) {
+          constexpr int m = s * 4 * NB + decltype(M)::value;
           constexpr int np = nj * (m + 1) / MF - nj * m / MF;  // fold FMAs behind this MFMA
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           if constexpr (fold && np > 0) __builtin_amdgcn_sched_group_barrier(0x002, np, 0);
@@ -229,7 +237,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
       }
     });
     if constexpr (decltype(FOLD)::value && !kFold && ks == 0)
-      Y[0][0] += acc[ai ^ 1][0][0] + acc[ai ^ 1][1][0];  // probe: keep both blocks' MFMAs live
+      Y[0][0] += acc[ai ^ 1][0][0] + acc[ai ^ 1][G::NB - 1][0];  // probe: keep both blocks' MFMAs live
   };
   using std::integral_constant;
   using T_ = integral_constant<bool, true>;
@@ -264,7 +272,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     // owning a pixel's tile merges them. Neighbours past this workgroup's 32 tiles: the pixel is written
     // as a partial max, and the next workgroup writes its part to p2 (pool2_straddles; lrn_pooled_merge).
     constexpr int kCS = 5 * 16 + 4;  // floats per tile; + 4 puts the four kg lane groups on distinct banks
-    static_assert(G::WM == 1 && G::BM == kConv2PoolTiles, "pool2 epilogue: one row of 32 tiles per workgroup");
+    static_assert(G::WM == 1 && G::NB == 2 && G::BM == kConv2PoolTiles, "pool2 epilogue: one wave row of 32 tiles");
     static_assert(G::kLdsBytes >= static_cast<size_t>(NW) * 32 * kCS * 4, "pool2 scratch");
     // LDS / global address spaces spelled out: with generic pointers every global store may alias the LDS
     // image, and the compiler serialises each pixel's LDS reads behind the previous pixel's store
@@ -372,14 +380,15 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     return;
   }
   constexpr int kTS = 16;  // reads conflict-free in the b128 lane groups; writes 2-way, free for ds_write_b32
-  static_assert(G::kLdsBytes >= static_cast<size_t>(NW) * 32 * kTS * 4, "epilogue scratch");
-  float* tr = lds + wave * 32 * kTS;
+  constexpr int TW = 16 * G::NB;  // tiles per wave
+  static_assert(G::kLdsBytes >= static_cast<size_t>(NW) * TW * kTS * 4, "epilogue scratch");
+  float* tr = lds + wave * TW * kTS;
   const OutView o = a.out;
-  int oy0[2], ox0[2], img[2], trd[2];
+  int oy0[G::NB], ox0[G::NB], img[G::NB], trd[G::NB];
   const int grp = 4 * (lane & 3);
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int t = (k * 64 + lane) >> 2, p = p0 + wm * 32 + t;
+  for (int k = 0; k < G::NB; ++k) {
+    const int t = (k * 64 + lane) >> 2, p = p0 + wm * TW + t;
     const int tj = p % a.tx, pq = p / a.tx;
     oy0[k] = p < a.P ? (pq % a.ty) * 4 : (1 << 28);  // out of range: never stored
     ox0[k] = tj * 4;
@@ -397,7 +406,7 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     // same-wave LDS accesses complete in order: the reads see the writes above, and the next q's
     // writes cannot overtake these reads
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < G::NB; ++k) {
       const f32x4 v4 = *reinterpret_cast<const f32x4*>(tr + trd[k]);
       const int oy = oy0[k] + q / 4, ox = ox0[k] + q % 4;
       if (oy < a.Ho && ox < a.Wo && (kStore || v4.x == -1.f))  // ABL 32: ReLU outputs are never -1

@@ -172,7 +172,7 @@ int main(int argc, char** argv) {
     std::printf("{\"conv\": 4, \"images\": %d, \"arm\": \"F(3,5) GEMM (production)\", \"us\": %.1f, \"tflops\": %.1f, "
                 "\"direct_equiv_tflops\": %.1f}\n",
                 images, t3, f3 / t3 * 1e-6, 2.0 * images * 27 * 27 * 256 * 96 * 25 / t3 * 1e-6);
-    for (int cfg = 0; cfg < 4; ++cfg)
+    for (int cfg = 0; cfg < 5; ++cfg)
       for (int abl : {0, 3, 16, 32}) {
         if (only_cfg >= 0 && cfg != only_cfg) continue;
         CHECK(hipMemset(y1, 0, ny * 4));
