@@ -89,7 +89,10 @@ hipError_t launch16_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
   if (abl == 0) return launch16<G, 0>(a, s, occ);
 #ifdef ANX_WGEMM_ABLATIONS
   if constexpr (std::is_same_v<G, F45>) {  // cost probes of the production shape only (compile time)
+    if (abl == 1) return launch16<G, 1>(a, s, occ);
+    if (abl == 2) return launch16<G, 2>(a, s, occ);
     if (abl == 3) return launch16<G, 3>(a, s, occ);
+    if (abl == 4) return launch16<G, 4>(a, s, occ);
     if (abl == 16) return launch16<G, 16>(a, s, occ);
     if (abl == 32) return launch16<G, 32>(a, s, occ);
   }

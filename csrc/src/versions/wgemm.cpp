@@ -173,7 +173,7 @@ int main(int argc, char** argv) {
                 "\"direct_equiv_tflops\": %.1f}\n",
                 images, t3, f3 / t3 * 1e-6, 2.0 * images * 27 * 27 * 256 * 96 * 25 / t3 * 1e-6);
     for (int cfg = 0; cfg < 5; ++cfg)
-      for (int abl : {0, 3, 16, 32}) {
+      for (int abl : {0, 1, 2, 3, 4, 16, 32}) {
         if (only_cfg >= 0 && cfg != only_cfg) continue;
         CHECK(hipMemset(y1, 0, ny * 4));
         if (hip::wino_gemm_conv2_f45(V4, U4, b, o1, w4.P, w4.ty, w4.tx, 27, 27, 256, true, nullptr, occ, abl, cfg) ==
