@@ -109,8 +109,9 @@ def parse():
                          "(-1 = the cost model's shed share on GPUs / off on the CPU rehearsal, 0 = off, >0 = that many)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu = gloo rehearsal (tests only)")
     ap.add_argument("--graph", type=int, default=0,
-                    help="dp, 1 GPU: the step as one captured HIP graph replayed each step (1), eager (0, default; "
-                         "measured equal: the step is GPU-bound), -1 auto")
+                    help="dp, 1 GPU: the step as one captured HIP graph replayed each step (1; joins the lanes per "
+                         "step: 231-236 k vs 322-323 k images/s free-running, profiles/r05_knob_ab/), eager (0, "
+                         "default), -1 auto")
     ap.add_argument("--no-b1", action="store_true", help="skip the batch-1 latency measurement")
     ap.add_argument("--lane-priority", type=int, default=0, help="dp: HIP stream priority of the side lanes (-1 = high)")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
