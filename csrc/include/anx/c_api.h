@@ -120,9 +120,9 @@ int anx_maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int F,
 int anx_conv_plan(int N, int Hp, int Wp, int C, int K, int F, int S, int groups, int* plan_out,
                   size_t* packed_floats, size_t* koff_ints);
 int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff);
-/* Per-engine kernel knobs (anx/knobs.hpp): names conv1_algo, conv2_algo, chunk1, chunk2, force_vec4,
-   force_scalar, bf16_glds, bf16_big, bf16_lrn_tile, conv1_occ, conv2_occ (anx/knobs.hpp).
-   set returns non-zero for an unknown name or an out-of-range value. */
+/* Per-engine kernel knobs: the field names of anx::Knobs (anx/knobs.hpp). set returns non-zero for an
+   unknown name, an out-of-range value or a failed workspace re-allocation (the knob is then unchanged);
+   it may free buffers a previously captured HIP graph names: re-capture after it. */
 int anx_engine_set_knob(void* engine, const char* name, int value);
 int anx_engine_get_knob(void* engine, const char* name, int* value);
 /* bf16 activation tap `i` of the last forward (FullEngine::tap) into dst; *elems = per-image count */

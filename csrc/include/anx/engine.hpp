@@ -50,7 +50,9 @@ class BlocksEngine {
   // Read at every launch: changing a knob between calls switches kernels. Use set_knob (it prepares
   // the weights / workspace the new setting needs outside any forward); a field written through
   // knobs() directly re-packs direct-path weights lazily and runs a conv without its Winograd workspace
-  // on the direct path.
+  // on the direct path. set_knob is a between-forwards operation: a change of conv2_tile or a conv algo
+  // frees and re-allocates transformed weights / workspaces, so a HIP graph captured before it (bench
+  // --graph) names freed buffers and must be re-captured. Throws (knobs restored) when a re-allocation fails.
   const Knobs& knobs() const { return k_; }
   int set_knob(const char* name, int value);  // 0, or -1 for a bad name / value (unchanged)
 

@@ -73,11 +73,15 @@ struct Knobs {
                            // multiplies, 16x16x4 MFMAs, wino_gemm16.hpp; one group of 96 channels only, else 3;
                            // bench step 305-309 k vs 293 k images/s, profiles/r05_f45/), 3 = F(3x3,5x5) (49
                            // points, 32x32x2 MFMAs: grouped Conv2 and the A/B arm)
+  int conv2_sched = 1;     // F(4x4,5x5) GEMM K-slice schedule: 1 = hand-scheduled (wino_gemm16_sched.inc: fragment
+                           // reads two groups ahead with counted lgkmcnt, alternating accumulators, the fold as one
+                           // packed burst at the slice start; bitwise identical), 0 = the compiler's schedule
 };
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
 // ANX_BF16_GLDS, ANX_BF16_BIG, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1,
-// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL, ANX_CONV2_POOL, ANX_CONV2_TILE when set.
+// ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL, ANX_CONV2_POOL, ANX_CONV2_TILE,
+// ANX_CONV2_SCHED when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

@@ -96,7 +96,7 @@ struct WinoPlan {
   int m;                  // output tile side
 };
 // m = 3: 96 or 48 channels per group and a multiple of 64 filters per group; m = 4: one group, 96
-// channels, a multiple of 32 filters (the fused GEMMs' shapes)
+// channels, a multiple of 64 filters (the fused GEMMs' shapes)
 bool wino_eligible(int F, int S, int C, int K, int groups, int m = 3);
 WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups, int m = 3);
 size_t wino_v_floats(const WinoPlan& w);  // V workspace [P][(m+4)^2][C]
@@ -168,7 +168,10 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
                            int cfg = -1);
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,
                            int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
-// The F(4x4,5x5) form (wino_gemm16.hpp): V [P][64][96], U [64][K][96], P tiles of 4x4 outputs, K % 32 == 0.
+// The F(4x4,5x5) form (wino_gemm16.hpp): V [P][64][96], U [64][K][96], P tiles of 4x4 outputs, K % 64 == 0.
+// abl 0 = the compiler-scheduled kernel, kConv2SchedAbl = the hand-scheduled slice (knob conv2_sched; bitwise
+// identical), other values = A/B-tool probes.
+constexpr int kConv2SchedAbl = 64 + 256 + 512;
 hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
                                int Ho, int Wo, int K, bool relu, hipStream_t s, int occ = 0, int abl = 0, int cfg = -1);
 // The same GEMM with pool2 (3x3 / 2 max) in its epilogue: the 27x27 conv2 map never reaches HBM. Pooled

@@ -364,9 +364,13 @@ int anx_conv_pack(const int* plan, const float* w_kcff, float* packed, int* koff
 }
 
 int anx_engine_set_knob(void* e, const char* name, int value) {
-  if (static_cast<anx::BlocksEngine*>(e)->set_knob(name, value) != 0)
-    return fail(std::string("bad knob or value: ") + (name ? name : "(null)"));
-  return 0;
+  // set_knob may (re)build weights and workspace (prepare(): hipMalloc / uploads that throw on failure):
+  // an exception must not cross the C ABI
+  return guarded("anx_engine_set_knob", [&] {
+    if (static_cast<anx::BlocksEngine*>(e)->set_knob(name, value) != 0)
+      return fail(std::string("bad knob or value: ") + (name ? name : "(null)"));
+    return 0;
+  });
 }
 int anx_engine_get_knob(void* e, const char* name, int* value) {
   if (anx::get_knob(static_cast<anx::BlocksEngine*>(e)->knobs(), name, value) != 0)

@@ -102,9 +102,16 @@ void BlocksEngine::prepare() {
     const hip::Conv1WinoPlan wp = hip::make_conv1_wino_plan(chunk_, d_.H, d_.W, k1.K, k1.F);
     std::vector<float> u;
     hip::conv1_wino_weights_host(k1.K, k1.F, w1h_.data(), u);
-    u1w_ = dev_upload(u);
+    // both buffers or neither (a failed allocation leaves the path off and retryable)
+    float* v = dev_alloc<float>(hip::conv1_wino_v_floats(wp));
+    try {
+      u1w_ = dev_upload(u);
+    } catch (...) {
+      (void)hipFree(v);
+      throw;
+    }
     wv1_cap_ = hip::conv1_wino_v_floats(wp);
-    wv1_ = dev_alloc<float>(wv1_cap_);
+    wv1_ = v;
   }
   if (u2w_ != nullptr && u2_m_ != tile2()) {  // the tile knob changed: other transformed weights / workspace
     for (float** q : {&u2w_, &wv_})
@@ -119,9 +126,15 @@ void BlocksEngine::prepare() {
     if (hip::wino_v_floats(wp) < (1UL << 31)) {
       std::vector<float> u;
       hip::wino_transform_weights_host(wp, w2h_.data(), u);
-      u2w_ = dev_upload(u);
+      float* v = dev_alloc<float>(hip::wino_v_floats(wp));
+      try {
+        u2w_ = dev_upload(u);
+      } catch (...) {
+        (void)hipFree(v);
+        throw;
+      }
       wv_cap_ = hip::wino_v_floats(wp);
-      wv_ = dev_alloc<float>(wv_cap_);
+      wv_ = v;
     }
   }
   // direct path: the full-image launch of min(max_batch, the Auto crossover) images
@@ -141,8 +154,17 @@ int BlocksEngine::tile2() const {
 }
 
 int BlocksEngine::set_knob(const char* name, int value) {
+  const Knobs before = k_;
   if (anx::set_knob(k_, name, value) != 0) return -1;
-  prepare();  // a knob may enable a path whose weights / workspace this engine has not built yet
+  try {
+    prepare();  // a knob may enable a path whose weights / workspace this engine has not built yet
+  } catch (...) {
+    // e.g. hipMalloc OOM building a Winograd workspace: keep the previous selection. prepare() builds
+    // lazily and a path whose buffers are null is not taken, so the engine stays usable; the caller
+    // (anx_engine_set_knob) turns the exception into an error code
+    k_ = before;
+    throw;
+  }
   return 0;
 }
 

@@ -71,6 +71,13 @@ hipError_t launch16(const wg::Args& a0, hipStream_t s, int occ) {
 // blocks instead of 8, one barrier and one refill wait per point (128 images alone: 273.2 us vs 291.8 with
 // 48-channel slices, 298.0 for the F(3x3,5x5) kernel; profiles/r05_f45/wg45k_128.log)
 using F45 = wg16::Cfg<1, 4, 96, 2>;
+// The production schedule of F45 (knob conv2_sched = 1): the hand-scheduled slice (ABL bit 64) with the fold
+// as one v_pk_fma_f32 burst at the slice start (fold mode 2 = 256, packed = 512) and the refill DMA issued by
+// the compiler. 128 images alone: 255-260 vs 272-277 us, bitwise identical; the fold behind every MFMA ran
+// 318 us, per group 287 / 263 (scalar / packed), the DMA moved into the statement 260-264
+// (profiles/r06_conv2_sched/).
+constexpr int kConv2Sched = kConv2SchedAbl;
+static_assert(kConv2Sched == 64 + 256 + 512, "fold burst, packed, DMA by the compiler");
 #ifdef ANX_WGEMM_ABLATIONS
 // measured alone at 128 images (profiles/r05_f45/wg45_128_v2.log, wg45k_128.log): 64 x 64 on 8 waves
 // 323 us, 128 x 32 317, 3-slot rings 303-315, 32 x 128 302: not kept as configurations
@@ -87,8 +94,20 @@ using F45_n1 = wg16::Cfg<2, 4, 96, 2, 1>;    // 32 x 64 on 8 waves of 16 x 16 (o
 template <class G>
 hipError_t launch16_abl(const wg::Args& a, hipStream_t s, int occ, int abl) {
   if (abl == 0) return launch16<G, 0>(a, s, occ);
+  if constexpr (std::is_same_v<G, F45>)
+    if (abl == kConv2Sched) return launch16<G, kConv2Sched>(a, s, occ);  // hand-scheduled slice (knob conv2_sched)
 #ifdef ANX_WGEMM_ABLATIONS
   if constexpr (std::is_same_v<G, F45>) {  // cost probes of the production shape only (compile time)
+    if (abl == 64) return launch16<G, 64>(a, s, occ);
+    if (abl == 65) return launch16<G, 65>(a, s, occ);
+    if (abl == 67) return launch16<G, 67>(a, s, occ);
+    // fold placement / packing / DMA placement of the hand-scheduled slice: 64 + 128 * fold mode + 512 * packed
+    // + 1024 * DMA mode (wino_gemm16_sched.inc)
+    if (abl == 704) return launch16<G, 704>(a, s, occ);
+    if (abl == 1856) return launch16<G, 1856>(a, s, occ);
+    if (abl == 2880) return launch16<G, 2880>(a, s, occ);
+    if (abl == 3904) return launch16<G, 3904>(a, s, occ);
+    if (abl == 2752) return launch16<G, 2752>(a, s, occ);
     if (abl == 1) return launch16<G, 1>(a, s, occ);
     if (abl == 2) return launch16<G, 2>(a, s, occ);
     if (abl == 3) return launch16<G, 3>(a, s, occ);
@@ -156,7 +175,7 @@ hipError_t wino_gemm_conv2(const float* V, const float* U, const float* bias, Ou
 hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx,
                                int Ho, int Wo, int K, bool relu, hipStream_t s, int occ, int abl, int cfg) {
   const long vb = static_cast<long>(P) * 64 * 96 * 4, ub = static_cast<long>(64) * K * 96 * 4;
-  if (K % 32 || vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
+  if (K % 64 || vb >= (1L << 31) || ub >= (1L << 31) || out.Cb % 4 || out.c_off % 4) return hipErrorInvalidValue;
   if (P == 0) return hipSuccess;
   wg::Args a{};
   a.V = V;

@@ -49,6 +49,8 @@ constexpr Coef64 make_coef64() {
 }
 static __constant__ Coef64 c_coef64 = make_coef64();
 
+#include "wino_gemm16_sched.inc"
+
 // LDS swizzle of the 16-B unit u of row r: u ^ swz16(r). ds_read_b128 is served in four 16-lane groups,
 // {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32 (MI355X_MICROARCH.md, LDS): with 48-float rows
 // a group's (row, unit) pairs land on 16 distinct 16-B slots iff the XOR of rows 0-3 / 4-7 / 8-11 / 12-15
@@ -94,12 +96,17 @@ struct Cfg {
   static_assert(NB == 1 || NB == 2, "one or two 16-tile blocks per wave");
 };
 
-// ABL (A/B tool only; production instantiates 0): bit0 no fold, bit1 no DMA refills, bit2 no barrier,
-// bit4 no sched_group_barrier pinning, bit5 no epilogue stores.
+// ABL: bit0 no fold, bit1 no DMA refills, bit2 no barrier, bit4 no sched_group_barrier pinning, bit5 no
+// epilogue stores (cost probes, A/B tool only); bit6 the hand-scheduled slice (wino_gemm16_sched.inc, knob
+// conv2_sched): fragment reads two groups ahead with counted waits, alternating accumulators, fold FMAs
+// behind every MFMA. Bitwise identical to the compiler-scheduled kernel.
 template <class G, int ABL, bool POOL = false>
 __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
   constexpr int KS = G::KS, BK = G::BK, NW = G::NW, NST = G::NST, U4 = G::U4, MF = G::MF, G4 = G::G4, NF = G::NF;
   constexpr bool kFold = !(ABL & 1), kDma = !(ABL & 2), kBar = !(ABL & 4), kPin = !(ABL & 16), kStore = !(ABL & 32);
+  constexpr bool kAsm = (ABL & 64) != 0;
+  static_assert(!kAsm || (G::G4 == 6 && G::NB == 2 && G::KS == 1 && G::NQ == 16 && G::NE == 8),
+                "the hand-scheduled slice is generated for one 96-channel point per slice, two 16x16 blocks");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -190,13 +197,69 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
       wg::wait_vm_lgkm<vm>();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
-    if constexpr (refill) issue(pb + nlit / KS, nlit % KS, nlit % NST);
-    if constexpr (ks == 0) {
+    if constexpr (refill && !(kAsm && ((ABL >> 10) & 3) != 0)) issue(pb + nlit / KS, nlit % KS, nlit % NST);
+    auto load_coef = [&] {
       const float* cr = c_coef64.v[ab];
 #pragma unroll
       for (int q = 0; q < G::NQ; ++q) cq[ai][q] = cr[q];
+    };
+    if constexpr (kAsm && fold) {
+      // the hand-scheduled slice reads the previous point's coefficients: make the compiler's wait for
+      // their scalar load land here, behind the barrier that already drained it, and not after the next
+      // point's load (it cannot see the barrier's lgkmcnt(0) and would wait for both)
+      asm volatile("" ::"s"(cq[ai ^ 1][0]), "s"(cq[ai ^ 1][1]), "s"(cq[ai ^ 1][2]), "s"(cq[ai ^ 1][3]),
+                   "s"(cq[ai ^ 1][4]), "s"(cq[ai ^ 1][5]), "s"(cq[ai ^ 1][6]), "s"(cq[ai ^ 1][7]), "s"(cq[ai ^ 1][8]),
+                   "s"(cq[ai ^ 1][9]), "s"(cq[ai ^ 1][10]), "s"(cq[ai ^ 1][11]), "s"(cq[ai ^ 1][12]),
+                   "s"(cq[ai ^ 1][13]), "s"(cq[ai ^ 1][14]), "s"(cq[ai ^ 1][15]));
     }
+    if constexpr (ks == 0) load_coef();
     constexpr int so = slot * G::STAGE * 4;
+    if constexpr (kAsm) {
+      constexpr int mode = (ABL >> 7) & 3, dm = refill ? (ABL >> 10) & 3 : 0;
+      constexpr bool pk = (ABL & 512) != 0;
+      static_assert((mode == 0 && !pk) || (mode == 1 && pk) || (mode == 2 && pk), "generated fold forms");
+      [[maybe_unused]] Dma d;
+      if constexpr (dm != 0) {
+        static_assert(G::A_MAX == 3 && G::B_MAX == 6 && G::A_INS % NW == 0 && G::B_INS % NW == 0, "DMA shape");
+        const int abn = pb + nlit / KS;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) d.voff[i] = voff[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) d.uoff[i] = uoff[i];
+#if __HIP_DEVICE_COMPILE__
+        d.vr = vr;
+        d.ur = ur;
+#endif
+        d.vso = (abn * a.vct) * 4;
+        d.uso = (abn * a.u_rows * G::C) * 4;
+        d.wb = static_cast<int>(reinterpret_cast<size_t>(lds3)) + wave * 1024;  // LDS byte address of my pieces
+      }
+      constexpr int rs = (nlit % NST) * G::STAGE * 4;
+      auto& a0 = acc[ai][0];
+      auto& a1 = acc[ai][1];
+      if constexpr (fold) {
+        const auto& p0 = acc[ai ^ 1][0];
+        const auto& p1 = acc[ai ^ 1][1];
+        const auto& c = cq[ai ^ 1];
+#define ANX_WG16_FOLD(F)                                                      \
+  if constexpr (dm == 0) F##_d0<so>(Y, a0, a1, p0, p1, c, ra0, ra1, rb);      \
+  if constexpr (dm == 1) F##_d1<so, rs>(Y, a0, a1, p0, p1, c, ra0, ra1, rb, d); \
+  if constexpr (dm == 2) F##_d2<so, rs>(Y, a0, a1, p0, p1, c, ra0, ra1, rb, d); \
+  if constexpr (dm == 3) F##_d3<so, rs>(Y, a0, a1, p0, p1, c, ra0, ra1, rb, d);
+        if constexpr (mode == 0) { ANX_WG16_FOLD(slice_fold0) }
+        if constexpr (mode == 1) { ANX_WG16_FOLD(slice_fold1p) }
+        if constexpr (mode == 2) { ANX_WG16_FOLD(slice_fold2p) }
+#undef ANX_WG16_FOLD
+      } else {
+        if constexpr (dm == 0) slice_first_d0<so>(a0, a1, ra0, ra1, rb);
+        if constexpr (dm == 1) slice_first_d1<so, rs>(a0, a1, ra0, ra1, rb, d);
+        if constexpr (dm == 2) slice_first_d2<so, rs>(a0, a1, ra0, ra1, rb, d);
+        if constexpr (dm == 3) slice_first_d3<so, rs>(a0, a1, ra0, ra1, rb, d);
+      }
+      if constexpr (decltype(FOLD)::value && !kFold)
+        Y[0][0] += acc[ai ^ 1][0][0] + acc[ai ^ 1][G::NB - 1][0];  // probe: keep both blocks' MFMAs live
+      return;
+    }
     constexpr int j0 = NF * ks / KS, nj = NF * (ks + 1) / KS - j0;
     constexpr int NB = G::NB;
     f32x4 fa0[2], fa1[2], fb[2];
@@ -255,6 +318,8 @@ __global__ void __launch_bounds__(G::NT, G::MINB) gemm16_kernel(wg::Args a) {
     static_for<0, G::UP * KS>([&](auto LIT) { slice(pb, LIT, F_{}, T_{}); });
   }
   static_for<G::NI * G::UP * KS, G::TOTAL>([&](auto IT) { slice(0, IT, T_{}, T_{}); });
+  // an MFMA's D read by a VALU: 12 wait states after the hand-scheduled slice's last MFMA (8-pass XDL)
+  if constexpr (kAsm) asm volatile("s_nop 7\n\ts_nop 3" ::: "memory");
   static_for<0, NF>([&](auto J) { fold_one(J, integral_constant<int, (G::NPT - 1) & 1>{}); });
 
   // Epilogue: bias + ReLU, then per output q one LDS transpose of the wave's 32 tiles x 16 filters so each

@@ -292,10 +292,10 @@ WinoPlan make_wino_plan(int N, int Hq, int Wq, int C, int K, int groups, int m) 
 
 bool wino_eligible(int F, int S, int C, int K, int groups, int m) {
   // the fused GEMMs' configurations: F(3,5) 96 or 48 channels per group and filters per group a multiple
-  // of 64; F(4,5) one group of 96 channels and a multiple of 32 filters
+  // of 64; F(4,5) one group of 96 channels and a multiple of 64 filters (its workgroup tile is 64 filters)
   if (F != wino::kR || S != 1 || groups < 1 || C % groups || K % groups) return false;
   const int Cg = C / groups, Kg = K / groups;
-  if (m == 4) return groups == 1 && C == 96 && K % 32 == 0;
+  if (m == 4) return groups == 1 && C == 96 && K % 64 == 0;
   return (Cg == 96 || Cg == 48) && Kg % 64 == 0;
 }
 
@@ -363,7 +363,9 @@ hipError_t wino_input(const WinoPlan& w, const float* x, float* V, hipStream_t s
 
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,
                       hipStream_t s, const Knobs& k) {
-  if (w.m == 4) return wino_gemm_conv2_f45(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.K, relu, s, k.conv2_occ);
+  if (w.m == 4)
+    return wino_gemm_conv2_f45(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.K, relu, s, k.conv2_occ,
+                               k.conv2_sched ? kConv2SchedAbl : 0);
   return wino_gemm_conv2(V, U, bias, out, w.P, w.ty, w.tx, w.Ho, w.Wo, w.C, w.K, w.groups, relu, s, k.conv2_occ);
 }
 

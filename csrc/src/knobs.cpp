@@ -43,6 +43,7 @@ const Field kFields[] = {
     {"conv2_sub", &Knobs::conv2_sub, nullptr, 0, 1 << 30, "ANX_CONV2_SUB"},
     {"conv2_pool", &Knobs::conv2_pool, nullptr, 0, 1, "ANX_CONV2_POOL"},
     {"conv2_tile", &Knobs::conv2_tile, nullptr, 3, 4, "ANX_CONV2_TILE"},
+    {"conv2_sched", &Knobs::conv2_sched, nullptr, 0, 1, "ANX_CONV2_SCHED"},
 };
 
 const Field* find(const char* name) {

@@ -78,12 +78,13 @@ double max_abs_diff(const std::vector<float>& a, const std::vector<float>& b, do
 }  // namespace
 
 int main(int argc, char** argv) {
-  int images = 300, iters = 20, only = 0, only_cfg = -1, occ = 0;
+  int images = 300, iters = 20, only = 0, only_cfg = -1, only_abl = -1, occ = 0;
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!std::strcmp(argv[i], "--images")) images = std::atoi(argv[i + 1]);
     else if (!std::strcmp(argv[i], "--iters")) iters = std::atoi(argv[i + 1]);
     else if (!std::strcmp(argv[i], "--conv")) only = std::atoi(argv[i + 1]);  // 1 or 2: that conv only; 4: Conv2 F(4x4,5x5)
     else if (!std::strcmp(argv[i], "--cfg")) only_cfg = std::atoi(argv[i + 1]);
+    else if (!std::strcmp(argv[i], "--abl")) only_abl = std::atoi(argv[i + 1]);
     else if (!std::strcmp(argv[i], "--occ")) occ = std::atoi(argv[i + 1]);  // workgroups-per-CU cap
   }
   if (images < 1 || images > 1400 || iters < 1) {
@@ -172,9 +173,11 @@ int main(int argc, char** argv) {
     std::printf("{\"conv\": 4, \"images\": %d, \"arm\": \"F(3,5) GEMM (production)\", \"us\": %.1f, \"tflops\": %.1f, "
                 "\"direct_equiv_tflops\": %.1f}\n",
                 images, t3, f3 / t3 * 1e-6, 2.0 * images * 27 * 27 * 256 * 96 * 25 / t3 * 1e-6);
+    std::vector<float> y_prod;  // cfg 0 abl 0 (the compiler-scheduled production kernel): bitwise reference
     for (int cfg = 0; cfg < 5; ++cfg)
-      for (int abl : {0, 1, 2, 3, 4, 16, 32}) {
+      for (int abl : {0, 64, 704, 832, 1856, 2880, 3904, 2752, 1, 65, 2, 3, 67, 4, 16, 32}) {
         if (only_cfg >= 0 && cfg != only_cfg) continue;
+        if (only_abl >= 0 && abl != only_abl && !(cfg == 0 && abl == 0)) continue;
         CHECK(hipMemset(y1, 0, ny * 4));
         if (hip::wino_gemm_conv2_f45(V4, U4, b, o1, w4.P, w4.ty, w4.tx, 27, 27, 256, true, nullptr, occ, abl, cfg) ==
             hipErrorInvalidValue)
@@ -185,10 +188,15 @@ int main(int argc, char** argv) {
             },
             iters);
         double rmax = 0;
-        const double d = max_abs_diff(download(y1, ny), ref, &rmax);
+        const auto yo = download(y1, ny);
+        const double d = max_abs_diff(yo, ref, &rmax);
+        if (cfg == 0 && abl == 0) y_prod = yo;
+        const bool bitwise = !y_prod.empty() && std::memcmp(yo.data(), y_prod.data(), ny * 4) == 0;
         std::printf("{\"conv\": 4, \"images\": %d, \"arm\": \"F(4,5) GEMM cfg=%d abl=%d\", \"us\": %.1f, \"tflops\": %.1f, "
-                    "\"direct_equiv_tflops\": %.1f, \"max_abs_diff_vs_f35\": %.3g, \"ref_max\": %.3g}\n",
-                    images, cfg, abl, t, f4 / t * 1e-6, 2.0 * images * 27 * 27 * 256 * 96 * 25 / t * 1e-6, d, rmax);
+                    "\"direct_equiv_tflops\": %.1f, \"max_abs_diff_vs_f35\": %.3g, \"ref_max\": %.3g, "
+                    "\"bitwise_vs_production\": %s}\n",
+                    images, cfg, abl, t, f4 / t * 1e-6, 2.0 * images * 27 * 27 * 256 * 96 * 25 / t * 1e-6, d, rmax,
+                    bitwise ? "true" : "false");
       }
     for (float* p : {x, U3, U4, V3, V4, y0, y1, b}) CHECK(hipFree(p));
   }

@@ -29,7 +29,9 @@ Names and values:
   ``conv2_pool`` (0, the default: the Conv2 GEMM writes its map and the pool2 + LRN kernel pools it; 1: pool2
   in the F(4x4,5x5) GEMM's epilogue for whole images, 125 MB less HBM traffic per 128 images, measured level
   on the bench step);
-  ``conv2_tile`` (Conv2's Winograd output tile: 3 = F(3x3,5x5), 4 = F(4x4,5x5), 21 % fewer multiplies).
+  ``conv2_tile`` (Conv2's Winograd output tile: 3 = F(3x3,5x5), 4 = F(4x4,5x5), 21 % fewer multiplies);
+  ``conv2_sched`` (1, the default: the F(4x4,5x5) GEMM's hand-scheduled K slice, bitwise equal to 0, the
+  compiler's schedule).
 """
 from __future__ import annotations
 
@@ -40,7 +42,7 @@ from .. import _native as nat
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
          "bf16_lrn_tile", "bf16_conv1", "bf16_pool1", "bf16_fc_cfg", "bf16_fc_minkt", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
-         "conv1_fused", "conv1_pool", "conv2_pool", "conv2_tile")
+         "conv1_fused", "conv1_pool", "conv2_pool", "conv2_tile", "conv2_sched")
 
 
 def knob_value(name: str, value) -> int:

@@ -535,3 +535,36 @@ def test_conv2_pool_epilogue_bitwise(cuda, N, kn, hw, mode):
     assert torch.equal(y, off(x))
     ref = blocks_forward_all(x, on.weights, on.b1, on.b2, device=cuda)
     torch.testing.assert_close(y.double(), ref.to(cuda), rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("N,kn", [(9, {}), (64, {}), (130, {}), (300, {}), (40, {"chunk1": 16, "conv2_sub": 24})])
+def test_conv2_hand_schedule_bitwise(cuda, N, kn):
+    """The F(4x4,5x5) Conv2 GEMM's hand-scheduled K slice (knob conv2_sched = 1, wino_gemm16_sched.inc: counted
+    fragment reads two groups ahead, the fold as a packed burst) gives the same bits as the compiler-scheduled
+    kernel (same fmaf order per accumulator and fold value), on partial workgroups, multi-round grids and
+    sub-chunked launches; the whole output against the fp64 oracle too."""
+    x = init_input(N, "rand", seed=29).to(cuda)
+    mk = lambda v: AlexNetBlocks(device=cuda, init="rand", seed=29, max_batch=N,
+                                 knobs={**WINO1, **WINO2, **kn, "conv2_tile": 4, "conv2_sched": v})
+    hand, comp = mk(1), mk(0)
+    assert hand.get_knob("conv2_sched") == 1 and comp.get_knob("conv2_sched") == 0
+    y = hand(x)
+    assert torch.equal(y, comp(x))
+    ref = blocks_forward_all(x, hand.weights, hand.b1, hand.b2, device=cuda)
+    torch.testing.assert_close(y.double(), ref.to(cuda), rtol=2e-5, atol=2e-6)
+
+
+def test_set_knob_rebuilds_conv2_workspace(cuda):
+    """conv2_tile switched 4 -> 3 -> 4 on one engine between forwards rebuilds the transformed weights and
+    the V workspace each time (BlocksEngine::prepare) and matches engines built fresh with that tile
+    (set_knob frees buffers a captured graph would still name, so it is a between-forwards
+    operation)."""
+    N = 24
+    x = init_input(N, "rand", seed=31).to(cuda)
+    fresh = {t: AlexNetBlocks(device=cuda, init="rand", seed=31, max_batch=N, knobs={**WINO2, "conv2_tile": t})(x)
+             for t in (3, 4)}
+    m = AlexNetBlocks(device=cuda, init="rand", seed=31, max_batch=N, knobs={**WINO2, "conv2_tile": 4})
+    for t in (4, 3, 4, 3):
+        m.set_knob("conv2_tile", t)
+        assert m.get_knob("conv2_tile") == t
+        assert torch.equal(m(x), fresh[t])
