@@ -27,9 +27,14 @@ MI355X". Workloads (--workload):
   reference's row split over every rank) | hybrid (batch first, rows only below one image per rank) |
   batch.
 
-Every workload's JSON carries ``model``: the modelled 1/2/4/8-GPU curve of its configuration
-(``"measured": false``; anx.parallel.cost), with this run's measured single-GPU rate in the model's
-throughput table when N = 1.
+Every workload's JSON carries a top-level ``model_curve``: the MODELLED 1/2/4/8-GPU curve of its
+configuration (``"measured": false``; anx.parallel.cost), with this run's measured single-GPU rate in the
+model's throughput table when N = 1. It is kept out of ``config`` so no modelled number sits among the
+measured ones.
+
+The dp run also carries ``v4`` and ``v5``: BASELINE configs 3 and 4 (the reference's multi-GPU programs)
+measured on the same ranks by the native runtimes, V5 with and without the pool1 halo exchange
+(:func:`reference_programs`; ``--no-ref-programs`` skips them).
 
 Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
 bench.py --gpus N``. Rank 0 prints ONE JSON line.
@@ -133,6 +138,11 @@ def parse():
                     help="dp, N>1: skip the post-window gather checksum / oracle verification step")
     ap.add_argument("--no-subrecords", action="store_true",
                     help="v5: skip the forced 2-way-row (halo on) sub-records per device transport")
+    ap.add_argument("--no-ref-programs", action="store_true",
+                    help="dp: skip the V4 / V5 secondary records (BASELINE configs 3 and 4) beside the headline")
+    ap.add_argument("--ref-steps", type=int, default=5, help="timed steps of each V4 / V5 secondary arm")
+    ap.add_argument("--ref-batch-v4", type=int, default=2, help="CPU rehearsal only: V4 secondary global batch")
+    ap.add_argument("--ref-batch-v5", type=int, default=3, help="CPU rehearsal only: V5 secondary global batch")
     ap.add_argument("--no-full", action="store_true",
                     help="blocks dp on GPUs: skip the secondary full-AlexNet bf16 (BASELINE config 5) measurement")
     ap.add_argument("--first-collective-s", type=float, default=float(os.environ.get("ANX_FIRST_COLLECTIVE_S", "240")),
@@ -152,18 +162,43 @@ def process_cold_b1() -> dict:
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "ANX_RANK", "ANX_WORLD_SIZE", "ANX_LOCAL_RANK")}
+    probe = os.path.join(os.path.dirname(exe), "anx_hipinit")
+
+    def bare():  # the bare HIP runtime's start-up in a fresh process without libanx (anx_hipinit)
+        if not os.path.exists(probe):
+            return None
+        try:
+            p = subprocess.run([probe, "pinned"], capture_output=True, text=True, timeout=120, env=env)
+            js = [json.loads(l[len("ANX_JSON "):]) for l in p.stdout.splitlines() if l.startswith("ANX_JSON ")]
+            return js[0] if p.returncode == 0 and js else None
+        except Exception:
+            return None
+
+    bare0 = bare()
     t0 = time.perf_counter()
     out = subprocess.run([exe, "--version", "v3", "--batch", "1", "--init", "rand", "--iters", "20"],
                          capture_output=True, text=True, timeout=300, env=env)
     wall = (time.perf_counter() - t0) * 1e3
+    bare1 = bare()
     recs = [json.loads(l[len("ANX_JSON "):]) for l in out.stdout.splitlines() if l.startswith("ANX_JSON ")]
     if out.returncode != 0 or not recs:
         return {"b1_process_cold_ms": None, "b1_process_note": f"anx v3 failed rc={out.returncode}"}
     r = recs[0]
-    return {"b1_process_cold_ms": round(r["cold_ms"], 3), "b1_process_wall_ms": round(wall, 1),
+    # the same steps as the anx child's `init` phase (hipInit .. first stream), timed in a process that does
+    # not load libanx, once before and once after the anx child: what the HIP runtime costs by itself
+    binit = [round(b["hip_init_ms"] + b["device_count_ms"] + b["context_ms"] + b["stream_ms"], 3)
+             for b in (bare0, bare1) if b]
+    ph = {k: round(v, 3) for k, v in (r.get("phases_cold") or {}).items()}
+    init_split = {}
+    if binit and "init" in ph:
+        init_split = {"init_bare_hip_ms": binit, "init_ours_ms": round(ph["init"] - min(binit), 3),
+                      "init_note": "init_bare_hip_ms: anx_hipinit (no libanx) before / after the anx child; "
+                                   "init_ours_ms = the child's init minus the faster bare probe (run-to-run noise "
+                                   "of the bare HIP start-up on these boxes is +-50 ms, profiles/r06_cold/)"}
+    return {"b1_process_cold_ms": round(r["cold_ms"], 3), "b1_process_wall_ms": round(wall, 1), **init_split,
             # where the cold time goes (init = HIP runtime / context, engine = weights + workspace, alloc,
             # h2d / compute / d2h of the first image)
-            "b1_process_phases_ms": {k: round(v, 3) for k, v in (r.get("phases_cold") or {}).items()},
+            "b1_process_phases_ms": ph,
             "b1_process_warm_ms": round(float(r["warm_ms"]), 4),
             "b1_process_cold_vs_reference": round(BASELINE_V3_MS / r["cold_ms"], 2),
             "b1_process_note": "anx --version v3 --batch 1 child: cold_ms from main() entry incl. HIP context "
@@ -320,11 +355,111 @@ def v5_halo_subrecords(a, world: int, rank: int, GB: int, dev, g) -> dict:
     return out
 
 
-def _match_arms(out: dict, a: str, b: str, key: str) -> None:
+def _native_arm(wl, GB: int, world: int, rank: int, steps: int, warmup: int, dev) -> dict:
+    """Time one native V4 / V5 runtime (warmup, then ``steps`` timed steps bracketed by a barrier and a
+    sync, max over ranks) and describe it: rate, halo exchange and bytes, phases, exact output checksum."""
+    from anx.parallel import selfcheck
+    wl.step(steps=warmup)
+    wl.sync()
+    wl.reset_phases()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    wl.step(steps=steps)
+    wl.sync()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    d, ph = wl.describe(), wl.phase_ms()
+    y = wl.output()
+    rec = {"global_batch": GB, "n_gpus": world, "steps": steps, "images_per_s": round(GB * steps / el, 1),
+           "ms_per_step": round(el * 1e3 / steps, 4), "row_ways": d.get("row_ways"),
+           "halo_exchange": d.get("halo_exchange"), "phases_ms": ph, "halo_p1_ms": ph.get("halo_p1")}
+    for k in ("transport", "decomp", "halo_bytes_per_step", "halo_transfers_per_step", "input_source", "lanes",
+              "h2d_bytes_per_step_rank", "staging"):
+        if k in d:
+            rec[k] = d[k]
+    if y is not None:
+        rec["output_crc"] = selfcheck.tensor_crc(y)
+    return rec
+
+
+def reference_programs(a, world: int, rank: int, dev, cuda: bool, g) -> dict:
+    """BASELINE configs 3 and 4 beside the dp headline, on the same ranks: the reference's
+    multi-GPU programs, V4 (256 images, host-staged scatter + per-rank rows) and V5 (1024 images,
+    device-resident, per-layer pool1 halo + gather), run by the native runtimes (anx/v4.hpp, anx/v5.hpp),
+    strong scaling. V5 runs twice: the cost model's pick (``auto``: usually a batch split, no halo) and a
+    forced row split with the halo exchange ON (``rows2``: 2-way row groups; ``rows`` at an odd rank count),
+    the latter once per device transport (RCCL, and the peer IPC transport at N > 1) with matching exact
+    checksums. At N = 1 the forced-halo arms are two ranks sharing the GPU (v5_halo_subrecords). CPU ranks
+    (tests) run the V5 runtime in host mode on a few images. Every arm sits in its own try/except: the
+    headline never depends on them."""
+    from anx.parallel.workloads import NativeV4, NativeV5
+    from anx.utils.init import init_weights
+    b1s, b2s = anx.config.blocks()
+    d = anx.blocks_dims()
+    w = init_weights("rand", 1234, b1s, b2s) if rank == 0 else None
+    gb4, gb5 = (a.ref_batch_v4, a.ref_batch_v5) if not cuda else (256, 1024)
+    steps, warm = (a.ref_steps, 1) if not cuda else (a.ref_steps, 2)
+    out = {"v4": {}, "v5": {}}
+
+    def batch_x(GB):
+        if rank != 0:
+            return None
+        gen = torch.Generator().manual_seed(4321)
+        return torch.rand((GB, d.H, d.W, d.C0), generator=gen) * 0.1
+
+    def arm(dst, name, make, GB):
+        wl = None
+        try:
+            wl = make()
+            wl.fill(batch_x(GB))
+            dst[name] = _native_arm(wl, GB, world, rank, steps, warm, dev)
+        except Exception as e:  # a secondary record never takes the headline down
+            dst[name] = {"error": repr(e)[:300]}
+        finally:
+            if wl is not None:
+                wl.close()
+
+    # V4 (BASELINE config 3): the runtime's default split
+    if cuda:
+        arm(out["v4"], "auto", lambda: NativeV4(gb4, w, specs=(b1s, b2s), decomp="auto", impl=a.impl), gb4)
+    else:
+        arm(out["v4"], "auto", lambda: NativeV5(gb4, w, specs=(b1s, b2s), decomp="auto", impl="host",
+                                                input_source="root", layer="overlap"), gb4)
+    # V5 (BASELINE config 4): auto, then the halo forced on
+    halo = "rows2" if world % 2 == 0 else "rows"
+    if cuda:
+        arm(out["v5"], "auto", lambda: NativeV5(gb5, w, specs=(b1s, b2s), decomp="auto", impl=a.impl,
+                                                input_source="local", lanes=a.lanes), gb5)
+        if world > 1:
+            for tr in ("rccl", "peer"):
+                arm(out["v5"], f"{halo}_{tr}", lambda: NativeV5(gb5, w, specs=(b1s, b2s), decomp=halo, transport=tr,
+                                                               impl=a.impl, input_source="local", lanes=a.lanes), gb5)
+            _match_arms(out["v5"], f"{halo}_rccl", f"{halo}_peer", "output_crc", prefix="")
+        else:
+            out["v5"].update({k.replace("v5_", ""): v for k, v in v5_halo_subrecords(a, world, rank, gb5, dev, g).items()})
+    else:
+        arm(out["v5"], "auto", lambda: NativeV5(gb5, w, specs=(b1s, b2s), decomp="auto", impl="host"), gb5)
+        if world > 1:
+            arm(out["v5"], f"{halo}_host", lambda: NativeV5(gb5, w, specs=(b1s, b2s), decomp=halo, impl="host"), gb5)
+    for k, v in (("v4", "BASELINE config 3: V4 scatter+halo, batch 256 (host-staged; native V4 runtime)"),
+                 ("v5", "BASELINE config 4: V5 GPU-aware, batch 1024 (device-resident halo + gather; native V5 "
+                        "runtime)")):
+        out[k]["config"] = v
+        out[k]["scaling"] = "strong"
+    return out
+
+
+def _match_arms(out: dict, a: str, b: str, key: str, prefix: str = "v5_rows2_") -> None:
     """The peer transport's cross-device ordering (flag write after the copy into the receiver's memory)
     checked on the node that runs it: both arms compute the same tiles with the same kernels, so their
     outputs must agree bit for bit; ``outputs_match`` goes into the second arm's record."""
-    ra, rb = out.get(f"v5_rows2_{a}") or {}, out.get(f"v5_rows2_{b}") or {}
+    ra, rb = out.get(f"{prefix}{a}") or {}, out.get(f"{prefix}{b}") or {}
     if ra.get(key) is not None and rb.get(key) is not None:
         rb["outputs_match_" + a] = ra[key] == rb[key]
 
@@ -413,13 +548,16 @@ def main():
         out_shape, flops = (d.Hp2, d.Wp2, d.C2), anx.flops_per_image()
 
     use_graph = False
-    root_b = B
+    root_b, root_note = B, None
     if wl is None and a.model == "blocks" and world > 1 and a.input_source == "local" and not a.no_gather:
+        from anx.parallel.pipeline import root_batch_for
         if a.root_batch > 0:
             root_b = min(B, a.root_batch)
         elif a.root_batch < 0 and cuda:
             from anx.parallel import cost
             root_b = cost.dp_root_batch(world, B)
+        # never a share that changes the root's lane or micro-batch count (8 x 32 images: 30 -> 32)
+        root_b, root_note = root_batch_for(root_b, B, a.micro, getattr(model, "lane_bounds", None))
     if wl is None:
         cfg = PipelineConfig(B, micro=a.micro, scatter=(a.input_source == "root"), gather=not a.no_gather,
                              root_batch=root_b,
@@ -554,6 +692,12 @@ def main():
     if cuda and wl is not None and a.workload == "v5" and not a.no_subrecords:
         subs = v5_halo_subrecords(a, world, rank, GB, dev, g)
     b1 = batch1_latency(dev) if (rank == 0 and cuda and not a.no_b1) else {}
+    refs = None
+    if wl is None and a.model == "blocks" and not a.no_ref_programs:
+        try:
+            refs = reference_programs(a, world, rank, dev, cuda, g)
+        except Exception as e:
+            refs = {"error": repr(e)[:300]}
     full = None
     if cuda and wl is None and not a.no_full:
         try:
@@ -574,8 +718,9 @@ def main():
             extra = {"input_source": a.input_source, "lanes": a.lanes, "hip_graph": use_graph, "knobs": a.knob,
                      "batch_per_gpu": B, "root_batch": root_b,
                      **({"root_batch_modelled": cfg.root_batch, **calib} if calib else {}),
-                     "root_batch_note": ("rank 0 sheds the share its gather ingest costs it (cost model "
-                                         "dp_root_batch; tools/probe_ingest.py)") if root_b != B else None,
+                     "root_batch_note": root_note or (("rank 0 sheds the share its gather ingest costs it (cost "
+                                                      "model dp_root_batch; tools/probe_ingest.py)")
+                                                     if root_b != B else None),
                      "input_batches_rotated": len(rot) or 1,
                      "input_bytes_rotated": sum(t.numel() * 4 for t in rot) or pipe._xb[0].numel() * 4,
                      "lane_sync": ("free-running lanes (%s start), per-lane gathers (forward_async)"
@@ -658,7 +803,6 @@ def main():
                 "mfma_tflops": round(imgs * mf / 1e12 / world, 2),
                 "mfma_tflops_note": "per GPU; fp32 matrix peak 157 TF/s (155 sustained)",
                 "vs_baseline_throughput": round(imgs / (1000.0 / BASELINE_V3_MS), 1),
-                "model": model,
                 **b1,
                 **b1p,
             },
@@ -671,6 +815,10 @@ def main():
                 rec["verify"] = verify
         if full is not None:
             rec["full_bf16"] = full
+        if refs is not None:
+            rec.update(refs) if "error" not in refs else rec.update({"reference_programs_error": refs["error"]})
+        if model is not None:  # modelled, not measured: outside the measured config
+            rec["model_curve"] = {"measured": False, **model}
         rec.update(subs)
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -2,6 +2,8 @@
 #include "anx/engine.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -9,6 +11,7 @@
 
 #include "anx/rng.hpp"
 #include "anx/trace.hpp"
+#include "anx/upload.hpp"
 
 #define ANX_TRY(expr)                          \
   do {                                         \
@@ -32,7 +35,7 @@ T* dev_alloc(size_t n) {
 template <class T>
 T* dev_upload(const std::vector<T>& h) {
   T* d = dev_alloc<T>(h.size());
-  check(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy H2D");
+  check(upload_h2d(d, h.data(), h.size() * sizeof(T)), "upload H2D");  // pinned staging (anx/upload.hpp)
   return d;
 }
 }  // namespace
@@ -76,17 +79,29 @@ BlocksEngine::BlocksEngine(const BlockSpec& b1, const BlockSpec& b2, int H, int 
   // reach their operands through 32-bit buffer offsets)
   chunk_ = static_cast<int>(std::min<size_t>(max_batch, ((1UL << 31) - 1) / (per_img * sizeof(float))));
   if (chunk_ < 1) throw std::invalid_argument("image too large for 32-bit kernel indexing");
+  // ANX_ENGINE_PHASES=1: where a cold engine's construction goes (stderr; diagnostics only)
+  static const bool phases = [] {
+    const char* e = std::getenv("ANX_ENGINE_PHASES");
+    return e && *e == '1';
+  }();
+  auto ms = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = phases ? ms() : 0;
   w1h_ = w.w1;
   w2h_ = w.w2;
   w1_ = dev_upload(w.w1);
   b1d_ = dev_upload(w.b1);
   w2_ = dev_upload(w.w2);
   b2d_ = dev_upload(w.b2);
+  const double t1 = phases ? ms() : 0;
   c1_ = dev_alloc<float>(static_cast<size_t>(chunk_) * d_.H1 * d_.W1 * d_.C1);
   q2_cap_ = static_cast<size_t>(max_batch) * (d_.Hp1 + 2 * b2.conv.P) * wq_ * d_.C1;
   q2_ = dev_alloc<float>(q2_cap_);
   c2_ = dev_alloc<float>(static_cast<size_t>(chunk_) * d_.H2 * d_.W2 * d_.C2);
+  const double t2 = phases ? ms() : 0;
   prepare();
+  if (phases)
+    std::fprintf(stderr, "ANX_ENGINE_PHASES uploads %.3f allocs %.3f prepare %.3f ms (max_batch %d)\n", t1 - t0, t2 - t1,
+                 ms() - t2, max_batch);
 }
 
 // What the current knobs can launch, prepared outside any forward (no allocation, upload or host
@@ -138,6 +153,12 @@ void BlocksEngine::prepare() {
     }
   }
   // direct path: the full-image launch of min(max_batch, the Auto crossover) images
+  static const bool phases = [] {
+    const char* e = std::getenv("ANX_ENGINE_PHASES");
+    return e && *e == '1';
+  }();
+  auto ms = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double tp = phases ? ms() : 0;
   const int n = std::max(1, std::min(max_batch_, chunk_));
   const int nd = k_.conv1_algo == ConvAlgo::Direct ? n : std::min(n, 8);
   if (!use_winograd(k_.conv1_algo, nd, d_.H1, d_.H1) || wv1_ == nullptr)
@@ -146,6 +167,7 @@ void BlocksEngine::prepare() {
   if (!use_winograd(k_.conv2_algo, nd2, d_.H2, d_.H2) || wv_ == nullptr)
     (void)pack2(hip::make_conv_plan(nd2, d_.Hp1 + 2 * k2.P, wq_, d_.C1, k2.K, k2.F, k2.S, k2.groups, k_.force_vec4,
                                     k_.force_scalar));
+  if (phases) std::fprintf(stderr, "ANX_ENGINE_PHASES direct-path packing %.3f ms\n", ms() - tp);
 }
 
 int BlocksEngine::tile2() const {

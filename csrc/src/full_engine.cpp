@@ -7,6 +7,7 @@
 #include <string>
 
 #include "anx/bf16_ops.hpp"
+#include "anx/upload.hpp"
 
 #define ANX_TRY(expr)                \
   do {                               \
@@ -54,7 +55,7 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
     L.groups = i == 1 ? groups2 : 1;
     L.host = w.w[i];
     L.bias = static_cast<float*>(dalloc(bn[i] * 4));
-    check(hipMemcpy(L.bias, w.b[i].data(), bn[i] * 4, hipMemcpyHostToDevice), "H2D bias");
+    check(upload_h2d(L.bias, w.b[i].data(), bn[i] * 4), "H2D bias");
   }
   // Conv1 polyphase (the fp32 Winograd Conv1's rewrite, conv1_wino.hip): space-to-depth by the stride
   // turns 11x11/4 over 3 channels into 3x3/1 over 48, so the implicit GEMM's A gathers are aligned
@@ -85,7 +86,7 @@ FullEngine::FullEngine(const FullWeights& w, int classes, int max_batch, int gro
     std::vector<uint16_t> rp;
     hip::pack_conv1_ring_weights(L.host.data(), rp);
     w1ring_ = dalloc(rp.size() * 2);
-    check(hipMemcpy(w1ring_, rp.data(), rp.size() * 2, hipMemcpyHostToDevice), "H2D conv1 ring weights");
+    check(upload_h2d(w1ring_, rp.data(), rp.size() * 2), "H2D conv1 ring weights");
   }
   {
     int dev = 0;
@@ -145,8 +146,8 @@ hipError_t FullEngine::conv(Layer& L, int N, int Hp, int Wp, const void* x, hip:
     if (L.koff) ANX_TRY(hipFree(L.koff));
     ANX_TRY(hipMalloc(&L.wp, pk.size() * 2));
     ANX_TRY(hipMalloc(&L.koff, ko.size() * 4));
-    ANX_TRY(hipMemcpy(L.wp, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
-    ANX_TRY(hipMemcpy(L.koff, ko.data(), ko.size() * 4, hipMemcpyHostToDevice));
+    ANX_TRY(upload_h2d(L.wp, pk.data(), pk.size() * 2));
+    ANX_TRY(upload_h2d(L.koff, ko.data(), ko.size() * 4));
     L.key = p.variant;
   }
   const bool fc = p.Hp == 1 && p.Wp == 1 && p.F == 1;

@@ -326,13 +326,19 @@ void V4Runtime::reset_phases() {
 std::string V4Runtime::describe_json() const {
   const Impl_& I = *p_;
   const PlanStats s = plan_stats(I.plan);
-  char b[640];
+  char b[900];
+  // V4's halo is in its input: a row group's ranks each DMA their output rows' receptive field (overlap
+  // tiles), so no exchange runs mid-network; with one row way (the cost model's usual pick) there is no
+  // halo at all. Said explicitly, as V5's describe does.
   std::snprintf(b, sizeof b,
                 "{\"staging\": \"shared pinned host segment, per-rank DMA\", \"chunks\": %d, \"groups\": %d, "
                 "\"row_ways\": %d, \"imbalance\": %.4f, \"conv1_redundancy\": %.4f, \"images_per_rank_max\": %g, "
-                "\"h2d_bytes_per_step_rank\": %zu, \"d2h_bytes_per_step_rank\": %zu, \"device\": %d}",
+                "\"h2d_bytes_per_step_rank\": %zu, \"d2h_bytes_per_step_rank\": %zu, \"device\": %d, "
+                "\"halo_exchange\": \"%s\"}",
                 I.C, s.groups, s.row_ways, s.imbalance, s.conv1_redundancy, s.images_max, h2d_bytes_per_step(),
-                d2h_bytes_per_step(), I.dev);
+                d2h_bytes_per_step(), I.dev,
+                s.row_ways > 1 ? "input halo rows in each rank's H2D (overlap tiles: no mid-network exchange)"
+                               : "none (batch split: every rank whole images)");
   return b;
 }
 

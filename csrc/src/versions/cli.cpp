@@ -31,6 +31,7 @@
 #include "anx/comm.hpp"
 #include "anx/cpu_engine.hpp"
 #include "anx/engine.hpp"
+#include "anx/upload.hpp"
 #include "anx/plan.hpp"
 #include "anx/rng.hpp"
 #include "anx/schedule.hpp"
@@ -370,16 +371,23 @@ int run_single(Setup& s) {
     hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
     cold.add("init", now_ms() - a0);
     a0 = now_ms();
+    set_upload_stream(st);  // the engine's weight uploads on this stream (the null stream's first use costs a queue)
     BlocksEngine eng(s.b1, s.b2, s.d.H, s.d.W, s.w, N, s.o.impl == "direct" ? Impl::Direct : Impl::Mfma, s.k);
     cold.add("engine", now_ms() - a0);
     a0 = now_ms();
-    float *dx, *dy;
+    float *dx, *dy, *hx, *hy;
     hip_check(hipMalloc(&dx, s.x.size() * 4), "hipMalloc");
     hip_check(hipMalloc(&dy, y.size() * 4), "hipMalloc");
+    // pinned I/O buffers: a copy from pageable memory would initialise the runtime's staged-copy path
+    // inside the timed region (9-10 ms on its first use, anx/upload.hpp); the image is written into the
+    // pinned buffer on the host, as a serving process receives it
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&hx), s.x.size() * 4, hipHostMallocDefault), "hipHostMalloc");
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&hy), y.size() * 4, hipHostMallocDefault), "hipHostMalloc");
+    std::memcpy(hx, s.x.data(), s.x.size() * 4);
     cold.add("alloc", now_ms() - a0);
     auto step = [&](Phases& ph) {
       double a = now_ms();
-      hip_check(hipMemcpyAsync(dx, s.x.data(), s.x.size() * 4, hipMemcpyHostToDevice, st), "H2D");
+      hip_check(hipMemcpyAsync(dx, hx, s.x.size() * 4, hipMemcpyHostToDevice, st), "H2D");
       hip_check(hipStreamSynchronize(st), "sync");
       ph.add("h2d", now_ms() - a);
       a = now_ms();
@@ -387,15 +395,19 @@ int run_single(Setup& s) {
       hip_check(hipStreamSynchronize(st), "sync");
       ph.add("compute", now_ms() - a);
       a = now_ms();
-      hip_check(hipMemcpyAsync(y.data(), dy, y.size() * 4, hipMemcpyDeviceToHost, st), "D2H");
+      hip_check(hipMemcpyAsync(hy, dy, y.size() * 4, hipMemcpyDeviceToHost, st), "D2H");
       hip_check(hipStreamSynchronize(st), "sync");
       ph.add("d2h", now_ms() - a);
     };
     step(cold);
     cold_ms = now_ms() - t0;
     for (int i = 0; i < s.o.iters; ++i) step(warm);
+    std::memcpy(y.data(), hy, y.size() * 4);
     hip_check(hipFree(dx), "free");
     hip_check(hipFree(dy), "free");
+    hip_check(hipHostFree(hx), "free");
+    hip_check(hipHostFree(hy), "free");
+    set_upload_stream(nullptr);
     hip_check(hipStreamDestroy(st), "free");
   }
   warm_ms = s.o.iters ? warm.total() / s.o.iters : 0;
@@ -765,6 +777,13 @@ int run_v5_steps(Setup& s, HostComm& c, V5Runtime& rt, int N, double t0) {
 int main(int argc, char** argv) {
   const Options o = parse(argc, argv);
   const RankInfo ri = rank_info_from_env();
+  // V3 is a one-image latency program: its copies (2.6 MB of weights, the image, the output) are small,
+  // and the runtime's first SDMA copy of a process brings the engine queue up (~8 ms on an MI355X box for
+  // any copy >= 64 KiB; 0.35 ms for 2.5 MiB through the blit kernels instead, anx_hipinit,
+  // profiles/r06_cold/). Read by the runtime at its first call, so set before anything touches HIP; an
+  // explicit HSA_ENABLE_SDMA in the environment wins. The multi-rank versions keep SDMA for their
+  // large per-step transfers.
+  if (o.version == "v3") setenv("HSA_ENABLE_SDMA", "0", 0);
   try {
     Setup s = make_setup(o, ri);
     if (o.version == "v1" || o.version == "v3") {

@@ -38,6 +38,15 @@ IMPLS = {"mfma": 0, "direct": 1}
 LANE_MIN = 16  # images per lane below which a forward stays on one stream (Winograd needs > 8)
 
 
+def split_lanes(n: int, lanes: int) -> list[int]:
+    """Image boundaries [0, ..., n] of ``n`` images over ``lanes`` stream lanes: one lane below
+    ``lanes * LANE_MIN`` images, else contiguous near-equal slices (pure arithmetic: the CPU tests check
+    the multi-GPU root share against it without a GPU)."""
+    if lanes <= 1 or n < lanes * LANE_MIN:
+        return [0, n]
+    return [n * i // lanes for i in range(lanes + 1)]
+
+
 def _tile_c(t: TilePlan) -> nat.TileC:
     return nat.TileC(t.inp.lo, t.inp.hi, t.c1.lo, t.c1.hi, t.p1.lo, t.p1.hi, t.q.lo, t.q.hi, t.c2.lo, t.c2.hi,
                      t.out.lo, t.out.hi)
@@ -275,10 +284,7 @@ class AlexNetBlocks:
 
     def lane_bounds(self, n: int) -> list[int]:
         """Image boundaries [0, ..., n] of the lanes :meth:`forward_async` runs ``n`` images on."""
-        L = 1 + len(self._lanes)
-        if L == 1 or n < L * LANE_MIN or not self.is_cuda:
-            return [0, n]
-        return [n * i // L for i in range(L + 1)]
+        return split_lanes(n, 1 + len(self._lanes) if self.is_cuda else 1)
 
     def join(self) -> None:
         """Make the current stream wait for every lane of :meth:`forward_async`."""

@@ -6,7 +6,8 @@ compute, ``MPI_Gatherv`` back (final_project/v4_mpi_cuda/src/main_mpi_cuda.cpp:5
 batch scale and MI355X-first:
 
 * the decomposition axis is the batch (images are independent; no halo traffic at all), the
-  row/halo decomposition of single images lives in :mod:`anx.parallel.strategies`;
+  row/halo decomposition of single images lives in the native V4 / V5 runtimes
+  (:mod:`anx.parallel.workloads`);
 * collectives are RCCL scatter/gather (grouped point-to-point from/to the root, one direct xGMI
   link per peer) issued asynchronously on RCCL's stream, split into micro-batches so the scatter
   of micro-batch i+1 and the gather of i-1 overlap the compute of i on the compute stream;
@@ -63,6 +64,26 @@ def micro_splits(B: int, M: int) -> list[tuple[int, int]]:
         out.append((lo, lo + s))
         lo += s
     return out
+
+
+def root_batch_for(rb: int, batch: int, micro: int, lane_bounds=None) -> tuple[int, str | None]:
+    """The root's share ``rb`` (e.g. the cost model's :func:`anx.parallel.cost.dp_root_batch`) made valid
+    for :meth:`ScatterComputeGather.set_root_batch`: the root must split its share into as many
+    micro-batches and stream lanes as a peer's ``batch`` (per-lane gathers pair lane i of every rank).
+    ``lane_bounds(n)``: the model's lane split (``AlexNetBlocks.lane_bounds`` or :func:`split_lanes`).
+    Returns the share (raised to the smallest valid one, never above ``batch``) and a note when it moved.
+    round-4/5 ADVICE: 8 GPUs x 32 images shed the root to 30, one lane against its peers' two."""
+    rb = max(1, min(int(rb), batch))
+    need = min(max(1, micro), batch)  # micro_splits(rb, M) must have as many parts as micro_splits(B, M)
+    if lane_bounds is not None:
+        lanes_b = len(lane_bounds(batch)) - 1
+        lo, hi = max(rb, need), batch
+        while lo < hi and len(lane_bounds(lo)) - 1 != lanes_b:  # lane counts grow with n: smallest valid share
+            lo += 1
+        need = lo
+    out = max(rb, need)
+    note = None if out == rb else f"root share {rb} raised to {out}: the root runs as many lanes / micro-batches as a peer"
+    return out, note
 
 
 @dataclass

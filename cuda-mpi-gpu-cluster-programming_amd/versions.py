@@ -31,7 +31,6 @@ import torch.distributed as dist
 from .config import blocks_dims, flops_per_image
 from .parallel import comm
 from .parallel.plan import OVERLAP, PER_LAYER
-from .parallel.strategies import replicate_forward
 from .parallel.tensor import filter_parallel_forward
 from .utils.init import init_input, init_weights
 from .utils.timer import PhaseTimer
@@ -182,7 +181,10 @@ def run(cfg: RunConfig) -> RunResult | None:
             if cfg.version == "v3" and device.type == "cuda":
                 with tm.phase("h2d"):
                     xx = x.to(device)
-            y = replicate_forward(model, xx, tm)
+            # P1 "broadcast-all" (V2.1, v2_mpi_only/2.1_broadcast_all/src/main.cpp:49-85) and V1 / V3: every
+            # rank computes the whole batch, rank 0's result is the answer (no gather, as the reference)
+            with tm.phase("compute"):
+                y = model(xx)
             if cfg.version == "v3" and device.type == "cuda":
                 with tm.phase("d2h"):
                     y = y.cpu()

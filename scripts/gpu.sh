@@ -50,7 +50,7 @@ pmc() {  # pmc NAME COUNTERS...: one counter pass over a short bench run
 
 for s in "$@"; do
   case $s in
-    tests) run tests 900 python -u -m pytest tests -x -q -m gpu --timeout 240 --timeout-method thread ;;
+    tests) run tests 900 python -u -m pytest tests -x -v -m gpu --timeout 170 --timeout-method thread ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 $BARGS ;;
     sweep) run sweep 600 python tools/sweep_batch.py --batches ${SWEEP:-64,128,256,300,600} --rounds 3 --iters 10 \

@@ -44,6 +44,13 @@ def test_bench_blocks_contract():
     # equivalent may not (Winograd does 4x fewer multiplies)
     assert 0 < c["mfma_tflops"] < 160
     assert abs(c["direct_equiv_tflops"] / c["mfma_tflops"] - c["gflop_per_image_direct"] / c["gflop_per_image_mfma"]) < 0.05
+    # BASELINE configs 3 / 4 beside the headline (native runtimes), the halo-on V5 arms on the shared GPU,
+    # and the modelled curve outside config
+    assert c["model"].startswith("AlexNet Blocks1-2") and rec["model_curve"]["measured"] is False
+    v4, v5 = rec["v4"], rec["v5"]
+    assert v4["auto"]["global_batch"] == 256 and v4["auto"]["images_per_s"] > 0 and "halo_exchange" in v4["auto"]
+    assert v5["auto"]["global_batch"] == 1024 and v5["auto"]["images_per_s"] > 0 and v5["auto"]["output_crc"] != 0
+    assert v5["rows2_peer"]["halo_bytes_per_step"] > 0 and v5["rows2_peer"]["outputs_match_loopback"] is True
 
 
 @pytest.mark.gpu

@@ -329,7 +329,8 @@ def test_bench_contract_gloo():
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
-           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "2", "--micro", "2", "--device", "cpu"]
+           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "2", "--micro", "2", "--device", "cpu",
+           "--no-ref-programs"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -347,7 +348,8 @@ def test_bench_root_batch_gloo():
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
-           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "2", "--root-batch", "1", "--device", "cpu"]
+           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "2", "--root-batch", "1", "--device", "cpu",
+           "--no-ref-programs"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -361,7 +363,7 @@ def _bench3(extra_env=None, extra_args=()):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "3",
            "--steps", "1", "--warmup", "0", "--batch-per-gpu", "4", "--root-batch", "2", "--device", "cpu",
-           *extra_args]
+           "--no-ref-programs", *extra_args]
     env = dict(os.environ, OMP_NUM_THREADS="1", **(extra_env or {}))
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -393,3 +395,38 @@ def test_bench_selfcheck_detects_corrupt_rank_gloo():
     rec = _bench3({"ANX_BENCH_CORRUPT_RANK": "2"}, ("--calibrate-root", "off"))
     assert rec["gather_verified"] is False and rec["verify"]["mismatched_ranks"] == [2]
     assert "calibration" not in rec["config"] and rec["config"]["root_batch"] == 2
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_reference_programs_gloo(world):
+    """The default dp run also measures BASELINE configs 3 and 4 on the same ranks:
+    ``v4`` and ``v5`` secondary objects from the native runtimes (host mode on CPU ranks), V5 both at the
+    cost model's pick and with the pool1 halo exchange forced on (2-way row groups; all ranks' rows at an
+    odd count), each with its rate, halo bytes, halo phase and an exact output checksum; the headline
+    record is unchanged and the modelled curve sits outside ``config``."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", str(world),
+           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "2", "--device", "cpu", "--ref-steps", "1",
+           "--ref-batch-v4", "2", "--ref-batch-v5", str(world)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == world and rec["scaling"] == "weak" and rec["config"]["parallelism"] == f"dp{world}"
+    assert rec["config"]["model"].startswith("AlexNet Blocks1-2")  # the model's name, not the modelled curve
+    v4, v5 = rec["v4"], rec["v5"]
+    assert v4["scaling"] == v5["scaling"] == "strong"
+    a4 = v4["auto"]
+    assert "error" not in a4, a4
+    assert a4["global_batch"] == 2 and a4["images_per_s"] > 0 and "halo_exchange" in a4 and "output_crc" in a4
+    a5 = v5["auto"]
+    assert "error" not in a5, a5
+    assert a5["global_batch"] == world and a5["images_per_s"] > 0 and isinstance(a5["output_crc"], int)
+    halo = v5["rows2_host" if world % 2 == 0 else "rows_host"]
+    assert "error" not in halo, halo
+    assert halo["row_ways"] == (2 if world % 2 == 0 else world)
+    assert halo["halo_exchange"].startswith("pool1 rows") and halo["halo_bytes_per_step"] > 0
+    assert halo["halo_p1_ms"] is not None and isinstance(halo["output_crc"], int)
