@@ -56,12 +56,18 @@ static __constant__ Coef64 c_coef64 = make_coef64();
 // a group's (row, unit) pairs land on 16 distinct 16-B slots iff the XOR of rows 0-3 / 4-7 / 8-11 / 12-15
 // is 0 / 2 / 3 / 1 (the 3x3 kernel's (r >> 2) & 3 left every group 2-way conflicted here: 49 % of this
 // kernel's LDS cycles, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, profiles/r05_f45/pmc_summary_lane1.md).
+// tools/lds_swizzle_check.py checks both tables against that lane-group model.
 template <int U4>
 __device__ __forceinline__ int swz16(int row) {
   if constexpr (U4 == 12)
     return (0x78 >> (2 * ((row >> 2) & 3))) & 3;
-  else if constexpr (U4 == 24)  // 96-float rows: a 3-bit XOR by row & 15 (searched; one 2-way slot per group left)
-    return static_cast<int>((0x13dd90722a48ULL >> (3 * (row & 15))) & 7);
+  else if constexpr (U4 == 24)
+    // 96-float rows (24 units): a row starts at slot 8 * (row & 1) mod 16, and a lane group reads unit 4s + kg
+    // of rows r16 with kg in {0,1} (or {2,3}). Within each row parity the group's 8 lanes must cover the 8
+    // low-3-bit values: XOR {0,2,4,6} over rows {0,2,12,14} and again over {4,6,8,10} (their kg differs by one,
+    // flipping bit 0), the same for the odd rows. Round 5's table (0x13dd90722a48) left every group 2-way
+    // conflicted (SQ_LDS_BANK_CONFLICT 49 % of SQ_LDS_IDX_ACTIVE, profiles/r05_f45/wg45_pmc_waits.md).
+    return (row & 2) | ((row >> 1) & 4);
   else
     return wg::swz<U4>(row);
 }
