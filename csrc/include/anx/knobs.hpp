@@ -51,10 +51,15 @@ struct Knobs {
                            // 1 = 2 phase rows x all columns, 0 = per-tile gathers from global memory
   int fuse_pool1 = 1;      // tile_forward of a tile that computes every pool1 row its conv2 window needs: pool1
                            // fused into the Winograd input transform (no window round trip), 0 = pool1 kernel
-  int conv1_fused = 1;     // Conv1 as one kernel (conv1_fused.hip: V built in LDS inside the GEMM, 32 tiles x 96
+  int conv1_fused = 2;     // Conv1 as one kernel (conv1_fused.hip: V built in LDS inside the GEMM, 32 tiles x 96
                            // filters per workgroup; bench step 277-278 k vs 252-254 k images/s,
                            // profiles/r04_conv1_fused_v3_bench_ab.jsonl), 0 = the band transform kernel + GEMM (the
-                           // general path: also every conv1 with K != 96)
+                           // general path: also every conv1 with K != 96). 2 (default since round 6) = with pool1 in
+                           // the epilogue, a private U ring per wave (each wave DMAs its own filter rows and waits
+                           // with its own vmcnt: barriers only where V is published, 5 instead of 25; main loop
+                           // 48.1 k -> 44.2 k clk per workgroup, bench 335-339 k vs 325-330 k images/s,
+                           // profiles/r06_conv1_upw/); 1 = the shared 3-slot ring (every wave's DMA, one barrier
+                           // per point)
   int conv1_pool = 1;      // fused tile_forward of whole images: pool1 in the one-kernel Conv1's epilogue (conv1_fused 1;
                            // the 55x55 map stays in LDS, pooled pixels go to the conv2 window, straddling windows'
                            // partial maxima to a side buffer merged by the Conv2 input transform), 0 = Conv1 writes its

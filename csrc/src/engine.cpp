@@ -352,7 +352,7 @@ bool BlocksEngine::fused_pool1(int N, const TilePlan& t) const {
 }
 
 bool BlocksEngine::conv1_pools(int N, const TilePlan& t) const {
-  if (!k_.conv1_pool || k_.conv1_fused != 1 || k_.conv1_sub > 0 || wv1_ == nullptr || !fused_pool1(N, t)) return false;
+  if (!k_.conv1_pool || k_.conv1_fused == 0 || k_.conv1_sub > 0 || wv1_ == nullptr || !fused_pool1(N, t)) return false;
   // whole images: every conv1 row, every pool1 row
   if (t.c1.lo != 0 || t.c1.hi != d_.H1 || t.p1.lo != 0 || t.p1.hi != d_.Hp1) return false;
   const int chunk = std::min(chunk_, k_.chunk1 > 0 ? k_.chunk1 : chunk_);
@@ -430,7 +430,7 @@ hipError_t BlocksEngine::tile_forward_conv1_pool(const float* x, int N, const Ti
       RoctxRange rx("anx conv1+pool1");
       const hip::Conv1WinoPlan w1 = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
       const hip::OutView win{q2_ + n0 * q_img, t.q.size(), wq_, d_.C1, t.p1.lo - t.q.lo, k2.P, 0};
-      ANX_TRY(hip::conv1_fused_pool(w1, x + n0 * in_img, u1w_, b1d_, win, c1_, d_.Hp1, d_.Wp1, true, s));
+      ANX_TRY(hip::conv1_fused_pool(w1, x + n0 * in_img, u1w_, b1d_, win, c1_, d_.Hp1, d_.Wp1, true, s, k_.conv1_fused == 2));
     }
     RoctxRange rx("anx conv2+pool2+lrn");
     const hip::Conv1WinoPlan w1 = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);

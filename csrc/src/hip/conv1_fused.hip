@@ -27,8 +27,13 @@
 // Reference op: convKernel (v3_cuda_only/src/layers_cuda.cu:20-46), one thread per output.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "anx/ops.hpp"
 #include "anx/hip_sync.hpp"
@@ -59,6 +64,15 @@ constexpr int kDummy = 2 * kVBuf + kUSlots * kUSlot;  // 1-KiB scratch for the d
 constexpr int kLdsFloats = kDummy + 256;
 constexpr size_t kLds = kLdsFloats * sizeof(float);
 static_assert(kLds <= 160 * 1024, "LDS");
+// UPW (knob conv1_fused = 2): a private U ring per wave. Each wave DMAs the 16 filter rows its B fragments read
+// (3 KiB per point, 3 pieces) into its own 2-slot ring, one point ahead, and waits for them with its own vmcnt:
+// no other wave's DMA is read, so only the V publish at an a-step's first point needs a barrier (5 per
+// workgroup instead of 25) and the waves drift between them. The two waves of a filter block load the same
+// rows (2x the U traffic, L2 -> LDS).
+constexpr int kUW = 16 * kCh;                                    // floats per wave per slot
+constexpr int kLdsFloatsW = 2 * kVBuf + kWaves * 2 * kUW;       // 145,408 B
+constexpr size_t kLdsW = kLdsFloatsW * sizeof(float);
+static_assert(kLdsW <= 160 * 1024 && kUW == 3 * 256, "per-wave U ring: three 1-KiB pieces per point");
 static_assert(kUSlot % 256 == 0 && kUPieces <= 2 * kWaves && kUPieces >= kWaves, "U ring pieces: 1 or 2 per wave");
 
 // V_a takes X' row u iff B^T[a][u] != 0
@@ -92,7 +106,8 @@ constexpr int kPoolList = 9 * kTiles * kOS;  // the slot list after the nine pos
 // then per listed pixel 12 ints: its 9 window pixels' LDS float offsets (-1: another workgroup's),
 // the destination's element offset, whether it goes to p1, padding (16-B aligned entries)
 constexpr int kPoolEnt = 12, kPoolOffs = (kPoolList + 1 + kPoolSlots + 3) / 4 * 4;
-static_assert(kPoolOffs + kPoolSlots * kPoolEnt <= kLdsFloats && kPoolSlots <= kNT, "pool1 slot list");
+static_assert(kPoolOffs + kPoolSlots * kPoolEnt <= kLdsFloats && kPoolOffs + kPoolSlots * kPoolEnt <= kLdsFloatsW &&
+                  kPoolSlots <= kNT, "pool1 slot list");
 static_assert(kTiles * 24 == kNT, "V build: one (tile, channel pair) per thread");
 
 template <int B, int E, class F>
@@ -123,9 +138,10 @@ struct Conv1FusedArgs {
   // ([N][Hp][Wp][96]), merged by the consumer (pool1_straddles()).
   float* p1;
   int Hp, Wp;
+  unsigned long long* dbg;  // ABL bit 64 (ANX_CONV1_PHASES diagnostics): per-workgroup stamps, else null
 };
 
-template <bool POOL, int ABL = 0>
+template <bool POOL, int ABL = 0, bool UPW = false>
 __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -135,6 +151,13 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   const int pt = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
   if (pt >= a.n_ptiles) return;  // whole workgroup, before any barrier
   const int p0 = pt * kTiles;
+  // ABL bit 64: wave 0's s_memtime at the phase boundaries (diagnostic build only; stamps go to a.dbg)
+  constexpr bool kStamp = (ABL & 64) != 0;
+  unsigned long long stamp[7] = {}, rt0 = 0;
+  if constexpr (kStamp) {
+    stamp[0] = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
 #if __HIP_DEVICE_COMPILE__
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), 0, a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
@@ -155,10 +178,27 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // second 1-KiB piece DMA zeros (out-of-range source) into a 1-KiB scratch row instead, so the compiler's (and the schedule's)
   // vmcnt values count the same ops on every wave (with a conditional second piece the compiler
   // assumed none and its waits for the X' rows also waited for the U DMA just issued).
+  // UPW: this wave's pieces: units i * 64 + lane of its 16 rows (filters 16 wn ..), swizzled as the shared ring
+  [[maybe_unused]] int uoffw[3];
+  [[maybe_unused]] lds_f32* const uringw = uring + wave * 2 * kUW;
+  if constexpr (UPW) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int U = i * 64 + lane, row = U / 12, u = (U - row * 12) ^ swz(row);
+      uoffw[i] = ((wn * 16 + row) * kCh + 4 * u) * 4;
+    }
+  }
   auto issue_u = [&](auto AB) {
     [[maybe_unused]] constexpr int ab = decltype(AB)::value;
     if constexpr ((ABL & 2) != 0) return;
 #if __HIP_DEVICE_COMPILE__
+    if constexpr (UPW) {
+      lds_f32* st = uringw + (ab % 2) * kUW;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + i * 256), 16, uoffw[i], ab * kUSlot * 4, 0, 0);
+      return;
+    }
     lds_f32* st = uring + (ab % kUSlots) * kUSlot;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (lds_void*)(st + wave * 256), 16, uoff[0], ab * kUSlot * 4, 0, 0);
     lds_f32* st2 = wave + kWaves < kUPieces ? st + (wave + kWaves) * 256 : lds3 + kDummy;  // scalar select
@@ -245,9 +285,9 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   const int r16 = lane & 15, h4 = lane >> 4;
   const int a_off = (wm * 16 + r16) * kVS + 4 * h4;
   const int brow = wn * 16 + r16;
-  int b_off[3];
+  int b_off[3];  // UPW: row r16 of this wave's ring slot (swz(brow) == swz(r16): 16 wn leaves bits 1-2)
 #pragma unroll
-  for (int g = 0; g < 3; ++g) b_off[g] = brow * kCh + 4 * ((4 * g + h4) ^ swz(brow));
+  for (int g = 0; g < 3; ++g) b_off[g] = (UPW ? r16 : brow) * kCh + 4 * ((4 * g + h4) ^ swz(brow));
   f32x4 Y[9];  // Y[q]: output q of the block's 4 accumulator rows
 #pragma unroll
   for (int q = 0; q < 9; ++q) Y[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -263,7 +303,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   f32x2 xrow[kN5][kN5];  // X' rows of this thread's (tile, channel pair), each loaded once (see late_load_pt)
   // prologue: U_0, U_1 in flight; the rows V_0 takes loaded (kept), V_0 built and stored
   issue_u(std::integral_constant<int, 0>{});
-  issue_u(std::integral_constant<int, 1>{});
+  if constexpr (!UPW) issue_u(std::integral_constant<int, 1>{});  // UPW: one point ahead (2 slots)
   t_zero();
   sfor<0, kN5>([&](auto Uc) {
     constexpr int u = decltype(Uc)::value;
@@ -277,6 +317,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   });
   v_store(0);
   t_zero();
+  if constexpr (kStamp) stamp[1] = __builtin_amdgcn_s_memtime();
 
   sfor<0, kN5>([&](auto Ac) {
     constexpr int av = decltype(Ac)::value;
@@ -288,14 +329,26 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
       // in flight past this barrier: the ops issued after U_p (at point p - 2: its X' row, if any; at
       // point p - 1: U_{p+1} and its X' row): this wave's U_p has landed, X' rows finish on their own
       constexpr int inflight = (p + 1 < kPts ? 2 : 0) + x_ops(p - 1) + x_ops(p - 2);
+      // UPW: U_p was issued at point p - 1 (the prologue for p = 0); after it only point p - 1's X' row loads
+      constexpr int inflight_w = x_ops(p - 1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((ABL & 4) != 0)
+      if constexpr (UPW) {
+        if constexpr (b == 0)
+          lds_barrier<inflight_w>();  // V_a published (and every wave past a-step a - 1's reads of its buffer)
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(inflight_w) : "memory");  // this wave's own U_p pieces
+      } else if constexpr ((ABL & 4) != 0)
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(inflight) : "memory");
       else
         lds_barrier<inflight>();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("" ::: "memory");
-      if constexpr (p + 2 < kPts) issue_u(std::integral_constant<int, p + 2>{});  // slot of point p - 1: free
+      if constexpr (UPW) {
+        // slot (p + 1) % 2 held U_{p-1}, read by this wave only, at point p - 1 (its MFMAs consumed the reads)
+        if constexpr (p + 1 < kPts) issue_u(std::integral_constant<int, p + 1>{});
+      } else if constexpr (p + 2 < kPts) {
+        issue_u(std::integral_constant<int, p + 2>{});  // slot of point p - 1: free
+      }
       if constexpr (loads_at(p) >= 0) {
         constexpr int r = loads_at(p);
 #pragma unroll
@@ -303,7 +356,8 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
       }
       __builtin_amdgcn_sched_barrier(0);  // loads issued before the MFMAs
       const float* vp = vb + b * kTiles * kVS + a_off;
-      const float* up = reinterpret_cast<const float*>(lds + 2 * kVBuf + (p % kUSlots) * kUSlot);
+      const float* up = UPW ? reinterpret_cast<const float*>(lds + 2 * kVBuf + wave * 2 * kUW + (p % 2) * kUW)
+                            : reinterpret_cast<const float*>(lds + 2 * kVBuf + (p % kUSlots) * kUSlot);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
@@ -353,6 +407,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
     });
   });
 
+  if constexpr (kStamp) stamp[2] = __builtin_amdgcn_s_memtime();
   // ---- epilogue: per output position q, bias + ReLU into an LDS image [32 tiles][96 filters], then
   // 16-B row-contiguous stores. D layout: lane holds col = lane & 15 (filter), rows 4 (lane >> 4) + i.
   const int f = wn * 16 + r16;
@@ -406,6 +461,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
       }
     }
     __syncthreads();  // position images and the zeroed count visible
+    if constexpr (kStamp) stamp[3] = __builtin_amdgcn_s_memtime();
     if (desc >= 0) plist[1 + atomicAdd(&plist[0], 1)] = desc;
     __syncthreads();
     const int nlist = plist[0];
@@ -434,6 +490,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         *reinterpret_cast<i32x4*>(ent + k * kPoolEnt + 4 * q) = i32x4{e[4 * q], e[4 * q + 1], e[4 * q + 2], e[4 * q + 3]};
     }
     __syncthreads();
+    if constexpr (kStamp) stamp[4] = __builtin_amdgcn_s_memtime();
     for (int it = tid; it < ((ABL & 32) != 0 ? 0 : nlist) * (kK / 4); it += kNT) {
       const int k = it / (kK / 4), fq = it - k * (kK / 4);
       const i32x4 e0 = *reinterpret_cast<const i32x4*>(ent + k * kPoolEnt);
@@ -449,6 +506,21 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         }
       float* dst = (e2.z ? a.p1 : o.base) + static_cast<size_t>(static_cast<unsigned>(e2.y)) + 4 * fq;
       *reinterpret_cast<f32x4*>(dst) = m;
+    }
+    if constexpr (kStamp) {
+      stamp[5] = __builtin_amdgcn_s_memtime();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pooled stores acknowledged
+      stamp[6] = __builtin_amdgcn_s_memtime();
+      if (tid == 0) {
+        unsigned long long* d = a.dbg + static_cast<size_t>(pt) * 10;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) d[i] = stamp[i];
+        d[7] = rt0;
+        d[8] = __builtin_amdgcn_s_memrealtime();
+        // HW_ID (CU / SE of this wave) and XCC_ID: which CU ran this workgroup (the gap to the next one)
+        d[9] = (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((31 << 11) | 20)) << 32) |
+               static_cast<unsigned>(__builtin_amdgcn_s_getreg((31 << 11) | 4));
+      }
     }
   } else {
     // all nine output positions' images at once (9 x 32 x 100 floats = 115 KB of the 128 KB): one
@@ -483,11 +555,46 @@ bool conv1_fused_eligible(const Conv1WinoPlan& w, const OutView& out) {
 }
 
 namespace {
+// ANX_CONV1_PHASES: medians of wave 0's phase clocks per workgroup, and per CU the gap between one
+// workgroup's end and the next one's start (s_memrealtime, 100 MHz)
+void conv1_phase_report(const std::vector<unsigned long long>& h, int n) {
+  auto median = [](std::vector<double> v) {
+    if (v.empty()) return 0.0;
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  const char* names[6] = {"prologue", "main loop", "epilogue: Y to LDS + barrier", "pool list + table",
+                          "pooled max + store issue", "store drain"};
+  std::vector<double> ph[6], life;
+  std::map<unsigned long long, std::vector<std::pair<unsigned long long, unsigned long long>>> per_cu;
+  for (int b = 0; b < n; ++b) {
+    const unsigned long long* d = &h[static_cast<size_t>(b) * 10];
+    if (d[0] == 0) continue;
+    for (int i = 0; i < 6; ++i) ph[i].push_back(static_cast<double>(d[i + 1] - d[i]));
+    life.push_back(static_cast<double>(d[8] - d[7]) * 10.0);  // ns
+    const unsigned long long hw = d[9] & 0xffffffffull, cu = ((d[9] >> 32) << 16) | ((hw >> 8) & 0xf) | ((hw >> 13) & 0x7) << 4 |
+                                                              ((hw >> 12) & 1) << 7;
+    per_cu[cu].push_back({d[7], d[8]});
+  }
+  std::vector<double> gaps;
+  for (auto& [cu, v] : per_cu) {
+    std::sort(v.begin(), v.end());
+    for (size_t i = 1; i < v.size(); ++i)
+      if (v[i].first >= v[i - 1].second) gaps.push_back(static_cast<double>(v[i].first - v[i - 1].second) * 10.0);
+  }
+  std::fprintf(stderr, "conv1 phases (median clk per workgroup, wave 0, %zu workgroups on %zu CUs):", ph[0].size(),
+               per_cu.size());
+  for (int i = 0; i < 6; ++i) std::fprintf(stderr, " %s %.0f;", names[i], median(ph[i]));
+  std::fprintf(stderr, " lifetime %.0f ns; gap to the next workgroup on the CU %.0f ns (median of %zu)\n",
+               median(life), median(gaps), gaps.size());
+}
+
 hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out,
-                              bool relu, hipStream_t s, float* p1, int Hp, int Wp) {
+                              bool relu, hipStream_t s, float* p1, int Hp, int Wp, bool upw = false) {
   static const hipError_t attr = [] {
     for (const void* k : {reinterpret_cast<const void*>(conv1_fused_kernel<false>),
-                          reinterpret_cast<const void*>(conv1_fused_kernel<true>)}) {
+                          reinterpret_cast<const void*>(conv1_fused_kernel<true>),
+                          reinterpret_cast<const void*>(conv1_fused_kernel<true, 0, true>)}) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -541,7 +648,35 @@ hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const floa
     return hipGetLastError();
   }
 #endif
-  if (p1 != nullptr)
+  static const bool phases = std::getenv("ANX_CONV1_PHASES") != nullptr;
+  if (phases && p1 != nullptr) {  // diagnostics: the stamped kernel, then a per-phase summary on stderr
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_fused_kernel<true, 64>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_fused_kernel<true, 64, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_set = true;
+    }
+    const size_t nb = static_cast<size_t>(a.n_ptiles) * 10;
+    unsigned long long* dbg = nullptr;
+    if (hipMalloc(&dbg, nb * 8) != hipSuccess) return hipErrorOutOfMemory;
+    a.dbg = dbg;
+    if (upw)
+      conv1_fused_kernel<true, 64, true><<<grid, kNT, kLdsW, s>>>(a);
+    else
+      conv1_fused_kernel<true, 64><<<grid, kNT, kLds, s>>>(a);
+    std::vector<unsigned long long> h(nb);
+    hipError_t e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), dbg, nb * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(dbg);
+    if (e != hipSuccess) return e;
+    conv1_phase_report(h, a.n_ptiles);
+    return hipGetLastError();
+  }
+  if (p1 != nullptr && upw)
+    conv1_fused_kernel<true, 0, true><<<grid, kNT, kLdsW, s>>>(a);
+  else if (p1 != nullptr)
     conv1_fused_kernel<true><<<grid, kNT, kLds, s>>>(a);
   else
     conv1_fused_kernel<false><<<grid, kNT, kLds, s>>>(a);
@@ -566,10 +701,10 @@ bool conv1_fused_pool_eligible(const Conv1WinoPlan& w, const OutView& window, in
 }
 
 hipError_t conv1_fused_pool(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView window,
-                            float* p1, int Hp, int Wp, bool relu, hipStream_t s) {
+                            float* p1, int Hp, int Wp, bool relu, hipStream_t s, bool upw) {
   if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
   if (p1 == nullptr || !conv1_fused_pool_eligible(w, window, Hp, Wp)) return hipErrorInvalidValue;
-  return conv1_fused_launch(w, x, U, bias, window, relu, s, p1, Hp, Wp);
+  return conv1_fused_launch(w, x, U, bias, window, relu, s, p1, Hp, Wp, upw);
 }
 
 }  // namespace anx::hip
