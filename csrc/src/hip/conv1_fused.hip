@@ -106,6 +106,10 @@ constexpr int kPoolList = 9 * kTiles * kOS;  // the slot list after the nine pos
 // then per listed pixel 12 ints: its 9 window pixels' LDS float offsets (-1: another workgroup's),
 // the destination's element offset, whether it goes to p1, padding (16-B aligned entries)
 constexpr int kPoolEnt = 12, kPoolOffs = (kPoolList + 1 + kPoolSlots + 3) / 4 * 4;
+// a row of 96 -inf after the table: a window pixel another workgroup owns reads it (no branch per read, so the
+// nine reads of a pooled pixel issue back to back behind one wait)
+constexpr int kPoolSent = kPoolOffs + kPoolSlots * kPoolEnt;
+static_assert(kPoolSent % 4 == 0 && kPoolSent + kK <= kLdsFloats && kPoolSent + kK <= kLdsFloatsW, "pool sentinel row");
 static_assert(kPoolOffs + kPoolSlots * kPoolEnt <= kLdsFloats && kPoolOffs + kPoolSlots * kPoolEnt <= kLdsFloatsW &&
                   kPoolSlots <= kNT, "pool1 slot list");
 static_assert(kTiles * 24 == kNT, "V build: one (tile, channel pair) per thread");
@@ -442,6 +446,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         tr[(q * kTiles + wm * 16 + 4 * h4 + i) * kOS + f] = v;
       }
     if (tid == 0) plist[0] = 0;
+    if (tid < kK) lds[kPoolSent + tid] = -INFINITY;
     const int ipt = a.ty * a.tx;  // tiles per image
     int desc = -1;
     if (tid < kPoolSlots) {
@@ -479,7 +484,8 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         for (int j = 0; j < 3; ++j) {
           const int x = 2 * px + j, txx = x / 3, rx = x - 3 * txx;
           const int lt = n * ipt + tyy * a.tx + txx - p0;
-          e[i * 3 + j] = static_cast<unsigned>(lt) < static_cast<unsigned>(kTiles) ? ((ry * 3 + rx) * kTiles + lt) * kOS : -1;
+          e[i * 3 + j] = static_cast<unsigned>(lt) < static_cast<unsigned>(kTiles) ? ((ry * 3 + rx) * kTiles + lt) * kOS
+                                                                                  : kPoolSent;
         }
       }
       e[9] = up ? ((n * a.Hp + py) * a.Wp + px) * kK : ((n * o.Hb + py + o.h_off) * o.Wb + px + o.w_off) * o.Cb + o.c_off;
@@ -497,13 +503,12 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
       const i32x4 e1 = *reinterpret_cast<const i32x4*>(ent + k * kPoolEnt + 4);
       const i32x4 e2 = *reinterpret_cast<const i32x4*>(ent + k * kPoolEnt + 8);
       const int off[9] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x};
-      f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      f32x4 v[9];
 #pragma unroll
-      for (int i = 0; i < 9; ++i)
-        if (off[i] >= 0) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(tr + off[i] + 4 * fq);
-          m = f32x4{fmaxf(m.x, v.x), fmaxf(m.y, v.y), fmaxf(m.z, v.z), fmaxf(m.w, v.w)};
-        }
+      for (int i = 0; i < 9; ++i) v[i] = *reinterpret_cast<const f32x4*>(tr + off[i] + 4 * fq);
+      f32x4 m = v[0];
+#pragma unroll
+      for (int i = 1; i < 9; ++i) m = f32x4{fmaxf(m.x, v[i].x), fmaxf(m.y, v[i].y), fmaxf(m.z, v[i].z), fmaxf(m.w, v[i].w)};
       float* dst = (e2.z ? a.p1 : o.base) + static_cast<size_t>(static_cast<unsigned>(e2.y)) + 4 * fq;
       *reinterpret_cast<f32x4*>(dst) = m;
     }
