@@ -156,7 +156,7 @@ __host__ __device__ inline bool pool1_straddles(int n, int py, int px, int ty1, 
 }
 bool conv1_fused_pool_eligible(const Conv1WinoPlan& w, const OutView& window, int Hp, int Wp);
 hipError_t conv1_fused_pool(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView window,
-                            float* p1, int Hp, int Wp, bool relu, hipStream_t s, bool upw = false);
+                            float* p1, int Hp, int Wp, bool relu, hipStream_t s, int um = 0);
 
 // The fused Winograd GEMM + output transform (wino_gemm.hip). V [P][points][C], U [points][K][C/groups]
 // (row = filter), bias + optional ReLU, NHWC store through `out` (Cb, c_off multiples of 4). P tiles of

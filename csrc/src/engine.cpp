@@ -430,7 +430,7 @@ hipError_t BlocksEngine::tile_forward_conv1_pool(const float* x, int N, const Ti
       RoctxRange rx("anx conv1+pool1");
       const hip::Conv1WinoPlan w1 = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);
       const hip::OutView win{q2_ + n0 * q_img, t.q.size(), wq_, d_.C1, t.p1.lo - t.q.lo, k2.P, 0};
-      ANX_TRY(hip::conv1_fused_pool(w1, x + n0 * in_img, u1w_, b1d_, win, c1_, d_.Hp1, d_.Wp1, true, s, k_.conv1_fused == 2));
+      ANX_TRY(hip::conv1_fused_pool(w1, x + n0 * in_img, u1w_, b1d_, win, c1_, d_.Hp1, d_.Wp1, true, s, k_.conv1_fused - 1));
     }
     RoctxRange rx("anx conv2+pool2+lrn");
     const hip::Conv1WinoPlan w1 = hip::make_conv1_wino_plan(n, t.in.size(), d_.W, k1.K, k1.F);

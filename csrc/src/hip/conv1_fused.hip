@@ -145,8 +145,12 @@ struct Conv1FusedArgs {
   unsigned long long* dbg;  // ABL bit 64 (ANX_CONV1_PHASES diagnostics): per-workgroup stamps, else null
 };
 
-template <bool POOL, int ABL = 0, bool UPW = false>
+// UM: where U lives -- 0 the shared 3-slot LDS ring (every wave's DMA, a barrier per point), 1 a private
+// 2-slot LDS ring per wave (own DMA, own vmcnt; barriers only at a-step starts), 2 registers (each wave loads
+// its B fragments from L2 one point ahead; no U in LDS at all)
+template <bool POOL, int ABL = 0, int UM = 0>
 __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
+  constexpr bool UPW = UM == 1, UREG = UM == 2;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: the DMA M0 values stay scalar
@@ -192,10 +196,19 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
       uoffw[i] = ((wn * 16 + row) * kCh + 4 * u) * 4;
     }
   }
+  // UREG: this wave's B fragments of point ab, g = 0..2: filter row brow, channels 16 g + 4 h4 .. +3
+  [[maybe_unused]] f32x4 ub[2][3];
+  [[maybe_unused]] const int ubo = ((wn * 16 + (lane & 15)) * kCh + 4 * (lane >> 4)) * 4;
   auto issue_u = [&](auto AB) {
     [[maybe_unused]] constexpr int ab = decltype(AB)::value;
     if constexpr ((ABL & 2) != 0) return;
 #if __HIP_DEVICE_COMPILE__
+    if constexpr (UREG) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        ub[ab & 1][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ur, ubo + 64 * g, ab * kUSlot * 4, 0));
+      return;
+    }
     if constexpr (UPW) {
       lds_f32* st = uringw + (ab % 2) * kUW;
 #pragma unroll
@@ -287,6 +300,8 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // ---- MFMA fragments (v_mfma_f32_16x16x4_f32): A[row = lane & 15][k = lane >> 4], B[k = lane >> 4][col =
   // lane & 15]; k-step 4g + i uses channel 16g + 4(lane >> 4) + i (one ds_read_b128 per operand per g)
   const int r16 = lane & 15, h4 = lane >> 4;
+  // the epilogue's bias, loaded here: issued at the epilogue it exposed a global-load latency per workgroup
+  const float bv = a.bias ? a.bias[wn * 16 + r16] : 0.f;
   const int a_off = (wm * 16 + r16) * kVS + 4 * h4;
   const int brow = wn * 16 + r16;
   int b_off[3];  // UPW: row r16 of this wave's ring slot (swz(brow) == swz(r16): 16 wn leaves bits 1-2)
@@ -307,7 +322,9 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   f32x2 xrow[kN5][kN5];  // X' rows of this thread's (tile, channel pair), each loaded once (see late_load_pt)
   // prologue: U_0, U_1 in flight; the rows V_0 takes loaded (kept), V_0 built and stored
   issue_u(std::integral_constant<int, 0>{});
-  if constexpr (!UPW) issue_u(std::integral_constant<int, 1>{});  // UPW: one point ahead (2 slots)
+  if constexpr (UM == 0) issue_u(std::integral_constant<int, 1>{});  // UPW / UREG: one point ahead (2 slots)
+  // (the compiler issues U_0 after the X' row loads of V_0; pinning it ahead of them measured slower: the
+  // rows are the prologue's critical path, 4.5 k -> 5.1 k clk, profiles/r06_conv1_upw/)
   t_zero();
   sfor<0, kN5>([&](auto Uc) {
     constexpr int u = decltype(Uc)::value;
@@ -336,7 +353,9 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
       // UPW: U_p was issued at point p - 1 (the prologue for p = 0); after it only point p - 1's X' row loads
       constexpr int inflight_w = x_ops(p - 1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (UPW) {
+      if constexpr (UREG) {
+        if constexpr (b == 0) lds_barrier<-1>();  // V_a published; U is in registers (the compiler waits for it)
+      } else if constexpr (UPW) {
         if constexpr (b == 0)
           lds_barrier<inflight_w>();  // V_a published (and every wave past a-step a - 1's reads of its buffer)
         else
@@ -347,7 +366,7 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
         lds_barrier<inflight>();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("" ::: "memory");
-      if constexpr (UPW) {
+      if constexpr (UPW || UREG) {
         // slot (p + 1) % 2 held U_{p-1}, read by this wave only, at point p - 1 (its MFMAs consumed the reads)
         if constexpr (p + 1 < kPts) issue_u(std::integral_constant<int, p + 1>{});
       } else if constexpr (p + 2 < kPts) {
@@ -366,7 +385,11 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
         const f32x4 af = *reinterpret_cast<const f32x4*>(vp + 16 * g);
-        const f32x4 bf = *reinterpret_cast<const f32x4*>(up + b_off[g]);
+        f32x4 bf;
+        if constexpr (UREG)
+          bf = ub[p & 1][g];
+        else
+          bf = *reinterpret_cast<const f32x4*>(up + b_off[g]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[i], acc, 0, 0, 0);
       }
@@ -415,7 +438,6 @@ __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
   // ---- epilogue: per output position q, bias + ReLU into an LDS image [32 tiles][96 filters], then
   // 16-B row-contiguous stores. D layout: lane holds col = lane & 15 (filter), rows 4 (lane >> 4) + i.
   const int f = wn * 16 + r16;
-  const float bv = a.bias ? a.bias[f] : 0.f;
   const OutView o = a.out;
   float* tr = lds;
   const int st = tid / (kK / 4), sq = tid - st * (kK / 4);  // this thread's store: tile st, filters 4 sq .. +3
@@ -595,11 +617,12 @@ void conv1_phase_report(const std::vector<unsigned long long>& h, int n) {
 }
 
 hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView out,
-                              bool relu, hipStream_t s, float* p1, int Hp, int Wp, bool upw = false) {
+                              bool relu, hipStream_t s, float* p1, int Hp, int Wp, int um = 0) {
   static const hipError_t attr = [] {
     for (const void* k : {reinterpret_cast<const void*>(conv1_fused_kernel<false>),
                           reinterpret_cast<const void*>(conv1_fused_kernel<true>),
-                          reinterpret_cast<const void*>(conv1_fused_kernel<true, 0, true>)}) {
+                          reinterpret_cast<const void*>(conv1_fused_kernel<true, 0, 1>),
+                          reinterpret_cast<const void*>(conv1_fused_kernel<true, 0, 2>)}) {
       const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -659,7 +682,9 @@ hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const floa
     if (!attr_set) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_fused_kernel<true, 64>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_fused_kernel<true, 64, true>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_fused_kernel<true, 64, 1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv1_fused_kernel<true, 64, 2>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr_set = true;
     }
@@ -667,8 +692,10 @@ hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const floa
     unsigned long long* dbg = nullptr;
     if (hipMalloc(&dbg, nb * 8) != hipSuccess) return hipErrorOutOfMemory;
     a.dbg = dbg;
-    if (upw)
-      conv1_fused_kernel<true, 64, true><<<grid, kNT, kLdsW, s>>>(a);
+    if (um == 1)
+      conv1_fused_kernel<true, 64, 1><<<grid, kNT, kLdsW, s>>>(a);
+    else if (um == 2)
+      conv1_fused_kernel<true, 64, 2><<<grid, kNT, kLds, s>>>(a);
     else
       conv1_fused_kernel<true, 64><<<grid, kNT, kLds, s>>>(a);
     std::vector<unsigned long long> h(nb);
@@ -679,8 +706,10 @@ hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const floa
     conv1_phase_report(h, a.n_ptiles);
     return hipGetLastError();
   }
-  if (p1 != nullptr && upw)
-    conv1_fused_kernel<true, 0, true><<<grid, kNT, kLdsW, s>>>(a);
+  if (p1 != nullptr && um == 1)
+    conv1_fused_kernel<true, 0, 1><<<grid, kNT, kLdsW, s>>>(a);
+  else if (p1 != nullptr && um == 2)
+    conv1_fused_kernel<true, 0, 2><<<grid, kNT, kLds, s>>>(a);
   else if (p1 != nullptr)
     conv1_fused_kernel<true><<<grid, kNT, kLds, s>>>(a);
   else
@@ -706,10 +735,10 @@ bool conv1_fused_pool_eligible(const Conv1WinoPlan& w, const OutView& window, in
 }
 
 hipError_t conv1_fused_pool(const Conv1WinoPlan& w, const float* x, const float* U, const float* bias, OutView window,
-                            float* p1, int Hp, int Wp, bool relu, hipStream_t s, bool upw) {
+                            float* p1, int Hp, int Wp, bool relu, hipStream_t s, int um) {
   if (w.P == 0 || w.H1 <= 0 || w.W1 <= 0) return hipSuccess;
   if (p1 == nullptr || !conv1_fused_pool_eligible(w, window, Hp, Wp)) return hipErrorInvalidValue;
-  return conv1_fused_launch(w, x, U, bias, window, relu, s, p1, Hp, Wp, upw);
+  return conv1_fused_launch(w, x, U, bias, window, relu, s, p1, Hp, Wp, um);
 }
 
 }  // namespace anx::hip

@@ -37,7 +37,7 @@ const Field kFields[] = {
     {"conv2_occ", &Knobs::conv2_occ, nullptr, -1, 8, "ANX_CONV2_OCC"},
     {"conv1_band", &Knobs::conv1_band, nullptr, 0, 2, "ANX_CONV1_BAND"},
     {"fuse_pool1", &Knobs::fuse_pool1, nullptr, 0, 1, "ANX_FUSE_POOL1"},
-    {"conv1_fused", &Knobs::conv1_fused, nullptr, 0, 2, "ANX_CONV1_FUSED"},
+    {"conv1_fused", &Knobs::conv1_fused, nullptr, 0, 3, "ANX_CONV1_FUSED"},
     {"conv1_pool", &Knobs::conv1_pool, nullptr, 0, 1, "ANX_CONV1_POOL"},
     {"conv1_sub", &Knobs::conv1_sub, nullptr, 0, 1 << 30, "ANX_CONV1_SUB"},
     {"conv2_sub", &Knobs::conv2_sub, nullptr, 0, 1 << 30, "ANX_CONV2_SUB"},

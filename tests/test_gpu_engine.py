@@ -570,17 +570,19 @@ def test_set_knob_rebuilds_conv2_workspace(cuda):
         assert torch.equal(m(x), fresh[t])
 
 
+@pytest.mark.parametrize("um", [2, 3])
 @pytest.mark.parametrize("N,kn", [(9, {}), (33, {}), (64, {}), (130, {}), (40, {"chunk1": 16})])
-def test_conv1_per_wave_u_ring_bitwise(cuda, N, kn):
+def test_conv1_per_wave_u_ring_bitwise(cuda, N, kn, um):
     """The one-kernel Conv1 with a private U ring per wave (knob conv1_fused = 2: each wave DMAs the filter
-    rows its own fragments read and waits for them with its own vmcnt; barriers only where V is published)
-    gives the same bits as the shared-ring kernel (same MFMA and fold order), partial workgroups and chunked
-    launches included; the whole output against the fp64 oracle too."""
+    rows its own fragments read and waits for them with its own vmcnt; barriers only where V is published) or
+    with U in registers (3: each wave loads its B fragments from L2 one point ahead) gives the same bits as the
+    shared-ring kernel (same MFMA and fold order), partial workgroups and chunked launches included; the whole
+    output against the fp64 oracle too."""
     x = init_input(N, "rand", seed=37).to(cuda)
     base = {**WINO1, **WINO2, **kn, "conv1_pool": 1}
-    upw = AlexNetBlocks(device=cuda, init="rand", seed=37, max_batch=N, knobs={**base, "conv1_fused": 2})
+    upw = AlexNetBlocks(device=cuda, init="rand", seed=37, max_batch=N, knobs={**base, "conv1_fused": um})
     ring = AlexNetBlocks(device=cuda, init="rand", seed=37, max_batch=N, knobs={**base, "conv1_fused": 1})
-    assert upw.get_knob("conv1_fused") == 2
+    assert upw.get_knob("conv1_fused") == um
     y = upw(x)
     assert torch.equal(y, ring(x))
     ref = blocks_forward_all(x, upw.weights, upw.b1, upw.b2, device=cuda)
