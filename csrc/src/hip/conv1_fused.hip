@@ -150,6 +150,8 @@ struct Conv1FusedArgs {
 // its B fragments from L2 one point ahead; no U in LDS at all)
 template <bool POOL, int ABL = 0, int UM = 0>
 __global__ void __launch_bounds__(kNT, 3) conv1_fused_kernel(Conv1FusedArgs a) {
+  // (two accumulation chains per point, odd k-steps on the second, measured slower with the per-wave ring:
+  // main loop 48.5 k vs 44.2 k clk, profiles/r06_conv1_upw/)
   constexpr bool UPW = UM == 1, UREG = UM == 2;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -710,6 +712,7 @@ hipError_t conv1_fused_launch(const Conv1WinoPlan& w, const float* x, const floa
     conv1_fused_kernel<true, 0, 1><<<grid, kNT, kLdsW, s>>>(a);
   else if (p1 != nullptr && um == 2)
     conv1_fused_kernel<true, 0, 2><<<grid, kNT, kLds, s>>>(a);
+
   else if (p1 != nullptr)
     conv1_fused_kernel<true><<<grid, kNT, kLds, s>>>(a);
   else
