@@ -68,12 +68,12 @@ struct Knobs {
                            // chunk (0 = the whole chunk); the V workspace is rewritten in place per sub-chunk, so
                            // a small one is written and re-read inside the 256 MB Infinity Cache
   int conv2_sub = 0;       // ... and per (pool1 + Conv2 input transform, Conv2 GEMM) pair
-  int conv2_pool = 0;      // tuning: 1 = for whole images on F(4x4,5x5) with LRN over 256 channels, pool2 in the Conv2
-                           // GEMM's epilogue (the 27x27 map never reaches HBM: -125 MB per 128 images; straddling
-                           // windows' partial maxima to a side buffer merged by the LRN kernel). Measured level with
-                           // 0 on the bench step (320.8-322.1 k vs 322.1-323.0 k: the GEMM runs 278 instead of 266 us,
-                           // the LRN 9.7 instead of 25.8; profiles/r05_conv2_pool/), so 0 = the GEMM writes its map
-                           // and maxpool_lrn pools it
+  int conv2_pool = 1;      // 1 (default since round 6) = for whole images on F(4x4,5x5) with LRN over 256 channels, pool2
+                           // in the Conv2 GEMM's epilogue (the 27x27 map never reaches HBM: -125 MB per 128 images;
+                           // straddling windows' partial maxima to a side buffer merged by the LRN kernel). Round 5
+                           // measured it level with the compiler-scheduled GEMM (320.8-322.1 k vs 322.1-323.0 k,
+                           // profiles/r05_conv2_pool/); with the hand-scheduled K slice it is +3 % (349.0-350.4 k vs
+                           // 338.1-340.9 k, profiles/r06_conv2_pool/). 0 = the GEMM writes its map and maxpool_lrn pools it
   int conv2_tile = 4;      // Conv2 Winograd output tile: 4 = F(4x4,5x5) (64 points per 16 outputs: 21 % fewer
                            // multiplies, 16x16x4 MFMAs, wino_gemm16.hpp; one group of 96 channels only, else 3;
                            // bench step 305-309 k vs 293 k images/s, profiles/r05_f45/), 3 = F(3x3,5x5) (49

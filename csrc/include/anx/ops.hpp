@@ -187,7 +187,7 @@ __host__ __device__ inline bool pool2_straddles(int n, int py, int px, int ty2, 
 }
 hipError_t wino_gemm_conv2_f45_pool(const float* V, const float* U, const float* bias, float* pooled, float* p2, int P,
                                     int ty, int tx, int Ho, int Wo, int Hp, int Wp, int K, bool relu, hipStream_t s,
-                                    int occ = 0);
+                                    int occ = 0, bool sched = false);
 
 
 // Dynamic LDS bytes that cap a kernel at `wgs` workgroups per CU (160 KiB LDS per CU): the larger of

@@ -451,7 +451,8 @@ hipError_t BlocksEngine::tile_forward_conv1_pool(const float* x, int N, const Ti
         ty2 = w.ty;
         tx2 = w.tx;
         ANX_TRY(hip::wino_gemm_conv2_f45_pool(wv_, u2w_, b2d_, c2_ + b0 * pimg, p2 + b0 * pimg, w.P, w.ty, w.tx, w.Ho,
-                                              w.Wo, d_.Hp2, d_.Wp2, w.K, true, s, k_.conv2_occ));
+                                              w.Wo, d_.Hp2, d_.Wp2, w.K, true, s, k_.conv2_occ,
+                                              k_.conv2_sched != 0));
       } else {
         const hip::OutView c2v{c2_ + b0 * c2_img, t.c2.size(), d_.W2, d_.C2, 0, 0, 0};
         ANX_TRY(hip::wino_conv2(w, wv_, u2w_, b2d_, c2v, true, s, k_));

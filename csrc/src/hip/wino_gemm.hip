@@ -207,7 +207,7 @@ hipError_t wino_gemm_conv2_f45(const float* V, const float* U, const float* bias
 
 hipError_t wino_gemm_conv2_f45_pool(const float* V, const float* U, const float* bias, float* pooled, float* p2, int P,
                                     int ty, int tx, int Ho, int Wo, int Hp, int Wp, int K, bool relu, hipStream_t s,
-                                    int occ) {
+                                    int occ, bool sched) {
   const long vb = static_cast<long>(P) * 64 * 96 * 4, ub = static_cast<long>(64) * K * 96 * 4;
   // the epilogue's window walk: 4x4 tiles covering the map, a window's tiles within tx + 1 raster steps
   // of its first (< one workgroup's 32), pooled dims of a 3x3 / 2 pool
@@ -235,7 +235,7 @@ hipError_t wino_gemm_conv2_f45_pool(const float* V, const float* U, const float*
   a.p2 = p2;
   a.Hp = Hp;
   a.Wp = Wp;
-  return launch16<F45, 0, true>(a, s, occ);
+  return sched ? launch16<F45, kConv2Sched, true>(a, s, occ) : launch16<F45, 0, true>(a, s, occ);
 }
 
 hipError_t wino_gemm_conv1(const float* V, const float* U, const float* bias, OutView out, int P, int ty, int tx, int Ho,

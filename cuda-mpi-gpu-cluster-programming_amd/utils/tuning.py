@@ -26,9 +26,9 @@ Names and values:
   default: Conv1 as one kernel, the polyphase input transform built in LDS inside the Winograd GEMM;
   0: the band transform kernel + GEMM); ``conv1_pool`` (1, the default: pool1 in that kernel's epilogue for
   whole images, the conv1 map never reaches HBM; 0: Conv1 writes its map and the input transform pools it);
-  ``conv2_pool`` (0, the default: the Conv2 GEMM writes its map and the pool2 + LRN kernel pools it; 1: pool2
-  in the F(4x4,5x5) GEMM's epilogue for whole images, 125 MB less HBM traffic per 128 images, measured level
-  on the bench step);
+  ``conv2_pool`` (1, the default since round 6: pool2 in the F(4x4,5x5) GEMM's epilogue for whole images, the
+  27x27 map never reaches HBM, +3 % on the bench step with the hand-scheduled GEMM; 0: the GEMM writes its map
+  and the pool2 + LRN kernel pools it);
   ``conv2_tile`` (Conv2's Winograd output tile: 3 = F(3x3,5x5), 4 = F(4x4,5x5), 21 % fewer multiplies);
   ``conv2_sched`` (1, the default: the F(4x4,5x5) GEMM's hand-scheduled K slice, bitwise equal to 0, the
   compiler's schedule).
