@@ -78,6 +78,8 @@ struct Knobs {
                            // multiplies, 16x16x4 MFMAs, wino_gemm16.hpp; one group of 96 channels only, else 3;
                            // bench step 305-309 k vs 293 k images/s, profiles/r05_f45/), 3 = F(3x3,5x5) (49
                            // points, 32x32x2 MFMAs: grouped Conv2 and the A/B arm)
+  int conv2_in_pg = 32;    // tuning: channels per workgroup of the Conv2 input transform after the pooled Conv1 (32: 31 KiB of
+                           // LDS; 16: 15.5 KiB, fits on a CU beside a per-wave-ring Conv1 workgroup)
   int conv2_sched = 1;     // F(4x4,5x5) GEMM K-slice schedule: 1 = hand-scheduled (wino_gemm16_sched.inc: fragment
                            // reads two groups ahead with counted lgkmcnt, alternating accumulators, the fold as one
                            // packed burst at the slice start; bitwise identical), 0 = the compiler's schedule

@@ -114,8 +114,10 @@ hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, i
 // Input transform of a conv2 window whose pool1 pixels were written by conv1_fused_pool: straddling
 // pixels take max(window, p1) (p1: [N][Hp][Wp][C], image 0 = tile-numbering image n_off of the Conv1
 // launch with ty1 x tx1 tiles per image). Window row R is pool1 row q_lo + R, column c pool1 column c - P.
+// pg: channels per workgroup, 32 (31 KiB of LDS, 512 threads) or 16 (15.5 KiB, 256 threads: fits beside a
+// Conv1 workgroup of the per-wave-ring kernel, 142 KiB, on one CU; knob conv2_in_pg).
 hipError_t wino_window_merge_input(const WinoPlan& w, const float* window, const float* p1, int n_off, int ty1, int tx1,
-                                   int q_lo, int Hp, int Wp, int P, float* V, hipStream_t s);
+                                   int q_lo, int Hp, int Wp, int P, float* V, hipStream_t s, int pg = 32);
 // Fused batched GEMM + output transform + bias + optional ReLU into `out` (wino_gemm.hpp); Knobs:
 // conv2_occ (workgroups per CU cap).
 hipError_t wino_conv2(const WinoPlan& w, const float* V, const float* U, const float* bias, OutView out, bool relu,

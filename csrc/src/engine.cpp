@@ -446,7 +446,7 @@ hipError_t BlocksEngine::tile_forward_conv1_pool(const float* x, int N, const Ti
       const hip::WinoPlan w = hip::make_wino_plan(m, t.q.size(), wq_, d_.C1, k2.K, k2.groups, u2_m_);
       if (hip::wino_v_floats(w) > wv_cap_) return hipErrorInvalidValue;
       ANX_TRY(hip::wino_window_merge_input(w, q2_ + (n0 + b0) * q_img, c1_ + b0 * p1_img, b0, w1.ty, w1.tx, t.q.lo,
-                                           d_.Hp1, d_.Wp1, k2.P, wv_, s));
+                                           d_.Hp1, d_.Wp1, k2.P, wv_, s, u2_m_ == 4 ? k_.conv2_in_pg : 32));
       if (pool2) {
         ty2 = w.ty;
         tx2 = w.tx;

@@ -257,17 +257,22 @@ hipError_t wino_pool_input(const WinoPlan& w, const float* c1, int H1, int W1, i
 }
 
 hipError_t wino_window_merge_input(const WinoPlan& w, const float* window, const float* p1, int n_off, int ty1, int tx1,
-                                   int q_lo, int Hp, int Wp, int P, float* V, hipStream_t s) {
-  constexpr int pg = 32;
-  if (w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * npt(w.m) >= (1L << 31)) return hipErrorInvalidValue;
+                                   int q_lo, int Hp, int Wp, int P, float* V, hipStream_t s, int pg) {
+  if ((pg != 32 && pg != 16) || w.C % pg || w.Wq > kMaxWq || static_cast<long>(w.P) * w.C * npt(w.m) >= (1L << 31))
+    return hipErrorInvalidValue;
   if (w.P == 0) return hipSuccess;
   const int groups = w.N * (w.C / pg);
   const unsigned grid = static_cast<unsigned>((groups + 7) / 8 * 8 * w.ty);
-  if (w.m == 4)
-    pool_wino_in_kernel<4, pg, 512, false, true><<<grid, 512, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp,
+  if (w.m == 4 && pg == 16)
+    pool_wino_in_kernel<4, 16, 256, false, true><<<grid, 256, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp,
                                                                       Wp, P, 0, w.ty, w.tx, p1, n_off, ty1, tx1);
+  else if (w.m == 4)
+    pool_wino_in_kernel<4, 32, 512, false, true><<<grid, 512, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp,
+                                                                      Wp, P, 0, w.ty, w.tx, p1, n_off, ty1, tx1);
+  else if (pg == 16)
+    return hipErrorInvalidValue;
   else
-    pool_wino_in_kernel<3, pg, 512, false, true><<<grid, 512, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp,
+    pool_wino_in_kernel<3, 32, 512, false, true><<<grid, 512, 0, s>>>(window, V, groups, 0, 0, w.C, w.Hq, w.Wq, q_lo, Hp,
                                                                       Wp, P, 0, w.ty, w.tx, p1, n_off, ty1, tx1);
   return hipGetLastError();
 }

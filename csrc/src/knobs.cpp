@@ -44,6 +44,7 @@ const Field kFields[] = {
     {"conv2_pool", &Knobs::conv2_pool, nullptr, 0, 1, "ANX_CONV2_POOL"},
     {"conv2_tile", &Knobs::conv2_tile, nullptr, 3, 4, "ANX_CONV2_TILE"},
     {"conv2_sched", &Knobs::conv2_sched, nullptr, 0, 1, "ANX_CONV2_SCHED"},
+    {"conv2_in_pg", &Knobs::conv2_in_pg, nullptr, 16, 32, "ANX_CONV2_IN_PG"},
 };
 
 const Field* find(const char* name) {
@@ -56,6 +57,7 @@ const Field* find(const char* name) {
 bool valid(const Field& f, int v) {
   if (v < f.lo || v > f.hi) return false;
   if (std::strcmp(f.name, "bf16_glds") == 0) return v == 0 || v == 2 || v == 3;
+  if (std::strcmp(f.name, "conv2_in_pg") == 0) return v == 16 || v == 32;
   if (std::strcmp(f.name, "bf16_big") == 0) return v < hip::kConvBf16BigCfgs;
   if (std::strcmp(f.name, "force_vec4") == 0) return hip::conv_variant_valid(0, v);
   if (std::strcmp(f.name, "force_scalar") == 0) return hip::conv_variant_valid(1, v);

@@ -42,7 +42,7 @@ from .. import _native as nat
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
          "bf16_lrn_tile", "bf16_conv1", "bf16_pool1", "bf16_fc_cfg", "bf16_fc_minkt", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
-         "conv1_fused", "conv1_pool", "conv2_pool", "conv2_tile", "conv2_sched")
+         "conv1_fused", "conv1_pool", "conv2_pool", "conv2_tile", "conv2_sched", "conv2_in_pg")
 
 
 def knob_value(name: str, value) -> int:
