@@ -268,3 +268,20 @@ def test_native_v4_shared_gpu(v5_reference, world, kw):
     assert err < 1e-5, (err, desc)
     assert set(phases) == {"h2d", "compute", "d2h"} and phases["h2d"] > 0
     assert desc["runtime"].startswith("native") and desc["h2d_bytes_per_step_rank"] > 0
+
+
+@pytest.mark.gpu
+def test_native_dp_program_two_ranks_lanes_loopback(cuda):
+    """The dp headline's program natively: two ranks sharing the GPU, each with its own 64
+    whole images placed on its device once (batch split, local input), run as 2 free-running lanes of 32,
+    gathered to rank 0 over the RCCL transport's code on the loopback communicator. Equal to one process's
+    forward of all 128 images (the kernels compute every output element the same way whatever the split)."""
+    ref = _reference(batch=128)
+    y, desc, phases = _run_v5(2, {"decomp": "batch", "transport": "loopback", "input_source": "local", "lanes": 2,
+                                  "pipeline": 1}, batch=128, steps=3)
+    y = torch.from_numpy(y)
+    assert desc["lane_path"] is True and desc["lanes"] == 2 and desc["row_ways"] == 1
+    assert desc["halo_exchange"].startswith("none") and desc["transport"].startswith("rccl")
+    assert y.shape == ref.shape
+    assert y.sub(ref).abs().max().item() / ref.abs().max().item() < 1e-5
+    assert phases["gather"] >= 0 and phases["compute"] > 0
