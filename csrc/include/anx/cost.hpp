@@ -42,9 +42,9 @@ enum class InputSource : int { Local = 0, Root = 1 };
 struct CostParams {
   // measured single-GPU throughput of the fp32 Blocks 1-2 engine (free-running stream lanes, one
   // lane below 32 images), images per GPU -> images/s, medians of tools/sweep_batch.py
-  // (profiles/r05_f45/sweep_lanes2_async.log, round 5 kernels; the bench step itself runs 306 k at 128)
+  // (profiles/r06_final/sweep_lanes2_async.log, round 6 kernels; the bench step itself runs 350 k at 128)
   std::vector<int> rate_images{1, 8, 16, 32, 64, 128, 256, 512, 1024};
-  std::vector<double> rate_img_s{11200, 54400, 118400, 182200, 249000, 296100, 300200, 303400, 296000};
+  std::vector<double> rate_img_s{11670, 55230, 140770, 197410, 286340, 330520, 332330, 335570, 327790};
   double min_step_ms = 0.08;     // a forward's kernel chain never takes less (batch 1: 0.081 ms, r01_algo_crossover)
   double stage1_share = 0.37;    // conv1 (+ its transform) share of one image's kernel time (r03 kernel table)
   double split_penalty = 1.03;   // per-layer row tiles: unfused pool1 + window (profiles/r03_fuse_pool1_bench_ab)

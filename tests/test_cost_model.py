@@ -37,7 +37,10 @@ def test_v5_local_input_moves_only_gather_and_halo():
     s = cost.step("v5", 8, 1024, 1, input_source="local")
     assert s["bytes"]["root_egress"] == 0 and s["egress_ms"] == 0
     assert s["bytes"]["root_ingress"] == 7 * 128 * OUT_IMG
-    assert s["bound"] == "compute"
+    # round-6 kernels: 128 images per rank compute in about the time the root takes to receive the 7
+    # peers' outputs, so the step sits at the compute / ingress balance point (never egress or halo)
+    assert s["bound"] in ("compute", "ingress")
+    assert s["ingress_ms"] <= 1.05 * s["compute_ms"] and s["halo_ms"] == 0
     # the root-scatter data flow is egress-bound at 8 ranks whatever the kernels do
     r = cost.step("v5", 8, 1024, -1, input_source="root")
     assert r["bound"] == "egress" and r["step_ms"] > 3 * s["step_ms"]
@@ -113,7 +116,15 @@ def test_dp_root_shed():
     assert s["bytes"]["root_ingress"] == 7 * 128 * OUT_IMG  # peers still send full batches
     assert s["images_per_s"] == pytest.approx(s["images"] / s["step_ms"] * 1e3, rel=1e-3)
     noshed = cost.step("dp", 8, 128, overrides="dp_root_shed=0")
-    assert noshed["root_batch"] == 128 and s["step_ms"] < noshed["step_ms"]
+    assert noshed["root_batch"] == 128
+    # at the ASSUMED 50 GB/s per xGMI link the round-6 kernels make the N=8 step ingress-bound (0.46 ms
+    # gather vs 0.39 ms compute), where the shed costs 16 of 1024 images (1.6 %); when the link is faster
+    # the step is compute-bound and the shed is what keeps rank 0 off the critical path (13 % of a step).
+    # The bench keeps the shed: the cheap side of an unmeasurable link rate.
+    assert s["bound"] == "ingress" and noshed["images_per_s"] < 1.02 * s["images_per_s"]
+    fast = "xgmi_gbps=150"
+    s, noshed = cost.step("dp", 8, 128, overrides=fast), cost.step("dp", 8, 128, overrides=fast + ";dp_root_shed=0")
+    assert s["bound"] == "compute" and s["step_ms"] < noshed["step_ms"]
     assert s["images_per_s"] > noshed["images_per_s"]
 
 
