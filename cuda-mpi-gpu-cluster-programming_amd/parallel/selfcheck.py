@@ -18,9 +18,12 @@ prove itself in its own JSON:
   span matches the peers' mean.
 * :class:`FirstCollectiveWatchdog` — a bounded wait for the first collectives with a rank-tagged error,
   instead of the backend's multi-minute default.
+* :class:`SecondaryDeadline` — a bounded wait for everything after the headline measurement: the
+  headline line is printed even if a secondary program hangs.
 """
 from __future__ import annotations
 
+import json
 import os
 import socket
 import sys
@@ -165,3 +168,54 @@ class FirstCollectiveWatchdog:
     def __exit__(self, *exc):
         self._done.set()
         return False
+
+
+class SecondaryDeadline:
+    """The headline's safety net for the work bench.py does after measuring it (batch-1 probes, the native
+    V4 / V5 programs of BASELINE configs 3-4, the bf16 extension, the closing barrier). Those programs'
+    device transports (RCCL point-to-point, peer IPC) meet real multi-GPU hardware for the first time in the
+    driver's N > 1 runs; a call that hangs there would otherwise take the already-measured headline with it.
+    If ``done()`` has not been called after ``seconds``, rank 0 prints ``rec`` (the headline record, built
+    before any secondary ran) with ``secondary_deadline: {seconds, pending_stage}`` unless the full record
+    was already printed, and every rank exits 0. ``emit(rec)`` prints the record exactly once.
+    ``hang="<stage>:<rank>"`` (tests) makes that rank block at that stage, as a hung transport would."""
+
+    def __init__(self, rank: int, seconds: float, rec: dict | None, hang: str | None = None):
+        self.rank, self.seconds, self.rec = rank, seconds, rec
+        self._hang = hang.rsplit(":", 1) if hang else None
+        self._stage = "start"
+        self._printed = False
+        self._lock = threading.Lock()
+        self._done = threading.Event()
+        if seconds > 0:
+            threading.Thread(target=self._watch, daemon=True).start()
+
+    def stage(self, name: str) -> None:
+        self._stage = name
+        if self._hang and self._hang[0] == name and int(self._hang[1]) == self.rank:
+            threading.Event().wait()  # never set: only the deadline ends this rank
+
+    def emit(self, rec: dict) -> None:
+        with self._lock:
+            if not self._printed:
+                self._printed = True
+                print(json.dumps(rec), flush=True)
+
+    def done(self) -> None:
+        self._done.set()
+
+    def _watch(self):
+        if self._done.wait(self.seconds):
+            return
+        sys.stderr.write(f"[bench rank {self.rank}] secondary records still running after {self.seconds:.0f} s "
+                         f"(stage: {self._stage}): headline kept, exiting 0\n")
+        sys.stderr.flush()
+        if self.rank == 0 and self.rec is not None:
+            with self._lock:
+                if not self._printed:
+                    self._printed = True
+                    r = dict(self.rec)
+                    r["secondary_deadline"] = {"seconds": self.seconds, "pending_stage": self._stage}
+                    sys.stdout.write(json.dumps(r) + "\n")
+                    sys.stdout.flush()
+        os._exit(0)

@@ -397,6 +397,26 @@ def test_bench_selfcheck_detects_corrupt_rank_gloo():
     assert "calibration" not in rec["config"] and rec["config"]["root_batch"] == 2
 
 
+def test_bench_secondary_deadline_keeps_headline_gloo():
+    """A secondary program that hangs on one rank (here rank 1 blocks where the native V4/V5 programs
+    start) cannot take the measured headline with it: past --secondary-deadline-s rank 0 prints the
+    headline record, marked with the pending stage, and every rank exits 0."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "1", "--warmup", "0", "--batch-per-gpu", "2", "--device", "cpu", "--secondary-deadline-s", "15"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", ANX_BENCH_HANG_STAGE="reference_programs:1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and rec["n_gpus"] == 2 and rec["gather_verified"] is True
+    assert rec["secondary_deadline"] == {"seconds": 15.0, "pending_stage": "reference_programs"}
+    assert "v4" not in rec and "v5" not in rec and "secondary_s" not in rec
+    assert "secondary records still running" in out.stderr
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_reference_programs_gloo(world):
     """The default dp run also measures BASELINE configs 3 and 4 on the same ranks:
