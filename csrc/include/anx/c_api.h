@@ -152,13 +152,14 @@ int anx_conv2d_mfma(const int* plan, const float* x, const float* wpacked, const
  * ranks; transport: "auto" | "rccl" | "peer" | "loopback"; chunks: 0 auto; pipeline: -1 auto, 0 off,
  * 1 on; peer_sync: "" | "flags" | "notes"; input_source: 0 local (device-resident, placed once by
  * set_input), 1 root (scattered every step); lanes: stream lanes of a halo-free rank (0 = default 2);
- * keep_log: keep the transport's transfer log (anx_v5_log). */
+ * keep_log: keep the transport's transfer log (anx_v5_log); root_images: a batch split's rank-0 share
+ * (the dp headline's root shedding; -1 = even). */
 int anx_v5_create(void** out, int rank, int world, int local_rank, int local_world, int nnodes,
                   const char* master_addr, int master_port, double timeout_s, const anx_block_c* b1,
                   const anx_block_c* b2, int H, int W, const float* w1, const float* bias1, const float* w2,
                   const float* bias2, int batch, int row_ways, int mode, const char* transport, int chunks,
                   int pipeline, int poison, int impl, const char* peer_sync, int input_source, int lanes,
-                  int keep_log);
+                  int keep_log, int root_images);
 int anx_v5_log(void* h, char* buf, size_t cap); /* this rank's issued transfers, one per line */
 int anx_v5_destroy(void* h);
 int anx_v5_set_input(void* h, const float* host_x); /* collective; rank 0's batch, others NULL */

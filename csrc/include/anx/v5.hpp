@@ -49,6 +49,10 @@ struct V5Options {
   int chunks = 0;                  // halo pipeline chunks per step (0 = auto)
   int pipeline = -1;               // scatter(k+1) / gather(k) on the io stream: -1 auto, 0 off, 1 on
   int lanes = 2;                   // stream lanes for a rank whose tile needs no halo (whole images, overlap tiles)
+  // batch split (one rank per group): rank 0's images, the rest split evenly over the peers -- the dp
+  // headline's root shedding (rank 0 also receives the gather, bench.py / cost.hpp dp_root_batch);
+  // -1 = an even split. Invalid with a row split.
+  int root_images = -1;
   bool poison = false;             // NaN-fill every consumed buffer after use (ordering tests)
   bool keep_log = false;           // keep the transport's log of issued transfers (tests)
   std::string peer_sync;           // peer transport ordering: "" (default) | flags | notes

@@ -123,13 +123,14 @@ int anx_v5_create(void** out, int rank, int world, int local_rank, int local_wor
                   const anx_block_c* b2, int H, int W, const float* w1, const float* bias1, const float* w2,
                   const float* bias2, int batch, int row_ways, int mode, const char* transport, int chunks,
                   int pipeline, int poison, int impl, const char* peer_sync, int input_source, int lanes,
-                  int keep_log) {
+                  int keep_log, int root_images) {
   return guarded("anx_v5_create", [&] {
     if (!out || !b1 || !b2) throw std::invalid_argument("null argument");
     const anx::RankInfo ri = rank_info(rank, world, local_rank, local_world, nnodes, master_addr, master_port);
     anx::V5Options o = options(batch, row_ways, mode, transport, chunks, input_source);
     o.lanes = lanes > 0 ? lanes : o.lanes;
     o.keep_log = keep_log != 0;
+    o.root_images = root_images;
     o.pipeline = pipeline;
     o.poison = poison != 0;
     o.impl = impl == 1 ? anx::Impl::Direct : anx::Impl::Mfma;

@@ -69,6 +69,15 @@ V5Layout make_v5_layout(int np, const BlockSpec& b1, const BlockSpec& b2, int H,
   if (!make_hybrid_plan(H, W, np, o.batch, L.row_ways, o.mode, L.plan, b1, b2))
     throw std::runtime_error("v5: invalid plan (row_ways " + std::to_string(L.row_ways) + " over " +
                              std::to_string(np) + " ranks)");
+  if (o.root_images >= 0 && np > 1) {  // root shedding: rank 0 takes root_images, the peers the rest evenly
+    HybridPlan& p = L.plan;
+    if (p.groups != np || o.root_images < 1 || o.batch - o.root_images < np - 1)
+      throw std::runtime_error("v5: root_images " + std::to_string(o.root_images) + " needs a batch split with >= 1 image "
+                               "per rank (" + std::to_string(o.batch) + " images over " + std::to_string(np) + " ranks)");
+    p.images[0] = RowRange{0, o.root_images};
+    const std::vector<RowRange> rest = split_rows(o.batch - o.root_images, np - 1);
+    for (int g = 1; g < np; ++g) p.images[g] = RowRange{o.root_images + rest[g - 1].lo, o.root_images + rest[g - 1].hi};
+  }
   const BlocksDims d = blocks_dims(H, W, b1, b2);
   const size_t in_row = static_cast<size_t>(d.W) * d.C0 * 4, out_row = static_cast<size_t>(d.Wp2) * d.C2 * 4;
   const size_t win_row = static_cast<size_t>(d.Wp1 + 2 * b2.conv.P) * d.C1 * 4;
@@ -749,6 +758,12 @@ std::string V5Runtime::describe_json() const {
                 nhalo ? "pool1 rows between row-group neighbours" : "none (batch split: every rank whole images)", nhalo,
                 halo_bytes);
   j += h;
+  std::string imgs = "\"images_per_rank\": [";  // the plan's per-rank batch share (root shedding: rank 0's differs)
+  for (int r = 0; r < lay_.plan.np; ++r) {
+    const TilePlan& t = lay_.plan.tile(r);
+    imgs += (r ? ", " : "") + std::to_string(t.out.empty() ? 0 : lay_.plan.images[lay_.plan.group_of[r]].size());
+  }
+  j += imgs + "], ";
   auto arr = [&](const char* name, double RankBytes::*f) {
     std::string a = "\"" + std::string(name) + "\": [";
     char t[32];

@@ -108,7 +108,7 @@ _SIGS = {
 _DIST_SIGS = {
     "anx_v5_create": (_I, [C.POINTER(_P), _I, _I, _I, _I, _I, C.c_char_p, _I, C.c_double, C.POINTER(BlockC),
                            C.POINTER(BlockC), _I, _I, _P, _P, _P, _P, _I, _I, _I, C.c_char_p, _I, _I, _I, _I,
-                           C.c_char_p, _I, _I, _I]),
+                           C.c_char_p, _I, _I, _I, _I]),
     "anx_v5_log": (_I, [_P, C.c_char_p, _SZ]),
     "anx_v5_destroy": (_I, [_P]),
     "anx_v5_set_input": (_I, [_P, _P]),

@@ -94,7 +94,7 @@ class NativeV5:
                  decomp: str = "auto", layer: str = PER_LAYER, transport: str = "auto", chunks: int = 0,
                  pipeline: int = -1, poison: bool = False, impl: str = "mfma", peer_sync: str = "",
                  port: int | None = None, timeout_s: float = 300.0, input_source: str = "local", lanes: int = 0,
-                 keep_log: bool = False):
+                 keep_log: bool = False, root_images: int = -1):
         if decomp not in V5_DECOMPS:
             raise ValueError(f"decomp must be one of {sorted(V5_DECOMPS)}")
         if layer not in (OVERLAP, PER_LAYER):
@@ -115,7 +115,7 @@ class NativeV5:
                       timeout_s, C.byref(nat.block_c(self.b1)), C.byref(nat.block_c(self.b2)), H, W, *ptrs, batch, rw,
                       1 if layer == PER_LAYER else 0, transport.encode(), chunks, pipeline, int(poison),
                       {"mfma": 0, "direct": 1, "host": 2}[impl], peer_sync.encode(), 1 if input_source == "root" else 0, lanes,
-                      int(keep_log))
+                      int(keep_log), root_images)
         self._h = h
         self.version, self.layer, self.input_source = "v5", layer, input_source
 

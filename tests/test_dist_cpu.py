@@ -254,7 +254,7 @@ def test_prefetch_pipeline_input_semantics():
         torch.testing.assert_close(ys[k].view_as(ref), ref, rtol=0, atol=0)
 
 
-def _workload_worker(rank, world, port, q, version, decomp, batch):
+def _workload_worker(rank, world, port, q, version, decomp, batch, root_images=-1):
     sys.path.insert(0, ROOT)
     import anx  # noqa: F401
     from anx.parallel.workloads import NativeV5
@@ -264,7 +264,7 @@ def _workload_worker(rank, world, port, q, version, decomp, batch):
     torch.set_num_threads(1)
     kw = dict(layer="overlap", input_source="root") if version == "v4" else dict(layer="per_layer")
     wl = NativeV5(batch, init_weights("rand", 4) if rank == 0 else None, decomp=decomp, impl="host",
-                  timeout_s=120, keep_log=True, **kw)
+                  timeout_s=120, keep_log=True, root_images=root_images, **kw)
     wl.fill(init_input(batch, "rand", seed=4) if rank == 0 else None)
     wl.step()
     wl.step()  # steady state: the other parity's buffers
@@ -305,6 +305,28 @@ def test_native_v5_host_gloo(version, decomp, world, batch):
     assert d["decomp"] == ("overlap" if version == "v4" else "per_layer")
     assert d["input_source"] == ("root" if version == "v4" else "local")
     assert nlog > 0
+
+
+def test_native_v5_host_root_shedding_gloo():
+    """The dp program with root shedding in the native runtime, host mode: rank 0
+    computes 1 image, the two peers 3 each, gathered to rank 0 -- bit for bit the single-process output."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_workload_worker, args=(r, 3, port, q, "v5", "batch", 7, 1)) for r in range(3)]
+    for p in procs:
+        p.start()
+    y, d, nlog = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, ROOT)
+    from anx.models.alexnet_blocks import AlexNetBlocks
+    from anx.utils.init import init_input
+    ref = AlexNetBlocks(init="rand", seed=4, device="cpu")(init_input(7, "rand", seed=4))
+    torch.testing.assert_close(y.view_as(ref), ref, rtol=0, atol=0)
+    assert d["images_per_rank"] == [1, 3, 3] and d["row_ways"] == 1
+    assert d["halo_exchange"].startswith("none")
 
 
 @pytest.mark.parametrize("workload", ["v4", "v5"])

@@ -271,17 +271,21 @@ def test_native_v4_shared_gpu(v5_reference, world, kw):
 
 
 @pytest.mark.gpu
-def test_native_dp_program_two_ranks_lanes_loopback(cuda):
-    """The dp headline's program natively: two ranks sharing the GPU, each with its own 64
-    whole images placed on its device once (batch split, local input), run as 2 free-running lanes of 32,
-    gathered to rank 0 over the RCCL transport's code on the loopback communicator. Equal to one process's
-    forward of all 128 images (the kernels compute every output element the same way whatever the split)."""
+@pytest.mark.parametrize("root_images", [-1, 48])
+def test_native_dp_program_two_ranks_lanes_loopback(cuda, root_images):
+    """The dp headline's program natively: two ranks sharing the GPU, each with its own
+    whole images placed on its device once (batch split, local input), run as 2 free-running lanes, gathered
+    to rank 0 over the RCCL transport's code on the loopback communicator; with root shedding (48: rank 0
+    computes 48 images as 2 lanes of 24, rank 1 80 as 2 of 40) or an even split (64 + 64). Bit for bit one
+    process's forward of all 128 images: every kernel computes an output element the same way whatever
+    batch it is launched with."""
     ref = _reference(batch=128)
     y, desc, phases = _run_v5(2, {"decomp": "batch", "transport": "loopback", "input_source": "local", "lanes": 2,
-                                  "pipeline": 1}, batch=128, steps=3)
+                                  "pipeline": 1, "root_images": root_images}, batch=128, steps=3)
     y = torch.from_numpy(y)
     assert desc["lane_path"] is True and desc["lanes"] == 2 and desc["row_ways"] == 1
+    assert desc["images_per_rank"] == ([64, 64] if root_images < 0 else [48, 80])
     assert desc["halo_exchange"].startswith("none") and desc["transport"].startswith("rccl")
     assert y.shape == ref.shape
-    assert y.sub(ref).abs().max().item() / ref.abs().max().item() < 1e-5
+    assert torch.equal(y, ref), y.sub(ref).abs().max().item()
     assert phases["gather"] >= 0 and phases["compute"] > 0
