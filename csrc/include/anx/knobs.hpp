@@ -83,12 +83,15 @@ struct Knobs {
   int conv2_sched = 1;     // F(4x4,5x5) GEMM K-slice schedule: 1 = hand-scheduled (wino_gemm16_sched.inc: fragment
                            // reads two groups ahead with counted lgkmcnt, alternating accumulators, the fold as one
                            // packed burst at the slice start; bitwise identical), 0 = the compiler's schedule
+  int lrn_wgs = 256;       // grid cap of the pool2-merge + LRN kernel after the pooled Conv2 GEMM (0 = one wave per pixel
+                           // pair, 1352 workgroups per 64 images): under the bench's co-running lanes fewer, longer
+                           // workgroups wait less for CU slots (+0.8-1.5 %, profiles/r06_lrn_grid/); same bits
 };
 
 // Built-in defaults, overridden by ANX_CONV1_ALGO, ANX_CONV2_ALGO, ANX_CHUNK1, ANX_CHUNK2,
 // ANX_BF16_GLDS, ANX_BF16_BIG, ANX_CONV1_OCC, ANX_CONV2_OCC, ANX_CONV1_BAND, ANX_FUSE_POOL1,
 // ANX_CONV1_SUB, ANX_CONV2_SUB, ANX_CONV1_FUSED, ANX_CONV1_POOL, ANX_CONV2_POOL, ANX_CONV2_TILE,
-// ANX_CONV2_SCHED when set.
+// ANX_CONV2_SCHED, ANX_LRN_WGS when set.
 Knobs default_knobs();
 
 // Name-based access for the C ABI / Python (names: the field names above). Returns 0, or -1 for

@@ -203,9 +203,11 @@ hipError_t maxpool_lrn(const float* x, float* y, int N, int H, int W, int C, int
                        float alpha, float beta, float k, LrnMode mode, hipStream_t s);
 // LRN of a pooled map written by wino_gemm_conv2_f45_pool (C == 256, size 5): pixel (n, py, px) is
 // max(pooled, p2) where pool2_straddles(n % sub, ...) (sub: images per GEMM launch, ty2 x tx2 tiles per
-// image), pooled alone elsewhere. Bit-identical to maxpool_lrn of the unpooled map.
+// image), pooled alone elsewhere. Bit-identical to maxpool_lrn of the unpooled map. max_wgs > 0 caps the
+// grid (knob lrn_wgs: each wave then walks several pixel pairs; same output bits).
 hipError_t lrn_pooled_merge(const float* pooled, const float* p2, float* y, int N, int Hp, int Wp, int C, int ty2,
-                            int tx2, int sub, int size, float alpha, float beta, float k, LrnMode mode, hipStream_t s);
+                            int tx2, int sub, int size, float alpha, float beta, float k, LrnMode mode, hipStream_t s,
+                            int max_wgs = 0);
 
 // Zero the rows of an NHWC buffer outside [row_lo, row_hi) and the W border (halo buffers).
 hipError_t fill(float* x, size_t n, float v, hipStream_t s);

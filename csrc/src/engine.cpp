@@ -461,7 +461,7 @@ hipError_t BlocksEngine::tile_forward_conv1_pool(const float* x, int N, const Ti
     if (pool2) {
       const LrnSpec& l = b2_.lrn;
       ANX_TRY(hip::lrn_pooled_merge(c2_, p2, y + n0 * y_img, n, d_.Hp2, d_.Wp2, d_.C2, ty2, tx2, s2, l.N, l.alpha, l.beta,
-                                    l.k, l.mode, s));
+                                    l.k, l.mode, s, k_.lrn_wgs));
     } else {
       ANX_TRY(pool2_chunk(n, t, y + n0 * y_img, s));
     }

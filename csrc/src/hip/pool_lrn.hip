@@ -236,14 +236,16 @@ __global__ void __launch_bounds__(kThreads) maxpool_lrn256_kernel(const float* _
 }  // namespace
 
 hipError_t lrn_pooled_merge(const float* pooled, const float* p2, float* y, int N, int Hp, int Wp, int C, int ty2,
-                            int tx2, int sub, int size, float alpha, float beta, float k, LrnMode mode, hipStream_t s) {
+                            int tx2, int sub, int size, float alpha, float beta, float k, LrnMode mode, hipStream_t s,
+                            int max_wgs) {
   const long P = static_cast<long>(N) * Hp * Wp;
   if (P == 0) return hipSuccess;
   if (C != 256 || size != 5 || sub < 1 || P * C >= (1L << 31)) return hipErrorInvalidValue;
   const float a = mode == LrnMode::DivN ? alpha / static_cast<float>(size) : alpha;
   constexpr int U = 2;  // pixels per wave step (as maxpool_lrn)
   const long waves = (P + U - 1) / U;
-  const unsigned g = static_cast<unsigned>((waves + kThreads / 64 - 1) / (kThreads / 64));
+  unsigned g = static_cast<unsigned>((waves + kThreads / 64 - 1) / (kThreads / 64));
+  if (max_wgs > 0 && g > static_cast<unsigned>(max_wgs)) g = static_cast<unsigned>(max_wgs);  // the waves walk the rest
   maxpool_lrn256_kernel<3, U, true><<<g, kThreads, 0, s>>>(pooled, y, static_cast<int>(P), Hp, Wp, 1, Hp, Wp, a, beta,
                                                            k, p2, ty2, tx2, sub);
   return hipGetLastError();

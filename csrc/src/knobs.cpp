@@ -45,6 +45,7 @@ const Field kFields[] = {
     {"conv2_tile", &Knobs::conv2_tile, nullptr, 3, 4, "ANX_CONV2_TILE"},
     {"conv2_sched", &Knobs::conv2_sched, nullptr, 0, 1, "ANX_CONV2_SCHED"},
     {"conv2_in_pg", &Knobs::conv2_in_pg, nullptr, 16, 32, "ANX_CONV2_IN_PG"},
+    {"lrn_wgs", &Knobs::lrn_wgs, nullptr, 0, 1 << 20, "ANX_LRN_WGS"},
 };
 
 const Field* find(const char* name) {

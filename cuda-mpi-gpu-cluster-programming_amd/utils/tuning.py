@@ -31,7 +31,8 @@ Names and values:
   and the pool2 + LRN kernel pools it);
   ``conv2_tile`` (Conv2's Winograd output tile: 3 = F(3x3,5x5), 4 = F(4x4,5x5), 21 % fewer multiplies);
   ``conv2_sched`` (1, the default: the F(4x4,5x5) GEMM's hand-scheduled K slice, bitwise equal to 0, the
-  compiler's schedule).
+  compiler's schedule); ``lrn_wgs`` (256, the default: grid cap of the pool2-merge + LRN kernel, its waves
+  walking the remaining pixels; 0 = one wave per pixel pair; same bits).
 """
 from __future__ import annotations
 
@@ -42,7 +43,7 @@ from .. import _native as nat
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 KNOBS = ("conv1_algo", "conv2_algo", "chunk1", "chunk2", "force_vec4", "force_scalar", "bf16_glds", "bf16_big",
          "bf16_lrn_tile", "bf16_conv1", "bf16_pool1", "bf16_fc_cfg", "bf16_fc_minkt", "conv1_occ", "conv2_occ", "conv1_band", "fuse_pool1", "conv1_sub", "conv2_sub",
-         "conv1_fused", "conv1_pool", "conv2_pool", "conv2_tile", "conv2_sched", "conv2_in_pg")
+         "conv1_fused", "conv1_pool", "conv2_pool", "conv2_tile", "conv2_sched", "conv2_in_pg", "lrn_wgs")
 
 
 def knob_value(name: str, value) -> int:

@@ -554,6 +554,19 @@ def test_conv2_hand_schedule_bitwise(cuda, N, kn):
     torch.testing.assert_close(y.double(), ref.to(cuda), rtol=2e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("N", [9, 64, 130])
+def test_lrn_grid_cap_bitwise(cuda, N):
+    """The pool2-merge + LRN kernel with its grid capped (knob lrn_wgs: waves walk several pixel pairs) gives
+    the same bits as one wave per pixel pair (lrn_wgs = 0), behind the pooled F(4x4,5x5) GEMM."""
+    x = init_input(N, "rand", seed=31).to(cuda)
+    mk = lambda v: AlexNetBlocks(device=cuda, init="rand", seed=31, max_batch=N,
+                                 knobs={**WINO1, **WINO2, "conv2_tile": 4, "conv2_pool": 1, "lrn_wgs": v})
+    capped, full, tiny = mk(256), mk(0), mk(3)
+    assert capped.get_knob("lrn_wgs") == 256 and full.get_knob("lrn_wgs") == 0
+    y = capped(x)
+    assert torch.equal(y, full(x)) and torch.equal(y, tiny(x))
+
+
 def test_set_knob_rebuilds_conv2_workspace(cuda):
     """conv2_tile switched 4 -> 3 -> 4 on one engine between forwards rebuilds the transformed weights and
     the V workspace each time (BlocksEngine::prepare) and matches engines built fresh with that tile
