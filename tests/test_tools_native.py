@@ -52,3 +52,24 @@ def test_convbench_all_layers(cuda, algo):
     assert out.returncode == 0, out.stderr
     lines = [l for l in out.stdout.splitlines() if "TFLOP/s" in l]
     assert len(lines) == 5 and all(l.endswith("OK") for l in lines), out.stdout
+
+
+def test_lane_timeline_synthetic_trace(tmp_path):
+    """tools/lane_timeline.py on a hand-made kernel trace: two queues whose kernels overlap, one 5 us idle
+    gap; union, overlap, gaps and per-kernel medians come out as constructed."""
+    import sys
+    hdr = ('"Kind","Agent_Id","Queue_Id","Stream_Id","Thread_Id","Dispatch_Id","Kernel_Id","Kernel_Name",'
+           '"Correlation_Id","Start_Timestamp","End_Timestamp"')
+    rows = [  # (queue, name, start ns, end ns)
+        (1, "conv1_fused_kernel<true>", 0, 100_000), (2, "gemm16_kernel<x>", 50_000, 150_000),
+        (1, "pool_wino_in_kernel<4>", 155_000, 175_000), (2, "maxpool_lrn256_kernel<3>", 160_000, 170_000),
+        (1, "__amd_rocclr_copyBuffer", 0, 500_000)]  # not a Blocks kernel: ignored
+    p = tmp_path / "t.csv"
+    p.write_text(hdr + "\n" + "\n".join(f'"KERNEL_DISPATCH","Agent 2",{q},0,1,{i},1,"{n}",{i},{s},{e}'
+                                        for i, (q, n, s, e) in enumerate(rows)) + "\n")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "lane_timeline.py"), str(p)],
+                         capture_output=True, text=True, check=True).stdout
+    assert "window: 4 dispatches, 175.0 us wall" in out
+    assert "any kernel running: 170.0 us" in out and "two or more: 60.0 us" in out
+    assert "idle gaps: 1, total 5.0 us" in out
+    assert "| `conv1_fused` | 1 | 100.0 | 100.0 |" in out
