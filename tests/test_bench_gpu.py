@@ -39,6 +39,8 @@ def test_bench_blocks_contract():
     assert c["input_batches_rotated"] >= 4 and c["input_bytes_rotated"] > (256 << 20)
     assert c["b1_engine_cold_ms"] > c["b1_warm_ms"] and "b1_cold_ms" not in c
     assert c["b1_process_cold_ms"] > c["b1_engine_cold_ms"] * 0.5 and c["b1_process_cold_vs_reference"] > 0
+    trials = sorted(c["b1_process_cold_trials_ms"])  # the record is the median fresh process
+    assert len(trials) == 3 and c["b1_process_cold_ms"] == trials[1] and c["b1_process_gap_s"] == 2.0
     assert c["gpu_max_hw_queues"] == "8"
     # the matrix-core work actually executed stays below the fp32 MFMA peak; the direct-convolution
     # equivalent may not (Winograd does 4x fewer multiplies)
